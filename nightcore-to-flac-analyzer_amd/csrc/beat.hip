@@ -1,0 +1,494 @@
+// beat.hip — tempo estimate + dynamic-programming beat tracker (K6, K7, K8).
+//
+// Restates librosa 0.11 ``beat.beat_track(onset_envelope=..., start_bpm=...)``
+// as called at tempo.py:45-50 (per 10 s window, hop 512) and tempo.py:159-164
+// (full signal, hop 64), on top of the tempogram mean from window_stage /
+// ibi.hip.  CPU restatement: oracle/ncref.py (tempo_from_tg, beat_local_score,
+// beat_track_dp, last_beat, trim_beats).
+//
+// One workgroup per sequence.  The DP (cumscore[i] = ls[i] + max_d cum[i-d] -
+// pen[d], d in [round(P/2), 2P]) is serial in i but every frame of a block of
+// round(P/2) consecutive frames depends only on frames before the block, so a
+// block is evaluated in parallel (waves over frames, lanes over candidates) with
+// one barrier per block: 43 barriers for a 431-frame window, 738 for a 3-min
+// hop-64 signal.  Short sequences keep every array in LDS; long ones (hop-64
+// IBI pass) use a global workspace that stays L2 resident.
+//
+// Decision arithmetic is float64 throughout (as librosa's numba kernels), with
+// FMA contraction disabled where librosa adds separately rounded products.
+#include "nc_block.h"
+#include "nc_engine.h"
+
+namespace nc {
+
+struct BeatArgs {
+  const float* onset;
+  const int64_t* off;
+  const int* len;
+  const double* tg;
+  int acw;
+  const double* start_bpm;
+  const int* prior_idx;  // nullable: start = start_bpm[prior_idx[s]]
+  const uint8_t* active; // nullable
+  int sr, hop;
+  double max_tempo;
+  float tightness;
+  int trim;
+  double* bpm_out;
+  int* lag_out;
+  int* nbeats_out;
+  double* margin_out;   // nullable
+  int* beats_out;       // nullable (frames, at off[s])
+  double* ws_ls;
+  double* ws_cum;
+  int* ws_back;
+  uint8_t* ws_marks;
+  int max_len;          // SMALL: LDS capacity in frames
+  int tab_cap;          // doubles for the window / penalty table
+};
+
+__host__ __device__ __forceinline__ size_t al16(size_t n) { return (n + 15) & ~(size_t)15; }
+
+template <int NT, bool SMALL>
+__global__ __launch_bounds__(NT) void tempo_beat_kernel(BeatArgs a) {
+#pragma clang fp contract(off)
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  __shared__ BlockScratch<NT> bs;
+  __shared__ int hist[256];
+  __shared__ int sh_int[4];
+  const int s = blockIdx.x;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  constexpr int NW = NT / 64;
+
+  if (a.active && !a.active[s]) {
+    if (threadIdx.x == 0) {
+      a.bpm_out[s] = 0.0;
+      a.lag_out[s] = 0;
+      a.nbeats_out[s] = 0;
+      if (a.margin_out) a.margin_out[s] = 0.0;
+    }
+    return;
+  }
+  const int N = a.len[s];
+  const int64_t off = a.off[s];
+  const float* onset = a.onset + off;
+  const double* tg = a.tg + (size_t)s * a.acw;
+  double* tab = reinterpret_cast<double*>(smem);
+  char* p = smem + al16((size_t)a.tab_cap * sizeof(double));
+  double *ls, *cum;
+  int* back;
+  uint8_t* marks;
+  if (SMALL) {
+    ls = reinterpret_cast<double*>(p);
+    cum = ls + a.max_len;
+    back = reinterpret_cast<int*>(cum + a.max_len);
+    marks = reinterpret_cast<uint8_t*>(back + a.max_len);
+  } else {
+    ls = a.ws_ls + off;
+    cum = a.ws_cum + off;
+    back = a.ws_back + off;
+    marks = a.ws_marks + off;
+  }
+
+  // ------------------------------------------------------------ any onset?
+  int nz = 0;
+  for (int i = threadIdx.x; i < N; i += NT) nz |= (onset[i] != 0.0f);
+  nz = block_max_i<NT>(nz, bs);
+  if (!nz) {  // beat_track: "if not onset_envelope.any(): return (0, [])"
+    if (threadIdx.x == 0) {
+      a.bpm_out[s] = 0.0;
+      a.lag_out[s] = 0;
+      a.nbeats_out[s] = 0;
+      if (a.margin_out) a.margin_out[s] = 0.0;
+    }
+    return;
+  }
+
+  // ------------------------------------------------------------ tempo: prior-weighted argmax
+  const double fs = (double)a.sr;
+  const double start = a.prior_idx ? a.start_bpm[a.prior_idx[s]] : a.start_bpm[s];
+  const double lstart = log2(start);
+  double bv = -INFINITY;
+  int bi = 0x7fffffff;
+  for (int k = threadIdx.x; k < a.acw; k += NT) {
+    double lp = -INFINITY;
+    if (k > 0) {
+      const double bpm = (60.0 * fs) / ((double)a.hop * (double)k);
+      if (bpm < a.max_tempo) {
+        const double d = (log2(bpm) - lstart) / 1.0;
+        lp = -0.5 * (d * d);
+      }
+    }
+    const double sc = log1p(1e6 * tg[k]) + lp;
+    if (np_better(sc, k, bv, bi)) {
+      bv = sc;
+      bi = k;
+    }
+  }
+  block_argmax<NT>(bv, bi, bs);
+  const int L = bi;
+  double sv = -INFINITY;
+  int si = 0x7fffffff;
+  for (int k = threadIdx.x; k < a.acw; k += NT) {
+    if (k == L) continue;
+    double lp = -INFINITY;
+    if (k > 0) {
+      const double bpm = (60.0 * fs) / ((double)a.hop * (double)k);
+      if (bpm < a.max_tempo) {
+        const double d = (log2(bpm) - lstart) / 1.0;
+        lp = -0.5 * (d * d);
+      }
+    }
+    const double sc = log1p(1e6 * tg[k]) + lp;
+    if (np_better(sc, k, sv, si)) {
+      sv = sc;
+      si = k;
+    }
+  }
+  block_argmax<NT>(sv, si, bs);
+  const double bpm = L > 0 ? (60.0 * fs) / ((double)a.hop * (double)L) : INFINITY;
+  const double P = rint((fs / (double)a.hop) * 60.0 / bpm);
+  if (threadIdx.x == 0) {
+    a.bpm_out[s] = bpm;
+    a.lag_out[s] = L;
+    if (a.margin_out) a.margin_out[s] = bv - sv;
+  }
+  const int K = 2 * (int)P + 1;
+  if (!(P >= 1.0) || K > a.tab_cap || (SMALL && N > a.max_len)) {
+    if (threadIdx.x == 0) a.nbeats_out[s] = (P >= 1.0) ? -1 : 0;  // -1: capacity error
+    return;
+  }
+  const int Pi = (int)P;
+
+  // ------------------------------------------------------------ normalise + local score
+  double sx = 0.0;
+  for (int i = threadIdx.x; i < N; i += NT) sx += (double)onset[i];
+  sx = block_sum<NT>(sx, bs);
+  const float mean32 = (float)(sx / (double)N);
+  double sq = 0.0;
+  for (int i = threadIdx.x; i < N; i += NT) {
+    const double d = (double)(onset[i] - mean32);
+    sq += d * d;
+  }
+  sq = block_sum<NT>(sq, bs);
+  const float std32 = (float)sqrt(sq / (double)(N - 1));
+  const float norm = std32 + 1.17549435e-38f;
+
+  for (int k = threadIdx.x; k < K; k += NT) {
+    const double v = ((double)(k - Pi) * 32.0) / P;
+    tab[k] = exp(-0.5 * (v * v));
+  }
+  __syncthreads();
+  double lmax = -INFINITY;
+  for (int i = threadIdx.x; i < N; i += NT) {
+    const int klo = max(0, i + Pi - N + 1), khi = min(i + Pi, K - 1);
+    double acc = 0.0;
+    for (int k = klo; k <= khi; ++k) acc = acc + tab[k] * (double)(onset[i + Pi - k] / norm);
+    ls[i] = acc;
+    lmax = fmax(lmax, acc);
+  }
+  lmax = block_max<NT>(lmax, bs);
+  const double thr = 0.01 * lmax;
+  int first = N;
+  for (int i = threadIdx.x; i < N; i += NT)
+    if (!(ls[i] < thr)) first = min(first, i);
+  const int i0 = block_min_i<NT>(first, bs);
+
+  // ------------------------------------------------------------ DP
+  const int dmin = (int)rint(P / 2.0);
+  const int dmax = 2 * Pi;
+  const double lP = log(P);
+  const double tight = (double)a.tightness;
+  __syncthreads();  // window table no longer needed
+  for (int d = threadIdx.x; d <= dmax; d += NT) {
+    const double t = log((double)d) - lP;
+    tab[d] = tight * (t * t);
+  }
+  __syncthreads();
+  const int B = max(dmin, 1);
+  for (int b0 = 0; b0 < N; b0 += B) {
+    const int b1 = min(N, b0 + B);
+    for (int i = b0 + wave; i < b1; i += NW) {
+      const int dhi = min(dmax, i);
+      double best = -INFINITY;
+      int bd = 0x7fffffff;
+      for (int d = dmin + lane; d <= dhi; d += 64) {
+        const double sc = cum[i - d] - tab[d];
+        if (sc > best || (sc == best && d < bd)) {
+          best = sc;
+          bd = d;
+        }
+      }
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) {
+        const double ov = __shfl_xor(best, o, 64);
+        const int od = __shfl_xor(bd, o, 64);
+        if (ov > best || (ov == best && od < bd)) {
+          best = ov;
+          bd = od;
+        }
+      }
+      if (lane == 0) {
+        const bool found = (dhi >= dmin) && (best > -INFINITY);
+        cum[i] = found ? ls[i] + best : ls[i];
+        back[i] = (i < i0 || !found) ? -1 : i - bd;
+      }
+    }
+    __syncthreads();
+  }
+
+  // ------------------------------------------------------------ last beat
+  for (int i = threadIdx.x; i < N; i += NT) {
+    const double x = cum[i];
+    const bool left = i > 0 ? (x > cum[i - 1]) : false;
+    const bool right = i < N - 1 ? (x >= cum[i + 1]) : true;
+    marks[i] = (left && right) ? 1 : 0;
+  }
+  int cnt = 0;
+  for (int i = threadIdx.x; i < N; i += NT) cnt += marks[i];
+  cnt = block_sum_i<NT>(cnt, bs);
+  int tail = N - 1;
+  if (cnt > 0) {
+    double med;
+    if (cnt & 1) {
+      med = block_kth_flagged<NT>(cum, marks, N, cnt / 2, hist, bs);
+    } else {
+      const double lo = block_kth_flagged<NT>(cum, marks, N, cnt / 2 - 1, hist, bs);
+      const double hi = block_kth_flagged<NT>(cum, marks, N, cnt / 2, hist, bs);
+      med = (lo + hi) / 2.0;
+    }
+    const double thr2 = 0.5 * med;
+    int t = -1;
+    for (int i = threadIdx.x; i < N; i += NT)
+      if (marks[i] && cum[i] >= thr2) t = max(t, i);
+    t = block_max_i<NT>(t, bs);
+    if (t >= 0) tail = t;
+  }
+
+  // ------------------------------------------------------------ backtrack
+  __syncthreads();
+  for (int i = threadIdx.x; i < N; i += NT) marks[i] = 0;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int n = tail;
+    while (n >= 0) {
+      marks[n] = 1;
+      n = back[n];
+    }
+  }
+  __syncthreads();
+
+  // ------------------------------------------------------------ ordered beat list (into back[])
+  const int chunk = (N + NT - 1) / NT;
+  const int c0 = min(N, (int)threadIdx.x * chunk), c1 = min(N, c0 + chunk);
+  int mine = 0;
+  for (int i = c0; i < c1; ++i) mine += marks[i];
+  int nb = 0;
+  int pos = block_exclusive_scan<NT>(mine, nb, bs);
+  __syncthreads();
+  for (int i = c0; i < c1; ++i)
+    if (marks[i]) back[pos++] = i;
+  __syncthreads();
+
+  // ------------------------------------------------------------ trim (0.5 RMS of smoothed beat scores)
+  double thr3 = 0.0;
+  if (a.trim) {
+    double e2 = 0.0;
+    const int cntsm = min(N, nb + 2);
+    for (int j = threadIdx.x; j < cntsm; j += NT) {
+      double v;
+      if (j < nb) {
+        const double xm = j > 0 ? ls[back[j - 1]] : 0.0;
+        const double xp = j + 1 < nb ? ls[back[j + 1]] : 0.0;
+        v = (0.5 * xm + ls[back[j]]) + 0.5 * xp;
+      } else if (j == nb) {
+        v = 0.5 * ls[back[nb - 1]];
+      } else {
+        v = 0.0;
+      }
+      e2 += v * v;
+    }
+    e2 = block_sum<NT>(e2, bs);
+    thr3 = 0.5 * sqrt(e2 / (double)cntsm);
+  }
+  int lo = N, hi = -1;
+  for (int i = threadIdx.x; i < N; i += NT)
+    if (ls[i] > thr3) {
+      lo = min(lo, i);
+      hi = max(hi, i);
+    }
+  lo = block_min_i<NT>(lo, bs);
+  hi = block_max_i<NT>(hi, bs);
+  // kept beats: lo <= frame <= hi, a contiguous run of the ordered list
+  int kfirst = nb, klast = -1;
+  for (int j = threadIdx.x; j < nb; j += NT) {
+    const int f = back[j];
+    if (f >= lo && f <= hi) {
+      kfirst = min(kfirst, j);
+      klast = max(klast, j);
+    }
+  }
+  kfirst = block_min_i<NT>(kfirst, bs);
+  klast = block_max_i<NT>(klast, bs);
+  const int nkeep = klast >= kfirst ? klast - kfirst + 1 : 0;
+  if (threadIdx.x == 0) a.nbeats_out[s] = nkeep;
+  if (a.beats_out)
+    for (int j = threadIdx.x; j < nkeep; j += NT) a.beats_out[off + j] = back[kfirst + j];
+  (void)sh_int;
+}
+
+// ---------------------------------------------------------------------------------------------
+// nc tempo prior (pipeline.py:174-183): median of the valid source window tempos
+// x (src_duration / nc_duration), or 120 when no source window is valid.
+template <int NT>
+__global__ __launch_bounds__(NT) void nc_prior_kernel(const double* bpm, const int* nbeats,
+                                                      const uint8_t* active, const int* src_w0,
+                                                      const int* src_w1, const int64_t* src_len,
+                                                      const int64_t* nc_len, int sr, int min_beats,
+                                                      double* prior_out) {
+  __shared__ BlockScratch<NT> bs;
+  __shared__ int hist[256];
+  __shared__ uint8_t flag[4096];
+  const int p = blockIdx.x;
+  const int w0 = src_w0[p], w1 = src_w1[p];
+  const int n = min(w1 - w0, 4096);
+  int cnt = 0;
+  for (int i = threadIdx.x; i < n; i += NT) {
+    const int w = w0 + i;
+    const uint8_t f = (active == nullptr || active[w]) && nbeats[w] >= min_beats;
+    flag[i] = f;
+    cnt += f;
+  }
+  cnt = block_sum_i<NT>(cnt, bs);
+  const double nc_dur = (double)nc_len[p] / (double)sr;
+  const double src_dur = (double)src_len[p] / (double)sr;
+  double prior = 120.0;
+  if (cnt > 0 && nc_dur > 0 && src_dur > 0) {
+    double med;
+    if (cnt & 1) {
+      med = block_kth_flagged<NT>(bpm + w0, flag, n, cnt / 2, hist, bs);
+    } else {
+      const double lo = block_kth_flagged<NT>(bpm + w0, flag, n, cnt / 2 - 1, hist, bs);
+      const double hi = block_kth_flagged<NT>(bpm + w0, flag, n, cnt / 2, hist, bs);
+      med = (lo + hi) / 2.0;
+    }
+    prior = med * (src_dur / nc_dur);
+  }
+  if (threadIdx.x == 0) prior_out[p] = prior;
+}
+
+// ---------------------------------------------------------------------------------------------
+// tempo.py:165-172: t = frames*hop/sr, ibis = diff(t), keep > 0.05 s; counts < min -> 0.
+template <int NT>
+__global__ __launch_bounds__(NT) void ibi_from_beats_kernel(const int* beats, const int64_t* off,
+                                                            const int* nbeats, int sr, int hop,
+                                                            int min_ibis, double* ibi_out, int* n_ibi) {
+  __shared__ BlockScratch<NT> bs;
+  const int s = blockIdx.x;
+  const int nb = nbeats[s];
+  const int64_t o = off[s];
+  if (nb < min_ibis + 1) {
+    if (threadIdx.x == 0) n_ibi[s] = 0;
+    return;
+  }
+  const int m = nb - 1;
+  const int chunk = (m + NT - 1) / NT;
+  const int c0 = min(m, (int)threadIdx.x * chunk), c1 = min(m, c0 + chunk);
+  auto ibi = [&](int j) {
+    const double t0 = (double)((long long)beats[o + j] * hop) / (double)sr;
+    const double t1 = (double)((long long)beats[o + j + 1] * hop) / (double)sr;
+    return t1 - t0;
+  };
+  int mine = 0;
+  for (int j = c0; j < c1; ++j) mine += ibi(j) > 0.05;
+  int tot = 0;
+  int pos = block_exclusive_scan<NT>(mine, tot, bs);
+  for (int j = c0; j < c1; ++j) {
+    const double v = ibi(j);
+    if (v > 0.05) ibi_out[o + pos++] = v;
+  }
+  if (threadIdx.x == 0) n_ibi[s] = tot < min_ibis ? 0 : tot;
+}
+
+// ---------------------------------------------------------------------------------------------
+int launch_tempo_beats(Context& ctx, BeatArgs a, int n_seq, int max_len, hipStream_t st) {
+  if (n_seq <= 0) return 0;
+  a.max_len = max_len;
+  a.max_tempo = 320.0;
+  a.tightness = 100.0f;
+  a.sr = a.sr ? a.sr : kSR;
+  // longest possible window table / penalty table: 2P+1 with P <= acw-1
+  a.tab_cap = 2 * (a.acw - 1) + 2;
+  const size_t tab = al16((size_t)a.tab_cap * sizeof(double));
+  const size_t small_lds = tab + (size_t)max_len * (8 + 8 + 4 + 1) + 16;
+  if (small_lds <= 64 * 1024) {
+    hipLaunchKernelGGL((tempo_beat_kernel<256, true>), dim3(n_seq), dim3(256), small_lds, st, a);
+  } else {
+    if (!a.ws_ls || !a.ws_cum || !a.ws_back || !a.ws_marks) {
+      set_error("tempo_beats: long sequences need the global workspace");
+      return -3;
+    }
+    if (tab > 120 * 1024) {
+      set_error("tempo_beats: tempogram window too long");
+      return -2;
+    }
+    hipLaunchKernelGGL((tempo_beat_kernel<1024, false>), dim3(n_seq), dim3(1024), tab, st, a);
+  }
+  NC_HIP(hipGetLastError());
+  return 0;
+}
+
+int launch_nc_prior(const double* bpm, const int* nbeats, const uint8_t* active, const int* src_w0,
+                    const int* src_w1, const int64_t* src_len, const int64_t* nc_len, int n_pairs,
+                    double* prior_out, hipStream_t st) {
+  if (n_pairs <= 0) return 0;
+  hipLaunchKernelGGL((nc_prior_kernel<256>), dim3(n_pairs), dim3(256), 0, st, bpm, nbeats, active, src_w0,
+                     src_w1, src_len, nc_len, kSR, 4, prior_out);
+  NC_HIP(hipGetLastError());
+  return 0;
+}
+
+int launch_ibi_from_beats(const int* beats, const int64_t* off, const int* nbeats, int n_seq, int hop,
+                          int min_ibis, double* ibi_out, int* n_ibi, hipStream_t st) {
+  if (n_seq <= 0) return 0;
+  hipLaunchKernelGGL((ibi_from_beats_kernel<256>), dim3(n_seq), dim3(256), 0, st, beats, off, nbeats, kSR,
+                     hop, min_ibis, ibi_out, n_ibi);
+  NC_HIP(hipGetLastError());
+  return 0;
+}
+
+}  // namespace nc
+
+namespace nc {
+int launch_tempo_beats_c(Context& ctx, const float* onset, const int64_t* off, const int* len, int n_seq,
+                         int max_len, const double* tg, int acw, const double* start_bpm, const int* prior_idx,
+                         const uint8_t* active, int hop, int trim, double* bpm_out, int* lag_out,
+                         int* nbeats_out, double* margin_out, int* beats_out, int64_t total_frames, void* ws,
+                         size_t ws_bytes, hipStream_t st) {
+  BeatArgs a{};
+  a.onset = onset;
+  a.off = off;
+  a.len = len;
+  a.tg = tg;
+  a.acw = acw;
+  a.start_bpm = start_bpm;
+  a.prior_idx = prior_idx;
+  a.active = active;
+  a.sr = kSR;
+  a.hop = hop;
+  a.trim = trim;
+  a.bpm_out = bpm_out;
+  a.lag_out = lag_out;
+  a.nbeats_out = nbeats_out;
+  a.margin_out = margin_out;
+  a.beats_out = beats_out;
+  if (ws && total_frames > 0 && ws_bytes >= (size_t)total_frames * 21) {
+    a.ws_ls = static_cast<double*>(ws);
+    a.ws_cum = a.ws_ls + total_frames;
+    a.ws_back = reinterpret_cast<int*>(a.ws_cum + total_frames);
+    a.ws_marks = reinterpret_cast<uint8_t*>(a.ws_back + total_frames);
+  }
+  (void)ctx;
+  return launch_tempo_beats(ctx, a, n_seq, max_len, st);
+}
+}  // namespace nc

@@ -1,0 +1,202 @@
+// nc_block.h — workgroup-level primitives (LDS reductions, scans, radix select).
+#pragma once
+#include "nc_device.h"
+
+namespace nc {
+
+// Workgroup scratch for reductions: at least NT/64 * 16 bytes.
+template <int NT>
+struct BlockScratch {
+  double d[NT / 64];
+  long long l[NT / 64];
+  int i[NT / 64];
+};
+
+template <int NT>
+__device__ __forceinline__ double block_sum(double v, BlockScratch<NT>& s) {
+  v = wave_sum(v);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  __syncthreads();
+  if (lane == 0) s.d[wave] = v;
+  __syncthreads();
+  double r = 0.0;
+#pragma unroll
+  for (int i = 0; i < NT / 64; ++i) r += s.d[i];
+  return r;
+}
+
+template <int NT>
+__device__ __forceinline__ double block_max(double v, BlockScratch<NT>& s) {
+  v = wave_max(v);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  __syncthreads();
+  if (lane == 0) s.d[wave] = v;
+  __syncthreads();
+  double r = s.d[0];
+#pragma unroll
+  for (int i = 1; i < NT / 64; ++i) r = fmax(r, s.d[i]);
+  return r;
+}
+
+__device__ __forceinline__ int wave_min_i(int v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = min(v, __shfl_xor(v, o, 64));
+  return v;
+}
+__device__ __forceinline__ int wave_max_i(int v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = max(v, __shfl_xor(v, o, 64));
+  return v;
+}
+__device__ __forceinline__ int wave_sum_i(int v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+template <int NT>
+__device__ __forceinline__ int block_min_i(int v, BlockScratch<NT>& s) {
+  v = wave_min_i(v);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  __syncthreads();
+  if (lane == 0) s.i[wave] = v;
+  __syncthreads();
+  int r = s.i[0];
+#pragma unroll
+  for (int i = 1; i < NT / 64; ++i) r = min(r, s.i[i]);
+  return r;
+}
+template <int NT>
+__device__ __forceinline__ int block_max_i(int v, BlockScratch<NT>& s) {
+  v = wave_max_i(v);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  __syncthreads();
+  if (lane == 0) s.i[wave] = v;
+  __syncthreads();
+  int r = s.i[0];
+#pragma unroll
+  for (int i = 1; i < NT / 64; ++i) r = max(r, s.i[i]);
+  return r;
+}
+template <int NT>
+__device__ __forceinline__ int block_sum_i(int v, BlockScratch<NT>& s) {
+  v = wave_sum_i(v);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  __syncthreads();
+  if (lane == 0) s.i[wave] = v;
+  __syncthreads();
+  int r = 0;
+#pragma unroll
+  for (int i = 0; i < NT / 64; ++i) r += s.i[i];
+  return r;
+}
+
+// Exclusive prefix sum of one int per thread (in thread order) + total.
+template <int NT>
+__device__ __forceinline__ int block_exclusive_scan(int v, int& total, BlockScratch<NT>& s) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  int incl = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int y = __shfl_up(incl, o, 64);
+    if (lane >= o) incl += y;
+  }
+  __syncthreads();
+  if (lane == 63) s.i[wave] = incl;
+  __syncthreads();
+  int base = 0, tot = 0;
+#pragma unroll
+  for (int i = 0; i < NT / 64; ++i) {
+    if (i < wave) base += s.i[i];
+    tot += s.i[i];
+  }
+  total = tot;
+  return base + incl - v;
+}
+
+// (value, index) argmax with numpy semantics: NaN wins, ties -> smallest index.
+__device__ __forceinline__ bool np_better(double a, int ia, double b, int ib) {
+  const bool na = a != a, nb = b != b;
+  if (na || nb) {
+    if (na && nb) return ia < ib;
+    return na;
+  }
+  if (a > b) return true;
+  if (a < b) return false;
+  return ia < ib;
+}
+__device__ __forceinline__ void wave_argmax(double& v, int& i) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const double ov = __shfl_xor(v, o, 64);
+    const int oi = __shfl_xor(i, o, 64);
+    if (np_better(ov, oi, v, i)) {
+      v = ov;
+      i = oi;
+    }
+  }
+}
+template <int NT>
+__device__ __forceinline__ void block_argmax(double& v, int& i, BlockScratch<NT>& s) {
+  wave_argmax(v, i);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  __syncthreads();
+  if (lane == 0) {
+    s.d[wave] = v;
+    s.i[wave] = i;
+  }
+  __syncthreads();
+  v = s.d[0];
+  i = s.i[0];
+#pragma unroll
+  for (int k = 1; k < NT / 64; ++k)
+    if (np_better(s.d[k], s.i[k], v, i)) {
+      v = s.d[k];
+      i = s.i[k];
+    }
+}
+
+__device__ __forceinline__ unsigned long long dkey(double x) {
+  unsigned long long u = (unsigned long long)__double_as_longlong(x);
+  return (u >> 63) ? ~u : (u | 0x8000000000000000ull);
+}
+__device__ __forceinline__ double dunkey(unsigned long long k) {
+  const unsigned long long u = (k >> 63) ? (k & 0x7FFFFFFFFFFFFFFFull) : ~k;
+  return __longlong_as_double((long long)u);
+}
+
+// k-th smallest (0-based) of vals[i] over i in [0,n) with flag[i] != 0.
+// 8 passes of 8-bit radix select; hist = 256 ints of LDS.
+template <int NT>
+__device__ double block_kth_flagged(const double* vals, const uint8_t* flag, int n, int k, int* hist,
+                                    BlockScratch<NT>& s) {
+  unsigned long long prefix = 0, mask = 0;
+  for (int shift = 56; shift >= 0; shift -= 8) {
+    for (int i = threadIdx.x; i < 256; i += NT) hist[i] = 0;
+    __syncthreads();
+    for (int i = threadIdx.x; i < n; i += NT) {
+      if (!flag[i]) continue;
+      const unsigned long long key = dkey(vals[i]);
+      if ((key & mask) == prefix) atomicAdd(&hist[(key >> shift) & 255], 1);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      int kk = k, d = 0;
+      for (; d < 256; ++d) {
+        if (kk < hist[d]) break;
+        kk -= hist[d];
+      }
+      s.l[0] = (long long)d;
+      s.i[0] = kk;
+    }
+    __syncthreads();
+    const unsigned long long d = (unsigned long long)s.l[0];
+    k = s.i[0];
+    prefix |= d << shift;
+    mask |= 255ull << shift;
+    __syncthreads();
+  }
+  return dunkey(prefix);
+}
+
+}  // namespace nc

@@ -1,0 +1,224 @@
+// nc_device.h — shared CDNA4 (gfx950) device helpers for the nightcore engine.
+//
+// * complex float2 arithmetic
+// * wave64 reductions (shuffle based; wave = 64 lanes on CDNA, never 32)
+// * a one-wave Stockham auto-sort FFT (mixed radix 4/8/16) working on an LDS
+//   buffer with a 1-in-16 pad (bank-conflict break for the stride-R writes of
+//   the first stage), inputs of stage 1 taken straight from registers.
+//
+// Every FFT here is forward (e^{-2 pi i nk/N}); inverses use the conjugation
+// identity.  Twiddles come from a 4096-entry table built on the host in double
+// precision (exp(-2 pi i m / 4096) rounded to f32), so one table serves all
+// N <= 4096.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define NC_WAVE 64
+
+namespace nc {
+
+__device__ __forceinline__ float2 cadd(float2 a, float2 b) { return make_float2(a.x + b.x, a.y + b.y); }
+__device__ __forceinline__ float2 csub(float2 a, float2 b) { return make_float2(a.x - b.x, a.y - b.y); }
+__device__ __forceinline__ float2 cmul(float2 a, float2 b) {
+  return make_float2(fmaf(a.x, b.x, -a.y * b.y), fmaf(a.x, b.y, a.y * b.x));
+}
+__device__ __forceinline__ float2 cconj(float2 a) { return make_float2(a.x, -a.y); }
+__device__ __forceinline__ float2 cscale(float2 a, float s) { return make_float2(a.x * s, a.y * s); }
+// multiply by -i
+__device__ __forceinline__ float2 cmul_mi(float2 a) { return make_float2(a.y, -a.x); }
+
+// ------------------------------------------------------------------ wave reductions
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ double wave_max(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// float <-> order-preserving int (for atomicMax on floats of either sign)
+__device__ __forceinline__ int f2ord(float f) {
+  int i = __float_as_int(f);
+  return i >= 0 ? i : i ^ 0x7FFFFFFF;
+}
+__device__ __forceinline__ float ord2f(int i) { return __int_as_float(i >= 0 ? i : i ^ 0x7FFFFFFF); }
+
+// ------------------------------------------------------------------ in-register DFTs
+// exp(-2 pi i m / 16) for the odd m (compile-time after unrolling)
+__device__ __forceinline__ float2 w16(int m) {
+  switch (m) {
+    case 1: return make_float2(9.238795325e-01f, -3.826834324e-01f);
+    case 3: return make_float2(3.826834324e-01f, -9.238795325e-01f);
+    case 5: return make_float2(-3.826834324e-01f, -9.238795325e-01f);
+    default: return make_float2(-9.238795325e-01f, -3.826834324e-01f);  // 7
+  }
+}
+
+// twiddle exp(-2 pi i k / R) * o with k, R compile-time after unrolling (k < R/2)
+template <int R>
+__device__ __forceinline__ float2 twr(int k, float2 o) {
+  const int m = k * (16 / R);
+  if (m == 0) return o;
+  if (m == 4) return cmul_mi(o);
+  const float s = 7.071067812e-01f;
+  if (m == 2) return make_float2(s * (o.x + o.y), s * (o.y - o.x));   // (s, -s)
+  if (m == 6) return make_float2(s * (o.y - o.x), -s * (o.x + o.y));  // (-s, -s)
+  return cmul(w16(m), o);
+}
+
+template <int R>
+struct DFT {
+  static __device__ __forceinline__ void run(float2* v) {
+    float2 e[R / 2], o[R / 2];
+#pragma unroll
+    for (int i = 0; i < R / 2; ++i) {
+      e[i] = v[2 * i];
+      o[i] = v[2 * i + 1];
+    }
+    DFT<R / 2>::run(e);
+    DFT<R / 2>::run(o);
+#pragma unroll
+    for (int k = 0; k < R / 2; ++k) {
+      const float2 t = twr<R>(k, o[k]);
+      v[k] = cadd(e[k], t);
+      v[k + R / 2] = csub(e[k], t);
+    }
+  }
+};
+template <>
+struct DFT<1> {
+  static __device__ __forceinline__ void run(float2*) {}
+};
+template <>
+struct DFT<2> {
+  static __device__ __forceinline__ void run(float2* v) {
+    const float2 a = v[0], b = v[1];
+    v[0] = cadd(a, b);
+    v[1] = csub(a, b);
+  }
+};
+template <>
+struct DFT<4> {
+  static __device__ __forceinline__ void run(float2* v) {
+    const float2 s02 = cadd(v[0], v[2]), d02 = csub(v[0], v[2]);
+    const float2 s13 = cadd(v[1], v[3]), d13 = cmul_mi(csub(v[1], v[3]));
+    v[0] = cadd(s02, s13);
+    v[2] = csub(s02, s13);
+    v[1] = cadd(d02, d13);
+    v[3] = csub(d02, d13);
+  }
+};
+
+// ------------------------------------------------------------------ Stockham wave FFT
+__device__ __forceinline__ int lpad(int i) { return i + (i >> 4); }
+template <int N>
+struct LdsSize {
+  static constexpr int value = N + N / 16;  // float2 elements
+};
+
+// Stage with radix R, NS = product of the previous radices.  Reads either LDS
+// (FROM_REGS = false) or a caller-provided register image of the stage-1 input
+// layout x[j + r*N/R], j = lane + 64 b.
+template <int N, int R, int NS>
+__device__ __forceinline__ void stockham_stage_regs(float2 (&v)[N / (R * 64)][R], float2* lds,
+                                                    const float2* __restrict__ tw, int lane) {
+  constexpr int NB = N / (R * 64);
+  static_assert(NB >= 1, "radix too large for one wave");
+#pragma unroll
+  for (int b = 0; b < NB; ++b) {
+    const int j = lane + 64 * b;
+    const int k = j % NS;
+    if (NS > 1) {
+#pragma unroll
+      for (int r = 1; r < R; ++r) v[b][r] = cmul(v[b][r], tw[(k * r * (4096 / (NS * R))) & 4095]);
+    }
+    DFT<R>::run(v[b]);
+  }
+#pragma unroll
+  for (int b = 0; b < NB; ++b) {
+    const int j = lane + 64 * b;
+    const int k = j % NS;
+    const int base = (j / NS) * NS * R + k;
+#pragma unroll
+    for (int r = 0; r < R; ++r) lds[lpad(base + r * NS)] = v[b][r];
+  }
+}
+
+template <int N, int R, int NS>
+__device__ __forceinline__ void stockham_stage(float2* lds, const float2* __restrict__ tw, int lane) {
+  constexpr int NB = N / (R * 64);
+  float2 v[NB][R];
+#pragma unroll
+  for (int b = 0; b < NB; ++b) {
+    const int j = lane + 64 * b;
+#pragma unroll
+    for (int r = 0; r < R; ++r) v[b][r] = lds[lpad(j + r * (N / R))];
+  }
+  stockham_stage_regs<N, R, NS>(v, lds, tw, lane);
+}
+
+// Radix plans: 512 = 8.8.8, 1024 = 16.16.4, 2048 = 16.16.8, 4096 = 16.16.16
+template <int N>
+struct Plan;
+template <>
+struct Plan<512> {
+  static constexpr int R0 = 8, R1 = 8, R2 = 8;
+};
+template <>
+struct Plan<1024> {
+  static constexpr int R0 = 16, R1 = 16, R2 = 4;
+};
+template <>
+struct Plan<2048> {
+  static constexpr int R0 = 16, R1 = 16, R2 = 8;
+};
+template <>
+struct Plan<4096> {
+  static constexpr int R0 = 16, R1 = 16, R2 = 16;
+};
+
+// Stage-1 input register image: in[b][r] = x[(lane + 64 b) + r * N / R0].
+template <int N>
+using FftIn = float2[N / (Plan<N>::R0 * 64)][Plan<N>::R0];
+
+// Full forward FFT; result in natural order in lds (padded indexing).
+// One wave; no block barrier needed (LDS ops of a wave complete in order and
+// every stage loads all of its inputs before its first store).
+template <int N>
+__device__ __forceinline__ void wave_fft(FftIn<N>& in, float2* lds, const float2* __restrict__ tw, int lane) {
+  constexpr int R0 = Plan<N>::R0, R1 = Plan<N>::R1, R2 = Plan<N>::R2;
+  static_assert(R0 * R1 * R2 == N, "plan");
+  stockham_stage_regs<N, R0, 1>(in, lds, tw, lane);
+  stockham_stage<N, R1, R0>(lds, tw, lane);
+  stockham_stage<N, R2, R0 * R1>(lds, tw, lane);
+}
+
+// Real-FFT split: Z = FFT_N(z), z[n] = x[2n] + i x[2n+1] (x real, length 2N).
+// Returns X[k] and X[N-k] for 0 <= k <= N/2.
+__device__ __forceinline__ void rfft_split(const float2* lds, const float2* __restrict__ tw, int N, int k,
+                                           float2& Xk, float2& XNk) {
+  const float2 a = lds[lpad(k & (N - 1))];
+  const float2 b = cconj(lds[lpad((N - k) & (N - 1))]);
+  const float2 E = cscale(cadd(a, b), 0.5f);
+  const float2 O = cmul_mi(cscale(csub(a, b), 0.5f));  // (a-b)/(2i)
+  const float2 W = tw[(k * (4096 / (2 * N))) & 4095];  // exp(-2 pi i k / 2N)
+  const float2 WO = cmul(W, O);
+  Xk = cadd(E, WO);
+  XNk = cconj(csub(E, WO));
+}
+
+}  // namespace nc

@@ -1,0 +1,66 @@
+// nc_engine.h — internal (C++) interface between the C-ABI layer and the HIP
+// kernels.  Not part of the public boundary (that is include/ncgpu.h).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <string>
+
+namespace nc {
+
+constexpr int kSR = 22050;
+constexpr int kNFFT = 2048;     // STFT / mel frame (onset_strength, piptrack)
+constexpr int kNMels = 128;
+constexpr int kCqtBins = 252;   // 7 octaves x 36
+constexpr int kCqtBpo = 36;
+constexpr int kCqtFilt = 36;    // filters per octave
+constexpr int kCqtNfft = 1024;
+constexpr int kNTunings = 100;  // tuning grid (-0.50 .. 0.49 step 0.01)
+constexpr int kHalfbandK = 23;  // decimator half length (47 taps)
+
+// Device-resident constant tables, built once per context (double precision on
+// the host, rounded to f32).
+struct Tables {
+  float2* tw4096 = nullptr;     // exp(-2 pi i m / 4096)
+  float* hann2048 = nullptr;    // periodic Hann, STFT window
+  float* hann_ac512 = nullptr;  // periodic Hann(344): tempogram window at hop 512
+  float* hann_ac64 = nullptr;   // periodic Hann(2756): tempogram window at hop 64
+  int ac512 = 0, ac64 = 0;
+  // Slaney mel filterbank (sr 22050, n_fft 2048, 128 bands, fmax 11025) in CSR
+  int* mel_lo = nullptr;
+  int* mel_len = nullptr;
+  int* mel_off = nullptr;
+  float* mel_w = nullptr;
+  // CQT: per tuning index, per filter: [lo, len, off] into a complex weight pool
+  int* cqt_lo = nullptr;        // [kNTunings][36]
+  int* cqt_len = nullptr;
+  int* cqt_off = nullptr;
+  float2* cqt_w = nullptr;      // sparse basis rows (octave-0 basis, sqrt(sr/my_sr) applied per octave)
+  float* cqt_inv_sqrt_len = nullptr;  // [kNTunings][252]  1/sqrt(lengths)
+  int cqt_maxlen = 0;
+  double* halfband = nullptr;   // 2K+1 taps
+};
+
+struct Context {
+  int device = 0;
+  int num_cu = 256;
+  hipStream_t stream = nullptr;
+  Tables t;
+};
+
+void build_tables(Context& ctx);
+void free_tables(Context& ctx);
+
+// error plumbing (thread-local message, int status)
+void set_error(const std::string& msg);
+
+}  // namespace nc
+
+#define NC_HIP(call)                                                                  \
+  do {                                                                                \
+    hipError_t _e = (call);                                                           \
+    if (_e != hipSuccess) {                                                           \
+      nc::set_error(std::string(#call) + ": " + hipGetErrorString(_e));              \
+      return -1;                                                                      \
+    }                                                                                 \
+  } while (0)

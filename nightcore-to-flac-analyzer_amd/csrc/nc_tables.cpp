@@ -1,0 +1,281 @@
+// nc_tables.cpp — constant tables built once per context on the host (double
+// precision, rounded to f32) and uploaded to HBM.
+//
+//   tw4096          exp(-2 pi i m / 4096)                     (all FFTs)
+//   hann2048        scipy.signal.get_window('hann', 2048)     (librosa.stft window)
+//   hann_ac512/64   get_window('hann', win) for the tempogram (feature.tempogram)
+//   mel CSR         librosa.filters.mel(sr=22050, n_fft=2048, n_mels=128, fmax=11025,
+//                   htk=False, norm='slaney', dtype=float32)
+//   halfband        the engine's soxr_hq replacement (oracle/ncref.py halfband_taps)
+//   CQT bases       librosa vqt filter basis (octave 0) for all 100 tuning values
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <complex>
+#include <cstring>
+#include <numeric>
+#include <vector>
+
+#include "nc_engine.h"
+
+namespace nc {
+
+namespace {
+
+std::vector<double> hann_periodic(int n) {
+  // scipy general_cosine(n+1, [0.5, 0.5])[:n]: 0.5 + 0.5 cos(-pi + j * 2pi/n)
+  std::vector<double> w(n);
+  const double step = (M_PI - (-M_PI)) / (double)n;
+  for (int j = 0; j < n; ++j) {
+    const double fac = (double)j * step + (-M_PI);
+    w[j] = 0.5 + 0.5 * std::cos(fac);
+  }
+  return w;
+}
+
+double hz_to_mel(double f) {
+  const double f_sp = 200.0 / 3;
+  const double min_log_hz = 1000.0, min_log_mel = min_log_hz / f_sp, logstep = std::log(6.4) / 27.0;
+  if (f >= min_log_hz) return min_log_mel + std::log(f / min_log_hz) / logstep;
+  return f / f_sp;
+}
+double mel_to_hz(double m) {
+  const double f_sp = 200.0 / 3;
+  const double min_log_hz = 1000.0, min_log_mel = min_log_hz / f_sp, logstep = std::log(6.4) / 27.0;
+  if (m >= min_log_mel) return min_log_hz * std::exp(logstep * (m - min_log_mel));
+  return f_sp * m;
+}
+
+template <typename T>
+T* upload(const std::vector<T>& v) {
+  T* d = nullptr;
+  if (hipMalloc(&d, std::max<size_t>(1, v.size()) * sizeof(T)) != hipSuccess) return nullptr;
+  if (!v.empty()) (void)hipMemcpy(d, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice);
+  return d;
+}
+
+std::vector<float> to_f32(const std::vector<double>& v) {
+  std::vector<float> o(v.size());
+  for (size_t i = 0; i < v.size(); ++i) o[i] = (float)v[i];
+  return o;
+}
+
+// ---------------------------------------------------------------- host FFT (double, radix 2)
+void fft_inplace(std::vector<std::complex<double>>& a) {
+  const size_t n = a.size();
+  for (size_t i = 1, j = 0; i < n; ++i) {
+    size_t bit = n >> 1;
+    for (; j & bit; bit >>= 1) j ^= bit;
+    j ^= bit;
+    if (i < j) std::swap(a[i], a[j]);
+  }
+  for (size_t len = 2; len <= n; len <<= 1) {
+    const double ang = -2 * M_PI / (double)len;
+    for (size_t i = 0; i < n; i += len)
+      for (size_t k = 0; k < len / 2; ++k) {
+        const std::complex<double> w(std::cos(ang * (double)k), std::sin(ang * (double)k));
+        const auto u = a[i + k], v = a[i + k + len / 2] * w;
+        a[i + k] = u + v;
+        a[i + k + len / 2] = u - v;
+      }
+  }
+}
+
+}  // namespace
+
+void build_tables(Context& ctx) {
+  Tables& t = ctx.t;
+  // twiddles
+  std::vector<float2> tw(4096);
+  for (int m = 0; m < 4096; ++m) {
+    const double a = 2.0 * M_PI * (double)m / 4096.0;
+    tw[m] = make_float2((float)std::cos(a), (float)-std::sin(a));
+  }
+  t.tw4096 = upload(tw);
+  t.hann2048 = upload(to_f32(hann_periodic(kNFFT)));
+  t.ac512 = (int)((int)(8.0 * kSR) / 512);
+  t.ac64 = (int)((int)(8.0 * kSR) / 64);
+  t.hann_ac512 = upload(to_f32(hann_periodic(t.ac512)));
+  t.hann_ac64 = upload(to_f32(hann_periodic(t.ac64)));
+
+  // mel filterbank (oracle/ncref.py mel_filter)
+  {
+    const int nb = 1 + kNFFT / 2, nm = kNMels;
+    const double fmin = 0.0, fmax = kSR / 2.0;
+    const double mmin = hz_to_mel(fmin), mmax = hz_to_mel(fmax);
+    std::vector<double> mel_f(nm + 2);
+    const double step = (mmax - mmin) / (double)(nm + 1);
+    for (int j = 0; j < nm + 2; ++j) mel_f[j] = mel_to_hz(j == nm + 1 ? mmax : (double)j * step + mmin);
+    std::vector<double> fft_f(nb);
+    for (int k = 0; k < nb; ++k) fft_f[k] = (double)k * ((double)kSR / (double)kNFFT);
+    std::vector<int> lo(nm), len(nm), offs(nm);
+    std::vector<float> wts;
+    for (int i = 0; i < nm; ++i) {
+      const double fd0 = mel_f[i + 1] - mel_f[i], fd1 = mel_f[i + 2] - mel_f[i + 1];
+      const double enorm = 2.0 / (mel_f[i + 2] - mel_f[i]);
+      std::vector<float> row(nb);
+      int first = -1, last = -1;
+      for (int k = 0; k < nb; ++k) {
+        const double lower = -(mel_f[i] - fft_f[k]) / fd0;
+        const double upper = (mel_f[i + 2] - fft_f[k]) / fd1;
+        float w = (float)std::max(0.0, std::min(lower, upper));
+        w = (float)((double)w * enorm);
+        row[k] = w;
+        if (w != 0.0f) {
+          if (first < 0) first = k;
+          last = k;
+        }
+      }
+      if (first < 0) first = last = 0;
+      lo[i] = first;
+      len[i] = last - first + 1;
+      offs[i] = (int)wts.size();
+      for (int k = first; k <= last; ++k) wts.push_back(row[k]);
+    }
+    t.mel_lo = upload(lo);
+    t.mel_len = upload(len);
+    t.mel_off = upload(offs);
+    t.mel_w = upload(wts);
+  }
+
+  // half-band decimator (oracle/ncref.py halfband_taps): 0.5 sinc(n/2) kaiser(n; 11), unit DC
+  {
+    const int K = kHalfbandK, M = 2 * K + 1;
+    const double beta = 11.0;
+    auto i0 = [](double x) {  // modified Bessel I0 (series)
+      double s = 1.0, term = 1.0;
+      for (int k = 1; k < 200; ++k) {
+        term *= (x / (2.0 * k)) * (x / (2.0 * k));
+        s += term;
+        if (term < 1e-18 * s) break;
+      }
+      return s;
+    };
+    std::vector<double> h(M);
+    double sum = 0.0;
+    for (int j = 0; j < M; ++j) {
+      const int n = j - K;
+      double v;
+      if (n == 0) v = 0.5;
+      else if (n % 2 == 0) v = 0.0;
+      else v = 0.5 * std::sin(M_PI * n / 2.0) / (M_PI * n / 2.0);
+      const double r = 2.0 * j / (M - 1) - 1.0;
+      v *= i0(beta * std::sqrt(std::max(0.0, 1.0 - r * r))) / i0(beta);
+      h[j] = v;
+      sum += v;
+    }
+    for (auto& v : h) v /= sum;
+    t.halfband = upload(h);
+  }
+
+  // CQT bases for every tuning on the 0.01-bin grid (oracle/ncref.py cqt_mag / vqt_filter_fft)
+  {
+    const double C1 = 440.0 * std::pow(2.0, (24 - 69) / 12.0);
+    const int nb = kCqtBins, bpo = kCqtBpo, nf = kCqtFilt, nfft = kCqtNfft, nbin = nfft / 2 + 1;
+    std::vector<int> clo(kNTunings * nf), clen(kNTunings * nf), coff(kNTunings * nf);
+    std::vector<float2> cw;
+    std::vector<float> isl(kNTunings * nb);
+    for (int ti = 0; ti < kNTunings; ++ti) {
+      // tuning grid: numpy linspace(-0.5, 0.5, 101) left edges
+      const double tuning = (double)ti * (1.0 / 100.0) + (-0.5);
+      const double fmin = C1 * std::pow(2.0, tuning / bpo);
+      std::vector<double> freqs(nb), logf(nb), alpha(nb);
+      {
+        std::vector<double> allr;
+        for (int o = 0; o < (nb + bpo - 1) / bpo; ++o)
+          for (int r = 0; r < bpo; ++r) allr.push_back(std::pow(2.0, (double)o) * std::pow(2.0, (double)r / bpo));
+        allr.resize(nb);
+        std::sort(allr.begin(), allr.end());
+        for (int k = 0; k < nb; ++k) freqs[k] = allr[k] * fmin;
+      }
+      for (int k = 0; k < nb; ++k) logf[k] = std::log2(freqs[k]);
+      for (int k = 0; k < nb; ++k) {
+        double bp;
+        if (k == 0) bp = 1.0 / (logf[1] - logf[0]);
+        else if (k == nb - 1) bp = 1.0 / (logf[nb - 1] - logf[nb - 2]);
+        else bp = 2.0 / (logf[k + 1] - logf[k - 1]);
+        const double r = std::pow(2.0, 2.0 / bp);
+        alpha[k] = (r - 1) / (r + 1);
+      }
+      for (int k = 0; k < nb; ++k) {
+        const double len = (1.0 / alpha[k]) * kSR / freqs[k];
+        isl[ti * nb + k] = (float)(1.0 / std::sqrt(len));
+      }
+      // octave 0 = top 36 bins at sr
+      for (int f = 0; f < nf; ++f) {
+        const int k = nb - nf + f;
+        const double fr = freqs[k];
+        const double ilen = (1.0 / alpha[k]) * kSR / fr;
+        const double a0 = std::floor(-ilen / 2.0), a1 = std::floor(ilen / 2.0);
+        const int n = (int)(a1 - a0);
+        std::vector<std::complex<double>> sig(n);
+        const std::vector<double> win = hann_periodic(n);
+        double l1 = 0.0;
+        for (int j = 0; j < n; ++j) {
+          const double ang = (a0 + j) * 2 * M_PI * fr / kSR;
+          sig[j] = std::complex<double>(std::cos(ang), std::sin(ang)) * win[j];
+          l1 += std::abs(sig[j]);
+        }
+        std::vector<std::complex<double>> buf(nfft, 0.0);
+        const int lp = (nfft - n) / 2;
+        for (int j = 0; j < n; ++j) {
+          const std::complex<float> c32((float)(sig[j] / l1).real(), (float)(sig[j] / l1).imag());
+          const double sc = ilen / (double)nfft;
+          const std::complex<float> s32((float)(c32.real() * sc), (float)(c32.imag() * sc));
+          buf[lp + j] = std::complex<double>(s32.real(), s32.imag());
+        }
+        fft_inplace(buf);
+        // sparsify_rows(quantile=0.01) over the nbin kept bins
+        std::vector<double> mags(nbin), srt(nbin);
+        double norm = 0.0;
+        for (int b = 0; b < nbin; ++b) {
+          mags[b] = std::abs(buf[b]);
+          norm += mags[b];
+        }
+        srt = mags;
+        std::sort(srt.begin(), srt.end());
+        double cum = 0.0;
+        int thr_idx = 0;
+        for (int b = 0; b < nbin; ++b) {
+          cum += srt[b] / norm;
+          if (!(cum < 0.01)) {
+            thr_idx = b;
+            break;
+          }
+        }
+        const double thr = srt[thr_idx];
+        int first = -1, last = -1;
+        for (int b = 0; b < nbin; ++b)
+          if (mags[b] >= thr) {
+            if (first < 0) first = b;
+            last = b;
+          }
+        clo[ti * nf + f] = first;
+        clen[ti * nf + f] = last - first + 1;
+        coff[ti * nf + f] = (int)cw.size();
+        for (int b = first; b <= last; ++b) {
+          const bool keep = mags[b] >= thr;
+          cw.push_back(keep ? make_float2((float)buf[b].real(), (float)buf[b].imag()) : make_float2(0.f, 0.f));
+        }
+        t.cqt_maxlen = std::max(t.cqt_maxlen, last - first + 1);
+      }
+    }
+    t.cqt_lo = upload(clo);
+    t.cqt_len = upload(clen);
+    t.cqt_off = upload(coff);
+    t.cqt_w = upload(cw);
+    t.cqt_inv_sqrt_len = upload(isl);
+  }
+}
+
+void free_tables(Context& ctx) {
+  Tables& t = ctx.t;
+  void* ptrs[] = {t.tw4096, t.hann2048, t.hann_ac512, t.hann_ac64, t.mel_lo,  t.mel_len, t.mel_off,
+                  t.mel_w,  t.cqt_lo,   t.cqt_len,    t.cqt_off,  t.cqt_w,   t.cqt_inv_sqrt_len, t.halfband};
+  for (void* p : ptrs)
+    if (p) (void)hipFree(p);
+  t = Tables();
+}
+
+}  // namespace nc

@@ -1,0 +1,120 @@
+// trim.hip — K1a: librosa.effects.trim(y, top_db) as called by io.strip_silence
+// (io.py:58-79).  oracle: ncref.trim / ncref.rms_frames.
+//
+//   ms[t]   = mean_{2048-sample centred frame t, zero padded} x^2     (hop 512)
+//   rms[t]  = sqrt(ms[t]) (f32);  db[t] = 10 log10(max(1e-10, rms^2)) - 10 log10(max(1e-10, max(rms)^2))
+//   start   = first(db > -top_db) * 512,  end = min(N, (last + 1) * 512)
+//
+// Kernel 1: one wave per frame (coalesced 8 KB loads, f64 accumulation, overlap
+// re-reads served by L2); kernel 2: one workgroup per file.
+#include "nc_block.h"
+#include "nc_engine.h"
+
+namespace nc {
+
+__global__ __launch_bounds__(256) void trim_frames_kernel(const float* sig, const int64_t* file_off,
+                                                          const int64_t* file_len, const int64_t* frame_base,
+                                                          int n_files, int64_t total_frames, float* ms_out) {
+  const int lane = threadIdx.x & 63;
+  const int64_t gw = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (gw >= total_frames) return;
+  // find the file (binary search over frame_base)
+  int lo = 0, hi = n_files - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (frame_base[mid] <= gw) lo = mid;
+    else hi = mid - 1;
+  }
+  const int f = lo;
+  const int64_t t = gw - frame_base[f];
+  const float* x = sig + file_off[f];
+  const int64_t N = file_len[f];
+  const int64_t s0 = t * 512 - 1024;
+  double acc = 0.0;
+#pragma unroll 8
+  for (int j = lane; j < 2048; j += 64) {
+    const int64_t i = s0 + j;
+    const double v = (i >= 0 && i < N) ? (double)x[i] : 0.0;
+    acc = fma(v, v, acc);
+  }
+  acc = wave_sum(acc);
+  if (lane == 0) ms_out[gw] = (float)(acc / 2048.0);
+}
+
+__global__ __launch_bounds__(256) void trim_bounds_kernel(const float* ms, const int64_t* frame_base,
+                                                          const int64_t* file_len, float top_db,
+                                                          int64_t* out_start, int64_t* out_end) {
+  __shared__ BlockScratch<256> bs;
+  const int f = blockIdx.x;
+  const int64_t N = file_len[f];
+  const int64_t T = 1 + N / 512;
+  const float* m = ms + frame_base[f];
+  double mx = -1.0;
+  for (int64_t t = threadIdx.x; t < T; t += 256) mx = fmax(mx, (double)sqrtf(m[t]));
+  mx = block_max<256>(mx, bs);
+  const float ref = (float)mx;
+  const float ref_db = 10.0f * log10f(fmaxf(1e-10f, ref * ref));
+  int first = 0x7fffffff, last = -1;
+  for (int64_t t = threadIdx.x; t < T; t += 256) {
+    const float r = sqrtf(m[t]);
+    const float db = 10.0f * log10f(fmaxf(1e-10f, r * r)) - ref_db;
+    if (db > -top_db) {
+      first = min(first, (int)t);
+      last = max(last, (int)t);
+    }
+  }
+  first = block_min_i<256>(first, bs);
+  last = block_max_i<256>(last, bs);
+  if (threadIdx.x == 0) {
+    if (last >= 0) {
+      out_start[f] = (int64_t)first * 512;
+      out_end[f] = min(N, ((int64_t)last + 1) * 512);
+    } else {
+      out_start[f] = 0;
+      out_end[f] = 0;
+    }
+  }
+}
+
+size_t trim_ws_bytes(const int64_t* host_file_len, int n_files) {
+  size_t frames = 0;
+  for (int f = 0; f < n_files; ++f) frames += 1 + host_file_len[f] / 512;
+  return frames * sizeof(float) + (size_t)(n_files + 1) * sizeof(int64_t) + 256;
+}
+
+// frame_base is computed on the device from file_len (exclusive scan, one block)
+__global__ void frame_base_kernel(const int64_t* file_len, int n_files, int64_t* frame_base) {
+  if (threadIdx.x == 0 && blockIdx.x == 0) {
+    int64_t acc = 0;
+    for (int f = 0; f < n_files; ++f) {
+      frame_base[f] = acc;
+      acc += 1 + file_len[f] / 512;
+    }
+    frame_base[n_files] = acc;
+  }
+}
+
+int launch_trim(Context& ctx, const float* sig, const int64_t* file_off, const int64_t* file_len, int n_files,
+                int64_t max_frames, float top_db, int64_t* out_start, int64_t* out_end, void* ws,
+                size_t ws_bytes, hipStream_t st) {
+  (void)ctx;
+  if (n_files <= 0) return 0;
+  // max_frames = total frames over all files (host knows the lengths)
+  const size_t need = (size_t)max_frames * sizeof(float) + (size_t)(n_files + 1) * sizeof(int64_t);
+  if (ws_bytes < need) {
+    set_error("trim: workspace too small");
+    return -3;
+  }
+  int64_t* frame_base = static_cast<int64_t*>(ws);
+  float* ms = reinterpret_cast<float*>(frame_base + n_files + 1);
+  hipLaunchKernelGGL(frame_base_kernel, dim3(1), dim3(64), 0, st, file_len, n_files, frame_base);
+  const int64_t blocks = (max_frames + 3) / 4;
+  hipLaunchKernelGGL(trim_frames_kernel, dim3((unsigned)blocks), dim3(256), 0, st, sig, file_off, file_len,
+                     frame_base, n_files, max_frames, ms);
+  hipLaunchKernelGGL(trim_bounds_kernel, dim3(n_files), dim3(256), 0, st, ms, frame_base, file_len, top_db,
+                     out_start, out_end);
+  NC_HIP(hipGetLastError());
+  return 0;
+}
+
+}  // namespace nc
