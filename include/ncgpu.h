@@ -109,6 +109,106 @@ int nc_tempo_prior(nc_ctx* ctx, const double* bpm, const int* nbeats, const uint
 int nc_ibi_from_beats(nc_ctx* ctx, const int* beats, const int64_t* off, const int* nbeats, int n_seq,
                       int hop, int min_ibis, double* ibi_out, int* n_ibi, void* stream);
 
+
+/* ---------------------------------------------------------------------------
+ * K9..K11  CQT chroma — replaces pitch._mean_chroma (pitch.py:55-64) =
+ * librosa.feature.chroma_cqt(y, sr=22050, bins_per_octave=36, hop_length=512)
+ * .mean(axis=1) for each chunk c = sig[chunk_off[c] .. +chunk_len[c]):
+ * tuning estimate (piptrack, 0.01-bin histogram) -> 7-octave CQT (252 bins,
+ * octave decimation by the engine's half-band FIR in place of soxr_hq) ->
+ * 12-bin chroma (n_chroma = 12: the reference's lag/3 quirk) ->
+ * per-frame inf-norm -> mean.  out_chroma[c*12 + k] (f32), out_tuning[c]
+ * (f32, bins), out_tuning_idx[c] (nullable; index on the 0.01 grid).
+ * total_len = sum of chunk_len; max_chunk_len = max of chunk_len.
+ * ------------------------------------------------------------------------- */
+size_t nc_chroma_workspace_bytes(const nc_ctx* ctx, int n_chunks, int64_t total_len);
+int nc_chroma_mean(nc_ctx* ctx, const float* sig, const int64_t* chunk_off, const int64_t* chunk_len,
+                   int n_chunks, int64_t total_len, int64_t max_chunk_len, float* out_chroma,
+                   float* out_tuning, int* out_tuning_idx, void* ws, size_t ws_bytes, void* stream);
+/* pitch._cyclic_xcorr_peak (pitch.py:67-85): lag_out[p] = wrapped argmax_k
+ * dot(chroma[src_idx[p]], roll(chroma[nc_idx[p]], -k)), in [-5, 6]. */
+int nc_chroma_lag(nc_ctx* ctx, const float* chroma, const int* src_idx, const int* nc_idx, int n_pairs,
+                  int* lag_out, void* stream);
+
+/* ---------------------------------------------------------------------------
+ * device glue between the kernels (so a batch needs no host round trip)
+ * nc_energy_gate   io.energy_gate (io.py:115-126) per group of windows
+ *                  [w0[g], w1[g]): active[w] = energy_db[w] >= max + threshold_db
+ * nc_collect_valid consensus._valid (consensus.py:236-240) of the per-window
+ *                  tempo lists: in window order, values of windows that are
+ *                  active, have nbeats >= min_beats (tempo.py:54-55) and a finite
+ *                  positive bpm -> out_values[w0[g] + i], count out_n[g]
+ * nc_pitch_hz      pitch.py:95,161-164: shift = lag/3.0, nc_hz = 440*2^(shift/12),
+ *                  src_hz = 440
+ * ------------------------------------------------------------------------- */
+/* io._rms_db (io.py:38-40) alone, for windows sig[win_off[w] .. +win_len) */
+int nc_window_energy(nc_ctx* ctx, const float* sig, const int64_t* win_off, int n_win, int win_len,
+                     double* energy_out, void* stream);
+int nc_energy_gate(nc_ctx* ctx, const double* energy_db, const int* w0, const int* w1, int n_groups,
+                   double threshold_db, uint8_t* active_out, void* stream);
+int nc_collect_valid(nc_ctx* ctx, const double* bpm, const int* nbeats, const uint8_t* active,
+                     const int* w0, const int* w1, int n_groups, int min_beats, double* out_values,
+                     int* out_n, void* stream);
+int nc_pitch_hz(nc_ctx* ctx, const int* lags, int n, double* shift_out, double* nc_hz, double* src_hz,
+                void* stream);
+
+/* ---------------------------------------------------------------------------
+ * K12  bootstrap ratio of medians — replaces consensus._bootstrap_ratio
+ * (consensus.py:243-267), consensus.compute_ibi_ratio (consensus.py:270-312)
+ * and the chunk-shift bootstrap of pitch.estimate_pitch_chroma
+ * (pitch.py:143-150).  Job j draws A = values[a_off[j] .. +a_n[j]) first and
+ * B = values[b_off[j] .. +b_n[j]) second (b_off/b_n NULL: single array) with
+ * numpy Generator(PCG64) choice(replace=True) semantics, bit-exact:
+ * seed[j*4 .. +4] = PCG64 {state_hi, state_lo, inc_hi, inc_lo} of
+ * np.random.default_rng(seed).  boot[i] = median(A*)/median(B*) (median(A*));
+ * point = median(A)/median(B); CI = numpy 'linear' percentiles given as
+ * (virtual index, gamma) pairs for the low and high quantile.  Jobs with
+ * a_n < min_n (or b_n < min_n) yield NaN (the reference's MIN_VALID gate).
+ * Workspace: job j uses job_cap[j] (>= a_n + b_n) values at byte offset
+ * job_ws_off[j]; size each with nc_bootstrap_job_bytes(cap, n_boot).
+ * ------------------------------------------------------------------------- */
+size_t nc_bootstrap_job_bytes(int cap, int n_boot);
+int nc_bootstrap_ratio(nc_ctx* ctx, const double* values, const int64_t* a_off, const int* a_n,
+                       const int64_t* b_off, const int* b_n, int n_jobs, int n_boot,
+                       const uint64_t* seed, double idx_lo, double gamma_lo, double idx_hi,
+                       double gamma_hi, int min_n, double* point_out, double* lo_out, double* hi_out,
+                       double* boot_out, const int64_t* job_ws_off, const int* job_cap, void* ws,
+                       size_t ws_bytes, void* stream);
+
+/* ---------------------------------------------------------------------------
+ * hop-64 IBI pass, part 1 — librosa.onset.onset_strength(y, sr, hop_length=hop)
+ * over whole files (tempo.py:158): file f = sig[file_off[f] .. +file_len[f]),
+ * onset_out at frame_base[f] (frame_base_out[n_files+1], written here:
+ * prefix of 1 + file_len/hop).  total_frames = sum(1 + file_len/hop).
+ * ------------------------------------------------------------------------- */
+size_t nc_ibi_onset_workspace_bytes(const nc_ctx* ctx, int n_files, int64_t total_frames);
+int nc_ibi_onset(nc_ctx* ctx, const float* sig, const int64_t* file_off, const int64_t* file_len,
+                 int n_files, int64_t total_frames, int hop, float* onset_out,
+                 int64_t* frame_base_out, void* ws, size_t ws_bytes, void* stream);
+/* part 2 — the tempogram mean (win_length = ac_size*sr/hop, 2756 at hop 64)
+ * that beat_track argmaxes (tempo.py:159), streamed instead of materialised:
+ * tg_out[f*acw + k]. */
+size_t nc_ibi_tempogram_workspace_bytes(const nc_ctx* ctx, int n_files, int hop);
+int nc_ibi_tempogram(nc_ctx* ctx, const float* onset, const int64_t* frame_base, int n_files, int hop,
+                     double* tg_out, void* ws, size_t ws_bytes, void* stream);
+
+/* ---------------------------------------------------------------------------
+ * K13  windowed waveform cross-correlation — the search loop of
+ * xcorr.estimate_speed_xcorr (xcorr.py:109-160).  The caller plans the
+ * reference's integer geometry: n_items dot products of `win` samples between
+ * sig[item_a[i]..] and sig[item_b[i]..]; job j owns windows [w0[j], w1[j]);
+ * window w has its self item win_self[w] (a.a), candidate items
+ * [cand0[w], cand1[w]) whose b positions are pb[item], its a position pa[w]
+ * and default exp_pb[w].  Outputs ratio_out[j] (np.polyfit slope) and
+ * quality_out[j] (median normalised correlation); (1, 0) with < 3 matches.
+ * scratch: dot/sqb = 2 * n_items doubles (caller-owned device memory).
+ * ------------------------------------------------------------------------- */
+int nc_xcorr_search(nc_ctx* ctx, const float* sig, const int64_t* item_a, const int64_t* item_b,
+                    int n_items, int win, double* dot, double* sqb, const int* w0, const int* w1,
+                    const int* win_self, const int* cand0, const int* cand1, const int64_t* pa,
+                    const int64_t* pb, const int64_t* exp_pb, int n_jobs, double* ratio_out,
+                    double* quality_out, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

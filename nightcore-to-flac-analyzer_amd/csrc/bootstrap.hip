@@ -1,0 +1,276 @@
+// bootstrap.hip — K12: the 2000-resample bootstrap ratio of medians.
+//
+// Replaces consensus._bootstrap_ratio (consensus.py:243-267; draw order nc then
+// src, point = median(nc)/median(src)), consensus.compute_ibi_ratio
+// (consensus.py:270-312; draw order src then nc, point = median(src)/median(nc))
+// and the single-array chunk-shift bootstrap of pitch.estimate_pitch_chroma
+// (pitch.py:143-150, seed 0).  In every case: A is drawn first, B second, and
+// boot[i] = median(A*) / median(B*)  (median(A*) when B is absent).
+//
+// Bit-exact numpy: rng = default_rng(seed) is PCG64 (128-bit LCG, XSL-RR
+// output); Generator.choice(a, n, replace=True) = integers(0, n) = Lemire's
+// bounded 32-bit draw on next_uint32(), which returns the LOW then the HIGH half
+// of each 64-bit output with the spare half buffered in the bit generator (so it
+// carries across calls); n == 1 consumes nothing.  Resample r starts at uint32
+// position s_r = sum_{q<r} consumed_q; with rare Lemire rejections the
+// positions are found by a fix-point (assume r*m, walk, prefix-sum, repeat until
+// stable) inside one workgroup, each thread jumping to its position with the
+// O(log n) LCG advance.  Medians: the resample's multiset is kept as counts per
+// rank of the sorted input, so the k-th smallest is a scan.  Percentiles use
+// numpy's 'linear' method (virtual index (n-1) q, lerp with the t >= 0.5 branch),
+// whose (index, gamma) the host computes with numpy's own formula.
+#include "nc_block.h"
+#include "nc_engine.h"
+
+namespace nc {
+
+typedef unsigned __int128 u128;
+
+__device__ __forceinline__ u128 pcg_mult() {
+  return ((u128)0x2360ED051FC65DA4ull << 64) | (u128)0x4385DF649FCCF645ull;
+}
+__device__ __forceinline__ uint64_t xsl_rr(u128 s) {
+  const uint64_t x = (uint64_t)(s >> 64) ^ (uint64_t)s;
+  const unsigned rot = (unsigned)(s >> 122);
+  return (x >> rot) | (x << ((64u - rot) & 63u));
+}
+__device__ __forceinline__ u128 pcg_advance(u128 state, u128 inc, uint64_t delta) {
+  u128 acc_mult = 1, acc_plus = 0, cur_mult = pcg_mult(), cur_plus = inc;
+  while (delta > 0) {
+    if (delta & 1) {
+      acc_mult *= cur_mult;
+      acc_plus = acc_plus * cur_mult + cur_plus;
+    }
+    cur_plus = (cur_mult + 1) * cur_plus;
+    cur_mult *= cur_mult;
+    delta >>= 1;
+  }
+  return acc_mult * state + acc_plus;
+}
+
+struct Gen32 {
+  u128 s, inc;
+  uint64_t out;
+  int half;
+  __device__ void init(u128 s0, u128 inc_, uint64_t u) {
+    inc = inc_;
+    s = pcg_advance(s0, inc, u / 2 + 1);
+    out = xsl_rr(s);
+    half = (int)(u & 1);
+  }
+  __device__ __forceinline__ uint32_t next() {
+    uint32_t v;
+    if (half) {
+      v = (uint32_t)(out >> 32);
+      s = s * pcg_mult() + inc;
+      out = xsl_rr(s);
+      half = 0;
+    } else {
+      v = (uint32_t)out;
+      half = 1;
+    }
+    return v;
+  }
+  // Lemire bounded draw in [0, n); returns index, adds consumed uint32s
+  __device__ __forceinline__ uint32_t bounded(uint32_t n, int& consumed) {
+    uint64_t m = (uint64_t)next() * n;
+    ++consumed;
+    uint32_t left = (uint32_t)m;
+    if (left < n) {
+      const uint32_t thr = (uint32_t)((0xFFFFFFFFu - (n - 1)) % n);
+      while (left < thr) {
+        m = (uint64_t)next() * n;
+        ++consumed;
+        left = (uint32_t)m;
+      }
+    }
+    return (uint32_t)(m >> 32);
+  }
+};
+
+constexpr int BT = 1024;
+
+__device__ __forceinline__ double lerp_np(double a, double b, double t) {
+  const double d = b - a;
+  return t >= 0.5 ? b - d * (1.0 - t) : a + d * t;
+}
+
+__global__ __launch_bounds__(BT) void bootstrap_kernel(BootArgs a) {
+  __shared__ BlockScratch<BT> bs;
+  __shared__ double sorted_boot[2048];
+  __shared__ int sh_changed;
+  const int j = blockIdx.x;
+  const int na = a.a_n[j];
+  const int nb = a.b_n ? a.b_n[j] : 0;
+  const bool hasB = a.b_n != nullptr;
+  if (na < a.min_n || (hasB && nb < a.min_n) || na <= 0) {
+    if (threadIdx.x == 0) {
+      a.point_out[j] = NAN;
+      a.lo_out[j] = NAN;
+      a.hi_out[j] = NAN;
+    }
+    return;
+  }
+  const double* A = a.values + a.a_off[j];
+  const double* B = hasB ? a.values + a.b_off[j] : nullptr;
+  const int cap = a.cap[j];
+  char* w = a.ws + a.ws_off[j];
+  int* rankA = reinterpret_cast<int*>(w);
+  int* rankB = rankA + na;
+  double* sortedA = reinterpret_cast<double*>(w + (((size_t)cap * 4 + 15) & ~(size_t)15));
+  double* sortedB = sortedA + na;
+  int64_t* start = reinterpret_cast<int64_t*>(sortedA + cap);
+  uint16_t* cnt = reinterpret_cast<uint16_t*>(start + a.n_boot);  // [n_boot][na + nb]
+
+  // ranks (stable: ties broken by index) and sorted values
+  for (int i = threadIdx.x; i < na; i += BT) {
+    const double v = A[i];
+    int r = 0;
+    for (int q = 0; q < na; ++q) {
+      const double u = A[q];
+      r += (u < v) || (u == v && q < i);
+    }
+    rankA[i] = r;
+    sortedA[r] = v;
+  }
+  for (int i = threadIdx.x; i < nb; i += BT) {
+    const double v = B[i];
+    int r = 0;
+    for (int q = 0; q < nb; ++q) {
+      const double u = B[q];
+      r += (u < v) || (u == v && q < i);
+    }
+    rankB[i] = r;
+    sortedB[r] = v;
+  }
+  __syncthreads();
+
+  const u128 s0 = ((u128)a.seed[j * 4 + 0] << 64) | (u128)a.seed[j * 4 + 1];
+  const u128 inc = ((u128)a.seed[j * 4 + 2] << 64) | (u128)a.seed[j * 4 + 3];
+  const int m = (na > 1 ? na : 0) + (nb > 1 ? nb : 0);  // uint32 draws per resample w/o rejection
+  const int nv = na + nb;
+  for (int r = threadIdx.x; r < a.n_boot; r += BT) start[r] = (int64_t)r * m;
+  __syncthreads();
+
+  for (int iter = 0; iter < 4096; ++iter) {
+    // walk: consumed count per resample (+ counts as a side effect)
+    int local_cons[(2048 + BT - 1) / BT];
+    int li = 0;
+    for (int r = threadIdx.x; r < a.n_boot; r += BT, ++li) {
+      uint16_t* c = cnt + (size_t)r * nv;
+      for (int q = 0; q < nv; ++q) c[q] = 0;
+      int consumed = 0;
+      if (m > 0) {
+        Gen32 g;
+        g.init(s0, inc, (uint64_t)start[r]);
+        if (na > 1)
+          for (int q = 0; q < na; ++q) c[rankA[g.bounded((uint32_t)na, consumed)]]++;
+        else
+          c[0] += (uint16_t)na;  // n == 1: every draw is index 0, no RNG consumed
+        if (hasB) {
+          if (nb > 1)
+            for (int q = 0; q < nb; ++q) c[na + rankB[g.bounded((uint32_t)nb, consumed)]]++;
+          else
+            c[na] += (uint16_t)nb;
+        }
+      } else {
+        c[0] += (uint16_t)na;
+        if (hasB) c[na] += (uint16_t)nb;
+      }
+      local_cons[li] = consumed;
+    }
+    // exclusive scan over resamples (thread-major: r = tid + BT*li)
+    if (threadIdx.x == 0) sh_changed = 0;
+    __syncthreads();
+    int64_t carry = 0;
+    for (int base = 0, l2 = 0; base < a.n_boot; base += BT, ++l2) {
+      const int r = base + threadIdx.x;
+      const int v = r < a.n_boot ? local_cons[l2] : 0;
+      int tot = 0;
+      const int ex = block_exclusive_scan<BT>(v, tot, bs);
+      if (r < a.n_boot) {
+        const int64_t ns = carry + ex;
+        if (ns != start[r]) {
+          start[r] = ns;
+          sh_changed = 1;
+        }
+      }
+      carry += tot;
+      __syncthreads();
+    }
+    __syncthreads();
+    if (!sh_changed) break;
+    __syncthreads();
+  }
+
+  // medians -> boot values
+  auto kth = [&](const uint16_t* c, int n, int k, const double* srt) {
+    int acc = 0;
+    for (int q = 0; q < n; ++q) {
+      acc += c[q];
+      if (acc > k) return srt[q];
+    }
+    return srt[n - 1];
+  };
+  auto med = [&](const uint16_t* c, int n, const double* srt) {
+    if (n & 1) return kth(c, n, n / 2, srt);
+    return (kth(c, n, n / 2 - 1, srt) + kth(c, n, n / 2, srt)) / 2.0;
+  };
+  for (int r = threadIdx.x; r < 2048; r += BT) {
+    double v = INFINITY;
+    if (r < a.n_boot) {
+      const uint16_t* c = cnt + (size_t)r * nv;
+      const double ma = med(c, na, sortedA);
+      v = hasB ? ma / med(c + na, nb, sortedB) : ma;
+      if (a.boot_out) a.boot_out[(size_t)j * a.n_boot + r] = v;
+    }
+    sorted_boot[r] = v;
+  }
+  __syncthreads();
+  // bitonic sort of 2048 doubles in LDS
+  for (int k = 2; k <= 2048; k <<= 1) {
+    for (int jj = k >> 1; jj > 0; jj >>= 1) {
+      for (int i = threadIdx.x; i < 2048; i += BT) {
+        const int ixj = i ^ jj;
+        if (ixj > i) {
+          const double x = sorted_boot[i], y = sorted_boot[ixj];
+          const bool up = (i & k) == 0;
+          if ((x > y) == up) {
+            sorted_boot[i] = y;
+            sorted_boot[ixj] = x;
+          }
+        }
+      }
+      __syncthreads();
+    }
+  }
+  if (threadIdx.x == 0) {
+    const int il = (int)a.idx_lo, ih = (int)a.idx_hi;
+    const int ilp = min(il + 1, a.n_boot - 1), ihp = min(ih + 1, a.n_boot - 1);
+    a.lo_out[j] = lerp_np(sorted_boot[il], sorted_boot[ilp], a.g_lo);
+    a.hi_out[j] = lerp_np(sorted_boot[ih], sorted_boot[ihp], a.g_hi);
+    const double pa = (na & 1) ? sortedA[na / 2] : (sortedA[na / 2 - 1] + sortedA[na / 2]) / 2.0;
+    double pb = 1.0;
+    if (hasB) pb = (nb & 1) ? sortedB[nb / 2] : (sortedB[nb / 2 - 1] + sortedB[nb / 2]) / 2.0;
+    a.point_out[j] = hasB ? pa / pb : pa;
+  }
+}
+
+size_t bootstrap_job_bytes(int cap, int n_boot) {
+  size_t b = (((size_t)cap * 4 + 15) & ~(size_t)15);
+  b += (size_t)cap * 8 + (size_t)n_boot * 8 + (size_t)n_boot * cap * 2;
+  return (b + 255) & ~(size_t)255;
+}
+
+int launch_bootstrap(const BootArgs& a, int n_jobs, hipStream_t st) {
+  if (n_jobs <= 0) return 0;
+  if (a.n_boot > 2048 || a.n_boot < 1) {
+    set_error("bootstrap: n_boot must be in [1, 2048]");
+    return -2;
+  }
+  hipLaunchKernelGGL(bootstrap_kernel, dim3(n_jobs), dim3(BT), 0, st, a);
+  NC_HIP(hipGetLastError());
+  return 0;
+}
+
+}  // namespace nc

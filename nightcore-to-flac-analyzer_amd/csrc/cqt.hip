@@ -171,8 +171,8 @@ __global__ __launch_bounds__(256) void tuning_peaks_kernel(PeakArgs a) {
       pk = (z > zm) && (z >= zp);
       if (pk) {
         // parabolic shift (librosa numba stencil, f64 arithmetic, stored f32)
-        const double aa = (double)sp + (double)sm - 2.0 * (double)s;
-        const double bb = ((double)sp - (double)sm) / 2.0;
+        const double aa = (double)(sp + sm) - 2.0 * (double)s;  // f32 add, then f64 (numba typing)
+        const double bb = (double)(sp - sm) / 2.0;
         const float shift = (fabs(bb) >= fabs(aa)) ? 0.0f : (float)(-bb / aa);
         const float avg = (sp - sm) / 2.0f;
         const float dskew = (0.5f * avg) * shift;
@@ -509,7 +509,7 @@ int launch_chroma_mean(Context& ctx, const float* sig, const int64_t* chunk_off,
   pa.tf_base = w.tf_base;
   pa.n_chunks = n;
   pa.total_tframes = tfr;  // upper bound; frames beyond tf_base[n] are skipped below
-  pa.tw = ctx.t.tw4096;
+  pa.tw = ctx.t.tw;
   pa.hann2048 = ctx.t.hann2048;
   pa.peak_pitch = w.peak_pitch;
   pa.peak_mag = w.peak_mag;
@@ -528,7 +528,7 @@ int launch_chroma_mean(Context& ctx, const float* sig, const int64_t* chunk_off,
   ca.tuning_idx = w.tuning_idx;
   ca.ws_oct = w.ws_oct;
   ca.nblk = kCqtBlk;
-  ca.tw = ctx.t.tw4096;
+  ca.tw = ctx.t.tw;
   ca.cqt_lo = ctx.t.cqt_lo;
   ca.cqt_len = ctx.t.cqt_len;
   ca.cqt_off = ctx.t.cqt_off;

@@ -33,6 +33,36 @@ int launch_trim(Context& ctx, const float* sig, const int64_t* file_off, const i
                 int64_t max_frames, float top_db, int64_t* out_start, int64_t* out_end, void* ws,
                 size_t ws_bytes, hipStream_t st);
 
+size_t chroma_ws_bytes(int n, int64_t total_len);
+int launch_chroma_mean(Context& ctx, const float* sig, const int64_t* chunk_off, const int64_t* chunk_len, int n,
+                       int64_t total_len, int64_t max_chunk_len, float* out_chroma, float* out_tuning,
+                       int* out_tuning_idx, void* ws, size_t ws_bytes, hipStream_t st);
+int launch_chroma_lag(const float* chroma, const int* src_idx, const int* nc_idx, int n_pairs, int* lag_out,
+                      hipStream_t st);
+
+size_t bootstrap_job_bytes(int cap, int n_boot);
+int launch_bootstrap(const BootArgs& a, int n_jobs, hipStream_t st);
+
+size_t ibi_onset_ws_bytes(int n_files, int64_t total_frames);
+int launch_ibi_onset(Context& ctx, const float* sig, const int64_t* file_off, const int64_t* file_len, int n_files,
+                     int64_t total_frames, int hop, float* onset_out, int64_t* frame_base_out, void* ws,
+                     size_t ws_bytes, hipStream_t st);
+size_t ibi_tg_ws_bytes(const Context& ctx, int n_files, int acw);
+int launch_ibi_tempogram(Context& ctx, const float* onset, const int64_t* frame_base, int n_files, int hop,
+                         double* tg_out, void* ws, size_t ws_bytes, hipStream_t st);
+
+int launch_xcorr(const float* sig, const int64_t* ia, const int64_t* ib, int n_items, int win, double* dot,
+                 double* sqb, const int* w0, const int* w1, const int* sw, const int* c0, const int* c1,
+                 const int64_t* pa, const int64_t* pbv, const int64_t* exp_pb, int n_jobs, double* ratio_out,
+                 double* quality_out, hipStream_t st);
+
+int launch_energy_gate(const double* energy, const int* w0, const int* w1, int n_groups, double gate_db,
+                       uint8_t* active, hipStream_t st);
+int launch_collect_valid(const double* bpm, const int* nbeats, const uint8_t* active, const int* w0, const int* w1,
+                         int n_groups, int min_beats, double* out_values, int* out_n, hipStream_t st);
+int launch_pitch_hz(const int* lags, int n, double* shift_out, double* nc_hz, double* src_hz, hipStream_t st);
+int launch_window_energy(const float* sig, const int64_t* off, int n, int win_len, double* out, hipStream_t st);
+
 }  // namespace nc
 
 struct nc_ctx {
@@ -83,7 +113,7 @@ int nc_create(int device, nc_ctx** out) {
   if (hipDeviceGetAttribute(&cu, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && cu > 0)
     c->c.num_cu = cu;
   nc::build_tables(c->c);
-  if (!c->c.t.tw4096 || !c->c.t.cqt_w || !c->c.t.halfband) {
+  if (!c->c.t.tw || !c->c.t.cqt_w || !c->c.t.halfband) {
     nc::free_tables(c->c);
     delete c;
     nc::set_error("nc_create: table allocation failed");
@@ -161,6 +191,127 @@ int nc_ibi_from_beats(nc_ctx* ctx, const int* beats, const int64_t* off, const i
   SET_DEVICE(ctx);
   return nc::launch_ibi_from_beats(beats, off, nbeats, n_seq, hop, min_ibis, ibi_out, n_ibi,
                                    (hipStream_t)stream);
+}
+
+size_t nc_chroma_workspace_bytes(const nc_ctx* ctx, int n_chunks, int64_t total_len) {
+  (void)ctx;
+  return nc::chroma_ws_bytes(n_chunks, total_len);
+}
+
+int nc_chroma_mean(nc_ctx* ctx, const float* sig, const int64_t* chunk_off, const int64_t* chunk_len, int n_chunks,
+                   int64_t total_len, int64_t max_chunk_len, float* out_chroma, float* out_tuning,
+                   int* out_tuning_idx, void* ws, size_t ws_bytes, void* stream) {
+  CHECK_CTX(ctx);
+  SET_DEVICE(ctx);
+  return nc::launch_chroma_mean(ctx->c, sig, chunk_off, chunk_len, n_chunks, total_len, max_chunk_len, out_chroma,
+                                out_tuning, out_tuning_idx, ws, ws_bytes, (hipStream_t)stream);
+}
+
+int nc_chroma_lag(nc_ctx* ctx, const float* chroma, const int* src_idx, const int* nc_idx, int n_pairs, int* lag_out,
+                  void* stream) {
+  CHECK_CTX(ctx);
+  SET_DEVICE(ctx);
+  return nc::launch_chroma_lag(chroma, src_idx, nc_idx, n_pairs, lag_out, (hipStream_t)stream);
+}
+
+int nc_window_energy(nc_ctx* ctx, const float* sig, const int64_t* win_off, int n_win, int win_len,
+                     double* energy_out, void* stream) {
+  CHECK_CTX(ctx);
+  SET_DEVICE(ctx);
+  return nc::launch_window_energy(sig, win_off, n_win, win_len, energy_out, (hipStream_t)stream);
+}
+
+int nc_energy_gate(nc_ctx* ctx, const double* energy_db, const int* w0, const int* w1, int n_groups,
+                   double threshold_db, uint8_t* active_out, void* stream) {
+  CHECK_CTX(ctx);
+  SET_DEVICE(ctx);
+  return nc::launch_energy_gate(energy_db, w0, w1, n_groups, threshold_db, active_out, (hipStream_t)stream);
+}
+
+int nc_collect_valid(nc_ctx* ctx, const double* bpm, const int* nbeats, const uint8_t* active, const int* w0,
+                     const int* w1, int n_groups, int min_beats, double* out_values, int* out_n, void* stream) {
+  CHECK_CTX(ctx);
+  SET_DEVICE(ctx);
+  return nc::launch_collect_valid(bpm, nbeats, active, w0, w1, n_groups, min_beats, out_values, out_n,
+                                  (hipStream_t)stream);
+}
+
+int nc_pitch_hz(nc_ctx* ctx, const int* lags, int n, double* shift_out, double* nc_hz, double* src_hz,
+                void* stream) {
+  CHECK_CTX(ctx);
+  SET_DEVICE(ctx);
+  return nc::launch_pitch_hz(lags, n, shift_out, nc_hz, src_hz, (hipStream_t)stream);
+}
+
+size_t nc_bootstrap_job_bytes(int cap, int n_boot) { return nc::bootstrap_job_bytes(cap, n_boot); }
+
+int nc_bootstrap_ratio(nc_ctx* ctx, const double* values, const int64_t* a_off, const int* a_n, const int64_t* b_off,
+                       const int* b_n, int n_jobs, int n_boot, const uint64_t* seed, double idx_lo, double gamma_lo,
+                       double idx_hi, double gamma_hi, int min_n, double* point_out, double* lo_out, double* hi_out,
+                       double* boot_out, const int64_t* job_ws_off, const int* job_cap, void* ws, size_t ws_bytes,
+                       void* stream) {
+  CHECK_CTX(ctx);
+  SET_DEVICE(ctx);
+  (void)ws_bytes;
+  nc::BootArgs a;
+  a.values = values;
+  a.a_off = a_off;
+  a.a_n = a_n;
+  a.b_off = b_off;
+  a.b_n = b_n;
+  a.n_boot = n_boot;
+  a.seed = seed;
+  a.idx_lo = idx_lo;
+  a.g_lo = gamma_lo;
+  a.idx_hi = idx_hi;
+  a.g_hi = gamma_hi;
+  a.point_out = point_out;
+  a.lo_out = lo_out;
+  a.hi_out = hi_out;
+  a.boot_out = boot_out;
+  a.ws_off = job_ws_off;
+  a.cap = job_cap;
+  a.ws = static_cast<char*>(ws);
+  a.min_n = min_n;
+  return nc::launch_bootstrap(a, n_jobs, (hipStream_t)stream);
+}
+
+size_t nc_ibi_onset_workspace_bytes(const nc_ctx* ctx, int n_files, int64_t total_frames) {
+  (void)ctx;
+  return nc::ibi_onset_ws_bytes(n_files, total_frames);
+}
+
+int nc_ibi_onset(nc_ctx* ctx, const float* sig, const int64_t* file_off, const int64_t* file_len, int n_files,
+                 int64_t total_frames, int hop, float* onset_out, int64_t* frame_base_out, void* ws, size_t ws_bytes,
+                 void* stream) {
+  CHECK_CTX(ctx);
+  SET_DEVICE(ctx);
+  return nc::launch_ibi_onset(ctx->c, sig, file_off, file_len, n_files, total_frames, hop, onset_out,
+                              frame_base_out, ws, ws_bytes, (hipStream_t)stream);
+}
+
+size_t nc_ibi_tempogram_workspace_bytes(const nc_ctx* ctx, int n_files, int hop) {
+  if (!ctx) return 0;
+  const int acw = hop == 64 ? ctx->c.t.ac64 : ctx->c.t.ac512;
+  return nc::ibi_tg_ws_bytes(ctx->c, n_files, acw);
+}
+
+int nc_ibi_tempogram(nc_ctx* ctx, const float* onset, const int64_t* frame_base, int n_files, int hop,
+                     double* tg_out, void* ws, size_t ws_bytes, void* stream) {
+  CHECK_CTX(ctx);
+  SET_DEVICE(ctx);
+  return nc::launch_ibi_tempogram(ctx->c, onset, frame_base, n_files, hop, tg_out, ws, ws_bytes,
+                                  (hipStream_t)stream);
+}
+
+int nc_xcorr_search(nc_ctx* ctx, const float* sig, const int64_t* item_a, const int64_t* item_b, int n_items,
+                    int win, double* dot, double* sqb, const int* w0, const int* w1, const int* win_self,
+                    const int* cand0, const int* cand1, const int64_t* pa, const int64_t* pb, const int64_t* exp_pb,
+                    int n_jobs, double* ratio_out, double* quality_out, void* stream) {
+  CHECK_CTX(ctx);
+  SET_DEVICE(ctx);
+  return nc::launch_xcorr(sig, item_a, item_b, n_items, win, dot, sqb, w0, w1, win_self, cand0, cand1, pa, pb,
+                          exp_pb, n_jobs, ratio_out, quality_out, (hipStream_t)stream);
 }
 
 }  // extern "C"

@@ -7,9 +7,9 @@
 //   the first stage), inputs of stage 1 taken straight from registers.
 //
 // Every FFT here is forward (e^{-2 pi i nk/N}); inverses use the conjugation
-// identity.  Twiddles come from a 4096-entry table built on the host in double
-// precision (exp(-2 pi i m / 4096) rounded to f32), so one table serves all
-// N <= 4096.
+// identity.  Twiddles come from an 8192-entry table built on the host in double
+// precision (exp(-2 pi i m / 8192) rounded to f32), so one table serves all
+// complex N <= 4096 (real 8192).
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -130,45 +130,48 @@ struct LdsSize {
   static constexpr int value = N + N / 16;  // float2 elements
 };
 
-// Stage with radix R, NS = product of the previous radices.  Reads either LDS
-// (FROM_REGS = false) or a caller-provided register image of the stage-1 input
-// layout x[j + r*N/R], j = lane + 64 b.
-template <int N, int R, int NS>
-__device__ __forceinline__ void stockham_stage_regs(float2 (&v)[N / (R * 64)][R], float2* lds,
-                                                    const float2* __restrict__ tw, int lane) {
-  constexpr int NB = N / (R * 64);
-  static_assert(NB >= 1, "radix too large for one wave");
+// Stage with radix R, NS = product of the previous radices, NT threads (lanes of
+// one wave when NT == 64, a whole workgroup otherwise; SYNC adds the barriers a
+// multi-wave in-place stage needs).  Stage-1 input comes from registers in the
+// layout x[j + r*N/R], j = tid + NT*b.
+template <int N, int R, int NS, int NT, bool SYNC>
+__device__ __forceinline__ void stockham_stage_regs(float2 (&v)[N / (R * NT)][R], float2* lds,
+                                                    const float2* __restrict__ tw, int tid) {
+  constexpr int NB = N / (R * NT);
+  static_assert(NB >= 1, "radix too large for the thread count");
 #pragma unroll
   for (int b = 0; b < NB; ++b) {
-    const int j = lane + 64 * b;
+    const int j = tid + NT * b;
     const int k = j % NS;
     if (NS > 1) {
 #pragma unroll
-      for (int r = 1; r < R; ++r) v[b][r] = cmul(v[b][r], tw[(k * r * (4096 / (NS * R))) & 4095]);
+      for (int r = 1; r < R; ++r) v[b][r] = cmul(v[b][r], tw[(k * r * (8192 / (NS * R))) & 8191]);
     }
     DFT<R>::run(v[b]);
   }
+  if (SYNC) __syncthreads();  // every thread has loaded this stage's inputs
 #pragma unroll
   for (int b = 0; b < NB; ++b) {
-    const int j = lane + 64 * b;
+    const int j = tid + NT * b;
     const int k = j % NS;
     const int base = (j / NS) * NS * R + k;
 #pragma unroll
     for (int r = 0; r < R; ++r) lds[lpad(base + r * NS)] = v[b][r];
   }
+  if (SYNC) __syncthreads();
 }
 
-template <int N, int R, int NS>
-__device__ __forceinline__ void stockham_stage(float2* lds, const float2* __restrict__ tw, int lane) {
-  constexpr int NB = N / (R * 64);
+template <int N, int R, int NS, int NT, bool SYNC>
+__device__ __forceinline__ void stockham_stage(float2* lds, const float2* __restrict__ tw, int tid) {
+  constexpr int NB = N / (R * NT);
   float2 v[NB][R];
 #pragma unroll
   for (int b = 0; b < NB; ++b) {
-    const int j = lane + 64 * b;
+    const int j = tid + NT * b;
 #pragma unroll
     for (int r = 0; r < R; ++r) v[b][r] = lds[lpad(j + r * (N / R))];
   }
-  stockham_stage_regs<N, R, NS>(v, lds, tw, lane);
+  stockham_stage_regs<N, R, NS, NT, SYNC>(v, lds, tw, tid);
 }
 
 // Radix plans: 512 = 8.8.8, 1024 = 16.16.4, 2048 = 16.16.8, 4096 = 16.16.16
@@ -191,20 +194,31 @@ struct Plan<4096> {
   static constexpr int R0 = 16, R1 = 16, R2 = 16;
 };
 
-// Stage-1 input register image: in[b][r] = x[(lane + 64 b) + r * N / R0].
-template <int N>
-using FftIn = float2[N / (Plan<N>::R0 * 64)][Plan<N>::R0];
+// Stage-1 input register image: in[b][r] = x[(tid + NT b) + r * N / R0].
+template <int N, int NT = 64>
+using FftIn = float2[N / (Plan<N>::R0 * NT)][Plan<N>::R0];
 
-// Full forward FFT; result in natural order in lds (padded indexing).
-// One wave; no block barrier needed (LDS ops of a wave complete in order and
-// every stage loads all of its inputs before its first store).
-template <int N>
-__device__ __forceinline__ void wave_fft(FftIn<N>& in, float2* lds, const float2* __restrict__ tw, int lane) {
+template <int N, int NT, bool SYNC>
+__device__ __forceinline__ void fft_impl(FftIn<N, NT>& in, float2* lds, const float2* __restrict__ tw, int tid) {
   constexpr int R0 = Plan<N>::R0, R1 = Plan<N>::R1, R2 = Plan<N>::R2;
   static_assert(R0 * R1 * R2 == N, "plan");
-  stockham_stage_regs<N, R0, 1>(in, lds, tw, lane);
-  stockham_stage<N, R1, R0>(lds, tw, lane);
-  stockham_stage<N, R2, R0 * R1>(lds, tw, lane);
+  stockham_stage_regs<N, R0, 1, NT, SYNC>(in, lds, tw, tid);
+  stockham_stage<N, R1, R0, NT, SYNC>(lds, tw, tid);
+  stockham_stage<N, R2, R0 * R1, NT, SYNC>(lds, tw, tid);
+}
+
+// One wave; no barrier needed (LDS ops of a wave complete in order and every
+// stage loads all of its inputs before its first store).  Natural-order output
+// in lds (padded indexing).
+template <int N>
+__device__ __forceinline__ void wave_fft(FftIn<N, 64>& in, float2* lds, const float2* __restrict__ tw, int lane) {
+  fft_impl<N, 64, false>(in, lds, tw, lane);
+}
+
+// Whole workgroup of NT threads (all must call); output valid after return.
+template <int N, int NT>
+__device__ __forceinline__ void block_fft(FftIn<N, NT>& in, float2* lds, const float2* __restrict__ tw, int tid) {
+  fft_impl<N, NT, true>(in, lds, tw, tid);
 }
 
 // Real-FFT split: Z = FFT_N(z), z[n] = x[2n] + i x[2n+1] (x real, length 2N).
@@ -215,7 +229,7 @@ __device__ __forceinline__ void rfft_split(const float2* lds, const float2* __re
   const float2 b = cconj(lds[lpad((N - k) & (N - 1))]);
   const float2 E = cscale(cadd(a, b), 0.5f);
   const float2 O = cmul_mi(cscale(csub(a, b), 0.5f));  // (a-b)/(2i)
-  const float2 W = tw[(k * (4096 / (2 * N))) & 4095];  // exp(-2 pi i k / 2N)
+  const float2 W = tw[(k * (8192 / (2 * N))) & 8191];  // exp(-2 pi i k / 2N)
   const float2 WO = cmul(W, O);
   Xk = cadd(E, WO);
   XNk = cconj(csub(E, WO));

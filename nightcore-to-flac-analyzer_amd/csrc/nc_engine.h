@@ -21,7 +21,7 @@ constexpr int kHalfbandK = 23;  // decimator half length (47 taps)
 // Device-resident constant tables, built once per context (double precision on
 // the host, rounded to f32).
 struct Tables {
-  float2* tw4096 = nullptr;     // exp(-2 pi i m / 4096)
+  float2* tw = nullptr;         // exp(-2 pi i m / 8192)
   float* hann2048 = nullptr;    // periodic Hann, STFT window
   float* hann_ac512 = nullptr;  // periodic Hann(344): tempogram window at hop 512
   float* hann_ac64 = nullptr;   // periodic Hann(2756): tempogram window at hop 64
@@ -46,6 +46,26 @@ struct Context {
   int num_cu = 256;
   hipStream_t stream = nullptr;
   Tables t;
+};
+
+// bootstrap.hip job description (see nc_bootstrap_ratio in include/ncgpu.h)
+struct BootArgs {
+  const double* values;
+  const int64_t* a_off;
+  const int* a_n;
+  const int64_t* b_off;  // nullable
+  const int* b_n;        // nullable
+  int n_boot;
+  const uint64_t* seed;  // [job][4] = state_hi, state_lo, inc_hi, inc_lo
+  double idx_lo, g_lo, idx_hi, g_hi;
+  double* point_out;
+  double* lo_out;
+  double* hi_out;
+  double* boot_out;      // nullable [job][n_boot]
+  const int64_t* ws_off; // [job] byte offsets into ws
+  const int* cap;        // [job] capacity (>= a_n + b_n)
+  char* ws;
+  int min_n;             // jobs with a_n < min_n (or b_n < min_n when B is present) are skipped
 };
 
 void build_tables(Context& ctx);

@@ -1,7 +1,7 @@
 // nc_tables.cpp — constant tables built once per context on the host (double
 // precision, rounded to f32) and uploaded to HBM.
 //
-//   tw4096          exp(-2 pi i m / 4096)                     (all FFTs)
+//   tw              exp(-2 pi i m / 8192)                     (all FFTs)
 //   hann2048        scipy.signal.get_window('hann', 2048)     (librosa.stft window)
 //   hann_ac512/64   get_window('hann', win) for the tempogram (feature.tempogram)
 //   mel CSR         librosa.filters.mel(sr=22050, n_fft=2048, n_mels=128, fmax=11025,
@@ -87,12 +87,12 @@ void fft_inplace(std::vector<std::complex<double>>& a) {
 void build_tables(Context& ctx) {
   Tables& t = ctx.t;
   // twiddles
-  std::vector<float2> tw(4096);
-  for (int m = 0; m < 4096; ++m) {
-    const double a = 2.0 * M_PI * (double)m / 4096.0;
+  std::vector<float2> tw(8192);
+  for (int m = 0; m < 8192; ++m) {
+    const double a = 2.0 * M_PI * (double)m / 8192.0;
     tw[m] = make_float2((float)std::cos(a), (float)-std::sin(a));
   }
-  t.tw4096 = upload(tw);
+  t.tw = upload(tw);
   t.hann2048 = upload(to_f32(hann_periodic(kNFFT)));
   t.ac512 = (int)((int)(8.0 * kSR) / 512);
   t.ac64 = (int)((int)(8.0 * kSR) / 64);
@@ -271,7 +271,7 @@ void build_tables(Context& ctx) {
 
 void free_tables(Context& ctx) {
   Tables& t = ctx.t;
-  void* ptrs[] = {t.tw4096, t.hann2048, t.hann_ac512, t.hann_ac64, t.mel_lo,  t.mel_len, t.mel_off,
+  void* ptrs[] = {t.tw, t.hann2048, t.hann_ac512, t.hann_ac64, t.mel_lo,  t.mel_len, t.mel_off,
                   t.mel_w,  t.cqt_lo,   t.cqt_len,    t.cqt_off,  t.cqt_w,   t.cqt_inv_sqrt_len, t.halfband};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);

@@ -215,7 +215,7 @@ __global__ __launch_bounds__(WS_THREADS) void window_stage_kernel(WinArgs a) {
         const int n = lane + 64 * r;
         const float Pa = pw[n], Pb = pw[512 - n];
         const float E = 0.5f * (Pa + Pb), Od = 0.5f * (Pa - Pb);
-        const float2 wv = a.tw[(4 * n) & 4095];  // (cos, -sin)
+        const float2 wv = a.tw[(8 * n) & 8191];  // exp(-2 pi i n/1024) = (cos, -sin)
         const float cs = wv.x, sn = -wv.y;
         in[0][r] = make_float2(E - Od * sn, -(Od * cs));
       }
@@ -306,7 +306,7 @@ int launch_window_stage(Context& ctx, const float* sig, const int64_t* win_off, 
   a.onset_out = onset_out;
   a.tg_out = tg_out;
   a.energy_out = energy_out;
-  a.tw = ctx.t.tw4096;
+  a.tw = ctx.t.tw;
   a.hann2048 = ctx.t.hann2048;
   a.wac = ctx.t.hann_ac512;
   a.mel_lo = ctx.t.mel_lo;

@@ -20,6 +20,7 @@ P = C.c_void_p
 I32 = C.c_int
 I64 = C.c_int64
 F32 = C.c_float
+D = C.c_double
 SZ = C.c_size_t
 
 # name -> (restype, argtypes); mirrors include/ncgpu.h
@@ -39,15 +40,20 @@ SIGNATURES = {
     "nc_tempo_prior": (I32, [P, P, P, P, P, P, P, P, I32, P, P]),
     "nc_ibi_from_beats": (I32, [P, P, P, P, I32, I32, I32, P, P, P]),
     "nc_chroma_workspace_bytes": (SZ, [P, I32, I64]),
-    "nc_chroma_mean": (I32, [P, P, P, P, I32, I64, P, P, P, SZ, P]),
-    "nc_chroma_lag": (I32, [P, P, P, I32, P, P]),
-    "nc_bootstrap_workspace_bytes": (SZ, [I32, I32]),
-    "nc_bootstrap_ratio": (I32, [P, P, P, P, P, P, P, I32, I32, P, P, P, I32, I32, P, P, P, SZ, P]),
+    "nc_chroma_mean": (I32, [P, P, P, P, I32, I64, I64, P, P, P, P, SZ, P]),
+    "nc_chroma_lag": (I32, [P, P, P, P, I32, P, P]),
+    "nc_window_energy": (I32, [P, P, P, I32, I32, P, P]),
+    "nc_energy_gate": (I32, [P, P, P, P, I32, D, P, P]),
+    "nc_collect_valid": (I32, [P, P, P, P, P, P, I32, I32, P, P, P]),
+    "nc_pitch_hz": (I32, [P, P, I32, P, P, P, P]),
+    "nc_bootstrap_job_bytes": (SZ, [I32, I32]),
+    "nc_bootstrap_ratio": (I32, [P, P, P, P, P, P, I32, I32, P, D, D, D, D, I32, P, P, P, P, P, P, P,
+                                 SZ, P]),
     "nc_ibi_onset_workspace_bytes": (SZ, [P, I32, I64]),
-    "nc_ibi_onset": (I32, [P, P, P, P, I32, I64, P, P, P, SZ, P]),
-    "nc_ibi_tempogram_workspace_bytes": (SZ, [P, I32, I64]),
-    "nc_ibi_tempogram": (I32, [P, P, P, P, I32, I64, P, P, SZ, P]),
-    "nc_xcorr_search": (I32, [P, P, P, P, P, P, I32, I32, I32, P, P, P]),
+    "nc_ibi_onset": (I32, [P, P, P, P, I32, I64, I32, P, P, P, SZ, P]),
+    "nc_ibi_tempogram_workspace_bytes": (SZ, [P, I32, I32]),
+    "nc_ibi_tempogram": (I32, [P, P, P, I32, I32, P, P, SZ, P]),
+    "nc_xcorr_search": (I32, [P, P, P, P, I32, I32, P, P, P, P, P, P, P, P, P, P, I32, P, P, P]),
 }
 
 

@@ -1,0 +1,672 @@
+"""The MI355X engine: batched, stream-ordered execution of ``pipeline.run`` for
+many (nightcore, source) pairs at once on one GPU.
+
+Flow for a batch of B pairs (2B files), everything between the two host
+synchronisations running on one HIP stream:
+
+  H2D signals (one buffer) -> nc_trim_bounds ............................ sync 1
+  host plan: src trim, windows (io.slice_windows), 20 s chunks (pitch.py:121-138)
+  H2D plan (one buffer)
+  nc_window_stage (all windows: energy, onset, tempogram mean)
+  nc_energy_gate -> nc_tempo_beats(src, prior 120) -> nc_tempo_prior
+  -> nc_tempo_beats(nc, per-pair prior) -> nc_collect_valid
+  nc_chroma_mean -> nc_chroma_lag -> nc_pitch_hz            (compute_pitch)
+  nc_bootstrap_ratio (tempo + pitch, seed 42; chunk shifts, seed 0)
+  nc_ibi_onset -> nc_ibi_tempogram -> nc_tempo_beats(hop 64) -> nc_ibi_from_beats
+  -> nc_bootstrap_ratio (IBI)                                (compute_ibi)
+  D2H results ............................................................ sync 2
+  host: AnalysisResult assembly (classification, Rubber Band, warnings, logs)
+
+The host never touches audio samples after the upload; there is no CPU path.
+"""
+from __future__ import annotations
+
+import math
+import threading
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import numpy as np
+import torch
+
+from . import _native
+from . import consensus as C
+
+SR = 22050
+HOP_LENGTH = 512
+IBI_HOP = 64
+MIN_BEATS = 4
+CHUNK_SEC = 20.0
+MIN_CHUNKS = 3
+REF_HZ = 440.0
+_ALIGN = 64
+
+
+# ------------------------------------------------------------------------------ helpers
+def seed_state(seed: int) -> List[int]:
+    """PCG64 state of np.random.default_rng(seed) as 4 uint64 (state hi/lo, inc hi/lo)."""
+    st = np.random.PCG64(seed).state["state"]
+    s, inc = int(st["state"]), int(st["inc"])
+    m = (1 << 64) - 1
+    return [(s >> 64) & m, s & m, (inc >> 64) & m, inc & m]
+
+
+def percentile_params(n_boot: int, ci: float) -> Tuple[float, float, float, float]:
+    """(virtual index, gamma) of np.percentile(.., alpha*100) and (1-alpha)*100, 'linear'."""
+    alpha = (1.0 - ci) / 2.0
+    out = []
+    for q in (alpha * 100, (1.0 - alpha) * 100):
+        quant = np.true_divide(np.float64(q), 100)
+        virt = np.float64(n_boot - 1) * quant
+        prev = np.floor(virt)
+        out += [float(prev), float(virt - prev)]
+    return tuple(out)
+
+
+class _Upload:
+    """Packs many small host arrays into one H2D copy; returns device views."""
+
+    def __init__(self):
+        self.parts: List[Tuple[str, np.ndarray]] = []
+
+    def add(self, name: str, arr, dtype):
+        a = np.ascontiguousarray(np.asarray(arr, dtype=dtype).reshape(-1))
+        self.parts.append((name, a))
+
+    def commit(self, dev: torch.device) -> Dict[str, torch.Tensor]:
+        offs, total = [], 0
+        for _, a in self.parts:
+            total = (total + 15) & ~15
+            offs.append(total)
+            total += a.nbytes
+        host = np.zeros(max(16, total), dtype=np.uint8)
+        for (_, a), o in zip(self.parts, offs):
+            host[o:o + a.nbytes] = a.view(np.uint8)
+        d = torch.from_numpy(host).to(dev)
+        out = {}
+        for (name, a), o in zip(self.parts, offs):
+            t = d[o:o + max(a.nbytes, a.itemsize)].view(_TORCH_DTYPE[a.dtype.str])
+            out[name] = t[:max(1, a.size)]
+        return out
+
+
+_TORCH_DTYPE = {np.dtype(np.float64).str: torch.float64, np.dtype(np.float32).str: torch.float32,
+                np.dtype(np.int64).str: torch.int64, np.dtype(np.int32).str: torch.int32,
+                np.dtype(np.uint8).str: torch.uint8, np.dtype(np.uint64).str: torch.uint64}
+
+
+@dataclass
+class DeviceSignals:
+    """Signals resident in HBM: one f32 buffer, per-file offset/length (samples)."""
+    buf: torch.Tensor
+    off: np.ndarray
+    length: np.ndarray
+
+    @property
+    def n_files(self) -> int:
+        return len(self.off)
+
+
+@dataclass
+class PairOutcome:
+    result: Optional[C.AnalysisResult] = None
+    error: Optional[BaseException] = None
+    logs: List[str] = field(default_factory=list)
+    detail: dict = field(default_factory=dict)
+
+
+@dataclass
+class Params:
+    window_sec: float = 10.0
+    hop_sec: float = 5.0
+    energy_gate_db: float = -40.0
+    silence_strip_db: Optional[float] = 60.0
+    src_trim_sec: float = 0.0
+    auto_align: bool = False
+    compute_pitch: bool = True
+    compute_ibi: bool = True
+
+
+# ------------------------------------------------------------------------------ engine
+class Engine:
+    def __init__(self, device: int = 0):
+        if not torch.cuda.is_available():
+            raise _native.NativeUnavailable("no HIP device visible to torch (ROCm); the engine has no CPU path")
+        self.device_index = device
+        self.dev = torch.device("cuda", device)
+        self.ctx = _native.Context(device)
+        self._ws: Dict[str, torch.Tensor] = {}
+        self.num_cu = self.ctx.lib.nc_num_cu(self.ctx.h)
+
+    # -------------------------------------------------------------- plumbing
+    def stream(self) -> int:
+        return torch.cuda.current_stream(self.dev).cuda_stream
+
+    def workspace(self, name: str, nbytes: int) -> torch.Tensor:
+        t = self._ws.get(name)
+        if t is None or t.numel() < nbytes:
+            t = torch.empty(int(max(256, nbytes * 1.1)), dtype=torch.uint8, device=self.dev)
+            self._ws[name] = t
+        return t
+
+    def call(self, name: str, *args):
+        self.ctx.call(name, *args)
+
+    def upload_signals(self, arrays: Sequence[np.ndarray]) -> DeviceSignals:
+        lens = np.array([len(a) for a in arrays], dtype=np.int64)
+        offs = np.zeros(len(arrays), dtype=np.int64)
+        tot = 0
+        for i, n in enumerate(lens):
+            offs[i] = tot
+            tot += (int(n) + _ALIGN - 1) // _ALIGN * _ALIGN
+        host = torch.zeros(max(_ALIGN, tot), dtype=torch.float32, pin_memory=True)
+        hv = host.numpy()
+        for a, o in zip(arrays, offs):
+            hv[o:o + len(a)] = np.asarray(a, dtype=np.float32)
+        buf = host.to(self.dev, non_blocking=True)
+        return DeviceSignals(buf, offs, lens)
+
+    # -------------------------------------------------------------- bootstrap (generic)
+    def bootstrap(self, jobs: Sequence[Tuple[np.ndarray, Optional[np.ndarray]]], seed: int,
+                  n_boot: int = C.N_BOOTSTRAP, ci: float = C.CI_LEVEL):
+        """[(A, B|None)] -> [(point, (lo, hi))] with numpy default_rng(seed) semantics."""
+        dev = self.dev
+        vals, a_off, a_n, b_off, b_n, caps = [], [], [], [], [], []
+        pos = 0
+        has_b = jobs[0][1] is not None
+        for A, B in jobs:
+            A = np.asarray(A, np.float64)
+            a_off.append(pos)
+            a_n.append(len(A))
+            vals.append(A)
+            pos += len(A)
+            if has_b:
+                B = np.asarray(B, np.float64)
+                b_off.append(pos)
+                b_n.append(len(B))
+                vals.append(B)
+                pos += len(B)
+            caps.append(len(A) + (len(B) if has_b else 0))
+        wsoff, tot = [], 0
+        for c in caps:
+            wsoff.append(tot)
+            tot += self.ctx.lib.nc_bootstrap_job_bytes(int(c), int(n_boot))
+        up = _Upload()
+        up.add("vals", np.concatenate(vals) if vals else np.zeros(1), np.float64)
+        up.add("a_off", a_off, np.int64)
+        up.add("a_n", a_n, np.int32)
+        up.add("b_off", b_off or [0], np.int64)
+        up.add("b_n", b_n or [0], np.int32)
+        up.add("seed", seed_state(seed) * len(jobs), np.uint64)
+        up.add("wsoff", wsoff, np.int64)
+        up.add("cap", caps, np.int32)
+        d = up.commit(dev)
+        n = len(jobs)
+        out = torch.empty(3 * n, dtype=torch.float64, device=dev)
+        ws = self.workspace("boot", tot)
+        il, gl, ih, gh = percentile_params(n_boot, ci)
+        self.call("nc_bootstrap_ratio", d["vals"].data_ptr(), d["a_off"].data_ptr(), d["a_n"].data_ptr(),
+                  d["b_off"].data_ptr() if has_b else None, d["b_n"].data_ptr() if has_b else None, n,
+                  n_boot, d["seed"].data_ptr(), il, gl, ih, gh, 1, out[0:n].data_ptr(),
+                  out[n:2 * n].data_ptr(), out[2 * n:3 * n].data_ptr(), None, d["wsoff"].data_ptr(),
+                  d["cap"].data_ptr(), ws.data_ptr(), ws.numel(), self.stream())
+        o = out.cpu().numpy()
+        return [(float(o[i]), (float(o[n + i]), float(o[2 * n + i]))) for i in range(n)]
+
+    # -------------------------------------------------------------- batched pipeline
+    def analyze(self, pairs: Optional[Sequence[Tuple[np.ndarray, np.ndarray]]] = None, params: Params = None,
+                signals: Optional[DeviceSignals] = None) -> List[PairOutcome]:
+        """Run pipeline.run's analysis for every (nc, src) pair.  ``signals``
+        (files ordered nc_0, src_0, nc_1, src_1, ...) may be passed already
+        resident in HBM; otherwise ``pairs`` are uploaded."""
+        p = params or Params()
+        if p.auto_align and p.src_trim_sec == 0.0:
+            raise NotImplementedError("auto_align (xcorr.find_content_offset) is not on the MI355X path yet")
+        if signals is None:
+            flat = []
+            for nc, src in pairs:
+                flat += [nc, src]
+            signals = self.upload_signals(flat)
+        dev, st = self.dev, self.stream()
+        nF = signals.n_files
+        B = nF // 2
+        outs = [PairOutcome() for _ in range(B)]
+
+        # ---------------------------------------------------------------- 1. trim (sync 1)
+        up = _Upload()
+        up.add("off", signals.off, np.int64)
+        up.add("len", signals.length, np.int64)
+        d0 = up.commit(dev)
+        if p.silence_strip_db is not None:
+            tot_frames = int(np.sum(1 + signals.length // 512))
+            wsb = self.ctx.lib.nc_trim_workspace_bytes(
+                signals.length.ctypes.data_as(_native.P), nF)
+            ws = self.workspace("trim", wsb)
+            se = torch.empty(2 * nF, dtype=torch.int64, device=dev)
+            self.call("nc_trim_bounds", signals.buf.data_ptr(), d0["off"].data_ptr(), d0["len"].data_ptr(), nF,
+                      tot_frames, float(p.silence_strip_db), se[:nF].data_ptr(), se[nF:].data_ptr(),
+                      ws.data_ptr(), ws.numel(), st)
+            se_h = se.cpu().numpy()
+            start, end = se_h[:nF], se_h[nF:]
+        else:
+            start, end = np.zeros(nF, np.int64), signals.length.copy()
+        f_off = signals.off + start
+        f_len = end - start
+        strip_len = f_len.copy()
+        lead = start / SR
+        trail = (signals.length - end) / SR
+        intro = [None] * B
+        if p.src_trim_sec > 0.0:
+            k = int(p.src_trim_sec * SR)
+            for b in range(B):
+                f = 2 * b + 1
+                cut = min(k, int(f_len[f]))
+                f_off[f] += cut
+                f_len[f] -= cut
+                intro[b] = p.src_trim_sec
+
+        # ---------------------------------------------------------------- 2. plan
+        win_n, hop_n = int(p.window_sec * SR), int(p.hop_sec * SR)
+        starts = []
+        for f in range(nF):
+            L = int(f_len[f])
+            s = np.arange(0, max(0, L - win_n) + 1, hop_n, dtype=np.int64) if L >= win_n and hop_n > 0 \
+                else np.zeros(0, np.int64)
+            starts.append(s)
+        # window order: all source windows (pair-major), then all nightcore windows
+        order = [2 * b + 1 for b in range(B)] + [2 * b for b in range(B)]
+        w0 = np.zeros(nF, np.int64)
+        w1 = np.zeros(nF, np.int64)
+        win_abs, pos = [], 0
+        for f in order:
+            w0[f] = pos
+            win_abs.append(f_off[f] + starts[f])
+            pos += len(starts[f])
+            w1[f] = pos
+        n_win = pos
+        n_src_w = int(sum(len(starts[2 * b + 1]) for b in range(B)))
+        win_abs = np.concatenate(win_abs) if win_abs else np.zeros(0, np.int64)
+        T = 1 + win_n // HOP_LENGTH
+        acw = int(int(8.0 * SR) // HOP_LENGTH)
+
+        chunk_off, chunk_len, pair_chunks = [], [], []
+        if p.compute_pitch:
+            cn = int(CHUNK_SEC * SR)
+            for b in range(B):
+                ns, nn = int(f_len[2 * b + 1]), int(f_len[2 * b])
+                n = min(ns // cn, nn // cn)
+                first = len(chunk_off) // 2
+                if n < 1:
+                    chunk_off += [f_off[2 * b + 1], f_off[2 * b]]
+                    chunk_len += [ns, nn]
+                    n = 1
+                else:
+                    for i in range(n):
+                        chunk_off += [f_off[2 * b + 1] + i * cn, f_off[2 * b] + i * cn]
+                        chunk_len += [cn, cn]
+                pair_chunks.append((first, first + n))
+        n_chunks = len(chunk_off)
+        n_cp = n_chunks // 2
+
+        up = _Upload()
+        up.add("win_off", win_abs if n_win else [0], np.int64)
+        up.add("w0", w0, np.int32)
+        up.add("w1", w1, np.int32)
+        up.add("on_off", np.arange(n_win, dtype=np.int64) * T if n_win else [0], np.int64)
+        up.add("on_len", np.full(max(1, n_win), T), np.int32)
+        up.add("src_w0", [w0[2 * b + 1] for b in range(B)], np.int32)
+        up.add("src_w1", [w1[2 * b + 1] for b in range(B)], np.int32)
+        up.add("src_len", [f_len[2 * b + 1] for b in range(B)], np.int64)
+        up.add("nc_len", [f_len[2 * b] for b in range(B)], np.int64)
+        nc_pair = np.concatenate([np.full(len(starts[2 * b]), b, np.int32) for b in range(B)]) \
+            if n_win - n_src_w else np.zeros(1, np.int32)
+        up.add("nc_pair", nc_pair, np.int32)
+        up.add("start120", [120.0], np.float64)
+        up.add("chunk_off", chunk_off or [0], np.int64)
+        up.add("chunk_len", chunk_len or [0], np.int64)
+        up.add("lag_src", np.arange(0, n_chunks, 2), np.int32)
+        up.add("lag_nc", np.arange(1, n_chunks, 2), np.int32)
+        up.add("f_off", f_off, np.int64)
+        up.add("f_len", f_len, np.int64)
+        d = up.commit(dev)
+
+        # ---------------------------------------------------------------- 3. per-window stage
+        f64 = dict(dtype=torch.float64, device=dev)
+        i32 = dict(dtype=torch.int32, device=dev)
+        onset = torch.empty(max(1, n_win * T), dtype=torch.float32, device=dev)
+        tg = torch.empty(max(1, n_win * acw), **f64)
+        energy = torch.empty(max(1, n_win), **f64)
+        active = torch.empty(max(1, n_win), dtype=torch.uint8, device=dev)
+        bpm = torch.zeros(max(1, n_win), **f64)
+        lag = torch.zeros(max(1, n_win), **i32)
+        nbeats = torch.zeros(max(1, n_win), **i32)
+        margin = torch.zeros(max(1, n_win), **f64)
+        prior = torch.empty(max(1, B), **f64)
+        tvals = torch.zeros(max(1, n_win), **f64)
+        tcount = torch.zeros(nF, **i32)
+        if n_win:
+            wsb = self.ctx.lib.nc_window_stage_workspace_bytes(self.ctx.h, n_win, win_n, HOP_LENGTH)
+            ws = self.workspace("win", wsb)
+            self.call("nc_window_stage", signals.buf.data_ptr(), d["win_off"].data_ptr(), None, n_win, win_n,
+                      HOP_LENGTH, onset.data_ptr(), tg.data_ptr(), energy.data_ptr(), ws.data_ptr(), ws.numel(), st)
+            self.call("nc_energy_gate", energy.data_ptr(), d["w0"].data_ptr(), d["w1"].data_ptr(), nF,
+                      float(p.energy_gate_db), active.data_ptr(), st)
+            if n_src_w:
+                self.call("nc_tempo_beats", onset.data_ptr(), d["on_off"].data_ptr(), d["on_len"].data_ptr(),
+                          n_src_w, T, tg.data_ptr(), acw, d["start120"].data_ptr(),
+                          torch.zeros(n_src_w, **i32).data_ptr(), active.data_ptr(), HOP_LENGTH, 1,
+                          bpm.data_ptr(), lag.data_ptr(), nbeats.data_ptr(), margin.data_ptr(), None, 0, None, 0,
+                          st)
+            self.call("nc_tempo_prior", bpm.data_ptr(), nbeats.data_ptr(), active.data_ptr(),
+                      d["src_w0"].data_ptr(), d["src_w1"].data_ptr(), d["src_len"].data_ptr(),
+                      d["nc_len"].data_ptr(), B, prior.data_ptr(), st)
+            n_nc_w = n_win - n_src_w
+            if n_nc_w:
+                self.call("nc_tempo_beats", onset.data_ptr(),
+                          d["on_off"][n_src_w:].data_ptr(), d["on_len"][n_src_w:].data_ptr(), n_nc_w, T,
+                          tg[n_src_w * acw:].data_ptr(), acw, prior.data_ptr(), d["nc_pair"].data_ptr(),
+                          active[n_src_w:].data_ptr(), HOP_LENGTH, 1, bpm[n_src_w:].data_ptr(),
+                          lag[n_src_w:].data_ptr(), nbeats[n_src_w:].data_ptr(), margin[n_src_w:].data_ptr(),
+                          None, 0, None, 0, st)
+            self.call("nc_collect_valid", bpm.data_ptr(), nbeats.data_ptr(), active.data_ptr(),
+                      d["w0"].data_ptr(), d["w1"].data_ptr(), nF, MIN_BEATS, tvals.data_ptr(),
+                      tcount.data_ptr(), st)
+        else:
+            prior.fill_(120.0)
+
+        # ---------------------------------------------------------------- 4. chroma
+        chroma = torch.zeros(max(1, n_chunks * 12), dtype=torch.float32, device=dev)
+        tuning = torch.zeros(max(1, n_chunks), dtype=torch.float32, device=dev)
+        clag = torch.zeros(max(1, n_cp), **i32)
+        pvals = torch.zeros(max(1, 3 * n_cp), **f64)   # [shift | nc_hz | src_hz]
+        if n_chunks:
+            tot_len = int(np.sum(chunk_len))
+            wsb = self.ctx.lib.nc_chroma_workspace_bytes(self.ctx.h, n_chunks, tot_len)
+            ws = self.workspace("chroma", wsb)
+            self.call("nc_chroma_mean", signals.buf.data_ptr(), d["chunk_off"].data_ptr(), d["chunk_len"].data_ptr(),
+                      n_chunks, tot_len, int(max(chunk_len)), chroma.data_ptr(), tuning.data_ptr(), None,
+                      ws.data_ptr(), ws.numel(), st)
+            self.call("nc_chroma_lag", chroma.data_ptr(), d["lag_src"].data_ptr(), d["lag_nc"].data_ptr(), n_cp,
+                      clag.data_ptr(), st)
+            self.call("nc_pitch_hz", clag.data_ptr(), n_cp, pvals[0:n_cp].data_ptr(),
+                      pvals[n_cp:2 * n_cp].data_ptr(), pvals[2 * n_cp:3 * n_cp].data_ptr(), st)
+
+        # ---------------------------------------------------------------- 5. bootstraps (tempo + pitch, seed 42)
+        n_boot = C.N_BOOTSTRAP
+        il, gl, ih, gh = percentile_params(n_boot, C.CI_LEVEL)
+        vals = torch.cat([tvals, pvals])
+        jobs_a_off, jobs_b_off, caps = [], [], []
+        for b in range(B):      # tempo: A = nc valid, B = src valid
+            jobs_a_off.append(w0[2 * b])
+            jobs_b_off.append(w0[2 * b + 1])
+            caps.append(max(1, (w1[2 * b] - w0[2 * b]) + (w1[2 * b + 1] - w0[2 * b + 1])))
+        pbase = tvals.numel()
+        for b in range(len(pair_chunks)):   # pitch: A = nc_hz, B = src_hz
+            c0, c1 = pair_chunks[b]
+            jobs_a_off.append(pbase + n_cp + c0)
+            jobs_b_off.append(pbase + 2 * n_cp + c0)
+            caps.append(2 * (c1 - c0))
+        n_pitch_jobs = len(pair_chunks)
+        nj = B + n_pitch_jobs
+        wsoff, tot = [], 0
+        for c in caps:
+            wsoff.append(tot)
+            tot += self.ctx.lib.nc_bootstrap_job_bytes(int(c), n_boot)
+        # shift bootstrap (pitch.py:143-150, seed 0, log only)
+        s_off, s_caps, s_wsoff, s_tot = [], [], [], 0
+        for b in range(n_pitch_jobs):
+            c0, c1 = pair_chunks[b]
+            s_off.append(pbase + c0)
+            s_caps.append(c1 - c0)
+            s_wsoff.append(s_tot)
+            s_tot += self.ctx.lib.nc_bootstrap_job_bytes(int(c1 - c0), n_boot)
+        up = _Upload()
+        up.add("a_off", jobs_a_off, np.int64)
+        up.add("b_off", jobs_b_off, np.int64)
+        up.add("seed", seed_state(42) * nj, np.uint64)
+        up.add("wsoff", wsoff, np.int64)
+        up.add("cap", caps, np.int32)
+        up.add("p_n", [c1 - c0 for c0, c1 in pair_chunks] or [0], np.int32)
+        up.add("s_off", s_off or [0], np.int64)
+        up.add("s_seed", seed_state(0) * max(1, n_pitch_jobs), np.uint64)
+        up.add("s_wsoff", s_wsoff or [0], np.int64)
+        up.add("s_cap", s_caps or [1], np.int32)
+        db = up.commit(dev)
+        nc_idx = torch.tensor([2 * b for b in range(B)], dtype=torch.long, device=dev)
+        src_idx = nc_idx + 1
+        a_n = torch.cat([tcount[nc_idx], db["p_n"][:n_pitch_jobs]]).to(torch.int32)
+        b_n = torch.cat([tcount[src_idx], db["p_n"][:n_pitch_jobs]]).to(torch.int32)
+        bout = torch.full((3 * nj,), float("nan"), **f64)
+        ws = self.workspace("boot", tot)
+        self.call("nc_bootstrap_ratio", vals.data_ptr(), db["a_off"].data_ptr(), a_n.data_ptr(),
+                  db["b_off"].data_ptr(), b_n.data_ptr(), nj, n_boot, db["seed"].data_ptr(), il, gl, ih, gh,
+                  C.MIN_VALID, bout[0:nj].data_ptr(), bout[nj:2 * nj].data_ptr(), bout[2 * nj:].data_ptr(), None,
+                  db["wsoff"].data_ptr(), db["cap"].data_ptr(), ws.data_ptr(), ws.numel(), st)
+        sout = torch.full((3 * max(1, n_pitch_jobs),), float("nan"), **f64)
+        if n_pitch_jobs:
+            ws2 = self.workspace("boot_s", s_tot)
+            self.call("nc_bootstrap_ratio", vals.data_ptr(), db["s_off"].data_ptr(), db["p_n"].data_ptr(), None,
+                      None, n_pitch_jobs, n_boot, db["s_seed"].data_ptr(), il, gl, ih, gh, MIN_CHUNKS,
+                      sout[0:n_pitch_jobs].data_ptr(), sout[n_pitch_jobs:2 * n_pitch_jobs].data_ptr(),
+                      sout[2 * n_pitch_jobs:3 * n_pitch_jobs].data_ptr(), None, db["s_wsoff"].data_ptr(),
+                      db["s_cap"].data_ptr(), ws2.data_ptr(), ws2.numel(), st)
+
+        # ---------------------------------------------------------------- 6. IBI pass
+        ibi = None
+        if p.compute_ibi:
+            ibi = self._ibi_pass(signals, d["f_off"], d["f_len"], f_len, prior, B)
+
+        # ---------------------------------------------------------------- 7. D2H (sync 2) + host assembly
+        host = {k: v.cpu().numpy() for k, v in dict(
+            energy=energy, active=active, bpm=bpm, nbeats=nbeats, lag=lag, margin=margin, prior=prior,
+            tcount=tcount, clag=clag, pvals=pvals, tuning=tuning, chroma=chroma, bout=bout, sout=sout).items()}
+        if ibi is not None:
+            ibi = {k: (v.cpu().numpy() if isinstance(v, torch.Tensor) else v) for k, v in ibi.items()}
+        for b in range(B):
+            outs[b] = self._assemble_pair(b, p, host, ibi, starts, w0, w1, f_len, strip_len, lead, trail,
+                                          intro[b], win_n, pair_chunks, n_cp, nj, n_pitch_jobs)
+        return outs
+
+    # -------------------------------------------------------------- IBI pass (tempo.py:120-173)
+    def ibi_core(self, buf, d_off, d_len, f_len, start_vals, pidx, hop: int = IBI_HOP, min_ibis: int = 4):
+        """onset(hop) -> streamed tempogram mean -> beat_track -> IBIs for every
+        file (tempo.py:158-172); start bpm of file f = start_vals[pidx[f]]."""
+        dev, st = self.dev, self.stream()
+        nF = len(f_len)
+        frames = 1 + np.asarray(f_len, np.int64) // hop
+        total = int(frames.sum())
+        onset = torch.empty(max(1, total), dtype=torch.float32, device=dev)
+        fbase = torch.empty(nF + 1, dtype=torch.int64, device=dev)
+        wsb = self.ctx.lib.nc_ibi_onset_workspace_bytes(self.ctx.h, nF, total)
+        ws = self.workspace("ibi_on", wsb)
+        self.call("nc_ibi_onset", buf.data_ptr(), d_off.data_ptr(), d_len.data_ptr(), nF, total, hop,
+                  onset.data_ptr(), fbase.data_ptr(), ws.data_ptr(), ws.numel(), st)
+        acw = int(int(8.0 * SR) // hop)
+        tg = torch.empty(nF * acw, dtype=torch.float64, device=dev)
+        wsb = self.ctx.lib.nc_ibi_tempogram_workspace_bytes(self.ctx.h, nF, hop)
+        ws = self.workspace("ibi_tg", wsb)
+        self.call("nc_ibi_tempogram", onset.data_ptr(), fbase.data_ptr(), nF, hop, tg.data_ptr(), ws.data_ptr(),
+                  ws.numel(), st)
+        lens = torch.tensor(frames, dtype=torch.int32, device=dev)
+        bpm = torch.zeros(nF, dtype=torch.float64, device=dev)
+        lag = torch.zeros(nF, dtype=torch.int32, device=dev)
+        nb = torch.zeros(nF, dtype=torch.int32, device=dev)
+        mg = torch.zeros(nF, dtype=torch.float64, device=dev)
+        beats = torch.empty(max(1, total), dtype=torch.int32, device=dev)
+        wsb = self.ctx.lib.nc_tempo_beats_workspace_bytes(total)
+        ws = self.workspace("ibi_beats", wsb)
+        self.call("nc_tempo_beats", onset.data_ptr(), fbase.data_ptr(), lens.data_ptr(), nF, int(frames.max()),
+                  tg.data_ptr(), acw, start_vals.data_ptr(), pidx.data_ptr(), None, hop, 1, bpm.data_ptr(),
+                  lag.data_ptr(), nb.data_ptr(), mg.data_ptr(), beats.data_ptr(), total, ws.data_ptr(), ws.numel(),
+                  st)
+        ibis = torch.empty(max(1, total), dtype=torch.float64, device=dev)
+        nibi = torch.zeros(nF, dtype=torch.int32, device=dev)
+        self.call("nc_ibi_from_beats", beats.data_ptr(), fbase.data_ptr(), nb.data_ptr(), nF, hop, min_ibis,
+                  ibis.data_ptr(), nibi.data_ptr(), st)
+        fb_h = np.concatenate([[0], np.cumsum(frames)]).astype(np.int64)
+        return dict(onset=onset, fbase=fbase, fbase_h=fb_h, frames=frames, tg=tg, bpm=bpm, lag=lag, nbeats=nb,
+                    margin=mg, beats=beats, ibis=ibis, nibi=nibi)
+
+    def _ibi_pass(self, signals, d_off, d_len, f_len, prior, B):
+        dev, st = self.dev, self.stream()
+        nF = 2 * B
+        starts = torch.cat([prior[:B], torch.tensor([120.0], dtype=torch.float64, device=dev)])
+        pidx = torch.tensor([f // 2 if f % 2 == 0 else B for f in range(nF)], dtype=torch.int32, device=dev)
+        core = self.ibi_core(signals.buf, d_off, d_len, f_len, starts, pidx)
+        frames, fb_h, ibis, nibi = core["frames"], core["fbase_h"], core["ibis"], core["nibi"]
+        nb, bpm, lag, mg = core["nbeats"], core["bpm"], core["lag"], core["margin"]
+        # bootstrap: A = src ibis, B = nc ibis (consensus.py:303-307), seed 42, need >= 4 each
+        caps = [int(frames[2 * b] // 32 + frames[2 * b + 1] // 32 + 4) for b in range(B)]
+        wsoff, tot = [], 0
+        for c in caps:
+            wsoff.append(tot)
+            tot += self.ctx.lib.nc_bootstrap_job_bytes(c, C.N_BOOTSTRAP)
+        up = _Upload()
+        up.add("a_off", [fb_h[2 * b + 1] for b in range(B)], np.int64)
+        up.add("b_off", [fb_h[2 * b] for b in range(B)], np.int64)
+        up.add("seed", seed_state(42) * B, np.uint64)
+        up.add("wsoff", wsoff, np.int64)
+        up.add("cap", caps, np.int32)
+        dd = up.commit(dev)
+        src_i = torch.arange(1, nF, 2, device=dev)
+        nc_i = torch.arange(0, nF, 2, device=dev)
+        a_n = nibi[src_i].contiguous()
+        b_n = nibi[nc_i].contiguous()
+        out = torch.full((3 * B,), float("nan"), dtype=torch.float64, device=dev)
+        ws = self.workspace("boot_ibi", tot)
+        il, gl, ih, gh = percentile_params(C.N_BOOTSTRAP, C.CI_LEVEL)
+        self.call("nc_bootstrap_ratio", ibis.data_ptr(), dd["a_off"].data_ptr(), a_n.data_ptr(),
+                  dd["b_off"].data_ptr(), b_n.data_ptr(), B, C.N_BOOTSTRAP, dd["seed"].data_ptr(), il, gl, ih, gh,
+                  4, out[0:B].data_ptr(), out[B:2 * B].data_ptr(), out[2 * B:].data_ptr(), None,
+                  dd["wsoff"].data_ptr(), dd["cap"].data_ptr(), ws.data_ptr(), ws.numel(), st)
+        return dict(out=out, nibi=nibi, nbeats=nb, bpm=bpm, lag=lag, margin=mg)
+
+    # -------------------------------------------------------------- host assembly + logs
+    def _assemble_pair(self, b, p: Params, h, ibi, starts, w0, w1, f_len, strip_len, lead, trail, intro,
+                       win_n, pair_chunks, n_cp, nj, n_pitch_jobs) -> PairOutcome:
+        out = PairOutcome()
+        L = out.logs.append
+        fn, fs = 2 * b, 2 * b + 1
+        nc_len, src_len = int(f_len[fn]), int(f_len[fs])
+        if p.silence_strip_db is not None:
+            L(f"Stripping silence (top_db={p.silence_strip_db} dB)…")
+            L(f"  nightcore: −{lead[fn]:.2f}s leading, −{trail[fn]:.2f}s trailing"
+              f"  →  {strip_len[fn] / SR:.1f} s")
+            L(f"  source:    −{lead[fs]:.2f}s leading, −{trail[fs]:.2f}s trailing"
+              f"  →  {strip_len[fs] / SR:.1f} s")
+        if p.src_trim_sec > 0.0:
+            L(f"Manual source trim: skipping {p.src_trim_sec:.2f}s from source start")
+        L(f"Slicing into {p.window_sec:.0f} s windows (hop {p.hop_sec:.0f} s)…")
+        L(f"  nightcore: {len(starts[fn])} windows  |  source: {len(starts[fs])} windows")
+        L(f"Energy gating (threshold {p.energy_gate_db} dB below peak)…")
+        act = h["active"]
+        src_w = [w for w in range(w0[fs], w1[fs]) if act[w]]
+        nc_w = [w for w in range(w0[fn], w1[fn]) if act[w]]
+        L(f"  after gating — nightcore: {len(nc_w)} windows  |  source: {len(src_w)} windows")
+        out.detail.update(energy_src=h["energy"][w0[fs]:w1[fs]].copy(), energy_nc=h["energy"][w0[fn]:w1[fn]].copy(),
+                          n_src_windows=len(src_w), n_nc_windows=len(nc_w),
+                          nc_duration=nc_len / SR, src_duration=src_len / SR)
+        if not nc_w or not src_w:
+            out.error = RuntimeError("All windows were discarded by the energy gate.  "
+                                     "Try raising --energy-gate (e.g. --energy-gate -60).")
+            return out
+
+        # pitch
+        pitch_boot = None
+        if p.compute_pitch:
+            L("Estimating pitch (chromagram cross-correlation)…")
+            c0, c1 = pair_chunks[b]
+            n = c1 - c0
+            lags = h["clag"][c0:c1].astype(int).tolist()
+            shifts = h["pvals"][c0:c1]
+            src_p = h["pvals"][2 * n_cp + c0:2 * n_cp + c1].tolist()
+            nc_p = h["pvals"][n_cp + c0:n_cp + c1].tolist()
+            point_st = float(np.median(shifts))
+            if n >= MIN_CHUNKS:
+                j = b
+                lo_st, hi_st = float(h["sout"][n_pitch_jobs + j]), float(h["sout"][2 * n_pitch_jobs + j])
+            else:
+                lo_st = hi_st = point_st
+                L(f"    Only {n} chunk(s) available (need ≥ {MIN_CHUNKS}) — "
+                  "pitch CI is degenerate; estimate may be less reliable.")
+            L(f"    Chroma xcorr: {point_st:+.3f} st  95% CI [{lo_st:+.3f}, {hi_st:+.3f}] st"
+              f"  ({n} chunk{'s' if n != 1 else ''})")
+            L("    essentia not available — skipping MELODIA refinement")
+            L("  Pitch method: chroma_xcorr")
+            method = "chroma_xcorr"
+            pj = len(w0) // 2 + b     # pitch job index: after the B tempo jobs
+            pitch_boot = (float(h["bout"][pj]), (float(h["bout"][nj + pj]), float(h["bout"][2 * nj + pj])))
+            out.detail.update(chunk_lags=lags, tuning=h["tuning"][2 * c0:2 * c1].copy(),
+                              chroma=h["chroma"][24 * c0:24 * c1].reshape(-1, 12).copy())
+        else:
+            L("Skipping pitch estimation.")
+            src_p, nc_p, method = [], [], None
+
+        # tempo
+        L("Estimating tempo (librosa)…")
+        tempos = {}
+        for side, ws_ in (("src", src_w), ("nc", nc_w)):
+            if side == "src":
+                L("  ← source →")
+            vals = []
+            for i, w in enumerate(ws_):
+                f = fs if side == "src" else fn
+                s0 = starts[f][w - w0[f]]
+                L(f"    tempo window {i + 1}/{len(ws_)}  [{s0 / SR:.1f}–{(s0 + win_n) / SR:.1f} s]")
+                vals.append(float(h["bpm"][w]) if h["nbeats"][w] >= MIN_BEATS else None)
+            L(f"    {sum(1 for v in vals if v is not None)}/{len(ws_)} windows yielded a confident tempo estimate")
+            tempos[side] = vals
+            if side == "src":
+                valid_src = [t for t in vals if t is not None]
+                nc_dur, src_dur = nc_len / SR, src_len / SR
+                if valid_src and nc_dur > 0 and src_dur > 0:
+                    med = float(np.median(valid_src))
+                    L(f"  NC tempo prior: {h['prior'][b]:.1f} BPM  "
+                      f"(src median {med:.1f} BPM × dur ratio {src_dur / nc_dur:.4f})")
+                L("  ← nightcore →")
+        out.detail.update(src_tempos=tempos["src"], nc_tempos=tempos["nc"], nc_start_bpm=float(h["prior"][b]),
+                          tempo_margin_src=h["margin"][src_w].copy(), tempo_margin_nc=h["margin"][nc_w].copy())
+        L("Computing consensus…")
+        try:
+            tempo_boot = (float(h["bout"][b]), (float(h["bout"][nj + b]), float(h["bout"][2 * nj + b])))
+            res = C.assemble(src_p, nc_p, tempos["src"], tempos["nc"], nc_duration=nc_len / SR,
+                             src_duration=src_len / SR, pitch_boot=pitch_boot, tempo_boot=tempo_boot)
+        except ValueError as exc:
+            out.error = exc
+            return out
+        res.intro_offset_sec = intro
+        res.pitch_method = method
+        if ibi is not None:
+            L("Computing IBI ratio (high-precision beat timestamps, hop=64)…")
+            nb_ = ibi["nibi"]
+            Bn = len(nb_) // 2
+            if nb_[2 * b] >= 4 and nb_[2 * b + 1] >= 4:
+                o = ibi["out"]
+                res.ibi_ratio = float(o[b])
+                res.ibi_ci = (float(o[Bn + b]), float(o[2 * Bn + b]))
+                L(f"  IBI ratio: {res.ibi_ratio:.6f}×  95% CI [{res.ibi_ci[0]:.6f}, {res.ibi_ci[1]:.6f}]")
+            else:
+                L("  IBI ratio: insufficient beats — skipped")
+            out.detail.update(ibi_nbeats=(int(ibi["nbeats"][2 * b]), int(ibi["nbeats"][2 * b + 1])),
+                              ibi_n=(int(nb_[2 * b]), int(nb_[2 * b + 1])),
+                              ibi_lag=(int(ibi["lag"][2 * b]), int(ibi["lag"][2 * b + 1])))
+        L("Done.")
+        out.result = res
+        return out
+
+
+_engines: Dict[Tuple[int, int], Engine] = {}
+_elock = threading.Lock()
+
+
+def get_engine(device: Optional[int] = None) -> Engine:
+    """One engine per (device, thread) — contexts are not shared across threads."""
+    if device is None:
+        device = torch.cuda.current_device() if torch.cuda.is_available() else 0
+    key = (device, threading.get_ident())
+    with _elock:
+        e = _engines.get(key)
+        if e is None:
+            e = Engine(device)
+            _engines[key] = e
+        return e

@@ -1,0 +1,124 @@
+"""Audio I/O, windowing, energy gating and silence stripping
+(drop-in for the reference's nightcore_analyzer/io.py).
+
+* ``load_audio`` (io.py:44-55) decodes on the CPU — file decode is out of the
+  engine's scope (north_star); WAV (PCM 8/16/24/32-bit, float) and ``.npy`` are
+  read with the standard library / numpy, down-mixed to mono float32 and, if
+  the file is not at 22 050 Hz, resampled with scipy's polyphase filter (the
+  reference uses librosa.load's soxr_hq; not bit-identical — see DESIGN.md).
+* ``strip_silence`` (io.py:58-79) runs ``nc_trim_bounds`` on the GPU.
+* ``slice_windows`` (io.py:82-112) returns views like the reference, with the
+  window energies computed by ``nc_window_energy`` on the GPU.
+* ``energy_gate`` (io.py:115-126) is the same list filter.
+"""
+from __future__ import annotations
+
+import wave
+from dataclasses import dataclass
+from pathlib import Path
+from typing import List
+
+import numpy as np
+
+SAMPLE_RATE: int = 22050
+WINDOW_SEC: float = 10.0
+HOP_SEC: float = 5.0
+ENERGY_GATE_DB: float = -40.0
+SILENCE_STRIP_DB: float = 60.0
+
+
+@dataclass
+class AudioWindow:
+    """One time slice of an audio file (io.py:27-34)."""
+    audio: np.ndarray
+    sample_rate: int
+    start_sec: float
+    end_sec: float
+    energy_db: float
+
+
+def _rms_db(audio: np.ndarray) -> float:
+    """20 log10(max(rms, 1e-10)) with float64 accumulation (io.py:38-40), on the GPU."""
+    from .engine import get_engine
+    from .ops import window_energies
+    return float(window_energies(get_engine(), audio, np.array([0]), len(audio))[0])
+
+
+def _read_wav(path: Path):
+    with wave.open(str(path), "rb") as w:
+        ch, width, sr, n = w.getnchannels(), w.getsampwidth(), w.getframerate(), w.getnframes()
+        raw = w.readframes(n)
+    if width == 1:
+        x = (np.frombuffer(raw, np.uint8).astype(np.float32) - 128.0) / 128.0
+    elif width == 2:
+        x = np.frombuffer(raw, "<i2").astype(np.float32) / 32768.0
+    elif width == 3:
+        b = np.frombuffer(raw, np.uint8).reshape(-1, 3).astype(np.int32)
+        v = b[:, 0] | (b[:, 1] << 8) | (b[:, 2] << 16)
+        v = np.where(v >= 1 << 23, v - (1 << 24), v)
+        x = v.astype(np.float32) / float(1 << 23)
+    elif width == 4:
+        x = np.frombuffer(raw, "<i4").astype(np.float32) / 2147483648.0
+    else:
+        raise ValueError(f"unsupported WAV sample width {width}")
+    return x.reshape(-1, ch).mean(axis=1).astype(np.float32), sr
+
+
+def load_audio(path: str, sr: int = SAMPLE_RATE) -> tuple[np.ndarray, int]:
+    """Decode *path* to mono float32 at *sr* Hz (io.py:44-55; decode stays on the CPU)."""
+    p = Path(path)
+    if p.suffix.lower() == ".npy":
+        y, file_sr = np.load(p, allow_pickle=False).astype(np.float32), sr
+        if y.ndim > 1:
+            y = y.mean(axis=0).astype(np.float32)
+    elif p.suffix.lower() == ".wav":
+        try:
+            y, file_sr = _read_wav(p)
+        except wave.Error:
+            import scipy.io.wavfile
+            file_sr, y = scipy.io.wavfile.read(p)
+            y = np.asarray(y, np.float32)
+            if y.ndim > 1:
+                y = y.mean(axis=1)
+            y = y.astype(np.float32)
+    else:
+        raise NotImplementedError(
+            f"{p.suffix} decoding is outside the engine (the reference uses librosa.load/soundfile, "
+            "not installed here); convert to WAV or .npy first")
+    if file_sr != sr:
+        import math
+        import scipy.signal
+        g = math.gcd(int(sr), int(file_sr))
+        y = scipy.signal.resample_poly(y.astype(np.float64), sr // g, file_sr // g).astype(np.float32)
+    return np.ascontiguousarray(y, dtype=np.float32), sr
+
+
+def strip_silence(audio: np.ndarray, sr: int, top_db: float = SILENCE_STRIP_DB) -> tuple[np.ndarray, float, float]:
+    """(trimmed view, leading_sec, trailing_sec) — librosa.effects.trim on the GPU."""
+    from .engine import get_engine
+    from .ops import trim_bounds
+    (start, end), = trim_bounds(get_engine(), [audio], top_db)
+    return audio[start:end], start / sr, (len(audio) - end) / sr
+
+
+def slice_windows(audio: np.ndarray, sr: int, window_sec: float = WINDOW_SEC,
+                  hop_sec: float = HOP_SEC) -> List[AudioWindow]:
+    win_n, hop_n = int(window_sec * sr), int(hop_sec * sr)
+    starts = []
+    s = 0
+    while s + win_n <= len(audio):
+        starts.append(s)
+        s += hop_n
+    if not starts:
+        return []
+    from .engine import get_engine
+    from .ops import window_energies
+    en = window_energies(get_engine(), audio, np.asarray(starts, np.int64), win_n)
+    return [AudioWindow(audio[s:s + win_n], sr, s / sr, (s + win_n) / sr, float(e)) for s, e in zip(starts, en)]
+
+
+def energy_gate(windows: List[AudioWindow], threshold_db: float = ENERGY_GATE_DB) -> List[AudioWindow]:
+    if not windows:
+        return windows
+    peak = max(w.energy_db for w in windows)
+    return [w for w in windows if w.energy_db >= peak + threshold_db]

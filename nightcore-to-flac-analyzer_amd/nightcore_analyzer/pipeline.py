@@ -1,0 +1,85 @@
+"""Full windowed consensus pipeline (drop-in for the reference's
+nightcore_analyzer/pipeline.py).
+
+``run`` keeps the reference's exact signature and behaviour (pipeline.py:23-216):
+load -> strip silence -> source trim -> windows -> energy gate -> pitch (chroma
+xcorr) -> source tempo -> nc tempo prior -> nc tempo -> consensus -> IBI ratio,
+with the same log lines and the same exceptions (RuntimeError when every
+window is gated out, ValueError when fewer than 3 valid tempo windows).  All
+analysis arithmetic runs on the MI355X through ``libncgpu``; ``run_batch``
+analyses many pairs in one device batch (the reference has no batch API, its
+``run`` is a batch of one); ``analyze`` is an alias of ``run``.
+"""
+from __future__ import annotations
+
+from typing import Callable, List, Optional, Sequence, Tuple, Union
+
+import numpy as np
+
+from .consensus import AnalysisResult
+from .io import ENERGY_GATE_DB, HOP_SEC, SILENCE_STRIP_DB, WINDOW_SEC, load_audio
+
+PathOrArray = Union[str, np.ndarray]
+
+
+def _params(window_sec, hop_sec, energy_gate_db, silence_strip_db, src_trim_sec, auto_align, compute_pitch,
+            compute_ibi=True):
+    from .engine import Params
+    return Params(window_sec=window_sec, hop_sec=hop_sec, energy_gate_db=energy_gate_db,
+                  silence_strip_db=silence_strip_db, src_trim_sec=src_trim_sec, auto_align=auto_align,
+                  compute_pitch=compute_pitch, compute_ibi=compute_ibi)
+
+
+def _load(x: PathOrArray, log, what: str, sr: int = 22050):
+    log(f"Loading {what} audio…")
+    if isinstance(x, np.ndarray):
+        y = np.ascontiguousarray(x, dtype=np.float32)
+    else:
+        y, sr = load_audio(x, sr=sr)
+    log(f"  {len(y) / sr:.1f} s  ({len(y):,} samples @ {sr} Hz)")
+    return y
+
+
+def run(nightcore_path: str, source_path: str, *, window_sec: float = WINDOW_SEC, hop_sec: float = HOP_SEC,
+        energy_gate_db: float = ENERGY_GATE_DB, silence_strip_db: Optional[float] = SILENCE_STRIP_DB,
+        src_trim_sec: float = 0.0, auto_align: bool = False, compute_pitch: bool = True,
+        log: Optional[Callable[[str], None]] = print) -> AnalysisResult:
+    """Analyse the tempo and pitch relationship between a nightcore track and its source."""
+    def _log(msg: str) -> None:
+        if log is not None:
+            log(msg)
+
+    nc = _load(nightcore_path, _log, "nightcore")
+    src = _load(source_path, _log, "source")
+    from .engine import get_engine
+    outcome, = get_engine().analyze([(nc, src)], _params(window_sec, hop_sec, energy_gate_db, silence_strip_db,
+                                                         src_trim_sec, auto_align, compute_pitch))
+    for line in outcome.logs:
+        _log(line)
+    if outcome.error is not None:
+        raise outcome.error
+    return outcome.result
+
+
+analyze = run
+
+
+def run_batch(pairs: Sequence[Tuple[PathOrArray, PathOrArray]], *, window_sec: float = WINDOW_SEC,
+              hop_sec: float = HOP_SEC, energy_gate_db: float = ENERGY_GATE_DB,
+              silence_strip_db: Optional[float] = SILENCE_STRIP_DB, src_trim_sec: float = 0.0,
+              compute_pitch: bool = True, compute_ibi: bool = True,
+              log: Optional[Callable[[str], None]] = None) -> List[Union[AnalysisResult, BaseException]]:
+    """Analyse many (nightcore, source) pairs in one GPU batch.  Returns, per
+    pair, the AnalysisResult or the exception ``run`` would have raised."""
+    quiet = (lambda m: None)
+    arrays = [(_load(n, quiet, "nightcore"), _load(s, quiet, "source")) for n, s in pairs]
+    from .engine import get_engine
+    outs = get_engine().analyze(arrays, _params(window_sec, hop_sec, energy_gate_db, silence_strip_db,
+                                                src_trim_sec, False, compute_pitch, compute_ibi))
+    res = []
+    for i, o in enumerate(outs):
+        if log is not None:
+            for line in o.logs:
+                log(f"[pair {i}] {line}")
+        res.append(o.error if o.error is not None else o.result)
+    return res

@@ -532,8 +532,9 @@ def piptrack(y, sr=22050, n_fft=2048, hop=None, fmin=150.0, fmax=4000.0, thresho
     fft_freqs = np.fft.rfftfreq(n=n_fft, d=1.0 / sr)
     avg = np.gradient(S, axis=0)
     Sd = S.astype(np.float64)
-    a = Sd[2:] + Sd[:-2] - 2 * Sd[1:-1]
-    b = (Sd[2:] - Sd[:-2]) / 2
+    # numba stencil typing: f32 + f32 -> f32 ; int * f32 -> f64 ; f32 / int -> f64
+    a = (S[2:] + S[:-2]).astype(np.float64) - 2 * Sd[1:-1]
+    b = (S[2:] - S[:-2]).astype(np.float64) / 2
     with np.errstate(divide="ignore", invalid="ignore"):
         sh = np.where(np.abs(b) >= np.abs(a), 0.0, -b / a)
     shift = np.zeros_like(S)

@@ -6,7 +6,7 @@ import pytest
 
 REPO = Path(__file__).resolve().parents[1]
 PKG = REPO / "nightcore-to-flac-analyzer_amd"
-for p in (str(PKG), str(REPO)):
+for p in (str(PKG), str(REPO), str(REPO / "tests")):
     if p not in sys.path:
         sys.path.insert(0, p)
 os.environ.setdefault("PYTHONDONTWRITEBYTECODE", "1")

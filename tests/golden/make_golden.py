@@ -197,29 +197,8 @@ def _result_fields(r) -> dict:
 
 
 # ----------------------------------------------------------------------------- cases
-PIPELINE_CASES = [
-    # name, seconds, seed, kind, kwargs, edits
-    ("sweep30", 30.0, 1000, "sweep", {}, None),
-    ("chords80", 80.0, 1001, "chords", {}, None),
-    ("chords80_nopitch", 80.0, 1001, "chords", {"compute_pitch": False}, None),
-    ("chords75_silence", 75.0, 1002, "chords", {"src_trim_sec": 1.5}, "silence"),
-    ("chords60_gate", 60.0, 1003, "chords", {"energy_gate_db": -20.0}, "quiet"),
-]
-
-
-def _edit(nc, src, how, seed):
-    rng = np.random.default_rng(seed)
-    if how == "silence":
-        src = np.concatenate([np.zeros(50_000, np.float32), src, np.zeros(30_001, np.float32)])
-        nc = np.concatenate([np.zeros(12_345, np.float32), nc])
-    elif how == "quiet":
-        # a 12 s stretch 30 dB down in the source -> some windows gated at -20 dB
-        a, b = 300_000, 300_000 + 12 * 22050
-        src = src.copy()
-        src[a:b] *= np.float32(10 ** (-30 / 20))
-        nc = nc.copy()
-        nc[:200_000] *= np.float32(10 ** (-25 / 20))
-    return nc, src
+sys.path.insert(0, str(OUT))
+from cases import PIPELINE_CASES, edit as _edit  # noqa: E402
 
 
 def gen_pipeline(mods, names=None):
