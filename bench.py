@@ -1,0 +1,188 @@
+#!/usr/bin/env python3
+"""Benchmark: 10 s windows/sec of the per-window hot path on MI355X.
+
+Workload (BASELINE.json configs[2], "config 3"): per GPU a batch of 64 synthetic
+3-min 22.05 kHz mono (nightcore, source) pairs (chords + clicks
+every 10 752 samples + -50 dBFS noise; nc = resample_poly(src, 4, 5)), seed
+1000 + global pair index.  One step = one pass of pipeline.run's analysis over
+the batch with the inputs already resident in HBM: silence trim, 10 s / 5 s
+windows (62 per pair), energy gate, onset + tempogram + tempo + beat tracking
+per window, nc tempo prior, 20 s-chunk CQT chroma (14 per pair) + lag,
+tempo/pitch bootstraps, result assembly.  The hop-64 IBI pass is not part of
+the windows/sec metric and is reported beside it.
+
+N > 1: one process per GPU (torch.distributed.run), each rank owns its own 64
+pairs (pairs are independent objects: no data-path collective; weak scaling);
+barrier + synchronize around the K timed steps, max elapsed over ranks.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+from concurrent.futures import ProcessPoolExecutor
+from pathlib import Path
+
+REPO = Path(__file__).resolve().parent
+sys.path.insert(0, str(REPO / "nightcore-to-flac-analyzer_amd"))
+sys.path.insert(0, str(REPO))
+
+HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
+WIN_BYTES = 220500 * 4         # algorithmic bytes per 10 s window
+CHUNK_BYTES = 441000 * 4       # algorithmic bytes per 20 s CQT chunk
+
+
+def _gen(args):
+    seconds, seed = args
+    from nightcore_analyzer import synth
+    return synth.make_pair(seconds, seed)
+
+
+def make_pairs(n, seconds, base_seed, workers):
+    with ProcessPoolExecutor(max_workers=workers) as ex:
+        return list(ex.map(_gen, [(seconds, base_seed + i) for i in range(n)]))
+
+
+def cpu_baseline(nc, src):
+    """The oracle (oracle/refglue.py, a CPU port of the reference glue on the
+    numpy restatement of librosa) on ONE pair of the batch, single thread."""
+    from threadpoolctl import threadpool_limits
+    from oracle import refglue
+    with threadpool_limits(limits=1):
+        t0 = time.perf_counter()
+        res = refglue.run_arrays(nc, src, compute_ibi=False)
+        dt = time.perf_counter() - t0
+    nw = len(refglue.slice_windows(nc)) + len(refglue.slice_windows(src))
+    return {"value": nw / dt, "unit": "windows/s", "cores": 1, "kind": "port",
+            "sample": f"pair 0 of the batch (3-min pair: {nw} windows + 7 CQT chunk pairs + bootstraps), "
+                      f"oracle/refglue.run_arrays(compute_ibi=False), 1 thread, {dt:.1f} s",
+            "tempo_ratio": res["tempo_ratio"], "pitch_ratio": res["pitch_ratio"]}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--pairs", type=int, default=64, help="pairs per GPU (config 3: 64)")
+    ap.add_argument("--seconds", type=float, default=180.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-ibi", action="store_true")
+    ap.add_argument("--workers", type=int, default=min(16, os.cpu_count() or 1))
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    from nightcore_analyzer import engine as E
+
+    pairs = make_pairs(args.pairs, args.seconds, 1000 + rank * args.pairs, max(1, args.workers // max(1, world)))
+    eng = E.get_engine(local)
+    flat = []
+    for nc, src in pairs:
+        flat += [nc, src]
+    signals = eng.upload_signals(flat)           # resident in HBM before timing
+    torch.cuda.synchronize()
+    params = E.Params(compute_ibi=False)
+
+    outs = eng.analyze(signals=signals, params=params)
+    bad = [i for i, o in enumerate(outs) if o.error is not None]
+    if bad:
+        raise RuntimeError(f"pairs {bad} failed: {outs[bad[0]].error}")
+    win_per_step = sum(o.detail["energy_src"].size + o.detail["energy_nc"].size for o in outs)
+    chunks_per_step = 2 * sum(len(o.detail["chunk_lags"]) for o in outs)
+    tr = outs[0].result.tempo_ratio
+    pr = outs[0].result.pitch_ratio
+    for _ in range(max(0, args.warmup - 1)):
+        eng.analyze(signals=signals, params=params)
+
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        eng.analyze(signals=signals, params=params)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([el], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+
+    # per-kernel timing with HIP events on the launch stream (separate, non-timed steps)
+    eng.start_timers()
+    ksteps = max(1, min(args.steps, 3))
+    for _ in range(ksteps):
+        eng.analyze(signals=signals, params=params)
+    timers = eng.stop_timers()
+    per = {k: (ms / n, n // ksteps) for k, (ms, n) in timers.items()}
+    alg = {"nc_window_stage": win_per_step * WIN_BYTES, "nc_chroma_mean": chunks_per_step * CHUNK_BYTES}
+    dom = max(alg, key=lambda k: per.get(k, (0, 0))[0])
+    avg_ms = per[dom][0]
+    achieved = alg[dom] / (avg_ms * 1e-3) / 1e9
+    step_ms = el / args.steps * 1e3
+
+    ibi = None
+    if not args.no_ibi and rank == 0:
+        sub = E.DeviceSignals(signals.buf, signals.off[:4], signals.length[:4])
+        eng.analyze(signals=sub, params=E.Params(compute_ibi=True))
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        o2 = eng.analyze(signals=sub, params=E.Params(compute_ibi=True))
+        torch.cuda.synchronize()
+        t_ibi = time.perf_counter() - t1
+        t1 = time.perf_counter()
+        eng.analyze(signals=sub, params=E.Params(compute_ibi=False))
+        torch.cuda.synchronize()
+        t_no = time.perf_counter() - t1
+        frames = int(sum(1 + int(n) // 64 for n in sub.length))
+        ibi = {"pairs": 2, "seconds_per_pair": (t_ibi - t_no) / 2, "hop64_frames_per_s": frames / max(1e-9, t_ibi - t_no),
+               "ibi_ratio_pair0": o2[0].result.ibi_ratio}
+
+    if rank == 0:
+        line = {
+            "metric": "10 s windows/sec (CQT+onset, 22.05 kHz mono) at 1/2/4/8 GPUs; % HBM roofline",
+            "value": world * win_per_step * args.steps / el,
+            "unit": "windows/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": step_ms,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic (SURVEY.md §8d chords+clicks+noise, nc = resample_poly(src, 4, 5)), resident in HBM",
+            "config": {"workload": "config 3: per GPU a batch of 64 x 3-min 22.05 kHz mono pairs; step = "
+                                   "pipeline.run analysis without the hop-64 IBI pass",
+                       "pairs_per_gpu": args.pairs, "windows_per_gpu_step": win_per_step,
+                       "cqt_chunks_per_gpu_step": chunks_per_step, "parallelism": f"dp{world} (pairs sharded)"},
+            "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                         "alg_bytes_per_launch": alg[dom], "avg_launch_ms": avg_ms},
+            "kernels_ms_per_step": {k: round(v[0] * v[1], 4) for k, v in per.items()},
+            "check": {"tempo_ratio_pair0": tr, "pitch_ratio_pair0": pr},
+        }
+        if ibi is not None:
+            line["ibi_pass"] = ibi
+        if world == 1 and not args.no_cpu_baseline:
+            line["cpu_baseline"] = cpu_baseline(*pairs[0])
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -75,6 +75,9 @@ def load():
     with _lock:
         if _lib is not None:
             return _lib
+        # torch-ROCm ships its own libamdhip64; load it first so libncgpu.so binds to
+        # the same HIP runtime instance (one device context, shared streams).
+        import torch  # noqa: F401
         if not _LIB_PATH.exists():
             raise NativeUnavailable(
                 f"{_LIB_PATH} not built: run `python -c 'import __graft_entry__ as g; g.build()'` "

@@ -137,6 +137,7 @@ class Engine:
         self.ctx = _native.Context(device)
         self._ws: Dict[str, torch.Tensor] = {}
         self.num_cu = self.ctx.lib.nc_num_cu(self.ctx.h)
+        self.timers: Optional[Dict[str, list]] = None
 
     # -------------------------------------------------------------- plumbing
     def stream(self) -> int:
@@ -150,7 +151,26 @@ class Engine:
         return t
 
     def call(self, name: str, *args):
+        if self.timers is None:
+            self.ctx.call(name, *args)
+            return
+        s = torch.cuda.current_stream(self.dev)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(s)
         self.ctx.call(name, *args)
+        e1.record(s)
+        self.timers.setdefault(name, []).append((e0, e1))
+
+    def start_timers(self):
+        """Record a HIP event pair around every entry-point launch (on the launch stream)."""
+        self.timers = {}
+
+    def stop_timers(self) -> Dict[str, Tuple[float, int]]:
+        """{entry point: (total ms, launches)}; synchronises."""
+        torch.cuda.synchronize(self.dev)
+        out = {k: (sum(a.elapsed_time(b) for a, b in v), len(v)) for k, v in (self.timers or {}).items()}
+        self.timers = None
+        return out
 
     def upload_signals(self, arrays: Sequence[np.ndarray]) -> DeviceSignals:
         lens = np.array([len(a) for a in arrays], dtype=np.int64)
