@@ -1,0 +1,57 @@
+"""Multi-process (gloo, world_size 2, CPU) tests of the pair sharding and the
+result gather used by bench.py / run_batch_distributed on N GPUs."""
+import os
+import socket
+
+import pytest
+import torch.multiprocessing as mp
+
+from nightcore_analyzer.distributed import shard_range
+
+
+def test_shard_range_covers_exactly():
+    for n in range(0, 40):
+        for w in (1, 2, 3, 8):
+            spans = [shard_range(n, w, r) for r in range(w)]
+            assert spans[0][0] == 0 and spans[-1][1] == n
+            assert all(a[1] == b[0] for a, b in zip(spans, spans[1:]))
+            sizes = [h - l for l, h in spans]
+            assert max(sizes) - min(sizes) <= 1
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, q):
+    import torch.distributed as dist
+    from nightcore_analyzer.distributed import run_batch_distributed
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+
+    def fake_analyze(pairs, scale):   # stands in for the GPU engine
+        return [("rank", rank, p * scale) for p in pairs]
+
+    out = run_batch_distributed(list(range(7)), analyze_fn=fake_analyze, scale=10)
+    q.put((rank, out))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_run_batch_distributed_gloo_world2():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in range(2))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    expect = [("rank", 0 if i < 4 else 1, i * 10) for i in range(7)]
+    assert res[0] == expect and res[1] == expect

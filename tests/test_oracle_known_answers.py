@@ -1,0 +1,81 @@
+"""Known-answer tests of the librosa restatement (oracle/ncref.py) from first
+principles — the only pinning available for librosa arithmetic, which is absent
+from this image ("parity unpinned" against real librosa)."""
+import numpy as np
+import pytest
+import scipy.signal
+
+from oracle import ncref, refglue
+from nightcore_analyzer import synth
+
+SR = 22050
+
+
+def _clicks(n, period, amp=0.5):
+    y = np.zeros(n, np.float32)
+    t = np.arange(600) / SR
+    burst = (amp * np.exp(-t / 0.005) * np.sin(2 * np.pi * 1500 * t)).astype(np.float32)
+    for b in range(0, n - 600, period):
+        y[b:b + 600] += burst
+    return y
+
+
+@pytest.mark.parametrize("lag", [17, 21, 25])
+def test_click_track_tempo_lag(lag):
+    """Clicks every lag*512 samples -> tempogram argmax at that lag -> 2583.984375/lag BPM."""
+    y = _clicks(220500, lag * 512) + np.random.default_rng(0).standard_normal(220500).astype(np.float32) * 1e-3
+    o = ncref.onset_strength(y, SR, 512)
+    bpm, L = ncref.tempo_from_tg(ncref.tempogram_mean(o, 344), SR, 512, 60 * SR / (512 * lag))
+    assert L == lag and bpm == 60.0 * SR / (512.0 * lag)
+
+
+def test_beats_are_evenly_spaced_on_a_click_track():
+    y = _clicks(220500, 21 * 512) + np.random.default_rng(1).standard_normal(220500).astype(np.float32) * 1e-3
+    o = ncref.onset_strength(y, SR, 512)
+    bpm, beats = ncref.beat_track(o, SR, 512, 120.0)
+    d = np.diff(beats)
+    assert len(beats) >= 15 and set(d.tolist()) <= {20, 21, 22} and np.median(d) == 21
+
+
+@pytest.mark.parametrize("k", [0, 2, 4, -3])
+def test_chroma_lag_of_transposed_chords(k):
+    # pitch-shift by an exact number of semitones via resampling the chord part only
+    up = 2 ** (k / 12.0)
+    t = np.arange(441000) / SR
+    rng = np.random.default_rng(3)
+    notes = [57, 60, 64]
+    src = sum(np.sin(2 * np.pi * 440 * 2 ** ((m - 69) / 12) * t + rng.random()) for m in notes).astype(np.float32) * 0.1
+    nc = sum(np.sin(2 * np.pi * 440 * 2 ** ((m - 69) / 12) * up * t + rng.random()) for m in notes).astype(np.float32) * 0.1
+    assert refglue.chunk_lag(src, nc) == (k if k <= 6 else k - 12)
+
+
+def test_trim_boundaries_of_padded_tone():
+    t = np.arange(3 * SR) / SR
+    tone = (0.3 * np.sin(2 * np.pi * 440 * t)).astype(np.float32)
+    y = np.concatenate([np.zeros(20480, np.float32), tone, np.zeros(30000, np.float32)])
+    _, (s, e) = ncref.trim(y, 60)
+    # first/last frames whose centred 2048-sample window overlaps the tone (t=39, t=171)
+    assert (s, e) == (39 * 512, 172 * 512)
+
+
+def test_ibi_period_exact_frames():
+    y = _clicks(30 * SR, 168 * 64) + np.random.default_rng(2).standard_normal(30 * SR).astype(np.float32) * 1e-3
+    ibis = refglue.estimate_ibis_global(y, SR)
+    assert ibis is not None and abs(np.median(ibis) * SR / 64 - 168) < 1e-9
+
+
+def test_halfband_decimator_response():
+    h = ncref.halfband_taps()
+    assert len(h) == 47 and abs(h.sum() - 1.0) < 1e-15
+    n = np.arange(-23, 24)
+    assert np.all(h[(n % 2 == 0) & (n != 0)] == 0.0)
+    w, H = scipy.signal.freqz(h, worN=8192, fs=1.0)
+    assert np.max(np.abs(np.abs(H[w <= 0.11]) - 1.0)) < 1e-4
+    assert np.max(20 * np.log10(np.maximum(np.abs(H[w >= 0.33]), 1e-300))) < -100.0
+
+
+def test_mel_filterbank_slaney_properties():
+    W = ncref.mel_filter(22050, 2048, 128)
+    assert W.shape == (128, 1025) and W.dtype == np.float32
+    # each FFT bin contributes to at most two adjacent bands; every band is non-empty
+    assert (np.count_nonzero(W, axis=0) <= 2).all() and (np.count_nonzero(W, axis=1) > 0).all()
