@@ -1,0 +1,108 @@
+"""GPU parity of the remaining components against the CPU oracle, through the
+drop-in module functions (io / tempo / pitch / xcorr), plus full-size (3-min,
+BASELINE config 2) properties."""
+import numpy as np
+import pytest
+import scipy.signal
+import torch
+
+from oracle import ncref, refglue
+from nightcore_analyzer import engine as E
+from nightcore_analyzer import io as nio
+from nightcore_analyzer import ops, pitch, synth, tempo, xcorr
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def eng():
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    return E.get_engine(0)
+
+
+def _silence_cases():
+    nc, src = synth.make_pair(12.0, 1007)
+    z = np.zeros
+    return [src, np.concatenate([z(33_333, np.float32), src, z(7_777, np.float32)]),
+            np.concatenate([z(1000, np.float32), src[:50_000] * np.float32(1e-4), src]),
+            z(40_000, np.float32), src[:1500].copy()]
+
+
+def test_trim_matches_oracle(eng):
+    cases = _silence_cases()
+    got = ops.trim_bounds(eng, cases, 60.0)
+    for y, g in zip(cases, got):
+        assert g == ncref.trim(y, 60.0)[1]
+    y = cases[1]
+    t, lead, trail = nio.strip_silence(y, 22050, 60.0)
+    rt, rlead, rtrail = refglue.strip_silence(y, 22050, 60.0)
+    assert len(t) == len(rt) and lead == rlead and trail == rtrail
+
+
+def test_slice_windows_energies(eng):
+    nc, src = synth.make_pair(40.0, 1008)
+    wins = nio.slice_windows(src, 22050)
+    ref = refglue.slice_windows(src, 22050)
+    assert [w.start_sec for w in wins] == [w.start_sec for w in ref]
+    assert np.max(np.abs(np.array([w.energy_db for w in wins]) - [w.energy_db for w in ref])) < 1e-9
+    assert [w.start_sec for w in nio.energy_gate(wins)] == [w.start_sec for w in refglue.energy_gate(ref)]
+
+
+def test_batch_estimate_tempo_and_logs(eng):
+    nc, src = synth.make_pair(40.0, 1009)
+    wins = nio.slice_windows(nc, 22050)
+    logs = []
+    got = tempo.batch_estimate_tempo(wins, log=logs.append, start_bpm=153.80859375)
+    ref = [refglue.estimate_tempo(w.audio, 22050, 153.80859375) for w in wins]
+    assert got == ref
+    assert logs[-1] == f"    {sum(r is not None for r in ref)}/{len(ref)} windows yielded a confident tempo estimate"
+
+
+def test_estimate_ibis_global_matches_oracle(eng):
+    nc, src = synth.make_pair(35.0, 1010)
+    for y, prior in ((src, 120.0), (nc, 153.80859375)):
+        got = tempo.estimate_ibis_global(y, 22050, start_bpm=prior)
+        ref = refglue.estimate_ibis_global(y, 22050, start_bpm=prior)
+        assert (got is None) == (ref is None)
+        np.testing.assert_array_equal(got, ref)
+
+
+def test_estimate_pitch_chroma_matches_oracle(eng):
+    nc, src = synth.make_pair(70.0, 1011)
+    logs = []
+    s_hz, n_hz, pt, ci, n = pitch.estimate_pitch_chroma(src, nc, 22050, log=logs.append)
+    r = refglue.estimate_pitch_chroma(src, nc, 22050)
+    assert (s_hz, n_hz, pt, ci, n) == r[:5]
+    assert pitch.estimate_pitch_combined(src, nc, 22050)[2] == "chroma_xcorr"
+
+
+@pytest.mark.parametrize("speed", [1.0, 1.01])
+def test_xcorr_speed_matches_oracle(eng, speed):
+    nc, src = synth.make_pair(60.0, 1012)
+    if speed == 1.0:
+        yb = src.copy()
+    else:
+        yb = scipy.signal.resample_poly(src.astype(np.float64), 100, 101).astype(np.float32)
+    g = xcorr.estimate_speed_xcorr_arrays(src, yb)
+    r = refglue.estimate_speed_xcorr_arrays(src, yb)
+    assert abs(g[0] - r[0]) < 1e-9 and abs(g[1] - r[1]) < 1e-5
+    assert xcorr.estimate_speed_xcorr_arrays(np.zeros(500_000, np.float32), yb) == (1.0, 0.0)
+
+
+def test_full_size_pair_properties(eng):
+    """BASELINE config 2 (one 3-min pair): exact window counts and duration ratio,
+    tempo on the expected grid lags (21 / 17), chroma lag +4 on every chunk, IBI ~1.25."""
+    nc, src = synth.make_pair(180.0, 1000)
+    out, = eng.analyze([(nc, src)], E.Params())
+    r, d = out.result, out.detail
+    assert len(d["energy_src"]) == 35 and len(d["energy_nc"]) == 27
+    assert r.src_duration / r.nc_duration == 1.25
+    assert all(t == 2583.984375 / 21 for t in r.src_tempos_raw)
+    assert all(t == 2583.984375 / 17 for t in r.nc_tempos_raw)
+    # 12-bin chroma lags sit near 4 (3.86 st), with near-ties the oracle reproduces
+    ref_lags = [refglue.chunk_lag(src[a:b], nc[c:dd]) for a, b, c, dd in refglue.chunk_plan(len(src), len(nc))]
+    assert d["chunk_lags"] == ref_lags
+    assert abs(r.pitch_ratio - 2 ** (float(np.median(ref_lags)) / 36)) < 1e-12
+    assert r.classification == "time_stretch_only"
+    assert abs(r.ibi_ratio - 1.25) < 0.01
