@@ -35,7 +35,7 @@ extern "C" {
 
 typedef struct nc_ctx nc_ctx;
 
-#define NCGPU_ABI_VERSION 1
+#define NCGPU_ABI_VERSION 2
 
 int nc_abi_version(void);
 const char* nc_last_error(void);
@@ -187,10 +187,13 @@ int nc_ibi_onset(nc_ctx* ctx, const float* sig, const int64_t* file_off, const i
                  int64_t* frame_base_out, void* ws, size_t ws_bytes, void* stream);
 /* part 2 — the tempogram mean (win_length = ac_size*sr/hop, 2756 at hop 64)
  * that beat_track argmaxes (tempo.py:159), streamed instead of materialised:
- * tg_out[f*acw + k]. */
-size_t nc_ibi_tempogram_workspace_bytes(const nc_ctx* ctx, int n_files, int hop);
-int nc_ibi_tempogram(nc_ctx* ctx, const float* onset, const int64_t* frame_base, int n_files, int hop,
-                     double* tg_out, void* ws, size_t ws_bytes, void* stream);
+ * tg_out[f*acw + k].  total_frames = frame_base[n_files]; max_frames = the
+ * largest per-file frame count (sizes the tile grid). */
+size_t nc_ibi_tempogram_workspace_bytes(const nc_ctx* ctx, int n_files, int64_t total_frames, int max_frames,
+                                        int hop);
+int nc_ibi_tempogram(nc_ctx* ctx, const float* onset, const int64_t* frame_base, int n_files,
+                     int64_t total_frames, int max_frames, int hop, double* tg_out, void* ws, size_t ws_bytes,
+                     void* stream);
 
 /* ---------------------------------------------------------------------------
  * K13  windowed waveform cross-correlation — the search loop of

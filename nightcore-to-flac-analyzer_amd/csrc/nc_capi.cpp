@@ -47,8 +47,9 @@ size_t ibi_onset_ws_bytes(int n_files, int64_t total_frames);
 int launch_ibi_onset(Context& ctx, const float* sig, const int64_t* file_off, const int64_t* file_len, int n_files,
                      int64_t total_frames, int hop, float* onset_out, int64_t* frame_base_out, void* ws,
                      size_t ws_bytes, hipStream_t st);
-size_t ibi_tg_ws_bytes(const Context& ctx, int n_files, int acw);
-int launch_ibi_tempogram(Context& ctx, const float* onset, const int64_t* frame_base, int n_files, int hop,
+size_t ibi_tg_ws_bytes(const Context& ctx, int n_files, int64_t total_frames, int max_frames, int hop);
+int launch_ibi_tempogram(Context& ctx, const float* onset, const int64_t* frame_base, int n_files,
+                         int64_t total_frames, int max_frames, int hop,
                          double* tg_out, void* ws, size_t ws_bytes, hipStream_t st);
 
 int launch_xcorr(const float* sig, const int64_t* ia, const int64_t* ib, int n_items, int win, double* dot,
@@ -290,18 +291,19 @@ int nc_ibi_onset(nc_ctx* ctx, const float* sig, const int64_t* file_off, const i
                               frame_base_out, ws, ws_bytes, (hipStream_t)stream);
 }
 
-size_t nc_ibi_tempogram_workspace_bytes(const nc_ctx* ctx, int n_files, int hop) {
+size_t nc_ibi_tempogram_workspace_bytes(const nc_ctx* ctx, int n_files, int64_t total_frames, int max_frames,
+                                        int hop) {
   if (!ctx) return 0;
-  const int acw = hop == 64 ? ctx->c.t.ac64 : ctx->c.t.ac512;
-  return nc::ibi_tg_ws_bytes(ctx->c, n_files, acw);
+  return nc::ibi_tg_ws_bytes(ctx->c, n_files, total_frames, max_frames, hop);
 }
 
-int nc_ibi_tempogram(nc_ctx* ctx, const float* onset, const int64_t* frame_base, int n_files, int hop,
-                     double* tg_out, void* ws, size_t ws_bytes, void* stream) {
+int nc_ibi_tempogram(nc_ctx* ctx, const float* onset, const int64_t* frame_base, int n_files,
+                     int64_t total_frames, int max_frames, int hop, double* tg_out, void* ws, size_t ws_bytes,
+                     void* stream) {
   CHECK_CTX(ctx);
   SET_DEVICE(ctx);
-  return nc::launch_ibi_tempogram(ctx->c, onset, frame_base, n_files, hop, tg_out, ws, ws_bytes,
-                                  (hipStream_t)stream);
+  return nc::launch_ibi_tempogram(ctx->c, onset, frame_base, n_files, total_frames, max_frames, hop, tg_out, ws,
+                                  ws_bytes, (hipStream_t)stream);
 }
 
 int nc_xcorr_search(nc_ctx* ctx, const float* sig, const int64_t* item_a, const int64_t* item_b, int n_items,

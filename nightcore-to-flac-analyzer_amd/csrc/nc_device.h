@@ -134,7 +134,7 @@ struct LdsSize {
 // one wave when NT == 64, a whole workgroup otherwise; SYNC adds the barriers a
 // multi-wave in-place stage needs).  Stage-1 input comes from registers in the
 // layout x[j + r*N/R], j = tid + NT*b.
-template <int N, int R, int NS, int NT, bool SYNC>
+template <int N, int R, int NS, int NT, bool SYNC, int TWN = 8192>
 __device__ __forceinline__ void stockham_stage_regs(float2 (&v)[N / (R * NT)][R], float2* lds,
                                                     const float2* __restrict__ tw, int tid) {
   constexpr int NB = N / (R * NT);
@@ -145,7 +145,7 @@ __device__ __forceinline__ void stockham_stage_regs(float2 (&v)[N / (R * NT)][R]
     const int k = j % NS;
     if (NS > 1) {
 #pragma unroll
-      for (int r = 1; r < R; ++r) v[b][r] = cmul(v[b][r], tw[(k * r * (8192 / (NS * R))) & 8191]);
+      for (int r = 1; r < R; ++r) v[b][r] = cmul(v[b][r], tw[(k * r * (TWN / (NS * R))) & (TWN - 1)]);
     }
     DFT<R>::run(v[b]);
   }
@@ -161,7 +161,7 @@ __device__ __forceinline__ void stockham_stage_regs(float2 (&v)[N / (R * NT)][R]
   if (SYNC) __syncthreads();
 }
 
-template <int N, int R, int NS, int NT, bool SYNC>
+template <int N, int R, int NS, int NT, bool SYNC, int TWN = 8192>
 __device__ __forceinline__ void stockham_stage(float2* lds, const float2* __restrict__ tw, int tid) {
   constexpr int NB = N / (R * NT);
   float2 v[NB][R];
@@ -171,7 +171,7 @@ __device__ __forceinline__ void stockham_stage(float2* lds, const float2* __rest
 #pragma unroll
     for (int r = 0; r < R; ++r) v[b][r] = lds[lpad(j + r * (N / R))];
   }
-  stockham_stage_regs<N, R, NS, NT, SYNC>(v, lds, tw, tid);
+  stockham_stage_regs<N, R, NS, NT, SYNC, TWN>(v, lds, tw, tid);
 }
 
 // Radix plans: 512 = 8.8.8, 1024 = 16.16.4, 2048 = 16.16.8, 4096 = 16.16.16
@@ -198,21 +198,24 @@ struct Plan<4096> {
 template <int N, int NT = 64>
 using FftIn = float2[N / (Plan<N>::R0 * NT)][Plan<N>::R0];
 
-template <int N, int NT, bool SYNC>
+template <int N, int NT, bool SYNC, int TWN = 8192>
 __device__ __forceinline__ void fft_impl(FftIn<N, NT>& in, float2* lds, const float2* __restrict__ tw, int tid) {
   constexpr int R0 = Plan<N>::R0, R1 = Plan<N>::R1, R2 = Plan<N>::R2;
   static_assert(R0 * R1 * R2 == N, "plan");
-  stockham_stage_regs<N, R0, 1, NT, SYNC>(in, lds, tw, tid);
-  stockham_stage<N, R1, R0, NT, SYNC>(lds, tw, tid);
-  stockham_stage<N, R2, R0 * R1, NT, SYNC>(lds, tw, tid);
+  static_assert(TWN >= N, "twiddle table too coarse for this FFT");
+  stockham_stage_regs<N, R0, 1, NT, SYNC, TWN>(in, lds, tw, tid);
+  stockham_stage<N, R1, R0, NT, SYNC, TWN>(lds, tw, tid);
+  stockham_stage<N, R2, R0 * R1, NT, SYNC, TWN>(lds, tw, tid);
 }
 
 // One wave; no barrier needed (LDS ops of a wave complete in order and every
 // stage loads all of its inputs before its first store).  Natural-order output
 // in lds (padded indexing).
-template <int N>
+// TWN is the length of the twiddle table tw[q] = exp(-2 pi i q / TWN): the
+// 8192-entry global table, or a smaller copy staged in LDS.
+template <int N, int TWN = 8192>
 __device__ __forceinline__ void wave_fft(FftIn<N, 64>& in, float2* lds, const float2* __restrict__ tw, int lane) {
-  fft_impl<N, 64, false>(in, lds, tw, lane);
+  fft_impl<N, 64, false, TWN>(in, lds, tw, lane);
 }
 
 // Whole workgroup of NT threads (all must call); output valid after return.
@@ -223,13 +226,14 @@ __device__ __forceinline__ void block_fft(FftIn<N, NT>& in, float2* lds, const f
 
 // Real-FFT split: Z = FFT_N(z), z[n] = x[2n] + i x[2n+1] (x real, length 2N).
 // Returns X[k] and X[N-k] for 0 <= k <= N/2.
+template <int TWN = 8192>
 __device__ __forceinline__ void rfft_split(const float2* lds, const float2* __restrict__ tw, int N, int k,
                                            float2& Xk, float2& XNk) {
   const float2 a = lds[lpad(k & (N - 1))];
   const float2 b = cconj(lds[lpad((N - k) & (N - 1))]);
   const float2 E = cscale(cadd(a, b), 0.5f);
   const float2 O = cmul_mi(cscale(csub(a, b), 0.5f));  // (a-b)/(2i)
-  const float2 W = tw[(k * (8192 / (2 * N))) & 8191];  // exp(-2 pi i k / 2N)
+  const float2 W = tw[(k * (TWN / (2 * N))) & (TWN - 1)];  // exp(-2 pi i k / 2N)
   const float2 WO = cmul(W, O);
   Xk = cadd(E, WO);
   XNk = cconj(csub(E, WO));

@@ -26,11 +26,14 @@ struct Tables {
   float* hann_ac512 = nullptr;  // periodic Hann(344): tempogram window at hop 512
   float* hann_ac64 = nullptr;   // periodic Hann(2756): tempogram window at hop 64
   int ac512 = 0, ac64 = 0;
+  double* wsq512 = nullptr;     // hann_ac512[j]^2 in f64 (lag-0 autocorrelation, the tempogram normaliser)
+  double* wsq64 = nullptr;      // hann_ac64[j]^2 in f64
   // Slaney mel filterbank (sr 22050, n_fft 2048, 128 bands, fmax 11025) in CSR
   int* mel_lo = nullptr;
   int* mel_len = nullptr;
   int* mel_off = nullptr;
   float* mel_w = nullptr;
+  int mel_nnz = 0;
   // CQT: per tuning index, per filter: [lo, len, off] into a complex weight pool
   int* cqt_lo = nullptr;        // [kNTunings][36]
   int* cqt_len = nullptr;

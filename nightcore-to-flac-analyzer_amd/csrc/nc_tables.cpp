@@ -98,6 +98,14 @@ void build_tables(Context& ctx) {
   t.ac64 = (int)((int)(8.0 * kSR) / 64);
   t.hann_ac512 = upload(to_f32(hann_periodic(t.ac512)));
   t.hann_ac64 = upload(to_f32(hann_periodic(t.ac64)));
+  {
+    auto sq = [](std::vector<double> v) {
+      for (double& x : v) x *= x;
+      return v;
+    };
+    t.wsq512 = upload(sq(hann_periodic(t.ac512)));
+    t.wsq64 = upload(sq(hann_periodic(t.ac64)));
+  }
 
   // mel filterbank (oracle/ncref.py mel_filter)
   {
@@ -137,6 +145,7 @@ void build_tables(Context& ctx) {
     t.mel_len = upload(len);
     t.mel_off = upload(offs);
     t.mel_w = upload(wts);
+    t.mel_nnz = (int)wts.size();
   }
 
   // half-band decimator (oracle/ncref.py halfband_taps): 0.5 sinc(n/2) kaiser(n; 11), unit DC
@@ -271,7 +280,7 @@ void build_tables(Context& ctx) {
 
 void free_tables(Context& ctx) {
   Tables& t = ctx.t;
-  void* ptrs[] = {t.tw, t.hann2048, t.hann_ac512, t.hann_ac64, t.mel_lo,  t.mel_len, t.mel_off,
+  void* ptrs[] = {t.tw, t.hann2048, t.hann_ac512, t.hann_ac64, t.wsq512, t.wsq64, t.mel_lo,  t.mel_len, t.mel_off,
                   t.mel_w,  t.cqt_lo,   t.cqt_len,    t.cqt_off,  t.cqt_w,   t.cqt_inv_sqrt_len, t.halfband};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);

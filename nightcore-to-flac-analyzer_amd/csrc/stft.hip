@@ -1,0 +1,192 @@
+// stft.hip — frame-parallel STFT -> power -> Slaney mel -> dB for every frame of
+// a batch of sequences (librosa.feature.melspectrogram + power_to_db inside
+// onset_strength; oracle/ncref.py mel_db).  Shared by the per-window tempo path
+// (hop 512, tempo.py:44 via librosa.onset.onset_strength) and the full-signal
+// IBI pass (hop 64, tempo.py:139).
+//
+// MI355X layout: a workgroup of SM_WAVES waves, one STFT frame per wave (the
+// 2048-point real frame is a 1024-point complex wave FFT, radix 16.16.4 through
+// an 8.7 KB LDS slot).  Workgroups are persistent and walk a CONTIGUOUS range of
+// frames, so the 4x frame overlap (n_fft 2048 / hop 512) is served from the
+// XCD's own L2.  Twiddles (2048 entries), the mel CSR weights and their row
+// descriptors are staged once per workgroup in LDS.  Per frame the kernel writes
+// the 128 dB values, the frame max (the power_to_db top_db clamp needs the
+// sequence max) and, optionally, the f64 energy of the hop-length slice the
+// frame is centred on (the io.slice_windows energy, io.py:38-40, fused into the
+// same HBM read).
+#include <algorithm>
+
+#include "nc_block.h"
+#include "nc_engine.h"
+#include "stft_args.h"
+
+namespace nc {
+
+constexpr int SM_WAVES = 12;
+constexpr int SM_THREADS = SM_WAVES * 64;
+constexpr int SM_TWN = 2048;  // LDS twiddle table exp(-2 pi i q / 2048)
+
+__device__ __forceinline__ int seq_of_frame(const int64_t* base, int n, int64_t g) {
+  int lo = 0, hi = n - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (base[mid] <= g) lo = mid;
+    else hi = mid - 1;
+  }
+  return lo;
+}
+
+__host__ __device__ __forceinline__ int al4(int n) { return (n + 3) & ~3; }
+
+size_t stft_mel_lds_bytes(int mel_nnz) {
+  return SM_TWN * sizeof(float2) + (size_t)al4(mel_nnz) * sizeof(float) + 3 * 128 * sizeof(int) +
+         (size_t)SM_WAVES * LdsSize<1024>::value * sizeof(float2);
+}
+
+__global__ __launch_bounds__(SM_THREADS) void stft_mel_kernel(StftMelArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  float2* sh_tw = reinterpret_cast<float2*>(smem);
+  float* sh_melw = reinterpret_cast<float*>(sh_tw + SM_TWN);
+  int* sh_mel = reinterpret_cast<int*>(sh_melw + al4(a.mel_nnz));  // lo[128] len[128] off[128]
+  const int lane0 = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  float2* fftbuf = reinterpret_cast<float2*>(sh_mel + 3 * 128) + wave * LdsSize<1024>::value;
+
+  for (int i = threadIdx.x; i < SM_TWN; i += SM_THREADS) sh_tw[i] = a.tw[i * (8192 / SM_TWN)];
+  for (int i = threadIdx.x; i < a.mel_nnz; i += SM_THREADS) sh_melw[i] = a.mel_w[i];
+  for (int i = threadIdx.x; i < 128; i += SM_THREADS) {
+    sh_mel[i] = a.mel_lo[i];
+    sh_mel[128 + i] = a.mel_len[i];
+    sh_mel[256 + i] = a.mel_off[i];
+  }
+  __syncthreads();
+  // lane l owns bands l and 127 - l (short low band + long high band)
+
+  const int64_t n_groups = (a.total_frames + SM_WAVES - 1) / SM_WAVES;
+  const int64_t gb = n_groups * blockIdx.x / gridDim.x, ge = n_groups * (blockIdx.x + 1) / gridDim.x;
+  for (int64_t grp = gb; grp < ge; ++grp) {
+    const int64_t g = grp * SM_WAVES + wave;
+    if (g >= a.total_frames) break;
+    int s;
+    int64_t t, L;
+    if (a.frame_base) {
+      s = seq_of_frame(a.frame_base, a.n_seq, g);
+      t = g - a.frame_base[s];
+    } else {
+      s = (int)(g / a.uniform_T);
+      t = g - (int64_t)s * a.uniform_T;
+    }
+    if (a.active && !a.active[s]) continue;
+    L = a.seq_len ? a.seq_len[s] : a.uniform_len;
+    const int64_t off = a.seq_off[s];
+    const float* x = a.sig + off;
+    const int64_t s0 = t * a.hop - 1024;
+
+    // Opaque lane id: every per-lane address and table load is recomputed each
+    // frame instead of being hoisted out of the loop (~140 extra VGPRs, which
+    // would cap occupancy at 2 waves/SIMD).
+    int lane = lane0;
+    asm volatile("" : "+v"(lane));
+    const float2* twl = sh_tw;
+    const float* hann = a.hann2048;
+    FftIn<1024> in;
+    double e = 0.0;
+    const bool interior = s0 >= 0 && s0 + 2048 <= L && ((off & 1) == 0);
+    if (interior) {
+      const float2* x2 = reinterpret_cast<const float2*>(x + s0);
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int n = lane + 64 * r;
+        const float2 v = x2[n];
+        const float2 h = reinterpret_cast<const float2*>(hann)[n];
+        if (r >= 8 && r < 12) {
+          const int q = 2 * n - 1024;
+          if (q < a.hop) {
+            e = fma((double)v.x, (double)v.x, e);
+            e = fma((double)v.y, (double)v.y, e);
+          }
+        }
+        in[0][r] = make_float2(v.x * h.x, v.y * h.y);
+      }
+    } else {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int n = lane + 64 * r;
+        const int64_t i0 = s0 + 2 * n;
+        const float x0 = (i0 >= 0 && i0 < L) ? x[i0] : 0.0f;
+        const float x1 = (i0 + 1 >= 0 && i0 + 1 < L) ? x[i0 + 1] : 0.0f;
+        if (r >= 8 && r < 12) {
+          const int q = 2 * n - 1024;
+          if (q < a.hop) {
+            e = fma((double)x0, (double)x0, e);
+            e = fma((double)x1, (double)x1, e);
+          }
+        }
+        in[0][r] = make_float2(x0 * hann[2 * n], x1 * hann[2 * n + 1]);
+      }
+    }
+    if (a.frame_energy) {
+      e = wave_sum(e);
+      if (lane == 0) a.frame_energy[g] = e;
+    }
+    wave_fft<1024, SM_TWN>(in, fftbuf, twl, lane);
+    float p1[9], p2[9];
+#pragma unroll
+    for (int m = 0; m < 9; ++m) {
+      const int k = lane + 64 * m;
+      if (k <= 512) {
+        float2 X, XN;
+        rfft_split<SM_TWN>(fftbuf, twl, 1024, k, X, XN);
+        p1[m] = fmaf(X.x, X.x, X.y * X.y);
+        p2[m] = fmaf(XN.x, XN.x, XN.y * XN.y);
+      }
+    }
+    float* pw = reinterpret_cast<float*>(fftbuf);
+#pragma unroll
+    for (int m = 0; m < 9; ++m) {
+      const int k = lane + 64 * m;
+      if (k <= 512) {
+        pw[k] = p1[m];
+        pw[1024 - k] = p2[m];
+      }
+    }
+    // lane l owns bands l and 127 - l (short low band + long high band)
+    const int lo0 = sh_mel[lane], len0 = sh_mel[128 + lane], off0 = sh_mel[256 + lane];
+    const int lo1 = sh_mel[127 - lane], len1 = sh_mel[255 - lane], off1 = sh_mel[383 - lane];
+    float acc0 = 0.0f, acc1 = 0.0f;
+#pragma unroll 4
+    for (int j = 0; j < len0; ++j) acc0 = fmaf(sh_melw[off0 + j], pw[lo0 + j], acc0);
+#pragma unroll 4
+    for (int j = 0; j < len1; ++j) acc1 = fmaf(sh_melw[off1 + j], pw[lo1 + j], acc1);
+    const float db0 = 10.0f * log10f(fmaxf(1e-10f, acc0));
+    const float db1 = 10.0f * log10f(fmaxf(1e-10f, acc1));
+    float* row = a.sdb + g * 128;
+    row[lane] = db0;
+    row[127 - lane] = db1;
+    const float mx = wave_max(fmaxf(db0, db1));
+    if (lane == 0) a.frame_max[g] = mx;
+  }
+}
+
+int launch_stft_mel(Context& ctx, const StftMelArgs& args, hipStream_t st) {
+  if (args.total_frames <= 0) return 0;
+  StftMelArgs a = args;
+  a.tw = ctx.t.tw;
+  a.hann2048 = ctx.t.hann2048;
+  a.mel_lo = ctx.t.mel_lo;
+  a.mel_len = ctx.t.mel_len;
+  a.mel_off = ctx.t.mel_off;
+  a.mel_w = ctx.t.mel_w;
+  a.mel_nnz = ctx.t.mel_nnz;
+  if (a.hop <= 0 || a.hop > 512 || (a.hop & 1)) {
+    set_error("stft_mel: hop must be even and <= 512");
+    return -2;
+  }
+  const size_t lds = stft_mel_lds_bytes(a.mel_nnz);
+  const int64_t n_groups = (a.total_frames + SM_WAVES - 1) / SM_WAVES;
+  const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(n_groups, (int64_t)ctx.num_cu * (lds <= 80 * 1024 ? 2 : 1)));
+  hipLaunchKernelGGL(stft_mel_kernel, dim3(grid), dim3(SM_THREADS), lds, st, a);
+  NC_HIP(hipGetLastError());
+  return 0;
+}
+
+}  // namespace nc

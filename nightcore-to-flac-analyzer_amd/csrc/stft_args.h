@@ -1,0 +1,35 @@
+// stft_args.h — argument block of stft_mel_kernel (stft.hip), shared with its callers.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace nc {
+
+struct Context;
+
+struct StftMelArgs {
+  const float* sig;
+  const int64_t* seq_off;     // [n_seq] sample offsets into sig
+  const int64_t* seq_len;     // [n_seq] or nullptr: every sequence is uniform_len long
+  const int64_t* frame_base;  // [n_seq + 1] or nullptr: every sequence has uniform_T frames
+  int64_t uniform_len;
+  int uniform_T;
+  int n_seq;
+  int64_t total_frames;
+  const uint8_t* active;  // nullable: frames of sequences with active[s] == 0 are skipped
+  int hop;
+  float* sdb;             // [total_frames][128]
+  float* frame_max;       // [total_frames]
+  double* frame_energy;   // nullable [total_frames]: sum x^2 over [t hop, (t+1) hop) of the sequence
+  const float2* tw;       // global 8192-entry table
+  const float* hann2048;
+  const int* mel_lo;
+  const int* mel_len;
+  const int* mel_off;
+  const float* mel_w;
+  int mel_nnz;
+};
+
+int launch_stft_mel(Context& ctx, const StftMelArgs& args, hipStream_t st);
+
+}  // namespace nc

@@ -51,8 +51,8 @@ SIGNATURES = {
                                  SZ, P]),
     "nc_ibi_onset_workspace_bytes": (SZ, [P, I32, I64]),
     "nc_ibi_onset": (I32, [P, P, P, P, I32, I64, I32, P, P, P, SZ, P]),
-    "nc_ibi_tempogram_workspace_bytes": (SZ, [P, I32, I32]),
-    "nc_ibi_tempogram": (I32, [P, P, P, I32, I32, P, P, SZ, P]),
+    "nc_ibi_tempogram_workspace_bytes": (SZ, [P, I32, I64, I32, I32]),
+    "nc_ibi_tempogram": (I32, [P, P, P, I32, I64, I32, I32, P, P, SZ, P]),
     "nc_xcorr_search": (I32, [P, P, P, P, I32, I32, P, P, P, P, P, P, P, P, P, P, I32, P, P, P]),
 }
 

@@ -503,10 +503,11 @@ class Engine:
                   onset.data_ptr(), fbase.data_ptr(), ws.data_ptr(), ws.numel(), st)
         acw = int(int(8.0 * SR) // hop)
         tg = torch.empty(nF * acw, dtype=torch.float64, device=dev)
-        wsb = self.ctx.lib.nc_ibi_tempogram_workspace_bytes(self.ctx.h, nF, hop)
+        fmax = int(frames.max())
+        wsb = self.ctx.lib.nc_ibi_tempogram_workspace_bytes(self.ctx.h, nF, total, fmax, hop)
         ws = self.workspace("ibi_tg", wsb)
-        self.call("nc_ibi_tempogram", onset.data_ptr(), fbase.data_ptr(), nF, hop, tg.data_ptr(), ws.data_ptr(),
-                  ws.numel(), st)
+        self.call("nc_ibi_tempogram", onset.data_ptr(), fbase.data_ptr(), nF, total, fmax, hop, tg.data_ptr(),
+                  ws.data_ptr(), ws.numel(), st)
         lens = torch.tensor(frames, dtype=torch.int32, device=dev)
         bpm = torch.zeros(nF, dtype=torch.float64, device=dev)
         lag = torch.zeros(nF, dtype=torch.int32, device=dev)

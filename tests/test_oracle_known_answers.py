@@ -79,3 +79,45 @@ def test_mel_filterbank_slaney_properties():
     assert W.shape == (128, 1025) and W.dtype == np.float32
     # each FFT bin contributes to at most two adjacent bands; every band is non-empty
     assert (np.count_nonzero(W, axis=0) <= 2).all() and (np.count_nonzero(W, axis=1) > 0).all()
+
+
+def _sliding_tempogram_mean(o, N):
+    """The engine's tempogram algorithm (csrc/nc_slide.h) in numpy: five sliding
+    f64 sums per lag instead of one FFT autocorrelation per frame."""
+    T, p = len(o), N // 2
+    x = np.pad(o, (p, p), mode="linear_ramp", end_values=(0, 0)).astype(np.float64)
+    w2 = ncref.hann(N).astype(np.float64) ** 2
+    ac0 = np.array([np.dot(w2, x[t:t + N] ** 2) for t in range(T)])
+    rinv = np.where(ac0 < np.finfo(np.float64).tiny, 1.0, 1.0 / np.where(ac0 == 0, 1, ac0))
+    th = 2 * np.pi / N
+    k = np.arange(N)
+    L = N - k
+    c, s = np.cos(th * k), np.sin(th * k)
+    A, B, C, D, E = 0.25 + 0.125 * c, -0.25 - 0.25 * c, 0.25 * s, 0.125 * c, -0.125 * s
+    j = np.arange(N)[:, None]
+    P = x[j] * x[np.minimum(j + k[None, :], len(x) - 1)] * (j < L[None, :])   # p_k[j], masked to j < L
+    S0 = P.sum(0)
+    Z1 = (np.exp(1j * th * j) * P).sum(0)
+    Z2 = (np.exp(2j * th * j) * P).sum(0)
+    e1L, e2L = np.exp(-1j * th * k), np.exp(-2j * th * k)
+    acc = np.zeros(N)
+    for t in range(T):
+        ac = A * S0 + B * Z1.real + C * Z1.imag + D * Z2.real + E * Z2.imag
+        acc += ac * rinv[t]
+        pt = x[t] * x[t + k]
+        pl = x[t + L] * x[t + N]
+        S0 = S0 - pt + pl
+        Z1 = np.exp(-1j * th) * (Z1 - pt + e1L * pl)
+        Z2 = np.exp(-2j * th) * (Z2 - pt + e2L * pl)
+    return acc / T
+
+
+@pytest.mark.parametrize("seed", [0, 1])
+def test_sliding_tempogram_identity_matches_fft_autocorrelation(seed):
+    """w[j]w[j+k] is a degree-2 trigonometric polynomial in j, so the Hann-windowed
+    autocorrelation slides in O(1) per frame; agreement is at f64 rounding level."""
+    rng = np.random.default_rng(seed)
+    o = (rng.random(431) * (rng.random(431) > 0.6)).astype(np.float32)
+    ref = ncref.tempogram_mean(o, 344)
+    got = _sliding_tempogram_mean(o, 344)
+    assert np.max(np.abs(got - ref)) < 1e-12
