@@ -47,6 +47,22 @@ def make_pairs(n, seconds, base_seed, workers):
         return list(ex.map(_gen, [(seconds, base_seed + i) for i in range(n)]))
 
 
+def _pmc_traffic(kernel_tag):
+    """HBM bytes per launch of the dominant kernel from the committed rocprofv3 PMC pass
+    (profiles/*_traffic.json, FETCH_SIZE x 2 + WRITE_SIZE per MI355X_MICROARCH.md), if one
+    exists for this workload; counters cannot be read from inside a timed run."""
+    best = None
+    for f in sorted((REPO / "profiles").glob("*_traffic.json")):
+        try:
+            d = json.loads(f.read_text())
+        except ValueError:
+            continue
+        k = d.get("kernels", {}).get(kernel_tag)
+        if k and d.get("workload") == "config3-64pairs":
+            best = {"bytes_per_launch": k["hbm_bytes_per_launch"], "source": f"profiles/{f.name}"}
+    return best
+
+
 def cpu_baseline(nc, src):
     """The oracle (oracle/refglue.py, a CPU port of the reference glue on the
     numpy restatement of librosa) on ONE pair of the batch, single thread."""
@@ -120,17 +136,25 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
 
-    # per-kernel timing with HIP events on the launch stream (separate, non-timed steps)
+    # per-kernel timing with HIP events on the launch stream (separate, non-timed steps): entry points
+    # (engine) and, inside them, the dominant kernels (libncgpu nc_profile_*, same stream)
     eng.start_timers()
+    eng.kernel_profile(True)
     ksteps = max(1, min(args.steps, 3))
     for _ in range(ksteps):
         eng.analyze(signals=signals, params=params)
     timers = eng.stop_timers()
+    ktimes = eng.kernel_times()
+    eng.kernel_profile(False)
     per = {k: (ms / n, n // ksteps) for k, (ms, n) in timers.items()}
-    alg = {"nc_window_stage": win_per_step * WIN_BYTES, "nc_chroma_mean": chunks_per_step * CHUNK_BYTES}
-    dom = max(alg, key=lambda k: per.get(k, (0, 0))[0])
-    avg_ms = per[dom][0]
-    achieved = alg[dom] / (avg_ms * 1e-3) / 1e9
+    kper = {k: (ms / n, n / ksteps) for k, (ms, n) in ktimes.items()}
+    # algorithmic bytes per launch = SURVEY.md §8d per-unit bytes x units per launch
+    units = {"stft_mel": (win_per_step, WIN_BYTES), "cqt_chroma": (chunks_per_step, CHUNK_BYTES)}
+    dom = max(units, key=lambda k: kper.get(k, (0, 0))[0] * kper.get(k, (0, 0))[1])
+    avg_ms, launches = kper[dom]
+    alg_per_launch = units[dom][0] / launches * units[dom][1]
+    achieved = alg_per_launch / (avg_ms * 1e-3) / 1e9
+    traffic = _pmc_traffic(dom)
     step_ms = el / args.steps * 1e3
 
     ibi = None
@@ -169,9 +193,13 @@ def main():
                        "pairs_per_gpu": args.pairs, "windows_per_gpu_step": win_per_step,
                        "cqt_chunks_per_gpu_step": chunks_per_step, "parallelism": f"dp{world} (pairs sharded)"},
             "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS,
-                         "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-                         "alg_bytes_per_launch": alg[dom], "avg_launch_ms": avg_ms},
-            "kernels_ms_per_step": {k: round(v[0] * v[1], 4) for k, v in per.items()},
+                         "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
+                         "traffic": traffic["bytes_per_launch"] if traffic else None,
+                         "traffic_source": traffic["source"] if traffic else None,
+                         "alg_bytes_per_launch": alg_per_launch, "avg_launch_ms": avg_ms,
+                         "launches_per_step": launches},
+            "kernels_ms_per_step": {k: round(v[0] * v[1], 4) for k, v in kper.items()},
+            "entry_points_ms_per_step": {k: round(v[0] * v[1], 4) for k, v in per.items()},
             "check": {"tempo_ratio_pair0": tr, "pitch_ratio_pair0": pr},
         }
         if ibi is not None:

@@ -48,6 +48,15 @@ int nc_destroy(nc_ctx* ctx);
 /* number of compute units seen by the context (256 on MI355X) */
 int nc_num_cu(const nc_ctx* ctx);
 
+/* Opt-in per-kernel timing (no reference equivalent; measurement only).  While
+ * enabled, the dominant kernels are bracketed by HIP events on their stream;
+ * nc_profile_read(tag) waits for the recorded launches, returns their summed
+ * duration and count, and resets the tag.  Tags: "stft_mel", "window_tg",
+ * "tuning_peaks", "decimate", "cqt_chroma", "trim_blocks", "tempo_beat",
+ * "tg_slide".  Enabling (or disabling) discards pending records. */
+int nc_profile_enable(nc_ctx* ctx, int on);
+int nc_profile_read(nc_ctx* ctx, const char* tag, double* total_ms, int* launches);
+
 /* ---------------------------------------------------------------------------
  * K1a  silence trim — replaces io.strip_silence (io.py:58-79) ->
  *      librosa.effects.trim(y, top_db) (io.py:76).

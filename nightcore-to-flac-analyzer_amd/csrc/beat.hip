@@ -422,7 +422,10 @@ int launch_tempo_beats(Context& ctx, BeatArgs a, int n_seq, int max_len, hipStre
   const size_t tab = al16((size_t)a.tab_cap * sizeof(double));
   const size_t small_lds = tab + (size_t)max_len * (8 + 8 + 4 + 1) + 16;
   if (small_lds <= 64 * 1024) {
-    hipLaunchKernelGGL((tempo_beat_kernel<256, true>), dim3(n_seq), dim3(256), small_lds, st, a);
+    {
+      KTimer kt_(ctx, "tempo_beat", st);
+      hipLaunchKernelGGL((tempo_beat_kernel<256, true>), dim3(n_seq), dim3(256), small_lds, st, a);
+    }
   } else {
     if (!a.ws_ls || !a.ws_cum || !a.ws_back || !a.ws_marks) {
       set_error("tempo_beats: long sequences need the global workspace");
@@ -432,7 +435,10 @@ int launch_tempo_beats(Context& ctx, BeatArgs a, int n_seq, int max_len, hipStre
       set_error("tempo_beats: tempogram window too long");
       return -2;
     }
-    hipLaunchKernelGGL((tempo_beat_kernel<1024, false>), dim3(n_seq), dim3(1024), tab, st, a);
+    {
+      KTimer kt_(ctx, "tempo_beat", st);
+      hipLaunchKernelGGL((tempo_beat_kernel<1024, false>), dim3(n_seq), dim3(1024), tab, st, a);
+    }
   }
   NC_HIP(hipGetLastError());
   return 0;

@@ -9,10 +9,10 @@
 //
 // Pipeline per chunk (one launch each, all chunks of the batch at once):
 //   1. decimate_kernel x6     y_{i+1} = sqrt(2) * halfband(y_i)[::2]  (soxr_hq replacement)
-//   2. tuning_peaks_kernel    STFT 2048/512 (Hann) -> piptrack peaks per frame (fixed slots)
+//   2. tuning_peaks_kernel    STFT 2048/512 (Hann) -> piptrack peaks, appended per chunk
 //   3. tuning_select_kernel   median(mag) -> residual histogram (0.01 bins) -> tuning index
-//   4. cqt_chroma_kernel      7 waves = 7 octaves of one frame: rect-window FFT 1024 ->
-//                             sparse basis[tuning] -> |C|/sqrt(len) -> 12-bin chroma ->
+//   4. cqt_chroma_kernel      (frame, octave) items per wave: rect-window FFT 1024 ->
+//                             sparse basis[tuning] (LDS) -> |C|/sqrt(len) -> 12-bin chroma ->
 //                             inf-norm -> per-block partial sums (f64)
 //   5. chroma_finalize_kernel mean over frames -> f32[12] per chunk
 //   6. chroma_lag_kernel      argmax_k dot(src, roll(nc, -k)), wrapped to [-5, 6]
@@ -68,28 +68,57 @@ __global__ void chroma_plan_kernel(const int64_t* chunk_len, int n, int64_t* oct
 }
 
 // ------------------------------------------------------------------------------ 1. decimation
+// out[m] = sqrt(2) * sum_{j=0}^{2K} h[j] in[2m - (j - K)]  (zero outside), accumulated in f64
+// in the oracle's order (ascending j, separate multiply and add: oracle/ncref.py decimate2).
+// One workgroup per DEC_OUT outputs; the 2 DEC_OUT + 2K input tile is staged in LDS and the
+// taps are wave-uniform (scalar loads); the zero taps of the half-band (even j - K != 0) are
+// skipped at compile time.
+constexpr int DEC_OUT = 1024;
+
 __global__ __launch_bounds__(256) void decimate_kernel(const float* sig, const int64_t* chunk_off,
                                                        const int64_t* oct_off, const int64_t* oct_len,
-                                                       float* ws_oct, int level, const double* taps,
-                                                       int K, int64_t max_out) {
+                                                       float* ws_oct, int level, const double* __restrict__ taps) {
+#pragma clang fp contract(off)
+  constexpr int K = kHalfbandK;
+  __shared__ float tile[2 * DEC_OUT + 2 * K + 1];
   const int c = blockIdx.y;
-  const int64_t m = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  const int64_t Lin = oct_len[c * 7 + level];
-  const int64_t Lout = oct_len[c * 7 + level + 1];
-  if (m >= Lout) return;
+  const int64_t Lin = oct_len[c * 7 + level], Lout = oct_len[c * 7 + level + 1];
+  const int64_t m0 = (int64_t)blockIdx.x * DEC_OUT;
+  if (m0 >= Lout) return;
   const float* in = level == 0 ? sig + chunk_off[c] : ws_oct + oct_off[c * 7 + level];
   float* out = ws_oct + oct_off[c * 7 + level + 1];
-  double acc = 0.0;
-  for (int j = 0; j <= 2 * K; ++j) {
-    const double h = taps[j];
-    if (h == 0.0) continue;
-    const int64_t i = 2 * m - (j - K);
-    if (i >= 0 && i < Lin) acc += h * (double)in[i];
+  const int64_t i0 = 2 * m0 - K;  // tile[u] = in[i0 + u]
+  for (int u = threadIdx.x; u < 2 * DEC_OUT + 2 * K + 1; u += 256) {
+    const int64_t i = i0 + u;
+    tile[u] = (i >= 0 && i < Lin) ? in[i] : 0.0f;
   }
-  out[m] = (float)(acc * 1.4142135623730951);
+  __syncthreads();
+#pragma unroll
+  for (int q = 0; q < DEC_OUT / 256; ++q) {
+    const int loc = threadIdx.x + 256 * q;
+    const int64_t m = m0 + loc;
+    if (m >= Lout) break;
+    const float* x = tile + 2 * loc + 2 * K;  // x[-j] = in[2m - (j - K)]
+    double acc = 0.0;
+#pragma unroll
+    for (int j = 0; j <= 2 * K; ++j) {
+      if (((j - K) & 1) == 0 && j != K) continue;
+      acc = acc + taps[j] * (double)x[-j];
+    }
+    out[m] = (float)(acc * 1.4142135623730951);
+  }
 }
 
 // ------------------------------------------------------------------------------ 2. tuning peaks
+// piptrack(y=chunk, sr, n_fft 2048, hop 512, fmin 150, fmax 4000, threshold 0.1) inside
+// estimate_tuning.  Persistent workgroups of TP_WAVES waves walk contiguous tuning frames
+// (one frame per wave, the stft_mel structure: LDS twiddles, laundered lane id).  The
+// peaks of a frame are appended to its chunk's region (peak_*[tf_base[c] * kPeakSlots ..])
+// at an atomically reserved position: the median and the histogram that consume them
+// do not depend on the order, so the result stays deterministic.
+constexpr int TP_WAVES = 14;
+using TpTw = StagedTw<1024>;
+
 struct PeakArgs {
   const float* sig;
   const int64_t* chunk_off;
@@ -97,98 +126,132 @@ struct PeakArgs {
   const int* n_tframes;
   const int64_t* tf_base;
   int n_chunks;
-  int64_t total_tframes;
+  int64_t total_tframes;  // upper bound of tf_base[n]
   const float2* tw;
   const float* hann2048;
-  float* peak_pitch;  // [total_tframes][kPeakSlots]
+  float* peak_pitch;      // chunk c region starts at tf_base[c] * kPeakSlots
   float* peak_mag;
-  int* peak_cnt;      // [total_tframes]
+  int* chunk_npk;         // [n] zeroed by the launcher
 };
 
-__global__ __launch_bounds__(256) void tuning_peaks_kernel(PeakArgs a) {
+__global__ __launch_bounds__(TP_WAVES * 64) void tuning_peaks_kernel(PeakArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  float2* fftbuf = reinterpret_cast<float2*>(smem) + wave * LdsSize<1024>::value;
-  const int64_t gf = (int64_t)blockIdx.x * 4 + wave;
-  if (gf >= a.total_tframes) return;
-  int lo = 0, hi = a.n_chunks - 1;
-  while (lo < hi) {
-    const int mid = (lo + hi + 1) >> 1;
-    if (a.tf_base[mid] <= gf) lo = mid;
-    else hi = mid - 1;
-  }
-  const int c = lo;
-  const int t = (int)(gf - a.tf_base[c]);
-  if (t >= a.n_tframes[c]) return;
-  const float* x = a.sig + a.chunk_off[c];
-  const int64_t L = a.chunk_len[c];
-  const int64_t s0 = (int64_t)t * 512 - 1024;
-  FftIn<1024> in;
-#pragma unroll
-  for (int r = 0; r < 16; ++r) {
-    const int n = lane + 64 * r;
-    const int64_t i0 = s0 + 2 * n;
-    const float x0 = (i0 >= 0 && i0 < L) ? x[i0] : 0.0f;
-    const float x1 = (i0 + 1 >= 0 && i0 + 1 < L) ? x[i0 + 1] : 0.0f;
-    in[0][r] = make_float2(x0 * a.hann2048[2 * n], x1 * a.hann2048[2 * n + 1]);
-  }
-  wave_fft<1024>(in, fftbuf, a.tw, lane);
-  float m1[9], m2[9];
-#pragma unroll
-  for (int m = 0; m < 9; ++m) {
-    const int k = lane + 64 * m;
-    if (k <= 512) {
-      float2 X, XN;
-      rfft_split(fftbuf, a.tw, 1024, k, X, XN);
-      m1[m] = hypotf(X.x, X.y);
-      m2[m] = hypotf(XN.x, XN.y);
+  float2* sh_tw = reinterpret_cast<float2*>(smem);
+  const int lane0 = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  float2* fftbuf = sh_tw + ((TpTw::size + 1) & ~1) + wave * LdsSize<1024>::value;
+  fill_staged_tw<1024>(sh_tw, a.tw, threadIdx.x, TP_WAVES * 64);
+  __syncthreads();
+  const int64_t n_groups = (a.total_tframes + TP_WAVES - 1) / TP_WAVES;
+  const int64_t gb = n_groups * blockIdx.x / gridDim.x, ge = n_groups * (blockIdx.x + 1) / gridDim.x;
+  for (int64_t grp = gb; grp < ge; ++grp) {
+    const int64_t gf = grp * TP_WAVES + wave;
+    if (gf >= a.total_tframes) break;
+    int lo = 0, hi = a.n_chunks - 1;
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (a.tf_base[mid] <= gf) lo = mid;
+      else hi = mid - 1;
     }
-  }
-  float* S = reinterpret_cast<float*>(fftbuf);
+    const int c = lo;
+    const int t = (int)(gf - a.tf_base[c]);
+    if (t >= a.n_tframes[c]) continue;
+    int lane = lane0;
+    asm volatile("" : "+v"(lane));
+    const int64_t off = a.chunk_off[c];
+    const float* x = a.sig + off;
+    const int64_t L = a.chunk_len[c];
+    const int64_t s0 = (int64_t)t * 512 - 1024;
+    FftIn<1024> in;
+    if (s0 >= 0 && s0 + 2048 <= L && ((off & 1) == 0)) {
+      const float2* x2 = reinterpret_cast<const float2*>(x + s0);
+      const float2* h2 = reinterpret_cast<const float2*>(a.hann2048);
 #pragma unroll
-  for (int m = 0; m < 9; ++m) {
-    const int k = lane + 64 * m;
-    if (k <= 512) {
-      S[k] = m1[m];
-      S[1024 - k] = m2[m];
-    }
-  }
-  // frame max over all 1025 bins
-  float mx = 0.0f;
-  for (int k = lane; k <= 1024; k += 64) mx = fmaxf(mx, S[k]);
-  mx = wave_max(mx);
-  const float ref = 0.1f * mx;
-  // bins inside [150, 4000) Hz: k*22050/2048 -> 14..371
-  const int klo = 14, khi = 371;
-  int base = 0;
-  for (int k0 = klo; k0 <= khi; k0 += 64) {
-    const int k = k0 + lane;
-    bool pk = false;
-    float pitch = 0.0f, mag = 0.0f;
-    if (k <= khi) {
-      const float sm = S[k - 1], s = S[k], sp = S[k + 1];
-      const float zm = sm > ref ? sm : 0.0f, z = s > ref ? s : 0.0f, zp = sp > ref ? sp : 0.0f;
-      pk = (z > zm) && (z >= zp);
-      if (pk) {
-        // parabolic shift (librosa numba stencil, f64 arithmetic, stored f32)
-        const double aa = (double)(sp + sm) - 2.0 * (double)s;  // f32 add, then f64 (numba typing)
-        const double bb = (double)(sp - sm) / 2.0;
-        const float shift = (fabs(bb) >= fabs(aa)) ? 0.0f : (float)(-bb / aa);
-        const float avg = (sp - sm) / 2.0f;
-        const float dskew = (0.5f * avg) * shift;
-        pitch = (float)((((double)k + (double)shift) * 22050.0) / 2048.0);
-        mag = s + dskew;
+      for (int r = 0; r < 16; ++r) {
+        const int n = lane + 64 * r;
+        const float2 v = x2[n], h = h2[n];
+        in[0][r] = make_float2(v.x * h.x, v.y * h.y);
+      }
+    } else {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int n = lane + 64 * r;
+        const int64_t i0 = s0 + 2 * n;
+        const float x0 = (i0 >= 0 && i0 < L) ? x[i0] : 0.0f;
+        const float x1 = (i0 + 1 >= 0 && i0 + 1 < L) ? x[i0 + 1] : 0.0f;
+        in[0][r] = make_float2(x0 * a.hann2048[2 * n], x1 * a.hann2048[2 * n + 1]);
       }
     }
-    const unsigned long long bal = __ballot(pk);
-    const int rank = __popcll(bal & ((1ull << lane) - 1ull));
-    if (pk && base + rank < kPeakSlots) {
-      a.peak_pitch[gf * kPeakSlots + base + rank] = pitch;
-      a.peak_mag[gf * kPeakSlots + base + rank] = mag;
+    wave_fft<1024, 0>(in, fftbuf, sh_tw, lane);
+    float m1[9], m2[9];
+#pragma unroll
+    for (int m = 0; m < 9; ++m) {
+      const int k = lane + 64 * m;
+      if (k <= 512) {
+        float2 X, XN;
+        rfft_split<0, TpTw::split>(fftbuf, sh_tw, 1024, k, X, XN);
+        m1[m] = hypotf(X.x, X.y);
+        m2[m] = hypotf(XN.x, XN.y);
+      }
     }
-    base += __popcll(bal);
+    float* S = reinterpret_cast<float*>(fftbuf);
+    float mx = 0.0f;
+#pragma unroll
+    for (int m = 0; m < 9; ++m) {
+      const int k = lane + 64 * m;
+      if (k <= 512) {
+        S[k] = m1[m];
+        S[1024 - k] = m2[m];
+        mx = fmaxf(mx, fmaxf(m1[m], m2[m]));
+      }
+    }
+    mx = wave_max(mx);
+    const float ref = 0.1f * mx;
+    // bins inside [150, 4000) Hz: k * 22050 / 2048 -> 14..371 (6 rounds of 64 lanes)
+    constexpr int klo = 14, khi = 371, NR = (khi - klo + 64) / 64;
+    float pitch[NR], mag[NR];
+    unsigned long long bal[NR];
+    int cnt = 0;
+#pragma unroll
+    for (int q = 0; q < NR; ++q) {
+      const int k = klo + 64 * q + lane;
+      bool pk = false;
+      pitch[q] = 0.0f;
+      mag[q] = 0.0f;
+      if (k <= khi) {
+        const float sm = S[k - 1], s = S[k], sp = S[k + 1];
+        const float zm = sm > ref ? sm : 0.0f, z = s > ref ? s : 0.0f, zp = sp > ref ? sp : 0.0f;
+        pk = (z > zm) && (z >= zp);
+        if (pk) {
+          // parabolic shift (librosa numba stencil, f64 arithmetic, stored f32)
+          const double aa = (double)(sp + sm) - 2.0 * (double)s;  // f32 add, then f64 (numba typing)
+          const double bb = (double)(sp - sm) / 2.0;
+          const float shift = (fabs(bb) >= fabs(aa)) ? 0.0f : (float)(-bb / aa);
+          const float avg = (sp - sm) / 2.0f;
+          const float dskew = (0.5f * avg) * shift;
+          pitch[q] = (float)((((double)k + (double)shift) * 22050.0) / 2048.0);
+          mag[q] = s + dskew;
+        }
+      }
+      bal[q] = __ballot(pk);
+      cnt += __popcll(bal[q]);
+    }
+    if (cnt == 0) continue;
+    int pos = 0;
+    if (lane == 0) pos = atomicAdd(&a.chunk_npk[c], cnt);
+    pos = __shfl(pos, 0, 64);
+    float* pp = a.peak_pitch + a.tf_base[c] * kPeakSlots;
+    float* pm = a.peak_mag + a.tf_base[c] * kPeakSlots;
+    const unsigned long long below = (1ull << lane) - 1ull;
+#pragma unroll
+    for (int q = 0; q < NR; ++q) {
+      if ((bal[q] >> lane) & 1ull) {
+        const int i = pos + __popcll(bal[q] & below);
+        pp[i] = pitch[q];
+        pm[i] = mag[q];
+      }
+      pos += __popcll(bal[q]);
+    }
   }
-  if (lane == 0) a.peak_cnt[gf] = min(base, kPeakSlots);
 }
 
 // ------------------------------------------------------------------------------ 3. tuning select
@@ -203,86 +266,111 @@ __device__ __forceinline__ int tuning_bin(float r) {
   return j;
 }
 
+__device__ __forceinline__ unsigned fkey(float f) {
+  const unsigned u = __float_as_uint(f);
+  return (u >> 31) ? ~u : (u | 0x80000000u);
+}
+__device__ __forceinline__ float funkey(unsigned k) {
+  return __uint_as_float((k >> 31) ? (k & 0x7fffffffu) : ~k);
+}
+
+__device__ __forceinline__ int wave_incl_scan_i(int v) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int u = __shfl_up(v, o, 64);
+    if (lane >= o) v += u;
+  }
+  return v;
+}
+
+// One workgroup per chunk: median of the peak magnitudes (4-pass 8-bit radix select over
+// the chunk's compact peak list, plus one pass for the upper middle of an even count),
+// then the 100-bin residual histogram and its first argmax (librosa estimate_tuning /
+// pitch_tuning, oracle/ncref.py).
 template <int NT>
 __global__ __launch_bounds__(NT) void tuning_select_kernel(const float* peak_pitch, const float* peak_mag,
-                                                           const int* peak_cnt, const int* n_tframes,
-                                                           const int64_t* tf_base, int* tuning_idx,
-                                                           float* tuning_val) {
+                                                           const int* chunk_npk, const int64_t* tf_base,
+                                                           int* tuning_idx, float* tuning_val) {
   __shared__ BlockScratch<NT> bs;
   __shared__ int hist[256];
   __shared__ int counts[100];
-  const int c = blockIdx.x;
-  const int64_t f0 = tf_base[c];
-  const int T = n_tframes[c];
-  // total peaks
-  int tot = 0;
-  for (int t = threadIdx.x; t < T; t += NT) tot += peak_cnt[f0 + t];
-  tot = block_sum_i<NT>(tot, bs);
-  // median of mags (all peaks have pitch > 0)
+  __shared__ int sel[2];
+  const int c = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int64_t base = tf_base[c] * kPeakSlots;
+  const float* mg = peak_mag + base;
+  const float* pt = peak_pitch + base;
+  const int N = chunk_npk[c];
   float thr = 0.0f;
-  if (tot > 0) {
-    // radix select over f32 keys (32 bits, 4 passes of 8 bits)
-    auto fkey = [](float f) {
-      unsigned u = __float_as_uint(f);
-      return (u >> 31) ? ~u : (u | 0x80000000u);
-    };
-    auto kth = [&](int k) {
-      unsigned prefix = 0, mask = 0;
-      for (int shift = 24; shift >= 0; shift -= 8) {
-        for (int i = threadIdx.x; i < 256; i += NT) hist[i] = 0;
-        __syncthreads();
-        for (int t = 0; t < T; ++t) {
-          const int n = peak_cnt[f0 + t];
-          for (int j = threadIdx.x; j < n; j += NT) {
-            const unsigned key = fkey(peak_mag[(f0 + t) * kPeakSlots + j]);
-            if ((key & mask) == prefix) atomicAdd(&hist[(key >> shift) & 255], 1);
-          }
-        }
-        __syncthreads();
-        if (threadIdx.x == 0) {
-          int kk = k, d = 0;
-          for (; d < 256; ++d) {
-            if (kk < hist[d]) break;
-            kk -= hist[d];
-          }
-          bs.i[0] = d;
-          bs.i[1] = kk;
-        }
-        __syncthreads();
-        prefix |= (unsigned)bs.i[0] << shift;
-        mask |= 255u << shift;
-        k = bs.i[1];
-        __syncthreads();
+  if (N > 0) {
+    int kk = (N - 1) / 2;
+    unsigned prefix = 0, mask = 0;
+    for (int shift = 24; shift >= 0; shift -= 8) {
+      for (int i = tid; i < 256; i += NT) hist[i] = 0;
+      __syncthreads();
+      for (int i = tid; i < N; i += NT) {
+        const unsigned key = fkey(mg[i]);
+        if ((key & mask) == prefix) atomicAdd(&hist[(key >> shift) & 255], 1);
       }
-      const unsigned u = (prefix >> 31) ? (prefix & 0x7fffffffu) : ~prefix;
-      return __uint_as_float(u);
-    };
-    if (tot & 1) thr = kth(tot / 2);
-    else {
-      const float lo = kth(tot / 2 - 1), hi = kth(tot / 2);
+      __syncthreads();
+      if (wave == 0) {
+        const int h0 = hist[4 * lane], h1 = hist[4 * lane + 1], h2 = hist[4 * lane + 2], h3 = hist[4 * lane + 3];
+        const int s = h0 + h1 + h2 + h3;
+        const int incl = wave_incl_scan_i(s), excl = incl - s;
+        if (excl <= kk && kk < incl) {
+          int r = kk - excl, d = 4 * lane;
+          const int hh[4] = {h0, h1, h2, h3};
+          for (int q = 0; q < 4; ++q) {
+            if (r < hh[q]) {
+              d = 4 * lane + q;
+              break;
+            }
+            r -= hh[q];
+          }
+          sel[0] = d;
+          sel[1] = r;
+        }
+      }
+      __syncthreads();
+      prefix |= (unsigned)sel[0] << shift;
+      mask |= 255u << shift;
+      kk = sel[1];
+      __syncthreads();
+    }
+    const float lo = funkey(prefix);
+    if (N & 1) {
+      thr = lo;
+    } else {
+      // upper middle: lo again if at least (N/2 + 1) keys are <= lo, else the smallest key above it
+      int le = 0;
+      float above = INFINITY;
+      for (int i = tid; i < N; i += NT) {
+        const float v = mg[i];
+        if (fkey(v) <= prefix) ++le;
+        else above = fminf(above, v);
+      }
+      le = block_sum_i<NT>(le, bs);
+      above = (float)(-block_max(-(double)above, bs));
+      const float hi = (le >= N / 2 + 1) ? lo : above;
       thr = (lo + hi) / 2.0f;
     }
   }
-  for (int i = threadIdx.x; i < 100; i += NT) counts[i] = 0;
+  for (int i = tid; i < 100; i += NT) counts[i] = 0;
   __syncthreads();
   int nsel = 0;
-  for (int t = 0; t < T; ++t) {
-    const int n = peak_cnt[f0 + t];
-    for (int j = threadIdx.x; j < n; j += NT) {
-      const float mg = peak_mag[(f0 + t) * kPeakSlots + j];
-      const float p = peak_pitch[(f0 + t) * kPeakSlots + j];
-      if (mg >= thr && p > 0.0f) {
-        const float o = log2f(p / 27.5f);
-        float r = fmodf(36.0f * o, 1.0f);
-        if (r < 0.0f) r += 1.0f;
-        if (r >= 0.5f) r -= 1.0f;
-        atomicAdd(&counts[tuning_bin(r)], 1);
-        ++nsel;
-      }
+  for (int i = tid; i < N; i += NT) {
+    const float m = mg[i], p = pt[i];
+    if (m >= thr && p > 0.0f) {
+      const float o = log2f(p / 27.5f);
+      float r = fmodf(36.0f * o, 1.0f);
+      if (r < 0.0f) r += 1.0f;
+      if (r >= 0.5f) r -= 1.0f;
+      atomicAdd(&counts[tuning_bin(r)], 1);
+      ++nsel;
     }
   }
   nsel = block_sum_i<NT>(nsel, bs);
-  if (threadIdx.x == 0) {
+  if (tid == 0) {
     int best = 50;
     if (nsel > 0) {
       best = 0;
@@ -295,6 +383,16 @@ __global__ __launch_bounds__(NT) void tuning_select_kernel(const float* peak_pit
 }
 
 // ------------------------------------------------------------------------------ 4. CQT + chroma
+// One workgroup per (chunk, CQ_FR frames).  Work items are (frame, octave) pairs, one per
+// wave: rect-window 1024-sample frame of the octave signal -> 512-point complex FFT + real
+// split -> 36 sparse basis rows of the chunk's tuning (staged in LDS once per workgroup)
+// -> |C| sqrt(sr/my_sr) / sqrt(len) into an LDS row tile.  Then per frame the 12-bin chroma
+// (bins 3c-1, 3c, 3c+1 of each octave, in ascending bin order), its inf-norm, and the f64
+// sum over the workgroup's frames.
+constexpr int CQ_WAVES = 8;
+constexpr int CQ_FR = 16;
+using CqTw = StagedTw<512>;
+
 struct CqtArgs {
   const float* sig;
   const int64_t* chunk_off;
@@ -303,7 +401,8 @@ struct CqtArgs {
   const int* n_frames;
   const int* tuning_idx;
   const float* ws_oct;
-  int nblk;
+  const int64_t* tf_base;  // partial rows of chunk c start at tf_base[c] / CQ_FR + c
+  int maxnnz;
   const float2* tw;
   const int* cqt_lo;
   const int* cqt_len;
@@ -313,38 +412,75 @@ struct CqtArgs {
   double* partial;  // [n][nblk][12]
 };
 
-constexpr int CQ_WAVES = 7;
+__host__ __device__ __forceinline__ int cq_al4(int n) { return (n + 3) & ~3; }
+
+size_t cqt_lds_bytes(int maxnnz) {
+  return sizeof(float2) * (cq_al4(CqTw::size) + (size_t)cq_al4(maxnnz)) + sizeof(int) * 3 * 36 +
+         sizeof(float) * (kCqtBins + CQ_FR * kCqtBins + 2 * CQ_FR * 12) + 16 +
+         sizeof(float2) * (size_t)CQ_WAVES * LdsSize<512>::value;
+}
 
 __global__ __launch_bounds__(CQ_WAVES * 64) void cqt_chroma_kernel(CqtArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int lane = threadIdx.x & 63, oct = threadIdx.x >> 6;
-  const int c = blockIdx.y, blk = blockIdx.x;
-  float2* fftbuf = reinterpret_cast<float2*>(smem) + oct * LdsSize<512>::value;
-  float* row = reinterpret_cast<float*>(reinterpret_cast<float2*>(smem) + CQ_WAVES * LdsSize<512>::value);
+  const int c = blockIdx.y, fb = blockIdx.x;
   const int T = a.n_frames[c];
+  const int t0 = fb * CQ_FR;
+  if (t0 >= T) return;
+  const int tid = threadIdx.x, lane0 = tid & 63, wave = tid >> 6;
+  float2* sh_tw = reinterpret_cast<float2*>(smem);
+  float2* sh_w = sh_tw + cq_al4(CqTw::size);
+  int* sh_desc = reinterpret_cast<int*>(sh_w + cq_al4(a.maxnnz));  // lo[36] len[36] off[36]
+  float* sh_isl = reinterpret_cast<float*>(sh_desc + 3 * 36);
+  float* sh_row = sh_isl + kCqtBins;              // [CQ_FR][252]
+  float* sh_ch = sh_row + CQ_FR * kCqtBins;       // [CQ_FR][12]
+  float* sh_nv = sh_ch + CQ_FR * 12;              // [CQ_FR][12]
+  // 16-byte aligned FFT slots after the tables (index arithmetic keeps the LDS address space)
+  const int fft_f = cq_al4((int)(sh_nv + CQ_FR * 12 - reinterpret_cast<float*>(smem)));
+  float2* fftbuf = reinterpret_cast<float2*>(reinterpret_cast<float*>(smem) + fft_f) + wave * LdsSize<512>::value;
   const int ti = a.tuning_idx[c];
-  const float* y = oct == 0 ? a.sig + a.chunk_off[c] : a.ws_oct + a.oct_off[c * 7 + oct];
-  const int64_t Ly = a.oct_len[c * 7 + oct];
-  const int hop = 512 >> oct;
-  const float oscale = sqrtf((float)(1 << oct));  // fft_basis *= sqrt(sr / my_sr)
-  double acc = 0.0;                               // lanes 0..11 of wave 0: chroma sums
-  for (int t = blk; t < T; t += a.nblk) {
+  const int woff0 = a.cqt_off[ti * kCqtFilt];
+  const int nnz = a.cqt_off[ti * kCqtFilt + kCqtFilt - 1] + a.cqt_len[ti * kCqtFilt + kCqtFilt - 1] - woff0;
+  fill_staged_tw<512>(sh_tw, a.tw, tid, CQ_WAVES * 64);
+  for (int i = tid; i < nnz; i += CQ_WAVES * 64) sh_w[i] = a.cqt_w[woff0 + i];
+  for (int i = tid; i < kCqtFilt; i += CQ_WAVES * 64) {
+    sh_desc[i] = a.cqt_lo[ti * kCqtFilt + i];
+    sh_desc[36 + i] = a.cqt_len[ti * kCqtFilt + i];
+    sh_desc[72 + i] = a.cqt_off[ti * kCqtFilt + i] - woff0;
+  }
+  for (int i = tid; i < kCqtBins; i += CQ_WAVES * 64) sh_isl[i] = a.cqt_isl[ti * kCqtBins + i];
+  __syncthreads();
+
+  const int nfr = min(CQ_FR, T - t0);
+  for (int it = wave; it < nfr * 7; it += CQ_WAVES) {
+    int lane = lane0;
+    asm volatile("" : "+v"(lane));
+    const int fl = it / 7, oct = it - 7 * fl;
+    const int t = t0 + fl;
+    const float* y = oct == 0 ? a.sig + a.chunk_off[c] : a.ws_oct + a.oct_off[c * 7 + oct];
+    const int64_t Ly = a.oct_len[c * 7 + oct];
+    const int hop = 512 >> oct;
     const int64_t s0 = (int64_t)t * hop - 512;
     FftIn<512> in;
+    if (s0 >= 0 && s0 + 1024 <= Ly && ((reinterpret_cast<uintptr_t>(y) & 7) == 0)) {
+      const float2* y2 = reinterpret_cast<const float2*>(y + s0);
 #pragma unroll
-    for (int r = 0; r < 8; ++r) {
-      const int n = lane + 64 * r;
-      const int64_t i0 = s0 + 2 * n;
-      const float x0 = (i0 >= 0 && i0 < Ly) ? y[i0] : 0.0f;
-      const float x1 = (i0 + 1 >= 0 && i0 + 1 < Ly) ? y[i0 + 1] : 0.0f;
-      in[0][r] = make_float2(x0, x1);
+      for (int r = 0; r < 8; ++r) in[0][r] = y2[lane + 64 * r];
+    } else {
+#pragma unroll
+      for (int r = 0; r < 8; ++r) {
+        const int n = lane + 64 * r;
+        const int64_t i0 = s0 + 2 * n;
+        const float x0 = (i0 >= 0 && i0 < Ly) ? y[i0] : 0.0f;
+        const float x1 = (i0 + 1 >= 0 && i0 + 1 < Ly) ? y[i0 + 1] : 0.0f;
+        in[0][r] = make_float2(x0, x1);
+      }
     }
-    wave_fft<512>(in, fftbuf, a.tw, lane);
+    wave_fft<512, 0>(in, fftbuf, sh_tw, lane);
     float2 d1[5], d2[5];
 #pragma unroll
     for (int m = 0; m < 5; ++m) {
       const int k = lane + 64 * m;
-      if (k <= 256) rfft_split(fftbuf, a.tw, 512, k, d1[m], d2[m]);
+      if (k <= 256) rfft_split<0, CqTw::split>(fftbuf, sh_tw, 512, k, d1[m], d2[m]);
     }
     float2* D = fftbuf;  // reuse as D[0..512] unpadded
 #pragma unroll
@@ -355,57 +491,68 @@ __global__ __launch_bounds__(CQ_WAVES * 64) void cqt_chroma_kernel(CqtArgs a) {
         D[512 - k] = d2[m];
       }
     }
-    // 36 filters: lanes 0..35
     if (lane < kCqtFilt) {
-      const int fi = ti * kCqtFilt + lane;
-      const int lo = a.cqt_lo[fi], len = a.cqt_len[fi], off = a.cqt_off[fi];
+      const int lo = sh_desc[lane], len = sh_desc[36 + lane], off = sh_desc[72 + lane];
       float re = 0.0f, im = 0.0f;
+#pragma unroll 4
       for (int j = 0; j < len; ++j) {
-        const float2 w = a.cqt_w[off + j];
+        const float2 w = sh_w[off + j];
         const float2 d = D[lo + j];
         re = fmaf(w.x, d.x, fmaf(-w.y, d.y, re));
         im = fmaf(w.x, d.y, fmaf(w.y, d.x, im));
       }
+      const float oscale = sqrtf((float)(1 << oct));  // fft_basis *= sqrt(sr / my_sr)
       const int bin = kCqtBins - kCqtFilt * (oct + 1) + lane;
-      row[bin] = hypotf(re * oscale, im * oscale) * a.cqt_isl[ti * kCqtBins + bin];
+      sh_row[fl * kCqtBins + bin] = hypotf(re * oscale, im * oscale) * sh_isl[bin];
     }
-    __syncthreads();
-    if (oct == 0) {
-      // chroma c <- CQT bins with (j mod 36) in {3c-1, 3c, 3c+1} (mod 36), ascending j
-      float ch = 0.0f;
-      if (lane < 12) {
-        // 3 bins per chroma per octave, octave-major, ascending within the octave
-        for (int o = 0; o < 7; ++o) {
-          const int b = 36 * o;
-          if (lane == 0) {
-            ch += row[b];
-            ch += row[b + 1];
-            ch += row[b + 35];
-          } else {
-            ch += row[b + 3 * lane - 1];
-            ch += row[b + 3 * lane];
-            ch += row[b + 3 * lane + 1];
-          }
-        }
-      }
-      float mx = (lane < 12) ? fabsf(ch) : 0.0f;
-      mx = wave_max(mx);
-      const double len = (mx < 1.17549435e-38f) ? 1.0 : (double)mx;
-      if (lane < 12) acc += (double)(float)((double)ch / len);
-    }
-    __syncthreads();
   }
-  if (oct == 0 && lane < 12) a.partial[((size_t)c * a.nblk + blk) * 12 + lane] = acc;
+  __syncthreads();
+  // chroma c <- CQT bins with (j mod 36) in {3c-1, 3c, 3c+1} (mod 36): octave-major, ascending
+  if (tid < nfr * 12) {
+    const int fl = tid / 12, cc = tid - 12 * fl;
+    const float* row = sh_row + fl * kCqtBins;
+    float ch = 0.0f;
+    for (int o = 0; o < 7; ++o) {
+      const int b = 36 * o;
+      if (cc == 0) {
+        ch += row[b];
+        ch += row[b + 1];
+        ch += row[b + 35];
+      } else {
+        ch += row[b + 3 * cc - 1];
+        ch += row[b + 3 * cc];
+        ch += row[b + 3 * cc + 1];
+      }
+    }
+    sh_ch[tid] = ch;
+  }
+  __syncthreads();
+  if (tid < nfr * 12) {
+    const int fl = tid / 12;
+    float mx = 0.0f;
+    for (int j = 0; j < 12; ++j) mx = fmaxf(mx, fabsf(sh_ch[fl * 12 + j]));
+    const double len = (mx < 1.17549435e-38f) ? 1.0 : (double)mx;
+    sh_nv[tid] = (float)((double)sh_ch[tid] / len);
+  }
+  __syncthreads();
+  if (tid < 12) {
+    double acc = 0.0;
+    for (int fl = 0; fl < nfr; ++fl) acc += (double)sh_nv[fl * 12 + tid];
+    a.partial[(a.tf_base[c] / CQ_FR + c + fb) * 12 + tid] = acc;
+  }
 }
 
-__global__ void chroma_finalize_kernel(const double* partial, int nblk, const int* n_frames, int n,
+__global__ void chroma_finalize_kernel(const double* partial, const int64_t* tf_base, const int* n_frames, int n,
                                        float* out_chroma) {
   const int c = blockIdx.x;
   const int k = threadIdx.x;
   if (k >= 12 || c >= n) return;
+  const int T = n_frames[c];
+  const int nb = (T + CQ_FR - 1) / CQ_FR;
+  const int64_t r0 = tf_base[c] / CQ_FR + c;
   double s = 0.0;
-  for (int b = 0; b < nblk; ++b) s += partial[((size_t)c * nblk + b) * 12 + k];
-  out_chroma[c * 12 + k] = (float)(s / (double)n_frames[c]);
+  for (int b = 0; b < nb; ++b) s += partial[(r0 + b) * 12 + k];
+  out_chroma[c * 12 + k] = (float)(s / (double)T);
 }
 
 // ------------------------------------------------------------------------------ 6. lag
@@ -439,36 +586,37 @@ struct ChromaWs {
   float* ws_oct;
   float* peak_pitch;
   float* peak_mag;
-  int* peak_cnt;
+  int* chunk_npk;
   double* partial;
   int* tuning_idx;
 };
 
 static inline size_t al256(size_t n) { return (n + 255) & ~(size_t)255; }
 
-constexpr int kCqtBlk = 32;  // frame blocks per chunk
-
 size_t chroma_ws_bytes(int n, int64_t total_len) {
   // octave buffers: < total_len * (1/2 + ... ) + padding; tuning frames <= total_len/512 + n
   const int64_t tfr = total_len / 512 + n;
   size_t b = 0;
   b += al256(sizeof(int64_t) * 7 * n) * 2;
-  b += al256(sizeof(int) * n) * 3;
+  b += al256(sizeof(int) * n) * 4;
   b += al256(sizeof(int64_t) * (n + 1));
   b += al256(sizeof(float) * (size_t)(total_len + 64 * 7 * (int64_t)n));
   b += al256(sizeof(float) * (size_t)tfr * kPeakSlots) * 2;
-  b += al256(sizeof(int) * (size_t)tfr);
-  b += al256(sizeof(double) * (size_t)n * kCqtBlk * 12);
+  b += al256(sizeof(double) * (size_t)(tfr / CQ_FR + n + 1) * 12);
   return b + 4096;
 }
 
 int launch_chroma_mean(Context& ctx, const float* sig, const int64_t* chunk_off, const int64_t* chunk_len, int n,
-                       int64_t total_len, int64_t max_chunk_len, float* out_chroma, float* out_tuning, int* out_tuning_idx, void* ws,
-                       size_t ws_bytes, hipStream_t st) {
+                       int64_t total_len, int64_t max_chunk_len, float* out_chroma, float* out_tuning,
+                       int* out_tuning_idx, void* ws, size_t ws_bytes, hipStream_t st) {
   if (n <= 0) return 0;
   if (ws_bytes < chroma_ws_bytes(n, total_len)) {
     set_error("chroma: workspace too small");
     return -3;
+  }
+  if (max_chunk_len <= 0) {
+    set_error("chroma: max_chunk_len must be positive");
+    return -2;
   }
   char* p = static_cast<char*>(ws);
   auto take = [&](size_t bytes) {
@@ -482,24 +630,26 @@ int launch_chroma_mean(Context& ctx, const float* sig, const int64_t* chunk_off,
   w.oct_len = reinterpret_cast<int64_t*>(take(sizeof(int64_t) * 7 * n));
   w.n_frames = reinterpret_cast<int*>(take(sizeof(int) * n));
   w.n_tframes = reinterpret_cast<int*>(take(sizeof(int) * n));
+  w.chunk_npk = reinterpret_cast<int*>(take(sizeof(int) * n));
   w.tuning_idx = out_tuning_idx ? out_tuning_idx : reinterpret_cast<int*>(take(sizeof(int) * n));
   w.tf_base = reinterpret_cast<int64_t*>(take(sizeof(int64_t) * (n + 1)));
   w.ws_oct = reinterpret_cast<float*>(take(sizeof(float) * (size_t)(total_len + 64 * 7 * (int64_t)n)));
   w.peak_pitch = reinterpret_cast<float*>(take(sizeof(float) * (size_t)tfr * kPeakSlots));
   w.peak_mag = reinterpret_cast<float*>(take(sizeof(float) * (size_t)tfr * kPeakSlots));
-  w.peak_cnt = reinterpret_cast<int*>(take(sizeof(int) * (size_t)tfr));
-  w.partial = reinterpret_cast<double*>(take(sizeof(double) * (size_t)n * kCqtBlk * 12));
+  w.partial = reinterpret_cast<double*>(take(sizeof(double) * (size_t)(tfr / CQ_FR + n + 1) * 12));
 
   hipLaunchKernelGGL(chroma_plan_kernel, dim3(1), dim3(64), 0, st, chunk_len, n, w.oct_off, w.oct_len, w.n_frames,
                      w.n_tframes, w.tf_base);
-  // host-side bound for grids: longest chunk
-  // (grid.x sized by total_len, threads beyond a chunk's length exit)
-  const int64_t max_chunk = max_chunk_len;
+  NC_HIP(hipMemsetAsync(w.chunk_npk, 0, sizeof(int) * n, st));
+  // grids are sized by the longest chunk; blocks past a chunk's own length exit
   for (int lvl = 0; lvl < 6; ++lvl) {
-    const int64_t mo = (max_chunk >> (lvl + 1)) + 1;
-    dim3 grid((unsigned)((mo + 255) / 256), (unsigned)n);
-    hipLaunchKernelGGL(decimate_kernel, grid, dim3(256), 0, st, sig, chunk_off, w.oct_off, w.oct_len, w.ws_oct,
-                       lvl, ctx.t.halfband, kHalfbandK, mo);
+    const int64_t mo = (max_chunk_len >> (lvl + 1)) + 1;
+    dim3 grid((unsigned)((mo + DEC_OUT - 1) / DEC_OUT), (unsigned)n);
+    {
+      KTimer kt_(ctx, "decimate", st);
+      hipLaunchKernelGGL(decimate_kernel, grid, dim3(256), 0, st, sig, chunk_off, w.oct_off, w.oct_len, w.ws_oct,
+                         lvl, ctx.t.halfband);
+    }
   }
   PeakArgs pa;
   pa.sig = sig;
@@ -508,17 +658,23 @@ int launch_chroma_mean(Context& ctx, const float* sig, const int64_t* chunk_off,
   pa.n_tframes = w.n_tframes;
   pa.tf_base = w.tf_base;
   pa.n_chunks = n;
-  pa.total_tframes = tfr;  // upper bound; frames beyond tf_base[n] are skipped below
+  pa.total_tframes = tfr;  // upper bound; frames past tf_base[n] are skipped
   pa.tw = ctx.t.tw;
   pa.hann2048 = ctx.t.hann2048;
   pa.peak_pitch = w.peak_pitch;
   pa.peak_mag = w.peak_mag;
-  pa.peak_cnt = w.peak_cnt;
-  // exact total tuning frames = sum(1 + len/512) <= tfr; extra waves find t >= n_tframes
-  hipLaunchKernelGGL(tuning_peaks_kernel, dim3((unsigned)((tfr + 3) / 4)), dim3(256),
-                     4 * LdsSize<1024>::value * sizeof(float2), st, pa);
-  hipLaunchKernelGGL((tuning_select_kernel<256>), dim3(n), dim3(256), 0, st, w.peak_pitch, w.peak_mag, w.peak_cnt,
-                     w.n_tframes, w.tf_base, w.tuning_idx, out_tuning);
+  pa.chunk_npk = w.chunk_npk;
+  {
+    const size_t lds = (((TpTw::size + 1) & ~1) + (size_t)TP_WAVES * LdsSize<1024>::value) * sizeof(float2);
+    const int64_t groups = (tfr + TP_WAVES - 1) / TP_WAVES;
+    const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(groups, ctx.num_cu));
+    {
+      KTimer kt_(ctx, "tuning_peaks", st);
+      hipLaunchKernelGGL(tuning_peaks_kernel, dim3(grid), dim3(TP_WAVES * 64), lds, st, pa);
+    }
+  }
+  hipLaunchKernelGGL((tuning_select_kernel<1024>), dim3(n), dim3(1024), 0, st, w.peak_pitch, w.peak_mag,
+                     w.chunk_npk, w.tf_base, w.tuning_idx, out_tuning);
   CqtArgs ca;
   ca.sig = sig;
   ca.chunk_off = chunk_off;
@@ -527,7 +683,8 @@ int launch_chroma_mean(Context& ctx, const float* sig, const int64_t* chunk_off,
   ca.n_frames = w.n_frames;
   ca.tuning_idx = w.tuning_idx;
   ca.ws_oct = w.ws_oct;
-  ca.nblk = kCqtBlk;
+  ca.tf_base = w.tf_base;
+  ca.maxnnz = ctx.t.cqt_maxnnz;
   ca.tw = ctx.t.tw;
   ca.cqt_lo = ctx.t.cqt_lo;
   ca.cqt_len = ctx.t.cqt_len;
@@ -535,9 +692,12 @@ int launch_chroma_mean(Context& ctx, const float* sig, const int64_t* chunk_off,
   ca.cqt_w = ctx.t.cqt_w;
   ca.cqt_isl = ctx.t.cqt_inv_sqrt_len;
   ca.partial = w.partial;
-  const size_t lds = CQ_WAVES * LdsSize<512>::value * sizeof(float2) + kCqtBins * sizeof(float) + 16;
-  hipLaunchKernelGGL(cqt_chroma_kernel, dim3(kCqtBlk, n), dim3(CQ_WAVES * 64), lds, st, ca);
-  hipLaunchKernelGGL(chroma_finalize_kernel, dim3(n), dim3(64), 0, st, w.partial, kCqtBlk, w.n_frames, n,
+  const int nblk = (int)((1 + max_chunk_len / 512 + CQ_FR - 1) / CQ_FR);
+  {
+    KTimer kt_(ctx, "cqt_chroma", st);
+    hipLaunchKernelGGL(cqt_chroma_kernel, dim3(nblk, n), dim3(CQ_WAVES * 64), cqt_lds_bytes(ca.maxnnz), st, ca);
+  }
+  hipLaunchKernelGGL(chroma_finalize_kernel, dim3(n), dim3(64), 0, st, w.partial, w.tf_base, w.n_frames, n,
                      out_chroma);
   NC_HIP(hipGetLastError());
   return 0;

@@ -254,7 +254,10 @@ int launch_ibi_tempogram(Context& ctx, const float* onset, const int64_t* frame_
   a.n_tblk = n_tblk;
   a.slab = slab;
   const size_t lds = TG_TB * sizeof(double) + (size_t)(TG_TB + N) * sizeof(float);
-  hipLaunchKernelGGL(tg_slide_kernel, dim3((N + TG_KB - 1) / TG_KB, n_tblk, n_files), dim3(TG_KB), lds, st, a);
+  {
+    KTimer kt_(ctx, "tg_slide", st);
+    hipLaunchKernelGGL(tg_slide_kernel, dim3((N + TG_KB - 1) / TG_KB, n_tblk, n_files), dim3(TG_KB), lds, st, a);
+  }
   hipLaunchKernelGGL(tg_reduce_kernel, dim3((N + 255) / 256, n_files), dim3(256), 0, st, slab, frame_base, n_tblk,
                      N, tg_out);
   NC_HIP(hipGetLastError());

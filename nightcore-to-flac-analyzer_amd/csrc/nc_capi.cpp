@@ -127,12 +127,30 @@ int nc_create(int device, nc_ctx** out) {
 int nc_destroy(nc_ctx* ctx) {
   CHECK_CTX(ctx);
   (void)hipSetDevice(ctx->c.device);
+  nc::free_timers(ctx->c);
   nc::free_tables(ctx->c);
   delete ctx;
   return 0;
 }
 
 int nc_num_cu(const nc_ctx* ctx) { return ctx ? ctx->c.num_cu : -1; }
+
+int nc_profile_enable(nc_ctx* ctx, int on) {
+  CHECK_CTX(ctx);
+  SET_DEVICE(ctx);
+  nc::profile_enable(ctx->c, on != 0);
+  return 0;
+}
+
+int nc_profile_read(nc_ctx* ctx, const char* tag, double* total_ms, int* launches) {
+  CHECK_CTX(ctx);
+  if (!tag || !total_ms || !launches) {
+    nc::set_error("nc_profile_read: null argument");
+    return -1;
+  }
+  SET_DEVICE(ctx);
+  return nc::profile_read(ctx->c, tag, total_ms, launches);
+}
 
 size_t nc_trim_workspace_bytes(const int64_t* host_file_len, int n_files) {
   return nc::trim_ws_bytes(host_file_len, n_files);

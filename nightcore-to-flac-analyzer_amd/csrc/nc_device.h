@@ -134,7 +134,10 @@ struct LdsSize {
 // one wave when NT == 64, a whole workgroup otherwise; SYNC adds the barriers a
 // multi-wave in-place stage needs).  Stage-1 input comes from registers in the
 // layout x[j + r*N/R], j = tid + NT*b.
-template <int N, int R, int NS, int NT, bool SYNC, int TWN = 8192>
+// Twiddles: TWN > 0 reads tw[q] = exp(-2 pi i q / TWN) (the 8192-entry global table or a
+// copy); TWN == 0 reads a per-stage table laid out [r - 1][k] starting at STO (see
+// StagedTw), whose reads are contiguous in k and so free of LDS bank conflicts.
+template <int N, int R, int NS, int NT, bool SYNC, int TWN = 8192, int STO = 0>
 __device__ __forceinline__ void stockham_stage_regs(float2 (&v)[N / (R * NT)][R], float2* lds,
                                                     const float2* __restrict__ tw, int tid) {
   constexpr int NB = N / (R * NT);
@@ -145,7 +148,9 @@ __device__ __forceinline__ void stockham_stage_regs(float2 (&v)[N / (R * NT)][R]
     const int k = j % NS;
     if (NS > 1) {
 #pragma unroll
-      for (int r = 1; r < R; ++r) v[b][r] = cmul(v[b][r], tw[(k * r * (TWN / (NS * R))) & (TWN - 1)]);
+      for (int r = 1; r < R; ++r)
+        v[b][r] = cmul(v[b][r], TWN > 0 ? tw[(k * r * (TWN > 0 ? TWN / (NS * R) : 1)) & (TWN - 1)]
+                                        : tw[STO + (r - 1) * NS + k]);
     }
     DFT<R>::run(v[b]);
   }
@@ -161,7 +166,7 @@ __device__ __forceinline__ void stockham_stage_regs(float2 (&v)[N / (R * NT)][R]
   if (SYNC) __syncthreads();
 }
 
-template <int N, int R, int NS, int NT, bool SYNC, int TWN = 8192>
+template <int N, int R, int NS, int NT, bool SYNC, int TWN = 8192, int STO = 0>
 __device__ __forceinline__ void stockham_stage(float2* lds, const float2* __restrict__ tw, int tid) {
   constexpr int NB = N / (R * NT);
   float2 v[NB][R];
@@ -171,7 +176,7 @@ __device__ __forceinline__ void stockham_stage(float2* lds, const float2* __rest
 #pragma unroll
     for (int r = 0; r < R; ++r) v[b][r] = lds[lpad(j + r * (N / R))];
   }
-  stockham_stage_regs<N, R, NS, NT, SYNC, TWN>(v, lds, tw, tid);
+  stockham_stage_regs<N, R, NS, NT, SYNC, TWN, STO>(v, lds, tw, tid);
 }
 
 // Radix plans: 512 = 8.8.8, 1024 = 16.16.4, 2048 = 16.16.8, 4096 = 16.16.16
@@ -202,10 +207,42 @@ template <int N, int NT, bool SYNC, int TWN = 8192>
 __device__ __forceinline__ void fft_impl(FftIn<N, NT>& in, float2* lds, const float2* __restrict__ tw, int tid) {
   constexpr int R0 = Plan<N>::R0, R1 = Plan<N>::R1, R2 = Plan<N>::R2;
   static_assert(R0 * R1 * R2 == N, "plan");
-  static_assert(TWN >= N, "twiddle table too coarse for this FFT");
-  stockham_stage_regs<N, R0, 1, NT, SYNC, TWN>(in, lds, tw, tid);
-  stockham_stage<N, R1, R0, NT, SYNC, TWN>(lds, tw, tid);
-  stockham_stage<N, R2, R0 * R1, NT, SYNC, TWN>(lds, tw, tid);
+  static_assert(TWN == 0 || TWN >= N, "twiddle table too coarse for this FFT");
+  stockham_stage_regs<N, R0, 1, NT, SYNC, TWN, 0>(in, lds, tw, tid);
+  stockham_stage<N, R1, R0, NT, SYNC, TWN, 0>(lds, tw, tid);
+  stockham_stage<N, R2, R0 * R1, NT, SYNC, TWN, (R1 - 1) * R0>(lds, tw, tid);
+}
+
+// Per-stage twiddle table of an N-point complex FFT (+ the real-split twiddles of
+// the 2N-point real transform), for TWN == 0:
+//   [0, s3)          stage 2: W_{R0 R1}^{k r}  at (r - 1) R0 + k
+//   [s3, split)      stage 3: W_N^{k r}        at s3 + (r - 1) R0 R1 + k
+//   [split, size)    split:   W_{2N}^{k}       at split + k, k <= N/2
+template <int N>
+struct StagedTw {
+  static constexpr int R0 = Plan<N>::R0, R1 = Plan<N>::R1, R2 = Plan<N>::R2;
+  static constexpr int s3 = (R1 - 1) * R0;
+  static constexpr int split = s3 + (R2 - 1) * R0 * R1;
+  static constexpr int size = split + N / 2 + 1;
+};
+
+// Fill the staged table from the global 8192-entry table (all threads of a workgroup).
+template <int N>
+__device__ __forceinline__ void fill_staged_tw(float2* dst, const float2* __restrict__ tw8192, int tid, int nt) {
+  using S = StagedTw<N>;
+  for (int i = tid; i < S::size; i += nt) {
+    int q;
+    if (i < S::s3) {
+      const int r = i / S::R0 + 1, k = i % S::R0;
+      q = k * r * (8192 / (S::R0 * S::R1));
+    } else if (i < S::split) {
+      const int ii = i - S::s3, r = ii / (S::R0 * S::R1) + 1, k = ii % (S::R0 * S::R1);
+      q = k * r * (8192 / N);
+    } else {
+      q = (i - S::split) * (8192 / (2 * N));
+    }
+    dst[i] = tw8192[q & 8191];
+  }
 }
 
 // One wave; no barrier needed (LDS ops of a wave complete in order and every
@@ -226,14 +263,14 @@ __device__ __forceinline__ void block_fft(FftIn<N, NT>& in, float2* lds, const f
 
 // Real-FFT split: Z = FFT_N(z), z[n] = x[2n] + i x[2n+1] (x real, length 2N).
 // Returns X[k] and X[N-k] for 0 <= k <= N/2.
-template <int TWN = 8192>
+template <int TWN = 8192, int SPLIT = 0>
 __device__ __forceinline__ void rfft_split(const float2* lds, const float2* __restrict__ tw, int N, int k,
                                            float2& Xk, float2& XNk) {
   const float2 a = lds[lpad(k & (N - 1))];
   const float2 b = cconj(lds[lpad((N - k) & (N - 1))]);
   const float2 E = cscale(cadd(a, b), 0.5f);
   const float2 O = cmul_mi(cscale(csub(a, b), 0.5f));  // (a-b)/(2i)
-  const float2 W = tw[(k * (TWN / (2 * N))) & (TWN - 1)];  // exp(-2 pi i k / 2N)
+  const float2 W = TWN > 0 ? tw[(k * (TWN > 0 ? TWN / (2 * N) : 1)) & (TWN - 1)] : tw[SPLIT + k];  // exp(-2 pi i k / 2N)
   const float2 WO = cmul(W, O);
   Xk = cadd(E, WO);
   XNk = cconj(csub(E, WO));

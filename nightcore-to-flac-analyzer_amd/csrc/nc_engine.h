@@ -41,15 +41,38 @@ struct Tables {
   float2* cqt_w = nullptr;      // sparse basis rows (octave-0 basis, sqrt(sr/my_sr) applied per octave)
   float* cqt_inv_sqrt_len = nullptr;  // [kNTunings][252]  1/sqrt(lengths)
   int cqt_maxlen = 0;
+  int cqt_maxnnz = 0;           // max over tunings of the 36 rows' total length
   double* halfband = nullptr;   // 2K+1 taps
 };
+
+struct KernelTimers;  // nc_prof.cpp
 
 struct Context {
   int device = 0;
   int num_cu = 256;
   hipStream_t stream = nullptr;
   Tables t;
+  KernelTimers* timers = nullptr;  // non-null while per-kernel profiling is enabled
 };
+
+// Brackets one kernel launch with HIP events on its stream when profiling is enabled
+// (nc_profile_enable); no-op otherwise.  Used to time the dominant kernels live.
+class KTimer {
+ public:
+  KTimer(Context& ctx, const char* tag, hipStream_t st);
+  ~KTimer();
+  KTimer(const KTimer&) = delete;
+  KTimer& operator=(const KTimer&) = delete;
+
+ private:
+  Context& ctx_;
+  const char* tag_;
+  hipStream_t st_;
+  void* stop_ = nullptr;
+};
+void free_timers(Context& ctx);
+void profile_enable(Context& ctx, bool on);
+int profile_read(Context& ctx, const char* tag, double* total_ms, int* launches);
 
 // bootstrap.hip job description (see nc_bootstrap_ratio in include/ncgpu.h)
 struct BootArgs {

@@ -270,6 +270,8 @@ void build_tables(Context& ctx) {
         t.cqt_maxlen = std::max(t.cqt_maxlen, last - first + 1);
       }
     }
+    for (int ti = 0; ti < kNTunings; ++ti)
+      t.cqt_maxnnz = std::max(t.cqt_maxnnz, coff[ti * nf + nf - 1] + clen[ti * nf + nf - 1] - coff[ti * nf]);
     t.cqt_lo = upload(clo);
     t.cqt_len = upload(clen);
     t.cqt_off = upload(coff);

@@ -22,9 +22,9 @@
 
 namespace nc {
 
-constexpr int SM_WAVES = 12;
+constexpr int SM_WAVES = 14;
 constexpr int SM_THREADS = SM_WAVES * 64;
-constexpr int SM_TWN = 2048;  // LDS twiddle table exp(-2 pi i q / 2048)
+using SmTw = StagedTw<1024>;  // per-stage twiddle table in LDS (conflict-free reads)
 
 __device__ __forceinline__ int seq_of_frame(const int64_t* base, int n, int64_t g) {
   int lo = 0, hi = n - 1;
@@ -39,19 +39,19 @@ __device__ __forceinline__ int seq_of_frame(const int64_t* base, int n, int64_t 
 __host__ __device__ __forceinline__ int al4(int n) { return (n + 3) & ~3; }
 
 size_t stft_mel_lds_bytes(int mel_nnz) {
-  return SM_TWN * sizeof(float2) + (size_t)al4(mel_nnz) * sizeof(float) + 3 * 128 * sizeof(int) +
+  return (size_t)al4(SmTw::size) * sizeof(float2) + (size_t)al4(mel_nnz) * sizeof(float) + 3 * 128 * sizeof(int) +
          (size_t)SM_WAVES * LdsSize<1024>::value * sizeof(float2);
 }
 
 __global__ __launch_bounds__(SM_THREADS) void stft_mel_kernel(StftMelArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   float2* sh_tw = reinterpret_cast<float2*>(smem);
-  float* sh_melw = reinterpret_cast<float*>(sh_tw + SM_TWN);
+  float* sh_melw = reinterpret_cast<float*>(sh_tw + al4(SmTw::size));
   int* sh_mel = reinterpret_cast<int*>(sh_melw + al4(a.mel_nnz));  // lo[128] len[128] off[128]
   const int lane0 = threadIdx.x & 63, wave = threadIdx.x >> 6;
   float2* fftbuf = reinterpret_cast<float2*>(sh_mel + 3 * 128) + wave * LdsSize<1024>::value;
 
-  for (int i = threadIdx.x; i < SM_TWN; i += SM_THREADS) sh_tw[i] = a.tw[i * (8192 / SM_TWN)];
+  fill_staged_tw<1024>(sh_tw, a.tw, threadIdx.x, SM_THREADS);
   for (int i = threadIdx.x; i < a.mel_nnz; i += SM_THREADS) sh_melw[i] = a.mel_w[i];
   for (int i = threadIdx.x; i < 128; i += SM_THREADS) {
     sh_mel[i] = a.mel_lo[i];
@@ -128,14 +128,14 @@ __global__ __launch_bounds__(SM_THREADS) void stft_mel_kernel(StftMelArgs a) {
       e = wave_sum(e);
       if (lane == 0) a.frame_energy[g] = e;
     }
-    wave_fft<1024, SM_TWN>(in, fftbuf, twl, lane);
+    wave_fft<1024, 0>(in, fftbuf, twl, lane);
     float p1[9], p2[9];
 #pragma unroll
     for (int m = 0; m < 9; ++m) {
       const int k = lane + 64 * m;
       if (k <= 512) {
         float2 X, XN;
-        rfft_split<SM_TWN>(fftbuf, twl, 1024, k, X, XN);
+        rfft_split<0, SmTw::split>(fftbuf, twl, 1024, k, X, XN);
         p1[m] = fmaf(X.x, X.x, X.y * X.y);
         p2[m] = fmaf(XN.x, XN.x, XN.y * XN.y);
       }
@@ -184,7 +184,10 @@ int launch_stft_mel(Context& ctx, const StftMelArgs& args, hipStream_t st) {
   const size_t lds = stft_mel_lds_bytes(a.mel_nnz);
   const int64_t n_groups = (a.total_frames + SM_WAVES - 1) / SM_WAVES;
   const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(n_groups, (int64_t)ctx.num_cu * (lds <= 80 * 1024 ? 2 : 1)));
-  hipLaunchKernelGGL(stft_mel_kernel, dim3(grid), dim3(SM_THREADS), lds, st, a);
+  {
+    KTimer kt_(ctx, "stft_mel", st);
+    hipLaunchKernelGGL(stft_mel_kernel, dim3(grid), dim3(SM_THREADS), lds, st, a);
+  }
   NC_HIP(hipGetLastError());
   return 0;
 }

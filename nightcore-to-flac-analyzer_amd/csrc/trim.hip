@@ -5,20 +5,22 @@
 //   rms[t]  = sqrt(ms[t]) (f32);  db[t] = 10 log10(max(1e-10, rms^2)) - 10 log10(max(1e-10, max(rms)^2))
 //   start   = first(db > -top_db) * 512,  end = min(N, (last + 1) * 512)
 //
-// Kernel 1: one wave per frame (coalesced 8 KB loads, f64 accumulation, overlap
-// re-reads served by L2); kernel 2: one workgroup per file.
+// Kernel 1: f64 sums of x^2 over 512-sample blocks (one wave per block, each sample
+// read once from HBM); kernel 2: one workgroup per file forms each frame's mean
+// from its 4 blocks, then the max and the first/last frames above -top_db.
 #include "nc_block.h"
 #include "nc_engine.h"
 
 namespace nc {
 
-__global__ __launch_bounds__(256) void trim_frames_kernel(const float* sig, const int64_t* file_off,
+// f64 sum of x^2 over each 512-sample block b = [512 b, 512 b + 512) of each file (one
+// wave per block, every sample read once); block b of file f at blk[frame_base[f] + b].
+__global__ __launch_bounds__(256) void trim_blocks_kernel(const float* sig, const int64_t* file_off,
                                                           const int64_t* file_len, const int64_t* frame_base,
-                                                          int n_files, int64_t total_frames, float* ms_out) {
+                                                          int n_files, int64_t total_frames, double* blk) {
   const int lane = threadIdx.x & 63;
   const int64_t gw = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (gw >= total_frames) return;
-  // find the file (binary search over frame_base)
   int lo = 0, hi = n_files - 1;
   while (lo < hi) {
     const int mid = (lo + hi + 1) >> 1;
@@ -26,37 +28,62 @@ __global__ __launch_bounds__(256) void trim_frames_kernel(const float* sig, cons
     else hi = mid - 1;
   }
   const int f = lo;
-  const int64_t t = gw - frame_base[f];
-  const float* x = sig + file_off[f];
+  const int64_t b = gw - frame_base[f];
+  const int64_t off = file_off[f];
   const int64_t N = file_len[f];
-  const int64_t s0 = t * 512 - 1024;
+  const int64_t s0 = b * 512;
   double acc = 0.0;
-#pragma unroll 8
-  for (int j = lane; j < 2048; j += 64) {
-    const int64_t i = s0 + j;
-    const double v = (i >= 0 && i < N) ? (double)x[i] : 0.0;
-    acc = fma(v, v, acc);
+  if (s0 + 512 <= N && ((off + s0) & 3) == 0) {
+    const float4* x4 = reinterpret_cast<const float4*>(sig + off + s0);
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const float4 v = x4[lane + 64 * q];
+      acc = fma((double)v.x, (double)v.x, acc);
+      acc = fma((double)v.y, (double)v.y, acc);
+      acc = fma((double)v.z, (double)v.z, acc);
+      acc = fma((double)v.w, (double)v.w, acc);
+    }
+  } else {
+    const float* x = sig + off;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int64_t i = s0 + lane + 64 * q;
+      const double v = i < N ? (double)x[i] : 0.0;
+      acc = fma(v, v, acc);
+    }
   }
   acc = wave_sum(acc);
-  if (lane == 0) ms_out[gw] = (float)(acc / 2048.0);
+  if (lane == 0) blk[gw] = acc;
 }
 
-__global__ __launch_bounds__(256) void trim_bounds_kernel(const float* ms, const int64_t* frame_base,
+// ms[t] = mean of x^2 over the centred 2048-sample frame t = blocks t-2 .. t+1 (zero outside)
+__device__ __forceinline__ float trim_ms(const double* blk, int64_t nblk, int64_t t) {
+  double s = 0.0;
+#pragma unroll
+  for (int d = -2; d <= 1; ++d) {
+    const int64_t b = t + d;
+    if (b >= 0 && b < nblk) s += blk[b];
+  }
+  return (float)(s / 2048.0);
+}
+
+__global__ __launch_bounds__(256) void trim_bounds_kernel(const double* blk_all, const int64_t* frame_base,
                                                           const int64_t* file_len, float top_db,
                                                           int64_t* out_start, int64_t* out_end) {
   __shared__ BlockScratch<256> bs;
   const int f = blockIdx.x;
   const int64_t N = file_len[f];
   const int64_t T = 1 + N / 512;
-  const float* m = ms + frame_base[f];
+  const int64_t nblk = (N + 511) / 512;
+  const double* blk = blk_all + frame_base[f];
   double mx = -1.0;
-  for (int64_t t = threadIdx.x; t < T; t += 256) mx = fmax(mx, (double)sqrtf(m[t]));
+  for (int64_t t = threadIdx.x; t < T; t += 256) mx = fmax(mx, (double)sqrtf(trim_ms(blk, nblk, t)));
   mx = block_max<256>(mx, bs);
   const float ref = (float)mx;
   const float ref_db = 10.0f * log10f(fmaxf(1e-10f, ref * ref));
   int first = 0x7fffffff, last = -1;
   for (int64_t t = threadIdx.x; t < T; t += 256) {
-    const float r = sqrtf(m[t]);
+    const float r = sqrtf(trim_ms(blk, nblk, t));
     const float db = 10.0f * log10f(fmaxf(1e-10f, r * r)) - ref_db;
     if (db > -top_db) {
       first = min(first, (int)t);
@@ -79,7 +106,7 @@ __global__ __launch_bounds__(256) void trim_bounds_kernel(const float* ms, const
 size_t trim_ws_bytes(const int64_t* host_file_len, int n_files) {
   size_t frames = 0;
   for (int f = 0; f < n_files; ++f) frames += 1 + host_file_len[f] / 512;
-  return frames * sizeof(float) + (size_t)(n_files + 1) * sizeof(int64_t) + 256;
+  return frames * sizeof(double) + (size_t)(n_files + 1) * sizeof(int64_t) + 256;
 }
 
 // frame_base is computed on the device from file_len (exclusive scan, one block)
@@ -100,18 +127,21 @@ int launch_trim(Context& ctx, const float* sig, const int64_t* file_off, const i
   (void)ctx;
   if (n_files <= 0) return 0;
   // max_frames = total frames over all files (host knows the lengths)
-  const size_t need = (size_t)max_frames * sizeof(float) + (size_t)(n_files + 1) * sizeof(int64_t);
+  const size_t need = (size_t)max_frames * sizeof(double) + (size_t)(n_files + 1) * sizeof(int64_t);
   if (ws_bytes < need) {
     set_error("trim: workspace too small");
     return -3;
   }
   int64_t* frame_base = static_cast<int64_t*>(ws);
-  float* ms = reinterpret_cast<float*>(frame_base + n_files + 1);
+  double* blk = reinterpret_cast<double*>(frame_base + n_files + 1);
   hipLaunchKernelGGL(frame_base_kernel, dim3(1), dim3(64), 0, st, file_len, n_files, frame_base);
   const int64_t blocks = (max_frames + 3) / 4;
-  hipLaunchKernelGGL(trim_frames_kernel, dim3((unsigned)blocks), dim3(256), 0, st, sig, file_off, file_len,
-                     frame_base, n_files, max_frames, ms);
-  hipLaunchKernelGGL(trim_bounds_kernel, dim3(n_files), dim3(256), 0, st, ms, frame_base, file_len, top_db,
+  {
+    KTimer kt_(ctx, "trim_blocks", st);
+    hipLaunchKernelGGL(trim_blocks_kernel, dim3((unsigned)blocks), dim3(256), 0, st, sig, file_off, file_len,
+                       frame_base, n_files, max_frames, blk);
+  }
+  hipLaunchKernelGGL(trim_bounds_kernel, dim3(n_files), dim3(256), 0, st, blk, frame_base, file_len, top_db,
                      out_start, out_end);
   NC_HIP(hipGetLastError());
   return 0;

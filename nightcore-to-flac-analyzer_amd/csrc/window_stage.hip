@@ -172,7 +172,10 @@ int launch_window_stage(Context& ctx, const float* sig, const int64_t* win_off, 
     set_error("window stage: window too long for LDS");
     return -2;
   }
-  hipLaunchKernelGGL(window_tg_kernel, dim3(n_win), dim3(WT_THREADS), lds, st, a);
+  {
+    KTimer kt_(ctx, "window_tg", st);
+    hipLaunchKernelGGL(window_tg_kernel, dim3(n_win), dim3(WT_THREADS), lds, st, a);
+  }
   NC_HIP(hipGetLastError());
   return 0;
 }

@@ -51,6 +51,12 @@ def seed_state(seed: int) -> List[int]:
     return [(s >> 64) & m, s & m, (inc >> 64) & m, inc & m]
 
 
+def h2d(arr, dtype, dev: torch.device) -> torch.Tensor:
+    """Small host array -> device tensor through pinned memory, without a host sync."""
+    a = np.ascontiguousarray(np.asarray(arr, dtype=dtype).reshape(-1))
+    return torch.from_numpy(a).pin_memory().to(dev, non_blocking=True)
+
+
 def percentile_params(n_boot: int, ci: float) -> Tuple[float, float, float, float]:
     """(virtual index, gamma) of np.percentile(.., alpha*100) and (1-alpha)*100, 'linear'."""
     alpha = (1.0 - ci) / 2.0
@@ -82,7 +88,8 @@ class _Upload:
         host = np.zeros(max(16, total), dtype=np.uint8)
         for (_, a), o in zip(self.parts, offs):
             host[o:o + a.nbytes] = a.view(np.uint8)
-        d = torch.from_numpy(host).to(dev)
+        # pinned staging + async copy: never waits for work already queued on the stream
+        d = torch.from_numpy(host).pin_memory().to(dev, non_blocking=True)
         out = {}
         for (name, a), o in zip(self.parts, offs):
             t = d[o:o + max(a.nbytes, a.itemsize)].view(_TORCH_DTYPE[a.dtype.str])
@@ -172,6 +179,24 @@ class Engine:
         self.timers = None
         return out
 
+    KERNEL_TAGS = ("stft_mel", "window_tg", "tuning_peaks", "decimate", "cqt_chroma", "trim_blocks", "tempo_beat",
+                   "tg_slide")
+
+    def kernel_profile(self, on: bool) -> None:
+        """Enable/disable the library's per-kernel HIP-event timers (nc_profile_enable)."""
+        self.ctx.call("nc_profile_enable", 1 if on else 0)
+
+    def kernel_times(self) -> Dict[str, Tuple[float, int]]:
+        """{kernel tag: (total ms, launches)} since the last read (nc_profile_read); waits for them."""
+        import ctypes as C
+        out = {}
+        for tag in self.KERNEL_TAGS:
+            ms, n = C.c_double(0.0), C.c_int(0)
+            self.ctx.call("nc_profile_read", tag.encode(), C.byref(ms), C.byref(n))
+            if n.value:
+                out[tag] = (ms.value, n.value)
+        return out
+
     def upload_signals(self, arrays: Sequence[np.ndarray]) -> DeviceSignals:
         lens = np.array([len(a) for a in arrays], dtype=np.int64)
         offs = np.zeros(len(arrays), dtype=np.int64)
@@ -235,10 +260,16 @@ class Engine:
 
     # -------------------------------------------------------------- batched pipeline
     def analyze(self, pairs: Optional[Sequence[Tuple[np.ndarray, np.ndarray]]] = None, params: Params = None,
-                signals: Optional[DeviceSignals] = None) -> List[PairOutcome]:
+                signals: Optional[DeviceSignals] = None, group_pairs: int = 16) -> List[PairOutcome]:
         """Run pipeline.run's analysis for every (nc, src) pair.  ``signals``
         (files ordered nc_0, src_0, nc_1, src_1, ...) may be passed already
-        resident in HBM; otherwise ``pairs`` are uploaded."""
+        resident in HBM; otherwise ``pairs`` are uploaded.
+
+        After one trim pass over all files (the only blocking read-back), pairs
+        are processed in groups of ``group_pairs``: the whole device pipeline of
+        group g is queued (plans uploaded through pinned memory, results copied
+        back asynchronously) before the host assembles the results of group g-1,
+        so host assembly overlaps device work."""
         p = params or Params()
         if p.auto_align and p.src_trim_sec == 0.0:
             raise NotImplementedError("auto_align (xcorr.find_content_offset) is not on the MI355X path yet")
@@ -247,29 +278,48 @@ class Engine:
             for nc, src in pairs:
                 flat += [nc, src]
             signals = self.upload_signals(flat)
-        dev, st = self.dev, self.stream()
-        nF = signals.n_files
-        B = nF // 2
-        outs = [PairOutcome() for _ in range(B)]
+        B = signals.n_files // 2
+        start, end = self._trim_all(signals, p)
+        outs: List[PairOutcome] = []
+        pending = None
+        gp = max(1, int(group_pairs))
+        for g0 in range(0, B, gp):
+            g1 = min(B, g0 + gp)
+            sl = slice(2 * g0, 2 * g1)
+            sub = DeviceSignals(signals.buf, signals.off[sl], signals.length[sl])
+            nxt = self._launch_group(sub, p, start[sl].copy(), end[sl].copy())
+            if pending is not None:
+                outs += self._finish_group(pending)
+            pending = nxt
+        if pending is not None:
+            outs += self._finish_group(pending)
+        return outs
 
-        # ---------------------------------------------------------------- 1. trim (sync 1)
+    def _trim_all(self, signals: DeviceSignals, p: Params) -> Tuple[np.ndarray, np.ndarray]:
+        """io.strip_silence bounds of every file (sync 1)."""
+        nF = signals.n_files
+        if p.silence_strip_db is None:
+            return np.zeros(nF, np.int64), signals.length.copy()
+        dev, st = self.dev, self.stream()
         up = _Upload()
         up.add("off", signals.off, np.int64)
         up.add("len", signals.length, np.int64)
         d0 = up.commit(dev)
-        if p.silence_strip_db is not None:
-            tot_frames = int(np.sum(1 + signals.length // 512))
-            wsb = self.ctx.lib.nc_trim_workspace_bytes(
-                signals.length.ctypes.data_as(_native.P), nF)
-            ws = self.workspace("trim", wsb)
-            se = torch.empty(2 * nF, dtype=torch.int64, device=dev)
-            self.call("nc_trim_bounds", signals.buf.data_ptr(), d0["off"].data_ptr(), d0["len"].data_ptr(), nF,
-                      tot_frames, float(p.silence_strip_db), se[:nF].data_ptr(), se[nF:].data_ptr(),
-                      ws.data_ptr(), ws.numel(), st)
-            se_h = se.cpu().numpy()
-            start, end = se_h[:nF], se_h[nF:]
-        else:
-            start, end = np.zeros(nF, np.int64), signals.length.copy()
+        tot_frames = int(np.sum(1 + signals.length // 512))
+        wsb = self.ctx.lib.nc_trim_workspace_bytes(signals.length.ctypes.data_as(_native.P), nF)
+        ws = self.workspace("trim", wsb)
+        se = torch.empty(2 * nF, dtype=torch.int64, device=dev)
+        self.call("nc_trim_bounds", signals.buf.data_ptr(), d0["off"].data_ptr(), d0["len"].data_ptr(), nF,
+                  tot_frames, float(p.silence_strip_db), se[:nF].data_ptr(), se[nF:].data_ptr(),
+                  ws.data_ptr(), ws.numel(), st)
+        se_h = se.cpu().numpy()
+        return se_h[:nF].copy(), se_h[nF:].copy()
+
+    def _launch_group(self, signals: DeviceSignals, p: Params, start: np.ndarray, end: np.ndarray) -> dict:
+        """Queue the whole device pipeline of one group of pairs; returns the pending group."""
+        dev, st = self.dev, self.stream()
+        nF = signals.n_files
+        B = nF // 2
         f_off = signals.off + start
         f_len = end - start
         strip_len = f_len.copy()
@@ -452,7 +502,7 @@ class Engine:
         up.add("s_wsoff", s_wsoff or [0], np.int64)
         up.add("s_cap", s_caps or [1], np.int32)
         db = up.commit(dev)
-        nc_idx = torch.tensor([2 * b for b in range(B)], dtype=torch.long, device=dev)
+        nc_idx = torch.arange(0, nF, 2, dtype=torch.long, device=dev)
         src_idx = nc_idx + 1
         a_n = torch.cat([tcount[nc_idx], db["p_n"][:n_pitch_jobs]]).to(torch.int32)
         b_n = torch.cat([tcount[src_idx], db["p_n"][:n_pitch_jobs]]).to(torch.int32)
@@ -476,16 +526,31 @@ class Engine:
         if p.compute_ibi:
             ibi = self._ibi_pass(signals, d["f_off"], d["f_len"], f_len, prior, B)
 
-        # ---------------------------------------------------------------- 7. D2H (sync 2) + host assembly
-        host = {k: v.cpu().numpy() for k, v in dict(
-            energy=energy, active=active, bpm=bpm, nbeats=nbeats, lag=lag, margin=margin, prior=prior,
-            tcount=tcount, clag=clag, pvals=pvals, tuning=tuning, chroma=chroma, bout=bout, sout=sout).items()}
+        # ---------------------------------------------------------------- 7. async D2H into pinned buffers
+        dev_out = dict(energy=energy, active=active, bpm=bpm, nbeats=nbeats, lag=lag, margin=margin, prior=prior,
+                       tcount=tcount, clag=clag, pvals=pvals, tuning=tuning, chroma=chroma, bout=bout, sout=sout)
         if ibi is not None:
-            ibi = {k: (v.cpu().numpy() if isinstance(v, torch.Tensor) else v) for k, v in ibi.items()}
-        for b in range(B):
-            outs[b] = self._assemble_pair(b, p, host, ibi, starts, w0, w1, f_len, strip_len, lead, trail,
-                                          intro[b], win_n, pair_chunks, n_cp, nj, n_pitch_jobs)
-        return outs
+            dev_out.update({"ibi_" + k: v for k, v in ibi.items() if isinstance(v, torch.Tensor)})
+        host = {}
+        for k, v in dev_out.items():
+            h = torch.empty(v.shape, dtype=v.dtype, pin_memory=True)
+            h.copy_(v, non_blocking=True)
+            host[k] = h
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(dev))
+        return dict(p=p, host=host, event=ev, has_ibi=ibi is not None, starts=starts, w0=w0, w1=w1, f_len=f_len,
+                    strip_len=strip_len, lead=lead, trail=trail, intro=intro, win_n=win_n,
+                    pair_chunks=pair_chunks, n_cp=n_cp, nj=nj, n_pitch_jobs=n_pitch_jobs, B=B)
+
+    def _finish_group(self, g: dict) -> List[PairOutcome]:
+        """Wait for one group's results (sync 2 of that group) and assemble them on the host."""
+        g["event"].synchronize()
+        h = {k: v.numpy() for k, v in g["host"].items()}
+        ibi = {k[4:]: v for k, v in h.items() if k.startswith("ibi_")} if g["has_ibi"] else None
+        return [self._assemble_pair(b, g["p"], h, ibi, g["starts"], g["w0"], g["w1"], g["f_len"], g["strip_len"],
+                                    g["lead"], g["trail"], g["intro"][b], g["win_n"], g["pair_chunks"], g["n_cp"],
+                                    g["nj"], g["n_pitch_jobs"])
+                for b in range(g["B"])]
 
     # -------------------------------------------------------------- IBI pass (tempo.py:120-173)
     def ibi_core(self, buf, d_off, d_len, f_len, start_vals, pidx, hop: int = IBI_HOP, min_ibis: int = 4):
@@ -508,7 +573,7 @@ class Engine:
         ws = self.workspace("ibi_tg", wsb)
         self.call("nc_ibi_tempogram", onset.data_ptr(), fbase.data_ptr(), nF, total, fmax, hop, tg.data_ptr(),
                   ws.data_ptr(), ws.numel(), st)
-        lens = torch.tensor(frames, dtype=torch.int32, device=dev)
+        lens = h2d(frames, np.int32, dev)
         bpm = torch.zeros(nF, dtype=torch.float64, device=dev)
         lag = torch.zeros(nF, dtype=torch.int32, device=dev)
         nb = torch.zeros(nF, dtype=torch.int32, device=dev)
@@ -531,8 +596,8 @@ class Engine:
     def _ibi_pass(self, signals, d_off, d_len, f_len, prior, B):
         dev, st = self.dev, self.stream()
         nF = 2 * B
-        starts = torch.cat([prior[:B], torch.tensor([120.0], dtype=torch.float64, device=dev)])
-        pidx = torch.tensor([f // 2 if f % 2 == 0 else B for f in range(nF)], dtype=torch.int32, device=dev)
+        starts = torch.cat([prior[:B], torch.full((1,), 120.0, dtype=torch.float64, device=dev)])
+        pidx = h2d([f // 2 if f % 2 == 0 else B for f in range(nF)], np.int32, dev)
         core = self.ibi_core(signals.buf, d_off, d_len, f_len, starts, pidx)
         frames, fb_h, ibis, nibi = core["frames"], core["fbase_h"], core["ibis"], core["nibi"]
         nb, bpm, lag, mg = core["nbeats"], core["bpm"], core["lag"], core["margin"]
