@@ -137,7 +137,7 @@ struct PeakArgs {
 __global__ __launch_bounds__(TP_WAVES * 64) void tuning_peaks_kernel(PeakArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   float2* sh_tw = reinterpret_cast<float2*>(smem);
-  const int lane0 = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int lane0 = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform (SGPR)
   float2* fftbuf = sh_tw + ((TpTw::size + 1) & ~1) + wave * LdsSize<1024>::value;
   fill_staged_tw<1024>(sh_tw, a.tw, threadIdx.x, TP_WAVES * 64);
   __syncthreads();
@@ -183,12 +183,13 @@ __global__ __launch_bounds__(TP_WAVES * 64) void tuning_peaks_kernel(PeakArgs a)
     }
     wave_fft<1024, 0>(in, fftbuf, sh_tw, lane);
     float m1[9], m2[9];
+    const int pa = lpad(lane), pb = lpad(1024 - lane);
 #pragma unroll
     for (int m = 0; m < 9; ++m) {
       const int k = lane + 64 * m;
       if (k <= 512) {
         float2 X, XN;
-        rfft_split<0, TpTw::split>(fftbuf, sh_tw, 1024, k, X, XN);
+        rfft_split_m<1024, 0, TpTw::split>(fftbuf, sh_tw, lane, m, pa, pb, X, XN);
         m1[m] = hypotf(X.x, X.y);
         m2[m] = hypotf(XN.x, XN.y);
       }
@@ -409,13 +410,20 @@ struct CqtArgs {
   const int* cqt_off;
   const float2* cqt_w;
   const float* cqt_isl;
+  const int* cqt_plo;      // [tuning][64] lane pieces
+  const int* cqt_plen;
+  const int* cqt_poff;
+  const int* cqt_partner;  // [tuning][36]
+  int klo, khi;            // FFT bins the rows touch
   double* partial;  // [n][nblk][12]
 };
+
+constexpr int CQ_SPLIT_R = 2;  // split rounds: 64 * CQ_SPLIT_R >= khi - klo + 1 (checked at launch)
 
 __host__ __device__ __forceinline__ int cq_al4(int n) { return (n + 3) & ~3; }
 
 size_t cqt_lds_bytes(int maxnnz) {
-  return sizeof(float2) * (cq_al4(CqTw::size) + (size_t)cq_al4(maxnnz)) + sizeof(int) * 3 * 36 +
+  return sizeof(float2) * (cq_al4(CqTw::size) + (size_t)cq_al4(maxnnz)) + sizeof(int) * (3 * 64 + 64) +
          sizeof(float) * (kCqtBins + CQ_FR * kCqtBins + 2 * CQ_FR * 12) + 16 +
          sizeof(float2) * (size_t)CQ_WAVES * LdsSize<512>::value;
 }
@@ -426,11 +434,11 @@ __global__ __launch_bounds__(CQ_WAVES * 64) void cqt_chroma_kernel(CqtArgs a) {
   const int T = a.n_frames[c];
   const int t0 = fb * CQ_FR;
   if (t0 >= T) return;
-  const int tid = threadIdx.x, lane0 = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane0 = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform (SGPR)
   float2* sh_tw = reinterpret_cast<float2*>(smem);
   float2* sh_w = sh_tw + cq_al4(CqTw::size);
-  int* sh_desc = reinterpret_cast<int*>(sh_w + cq_al4(a.maxnnz));  // lo[36] len[36] off[36]
-  float* sh_isl = reinterpret_cast<float*>(sh_desc + 3 * 36);
+  int* sh_desc = reinterpret_cast<int*>(sh_w + cq_al4(a.maxnnz));  // lo[64] len[64] off[64] partner[64]
+  float* sh_isl = reinterpret_cast<float*>(sh_desc + 4 * 64);
   float* sh_row = sh_isl + kCqtBins;              // [CQ_FR][252]
   float* sh_ch = sh_row + CQ_FR * kCqtBins;       // [CQ_FR][12]
   float* sh_nv = sh_ch + CQ_FR * 12;              // [CQ_FR][12]
@@ -442,10 +450,11 @@ __global__ __launch_bounds__(CQ_WAVES * 64) void cqt_chroma_kernel(CqtArgs a) {
   const int nnz = a.cqt_off[ti * kCqtFilt + kCqtFilt - 1] + a.cqt_len[ti * kCqtFilt + kCqtFilt - 1] - woff0;
   fill_staged_tw<512>(sh_tw, a.tw, tid, CQ_WAVES * 64);
   for (int i = tid; i < nnz; i += CQ_WAVES * 64) sh_w[i] = a.cqt_w[woff0 + i];
-  for (int i = tid; i < kCqtFilt; i += CQ_WAVES * 64) {
-    sh_desc[i] = a.cqt_lo[ti * kCqtFilt + i];
-    sh_desc[36 + i] = a.cqt_len[ti * kCqtFilt + i];
-    sh_desc[72 + i] = a.cqt_off[ti * kCqtFilt + i] - woff0;
+  for (int i = tid; i < 64; i += CQ_WAVES * 64) {
+    sh_desc[i] = a.cqt_plo[ti * 64 + i];
+    sh_desc[64 + i] = a.cqt_plen[ti * 64 + i];
+    sh_desc[128 + i] = a.cqt_poff[ti * 64 + i];
+    sh_desc[192 + i] = i < kCqtFilt ? a.cqt_partner[ti * kCqtFilt + i] : -1;
   }
   for (int i = tid; i < kCqtBins; i += CQ_WAVES * 64) sh_isl[i] = a.cqt_isl[ti * kCqtBins + i];
   __syncthreads();
@@ -476,31 +485,44 @@ __global__ __launch_bounds__(CQ_WAVES * 64) void cqt_chroma_kernel(CqtArgs a) {
       }
     }
     wave_fft<512, 0>(in, fftbuf, sh_tw, lane);
-    float2 d1[5], d2[5];
+    // real split for the bins the rows touch only: X[k], k in [klo, khi] (all < 256)
+    float2 xk[CQ_SPLIT_R];
+    const int nk = a.khi - a.klo + 1;
 #pragma unroll
-    for (int m = 0; m < 5; ++m) {
-      const int k = lane + 64 * m;
-      if (k <= 256) rfft_split<0, CqTw::split>(fftbuf, sh_tw, 512, k, d1[m], d2[m]);
-    }
-    float2* D = fftbuf;  // reuse as D[0..512] unpadded
-#pragma unroll
-    for (int m = 0; m < 5; ++m) {
-      const int k = lane + 64 * m;
-      if (k <= 256) {
-        D[k] = d1[m];
-        D[512 - k] = d2[m];
+    for (int m = 0; m < CQ_SPLIT_R; ++m) {
+      const int k = a.klo + lane + 64 * m;
+      if (lane + 64 * m < nk) {
+        const float2 za = fftbuf[lpad(k)];
+        const float2 zb = cconj(fftbuf[lpad(512 - k)]);
+        const float2 E = cscale(cadd(za, zb), 0.5f);
+        const float2 O = cmul_mi(cscale(csub(za, zb), 0.5f));
+        xk[m] = cadd(E, cmul(sh_tw[CqTw::split + k], O));
       }
     }
-    if (lane < kCqtFilt) {
-      const int lo = sh_desc[lane], len = sh_desc[36 + lane], off = sh_desc[72 + lane];
+    float2* D = fftbuf;  // reuse as D[k] unpadded (all Z reads above precede these writes)
+#pragma unroll
+    for (int m = 0; m < CQ_SPLIT_R; ++m)
+      if (lane + 64 * m < nk) D[a.klo + lane + 64 * m] = xk[m];
+    {
+      // lane piece of a sparse row (complex64 accumulation in row order), then the
+      // row's second half (partner lane) is added to its first half
+      const int lo = sh_desc[lane], len = sh_desc[64 + lane], off = sh_desc[128 + lane];
       float re = 0.0f, im = 0.0f;
-#pragma unroll 4
+#pragma unroll 2
       for (int j = 0; j < len; ++j) {
         const float2 w = sh_w[off + j];
         const float2 d = D[lo + j];
         re = fmaf(w.x, d.x, fmaf(-w.y, d.y, re));
         im = fmaf(w.x, d.y, fmaf(w.y, d.x, im));
       }
+      const int partner = sh_desc[192 + lane];
+      const float re2 = __shfl(re, partner < 0 ? lane : partner, 64);
+      const float im2 = __shfl(im, partner < 0 ? lane : partner, 64);
+      if (partner >= 0) {
+        re += re2;
+        im += im2;
+      }
+      if (lane >= kCqtFilt) continue;
       const float oscale = sqrtf((float)(1 << oct));  // fft_basis *= sqrt(sr / my_sr)
       const int bin = kCqtBins - kCqtFilt * (oct + 1) + lane;
       sh_row[fl * kCqtBins + bin] = hypotf(re * oscale, im * oscale) * sh_isl[bin];
@@ -691,6 +713,16 @@ int launch_chroma_mean(Context& ctx, const float* sig, const int64_t* chunk_off,
   ca.cqt_off = ctx.t.cqt_off;
   ca.cqt_w = ctx.t.cqt_w;
   ca.cqt_isl = ctx.t.cqt_inv_sqrt_len;
+  ca.cqt_plo = ctx.t.cqt_plo;
+  ca.cqt_plen = ctx.t.cqt_plen;
+  ca.cqt_poff = ctx.t.cqt_poff;
+  ca.cqt_partner = ctx.t.cqt_partner;
+  ca.klo = ctx.t.cqt_klo;
+  ca.khi = ctx.t.cqt_khi;
+  if (ca.klo < 1 || ca.khi >= 256 || ca.khi - ca.klo + 1 > 64 * CQ_SPLIT_R) {
+    set_error("chroma: CQT basis bin range outside the split schedule");
+    return -2;
+  }
   ca.partial = w.partial;
   const int nblk = (int)((1 + max_chunk_len / 512 + CQ_FR - 1) / CQ_FR);
   {

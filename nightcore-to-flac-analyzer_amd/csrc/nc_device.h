@@ -123,6 +123,15 @@ struct DFT<4> {
   }
 };
 
+// Wave-uniform values the compiler cannot prove uniform (derived from the wave id or
+// from loads indexed by it): pin them to SGPRs so addressing stays scalar.
+__device__ __forceinline__ int uniform32(int v) { return __builtin_amdgcn_readfirstlane(v); }
+__device__ __forceinline__ int64_t uniform64(int64_t v) {
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)v);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)((uint64_t)v >> 32));
+  return (int64_t)(((uint64_t)hi << 32) | lo);
+}
+
 // ------------------------------------------------------------------ Stockham wave FFT
 __device__ __forceinline__ int lpad(int i) { return i + (i >> 4); }
 template <int N>
@@ -155,13 +164,21 @@ __device__ __forceinline__ void stockham_stage_regs(float2 (&v)[N / (R * NT)][R]
     DFT<R>::run(v[b]);
   }
   if (SYNC) __syncthreads();  // every thread has loaded this stage's inputs
+  // lpad(i + off) == lpad(i) + off * 17 / 16 whenever off % 16 == 0, so strides that
+  // are multiples of 16 become immediate LDS offsets instead of per-access index math
 #pragma unroll
   for (int b = 0; b < NB; ++b) {
     const int j = tid + NT * b;
     const int k = j % NS;
     const int base = (j / NS) * NS * R + k;
+    if constexpr (NS % 16 == 0) {
+      float2* p = lds + lpad(base);
 #pragma unroll
-    for (int r = 0; r < R; ++r) lds[lpad(base + r * NS)] = v[b][r];
+      for (int r = 0; r < R; ++r) p[r * NS * 17 / 16] = v[b][r];
+    } else {
+#pragma unroll
+      for (int r = 0; r < R; ++r) lds[lpad(base + r * NS)] = v[b][r];
+    }
   }
   if (SYNC) __syncthreads();
 }
@@ -170,11 +187,19 @@ template <int N, int R, int NS, int NT, bool SYNC, int TWN = 8192, int STO = 0>
 __device__ __forceinline__ void stockham_stage(float2* lds, const float2* __restrict__ tw, int tid) {
   constexpr int NB = N / (R * NT);
   float2 v[NB][R];
+  if constexpr (NT % 16 == 0 && (N / R) % 16 == 0) {
+    const float2* p = lds + lpad(tid);
 #pragma unroll
-  for (int b = 0; b < NB; ++b) {
-    const int j = tid + NT * b;
+    for (int b = 0; b < NB; ++b)
 #pragma unroll
-    for (int r = 0; r < R; ++r) v[b][r] = lds[lpad(j + r * (N / R))];
+      for (int r = 0; r < R; ++r) v[b][r] = p[(NT * b + r * (N / R)) * 17 / 16];
+  } else {
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+      const int j = tid + NT * b;
+#pragma unroll
+      for (int r = 0; r < R; ++r) v[b][r] = lds[lpad(j + r * (N / R))];
+    }
   }
   stockham_stage_regs<N, R, NS, NT, SYNC, TWN, STO>(v, lds, tw, tid);
 }
@@ -263,6 +288,24 @@ __device__ __forceinline__ void block_fft(FftIn<N, NT>& in, float2* lds, const f
 
 // Real-FFT split: Z = FFT_N(z), z[n] = x[2n] + i x[2n+1] (x real, length 2N).
 // Returns X[k] and X[N-k] for 0 <= k <= N/2.
+// rfft_split for k = lane + 64 m (m compile-time after unrolling) with the padded LDS
+// indices folded: pa = lpad(lane), pb = lpad(N - lane); Z[N-k] sits at pb - 68 m except
+// for k == 0, which wraps to Z[0].  Same arithmetic as rfft_split.
+template <int N, int TWN, int SPLIT>
+__device__ __forceinline__ void rfft_split_m(const float2* lds, const float2* __restrict__ tw, int lane, int m,
+                                             int pa, int pb, float2& Xk, float2& XNk) {
+  const int k = lane + 64 * m;
+  const float2 a = lds[pa + 68 * m];
+  const int ib = (m == 0 && lane == 0) ? 0 : pb - 68 * m;
+  const float2 b = cconj(lds[ib]);
+  const float2 E = cscale(cadd(a, b), 0.5f);
+  const float2 O = cmul_mi(cscale(csub(a, b), 0.5f));  // (a-b)/(2i)
+  const float2 W = TWN > 0 ? tw[(k * (TWN > 0 ? TWN / (2 * N) : 1)) & (TWN - 1)] : tw[SPLIT + k];
+  const float2 WO = cmul(W, O);
+  Xk = cadd(E, WO);
+  XNk = cconj(csub(E, WO));
+}
+
 template <int TWN = 8192, int SPLIT = 0>
 __device__ __forceinline__ void rfft_split(const float2* lds, const float2* __restrict__ tw, int N, int k,
                                            float2& Xk, float2& XNk) {

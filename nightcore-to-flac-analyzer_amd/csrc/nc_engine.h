@@ -42,6 +42,11 @@ struct Tables {
   float* cqt_inv_sqrt_len = nullptr;  // [kNTunings][252]  1/sqrt(lengths)
   int cqt_maxlen = 0;
   int cqt_maxnnz = 0;           // max over tunings of the 36 rows' total length
+  int* cqt_plo = nullptr;       // [kNTunings][64] lane pieces of the rows (see nc_tables.cpp)
+  int* cqt_plen = nullptr;
+  int* cqt_poff = nullptr;
+  int* cqt_partner = nullptr;   // [kNTunings][36] lane holding a row's second half, or -1
+  int cqt_klo = 0, cqt_khi = 0; // FFT bins any row touches (over all tunings)
   double* halfband = nullptr;   // 2K+1 taps
 };
 

@@ -272,6 +272,40 @@ void build_tables(Context& ctx) {
     }
     for (int ti = 0; ti < kNTunings; ++ti)
       t.cqt_maxnnz = std::max(t.cqt_maxnnz, coff[ti * nf + nf - 1] + clen[ti * nf + nf - 1] - coff[ti * nf]);
+    // 64-lane schedule of the 36 sparse rows: the (64 - 36) longest rows are split in two
+    // halves, the second half on a partner lane >= 36 (weight offsets relative to the
+    // tuning's first row); every lane then walks <= ceil(maxlen / 2) taps.
+    std::vector<int> plo(kNTunings * 64, 0), plen(kNTunings * 64, 0), poff(kNTunings * 64, 0);
+    std::vector<int> ppart(kNTunings * nf, -1);
+    t.cqt_klo = nbin;
+    t.cqt_khi = 0;
+    for (int ti = 0; ti < kNTunings; ++ti) {
+      std::vector<int> order(nf);
+      for (int f = 0; f < nf; ++f) order[f] = f;
+      std::stable_sort(order.begin(), order.end(),
+                       [&](int x, int y) { return clen[ti * nf + x] > clen[ti * nf + y]; });
+      std::vector<char> split(nf, 0);
+      for (int i = 0; i < 64 - nf && i < nf; ++i) split[order[i]] = 1;
+      int next = nf;
+      const int base = coff[ti * nf];
+      for (int f = 0; f < nf; ++f) {
+        const int lo = clo[ti * nf + f], len = clen[ti * nf + f], off = coff[ti * nf + f] - base;
+        t.cqt_klo = std::min(t.cqt_klo, lo);
+        t.cqt_khi = std::max(t.cqt_khi, lo + len - 1);
+        if (split[f]) {
+          const int h = (len + 1) / 2;
+          plo[ti * 64 + f] = lo, plen[ti * 64 + f] = h, poff[ti * 64 + f] = off;
+          plo[ti * 64 + next] = lo + h, plen[ti * 64 + next] = len - h, poff[ti * 64 + next] = off + h;
+          ppart[ti * nf + f] = next++;
+        } else {
+          plo[ti * 64 + f] = lo, plen[ti * 64 + f] = len, poff[ti * 64 + f] = off;
+        }
+      }
+    }
+    t.cqt_plo = upload(plo);
+    t.cqt_plen = upload(plen);
+    t.cqt_poff = upload(poff);
+    t.cqt_partner = upload(ppart);
     t.cqt_lo = upload(clo);
     t.cqt_len = upload(clen);
     t.cqt_off = upload(coff);
@@ -283,7 +317,8 @@ void build_tables(Context& ctx) {
 void free_tables(Context& ctx) {
   Tables& t = ctx.t;
   void* ptrs[] = {t.tw, t.hann2048, t.hann_ac512, t.hann_ac64, t.wsq512, t.wsq64, t.mel_lo,  t.mel_len, t.mel_off,
-                  t.mel_w,  t.cqt_lo,   t.cqt_len,    t.cqt_off,  t.cqt_w,   t.cqt_inv_sqrt_len, t.halfband};
+                  t.mel_w,  t.cqt_lo,   t.cqt_len,    t.cqt_off,  t.cqt_w,   t.cqt_inv_sqrt_len, t.halfband,
+                  t.cqt_plo, t.cqt_plen, t.cqt_poff, t.cqt_partner};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   t = Tables();

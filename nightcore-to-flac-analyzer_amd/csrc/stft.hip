@@ -48,7 +48,7 @@ __global__ __launch_bounds__(SM_THREADS) void stft_mel_kernel(StftMelArgs a) {
   float2* sh_tw = reinterpret_cast<float2*>(smem);
   float* sh_melw = reinterpret_cast<float*>(sh_tw + al4(SmTw::size));
   int* sh_mel = reinterpret_cast<int*>(sh_melw + al4(a.mel_nnz));  // lo[128] len[128] off[128]
-  const int lane0 = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int lane0 = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform (SGPR)
   float2* fftbuf = reinterpret_cast<float2*>(sh_mel + 3 * 128) + wave * LdsSize<1024>::value;
 
   fill_staged_tw<1024>(sh_tw, a.tw, threadIdx.x, SM_THREADS);
@@ -75,9 +75,11 @@ __global__ __launch_bounds__(SM_THREADS) void stft_mel_kernel(StftMelArgs a) {
       s = (int)(g / a.uniform_T);
       t = g - (int64_t)s * a.uniform_T;
     }
+    s = uniform32(s);
+    t = uniform64(t);
     if (a.active && !a.active[s]) continue;
-    L = a.seq_len ? a.seq_len[s] : a.uniform_len;
-    const int64_t off = a.seq_off[s];
+    L = uniform64(a.seq_len ? a.seq_len[s] : a.uniform_len);
+    const int64_t off = uniform64(a.seq_off[s]);
     const float* x = a.sig + off;
     const int64_t s0 = t * a.hop - 1024;
 
@@ -130,12 +132,13 @@ __global__ __launch_bounds__(SM_THREADS) void stft_mel_kernel(StftMelArgs a) {
     }
     wave_fft<1024, 0>(in, fftbuf, twl, lane);
     float p1[9], p2[9];
+    const int pa = lpad(lane), pb = lpad(1024 - lane);
 #pragma unroll
     for (int m = 0; m < 9; ++m) {
       const int k = lane + 64 * m;
       if (k <= 512) {
         float2 X, XN;
-        rfft_split<0, SmTw::split>(fftbuf, twl, 1024, k, X, XN);
+        rfft_split_m<1024, 0, SmTw::split>(fftbuf, twl, lane, m, pa, pb, X, XN);
         p1[m] = fmaf(X.x, X.x, X.y * X.y);
         p2[m] = fmaf(XN.x, XN.x, XN.y * XN.y);
       }

@@ -145,6 +145,8 @@ class Engine:
         self._ws: Dict[str, torch.Tensor] = {}
         self.num_cu = self.ctx.lib.nc_num_cu(self.ctx.h)
         self.timers: Optional[Dict[str, list]] = None
+        # the chroma chain runs on its own stream, concurrently with the window/tempo chain
+        self.chroma_stream = torch.cuda.Stream(self.dev)
 
     # -------------------------------------------------------------- plumbing
     def stream(self) -> int:
@@ -400,7 +402,33 @@ class Engine:
         up.add("f_len", f_len, np.int64)
         d = up.commit(dev)
 
-        # ---------------------------------------------------------------- 3. per-window stage
+        # ---------------------------------------------------------------- 3. chroma (stream 2)
+        # runs concurrently with the window/tempo chain; joined before the bootstraps
+        chroma = torch.zeros(max(1, n_chunks * 12), dtype=torch.float32, device=dev)
+        tuning = torch.zeros(max(1, n_chunks), dtype=torch.float32, device=dev)
+        clag = torch.zeros(max(1, n_cp), dtype=torch.int32, device=dev)
+        pvals = torch.zeros(max(1, 3 * n_cp), dtype=torch.float64, device=dev)   # [shift | nc_hz | src_hz]
+        s1, s2 = torch.cuda.current_stream(dev), self.chroma_stream
+        ev_plan = torch.cuda.Event()
+        ev_plan.record(s1)
+        s2.wait_event(ev_plan)
+        st2 = s2.cuda_stream
+        if n_chunks:
+            tot_len = int(np.sum(chunk_len))
+            wsb = self.ctx.lib.nc_chroma_workspace_bytes(self.ctx.h, n_chunks, tot_len)
+            ws_c = self.workspace("chroma", wsb)
+            ws_c.record_stream(s2)  # used on stream 2: not reusable until that work is done
+            self.call("nc_chroma_mean", signals.buf.data_ptr(), d["chunk_off"].data_ptr(), d["chunk_len"].data_ptr(),
+                      n_chunks, tot_len, int(max(chunk_len)), chroma.data_ptr(), tuning.data_ptr(), None,
+                      ws_c.data_ptr(), ws_c.numel(), st2)
+            self.call("nc_chroma_lag", chroma.data_ptr(), d["lag_src"].data_ptr(), d["lag_nc"].data_ptr(), n_cp,
+                      clag.data_ptr(), st2)
+            self.call("nc_pitch_hz", clag.data_ptr(), n_cp, pvals[0:n_cp].data_ptr(),
+                      pvals[n_cp:2 * n_cp].data_ptr(), pvals[2 * n_cp:3 * n_cp].data_ptr(), st2)
+        ev_chroma = torch.cuda.Event()
+        ev_chroma.record(s2)
+
+        # ---------------------------------------------------------------- 4. per-window stage
         f64 = dict(dtype=torch.float64, device=dev)
         i32 = dict(dtype=torch.int32, device=dev)
         onset = torch.empty(max(1, n_win * T), dtype=torch.float32, device=dev)
@@ -444,24 +472,8 @@ class Engine:
         else:
             prior.fill_(120.0)
 
-        # ---------------------------------------------------------------- 4. chroma
-        chroma = torch.zeros(max(1, n_chunks * 12), dtype=torch.float32, device=dev)
-        tuning = torch.zeros(max(1, n_chunks), dtype=torch.float32, device=dev)
-        clag = torch.zeros(max(1, n_cp), **i32)
-        pvals = torch.zeros(max(1, 3 * n_cp), **f64)   # [shift | nc_hz | src_hz]
-        if n_chunks:
-            tot_len = int(np.sum(chunk_len))
-            wsb = self.ctx.lib.nc_chroma_workspace_bytes(self.ctx.h, n_chunks, tot_len)
-            ws = self.workspace("chroma", wsb)
-            self.call("nc_chroma_mean", signals.buf.data_ptr(), d["chunk_off"].data_ptr(), d["chunk_len"].data_ptr(),
-                      n_chunks, tot_len, int(max(chunk_len)), chroma.data_ptr(), tuning.data_ptr(), None,
-                      ws.data_ptr(), ws.numel(), st)
-            self.call("nc_chroma_lag", chroma.data_ptr(), d["lag_src"].data_ptr(), d["lag_nc"].data_ptr(), n_cp,
-                      clag.data_ptr(), st)
-            self.call("nc_pitch_hz", clag.data_ptr(), n_cp, pvals[0:n_cp].data_ptr(),
-                      pvals[n_cp:2 * n_cp].data_ptr(), pvals[2 * n_cp:3 * n_cp].data_ptr(), st)
-
         # ---------------------------------------------------------------- 5. bootstraps (tempo + pitch, seed 42)
+        s1.wait_event(ev_chroma)
         n_boot = C.N_BOOTSTRAP
         il, gl, ih, gh = percentile_params(n_boot, C.CI_LEVEL)
         vals = torch.cat([tvals, pvals])
@@ -538,7 +550,8 @@ class Engine:
             host[k] = h
         ev = torch.cuda.Event()
         ev.record(torch.cuda.current_stream(dev))
-        return dict(p=p, host=host, event=ev, has_ibi=ibi is not None, starts=starts, w0=w0, w1=w1, f_len=f_len,
+        return dict(p=p, host=host, event=ev, keep=(d, chroma, tuning, clag, pvals), has_ibi=ibi is not None,
+                    starts=starts, w0=w0, w1=w1, f_len=f_len,
                     strip_len=strip_len, lead=lead, trail=trail, intro=intro, win_n=win_n,
                     pair_chunks=pair_chunks, n_cp=n_cp, nj=nj, n_pitch_jobs=n_pitch_jobs, B=B)
 
