@@ -63,20 +63,42 @@ def _pmc_traffic(kernel_tag):
     return best
 
 
-def cpu_baseline(nc, src):
-    """The oracle (oracle/refglue.py, a CPU port of the reference glue on the
-    numpy restatement of librosa) on ONE pair of the batch, single thread."""
+def _cpu_worker(args):
+    """One CPU worker: regenerate its pair (untimed), wait for the others, then time
+    oracle/refglue.run_arrays on it with BLAS/OMP limited to one thread."""
+    seconds, seed, barrier = args
     from threadpoolctl import threadpool_limits
+    from nightcore_analyzer import synth
     from oracle import refglue
-    with threadpool_limits(limits=1):
-        t0 = time.perf_counter()
-        res = refglue.run_arrays(nc, src, compute_ibi=False)
-        dt = time.perf_counter() - t0
+    nc, src = synth.make_pair(seconds, seed)
     nw = len(refglue.slice_windows(nc)) + len(refglue.slice_windows(src))
-    return {"value": nw / dt, "unit": "windows/s", "cores": 1, "kind": "port",
-            "sample": f"pair 0 of the batch (3-min pair: {nw} windows + 7 CQT chunk pairs + bootstraps), "
-                      f"oracle/refglue.run_arrays(compute_ibi=False), 1 thread, {dt:.1f} s",
-            "tempo_ratio": res["tempo_ratio"], "pitch_ratio": res["pitch_ratio"]}
+    ncp = len(refglue.chunk_plan(len(src), len(nc)))
+    barrier.wait()
+    with threadpool_limits(limits=1):
+        t0 = time.time()
+        res = refglue.run_arrays(nc, src, compute_ibi=False)
+        t1 = time.time()
+    return nw, t0, t1, res["tempo_ratio"], res["pitch_ratio"], ncp
+
+
+def cpu_baseline(seconds, base_seed, workers):
+    """The oracle (oracle/refglue.py, the CPU port of the reference glue on the numpy
+    restatement of librosa) on the first `workers` pairs of the batch, one pair per
+    process, one thread each (SURVEY.md §8d: process pool, BLAS threads = 1);
+    windows/s = all windows / (last finish - first start)."""
+    import multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    with ctx.Manager() as m:
+        barrier = m.Barrier(workers)
+        with ctx.Pool(workers) as pool:
+            rows = pool.map(_cpu_worker, [(seconds, base_seed + i, barrier) for i in range(workers)])
+    nw = sum(r[0] for r in rows)
+    wall = max(r[2] for r in rows) - min(r[1] for r in rows)
+    return {"value": nw / wall, "unit": "windows/s", "cores": workers, "kind": "port",
+            "sample": f"pairs 0..{workers - 1} of the batch ({nw} windows + {sum(r[5] for r in rows)} CQT chunk pairs + "
+                      f"bootstraps), oracle/refglue.run_arrays(compute_ibi=False), {workers} processes x 1 thread, "
+                      f"{wall:.1f} s wall, {sum(r[2] - r[1] for r in rows):.1f} s CPU",
+            "tempo_ratio": rows[0][3], "pitch_ratio": rows[0][4]}
 
 
 def main():
@@ -88,6 +110,7 @@ def main():
     ap.add_argument("--seconds", type=float, default=180.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-ibi", action="store_true")
+    ap.add_argument("--cpu-workers", type=int, default=8, help="CPU baseline processes (one pair each)")
     ap.add_argument("--workers", type=int, default=min(16, os.cpu_count() or 1))
     args = ap.parse_args()
 
@@ -205,7 +228,7 @@ def main():
         if ibi is not None:
             line["ibi_pass"] = ibi
         if world == 1 and not args.no_cpu_baseline:
-            line["cpu_baseline"] = cpu_baseline(*pairs[0])
+            line["cpu_baseline"] = cpu_baseline(args.seconds, 1000, args.cpu_workers)
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.barrier()
