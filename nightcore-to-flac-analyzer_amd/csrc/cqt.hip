@@ -79,18 +79,26 @@ __global__ __launch_bounds__(256) void decimate_kernel(const float* sig, const i
                                                        const int64_t* oct_off, const int64_t* oct_len,
                                                        float* ws_oct, int level, const double* __restrict__ taps) {
 #pragma clang fp contract(off)
-  constexpr int K = kHalfbandK;
-  __shared__ float tile[2 * DEC_OUT + 2 * K + 1];
+  constexpr int K = kHalfbandK;       // 23: taps j - K odd (24 of them) plus the centre
+  constexpr int H = (K + 1) / 2;      // 12
+  // in[2m - n] with n = j - K: the centre reads the even phase at m, odd n read the odd
+  // phase at m + c, c = (-n - 1) / 2 in [-H, H - 1].  Both phases are staged in LDS as f64
+  // (deinterleaved: consecutive lanes read consecutive words, no bank conflicts).
+  __shared__ double te[DEC_OUT];
+  __shared__ double to[DEC_OUT + 2 * H];
   const int c = blockIdx.y;
   const int64_t Lin = oct_len[c * 7 + level], Lout = oct_len[c * 7 + level + 1];
   const int64_t m0 = (int64_t)blockIdx.x * DEC_OUT;
   if (m0 >= Lout) return;
   const float* in = level == 0 ? sig + chunk_off[c] : ws_oct + oct_off[c * 7 + level];
   float* out = ws_oct + oct_off[c * 7 + level + 1];
-  const int64_t i0 = 2 * m0 - K;  // tile[u] = in[i0 + u]
-  for (int u = threadIdx.x; u < 2 * DEC_OUT + 2 * K + 1; u += 256) {
-    const int64_t i = i0 + u;
-    tile[u] = (i >= 0 && i < Lin) ? in[i] : 0.0f;
+  for (int u = threadIdx.x; u < DEC_OUT; u += 256) {
+    const int64_t i = 2 * (m0 + u);
+    te[u] = (i < Lin) ? (double)in[i] : 0.0;
+  }
+  for (int u = threadIdx.x; u < DEC_OUT + 2 * H; u += 256) {
+    const int64_t i = 2 * (m0 + u - H) + 1;  // odd phase at m0 + u - H
+    to[u] = (i >= 0 && i < Lin) ? (double)in[i] : 0.0;
   }
   __syncthreads();
 #pragma unroll
@@ -98,12 +106,15 @@ __global__ __launch_bounds__(256) void decimate_kernel(const float* sig, const i
     const int loc = threadIdx.x + 256 * q;
     const int64_t m = m0 + loc;
     if (m >= Lout) break;
-    const float* x = tile + 2 * loc + 2 * K;  // x[-j] = in[2m - (j - K)]
     double acc = 0.0;
 #pragma unroll
-    for (int j = 0; j <= 2 * K; ++j) {
-      if (((j - K) & 1) == 0 && j != K) continue;
-      acc = acc + taps[j] * (double)x[-j];
+    for (int j = 0; j <= 2 * K; ++j) {  // the oracle's order: ascending j, multiply then add
+      const int n = j - K;
+      if (n == 0) {
+        acc = acc + taps[j] * te[loc];
+      } else if (n & 1) {
+        acc = acc + taps[j] * to[loc + H + (-n - 1) / 2];
+      }
     }
     out[m] = (float)(acc * 1.4142135623730951);
   }

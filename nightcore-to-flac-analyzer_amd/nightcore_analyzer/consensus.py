@@ -107,9 +107,17 @@ class AnalysisResult:
 
 
 # --------------------------------------------------------------------------- host decisions
+def _median(values) -> float:
+    """np.median of a non-empty sequence of finite floats, bit for bit: the middle
+    element, or (a + b) / 2 of the two middle ones (numpy's mean of two values)."""
+    v = sorted(values)
+    m = len(v) // 2
+    return float(v[m]) if len(v) & 1 else (float(v[m - 1]) + float(v[m])) / 2.0
+
+
 def _valid(values: List[Optional[float]]) -> np.ndarray:
     """consensus.py:236-240: drop None / NaN / inf / non-positive."""
-    return np.array([v for v in values if v is not None and np.isfinite(v) and v > 0],
+    return np.array([v for v in values if v is not None and math.isfinite(v) and v > 0],
                     dtype=np.float64)
 
 
@@ -262,8 +270,8 @@ def assemble(src_pitches, nc_pitches, src_tempos, nc_tempos, *, nc_duration, src
         tempo_ratio = 1.0 / tempo_ratio
         tempo_ci = (1.0 / tempo_ci[1], 1.0 / tempo_ci[0])
         corrected = True
-    nc_med = float(np.median(nc_t)) if len(nc_t) > 0 else None
-    src_med = float(np.median(src_t)) if len(src_t) > 0 else None
+    nc_med = _median(nc_t.tolist()) if len(nc_t) > 0 else None
+    src_med = _median(src_t.tolist()) if len(src_t) > 0 else None
     return AnalysisResult(
         tempo_ratio=tempo_ratio, pitch_ratio=pitch_ratio, tempo_ci=tempo_ci, pitch_ci=pitch_ci,
         classification=_classify(tempo_ratio, pitch_ratio, tempo_ci, pitch_ci),

@@ -23,6 +23,7 @@ from __future__ import annotations
 
 import math
 import threading
+import time
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional, Sequence, Tuple
 
@@ -134,6 +135,21 @@ class Params:
     compute_ibi: bool = True
 
 
+def _group_bounds(B: int, group_pairs: int) -> List[Tuple[int, int]]:
+    """Pair groups of about group_pairs; the last one is halved so that the host
+    assembly left exposed after the final device work stays short."""
+    gp = max(1, int(group_pairs))
+    sizes = [gp] * (B // gp) + ([B % gp] if B % gp else [])
+    if len(sizes) > 1 and sizes[-1] >= 8:
+        last = sizes.pop()
+        sizes += [last - last // 2, last // 2]
+    out, g0 = [], 0
+    for n in sizes:
+        out.append((g0, g0 + n))
+        g0 += n
+    return out
+
+
 # ------------------------------------------------------------------------------ engine
 class Engine:
     def __init__(self, device: int = 0):
@@ -145,6 +161,7 @@ class Engine:
         self._ws: Dict[str, torch.Tensor] = {}
         self.num_cu = self.ctx.lib.nc_num_cu(self.ctx.h)
         self.timers: Optional[Dict[str, list]] = None
+        self.host_stats: Optional[Dict[str, float]] = None  # {phase: seconds} when enabled
         # the chroma chain runs on its own stream, concurrently with the window/tempo chain
         self.chroma_stream = torch.cuda.Stream(self.dev)
 
@@ -281,15 +298,20 @@ class Engine:
                 flat += [nc, src]
             signals = self.upload_signals(flat)
         B = signals.n_files // 2
+        hs = self.host_stats
+        t0 = time.perf_counter()
         start, end = self._trim_all(signals, p)
+        if hs is not None:
+            hs["trim"] = hs.get("trim", 0.0) + time.perf_counter() - t0
         outs: List[PairOutcome] = []
         pending = None
-        gp = max(1, int(group_pairs))
-        for g0 in range(0, B, gp):
-            g1 = min(B, g0 + gp)
+        for g0, g1 in _group_bounds(B, group_pairs):
             sl = slice(2 * g0, 2 * g1)
             sub = DeviceSignals(signals.buf, signals.off[sl], signals.length[sl])
+            t0 = time.perf_counter()
             nxt = self._launch_group(sub, p, start[sl].copy(), end[sl].copy())
+            if hs is not None:
+                hs["launch"] = hs.get("launch", 0.0) + time.perf_counter() - t0
             if pending is not None:
                 outs += self._finish_group(pending)
             pending = nxt
@@ -557,13 +579,25 @@ class Engine:
 
     def _finish_group(self, g: dict) -> List[PairOutcome]:
         """Wait for one group's results (sync 2 of that group) and assemble them on the host."""
+        hs = self.host_stats
+        t0 = time.perf_counter()
         g["event"].synchronize()
+        t1 = time.perf_counter()
         h = {k: v.numpy() for k, v in g["host"].items()}
+        # python-list views for the scalar accesses of the per-pair assembly loops
+        for k in ("active", "bpm", "nbeats", "prior", "clag", "pvals", "bout", "sout"):
+            h[k + "_l"] = h[k].tolist()
+        g["starts_l"] = [x.tolist() for x in g["starts"]]
+        g["w0"], g["w1"] = g["w0"].tolist(), g["w1"].tolist()
         ibi = {k[4:]: v for k, v in h.items() if k.startswith("ibi_")} if g["has_ibi"] else None
-        return [self._assemble_pair(b, g["p"], h, ibi, g["starts"], g["w0"], g["w1"], g["f_len"], g["strip_len"],
-                                    g["lead"], g["trail"], g["intro"][b], g["win_n"], g["pair_chunks"], g["n_cp"],
-                                    g["nj"], g["n_pitch_jobs"])
-                for b in range(g["B"])]
+        out = [self._assemble_pair(b, g["p"], h, ibi, g["starts_l"], g["w0"], g["w1"], g["f_len"], g["strip_len"],
+                                   g["lead"], g["trail"], g["intro"][b], g["win_n"], g["pair_chunks"], g["n_cp"],
+                                   g["nj"], g["n_pitch_jobs"])
+               for b in range(g["B"])]
+        if hs is not None:
+            hs["wait"] = hs.get("wait", 0.0) + t1 - t0
+            hs["assemble"] = hs.get("assemble", 0.0) + time.perf_counter() - t1
+        return out
 
     # -------------------------------------------------------------- IBI pass (tempo.py:120-173)
     def ibi_core(self, buf, d_off, d_len, f_len, start_vals, pidx, hop: int = IBI_HOP, min_ibis: int = 4):
@@ -658,7 +692,7 @@ class Engine:
         L(f"Slicing into {p.window_sec:.0f} s windows (hop {p.hop_sec:.0f} s)…")
         L(f"  nightcore: {len(starts[fn])} windows  |  source: {len(starts[fs])} windows")
         L(f"Energy gating (threshold {p.energy_gate_db} dB below peak)…")
-        act = h["active"]
+        act = h["active_l"]
         src_w = [w for w in range(w0[fs], w1[fs]) if act[w]]
         nc_w = [w for w in range(w0[fn], w1[fn]) if act[w]]
         L(f"  after gating — nightcore: {len(nc_w)} windows  |  source: {len(src_w)} windows")
@@ -676,14 +710,15 @@ class Engine:
             L("Estimating pitch (chromagram cross-correlation)…")
             c0, c1 = pair_chunks[b]
             n = c1 - c0
-            lags = h["clag"][c0:c1].astype(int).tolist()
+            lags = h["clag_l"][c0:c1]
             shifts = h["pvals"][c0:c1]
-            src_p = h["pvals"][2 * n_cp + c0:2 * n_cp + c1].tolist()
-            nc_p = h["pvals"][n_cp + c0:n_cp + c1].tolist()
-            point_st = float(np.median(shifts))
+            pv = h["pvals_l"]
+            src_p = pv[2 * n_cp + c0:2 * n_cp + c1]
+            nc_p = pv[n_cp + c0:n_cp + c1]
+            point_st = C._median(shifts.tolist())
             if n >= MIN_CHUNKS:
                 j = b
-                lo_st, hi_st = float(h["sout"][n_pitch_jobs + j]), float(h["sout"][2 * n_pitch_jobs + j])
+                lo_st, hi_st = h["sout_l"][n_pitch_jobs + j], h["sout_l"][2 * n_pitch_jobs + j]
             else:
                 lo_st = hi_st = point_st
                 L(f"    Only {n} chunk(s) available (need ≥ {MIN_CHUNKS}) — "
@@ -694,7 +729,8 @@ class Engine:
             L("  Pitch method: chroma_xcorr")
             method = "chroma_xcorr"
             pj = len(w0) // 2 + b     # pitch job index: after the B tempo jobs
-            pitch_boot = (float(h["bout"][pj]), (float(h["bout"][nj + pj]), float(h["bout"][2 * nj + pj])))
+            bo = h["bout_l"]
+            pitch_boot = (bo[pj], (bo[nj + pj], bo[2 * nj + pj]))
             out.detail.update(chunk_lags=lags, tuning=h["tuning"][2 * c0:2 * c1].copy(),
                               chroma=h["chroma"][24 * c0:24 * c1].reshape(-1, 12).copy())
         else:
@@ -708,26 +744,29 @@ class Engine:
             if side == "src":
                 L("  ← source →")
             vals = []
+            f = fs if side == "src" else fn
+            st_f, base = starts[f], w0[f]
+            bpm_l, nb_l, nws = h["bpm_l"], h["nbeats_l"], len(ws_)
             for i, w in enumerate(ws_):
-                f = fs if side == "src" else fn
-                s0 = starts[f][w - w0[f]]
-                L(f"    tempo window {i + 1}/{len(ws_)}  [{s0 / SR:.1f}–{(s0 + win_n) / SR:.1f} s]")
-                vals.append(float(h["bpm"][w]) if h["nbeats"][w] >= MIN_BEATS else None)
+                s0 = st_f[w - base]
+                L(f"    tempo window {i + 1}/{nws}  [{s0 / SR:.1f}–{(s0 + win_n) / SR:.1f} s]")
+                vals.append(bpm_l[w] if nb_l[w] >= MIN_BEATS else None)
             L(f"    {sum(1 for v in vals if v is not None)}/{len(ws_)} windows yielded a confident tempo estimate")
             tempos[side] = vals
             if side == "src":
                 valid_src = [t for t in vals if t is not None]
                 nc_dur, src_dur = nc_len / SR, src_len / SR
                 if valid_src and nc_dur > 0 and src_dur > 0:
-                    med = float(np.median(valid_src))
-                    L(f"  NC tempo prior: {h['prior'][b]:.1f} BPM  "
+                    med = C._median(valid_src)
+                    L(f"  NC tempo prior: {h['prior_l'][b]:.1f} BPM  "
                       f"(src median {med:.1f} BPM × dur ratio {src_dur / nc_dur:.4f})")
                 L("  ← nightcore →")
-        out.detail.update(src_tempos=tempos["src"], nc_tempos=tempos["nc"], nc_start_bpm=float(h["prior"][b]),
+        out.detail.update(src_tempos=tempos["src"], nc_tempos=tempos["nc"], nc_start_bpm=h["prior_l"][b],
                           tempo_margin_src=h["margin"][src_w].copy(), tempo_margin_nc=h["margin"][nc_w].copy())
         L("Computing consensus…")
         try:
-            tempo_boot = (float(h["bout"][b]), (float(h["bout"][nj + b]), float(h["bout"][2 * nj + b])))
+            bo = h["bout_l"]
+            tempo_boot = (bo[b], (bo[nj + b], bo[2 * nj + b]))
             res = C.assemble(src_p, nc_p, tempos["src"], tempos["nc"], nc_duration=nc_len / SR,
                              src_duration=src_len / SR, pitch_boot=pitch_boot, tempo_boot=tempo_boot)
         except ValueError as exc:

@@ -98,3 +98,20 @@ def test_export_schema_roundtrip(tmp_path, golden_units):
     export.export_csv(r, tmp_path / "r.csv")
     header = (tmp_path / "r.csv").read_text().splitlines()[0].split(",")
     assert header[0] == "classification" and header[-1] == "warnings" and len(header) == 24
+
+
+def test_median_is_numpy_median_bit_for_bit():
+    rng = np.random.default_rng(3)
+    for n in range(1, 80):
+        x = rng.random(n) * 300.0
+        assert C._median(x.tolist()) == float(np.median(x))
+    assert C._median([2583.984375 / 21] * 4) == 2583.984375 / 21
+
+
+def test_pair_groups_cover_the_batch_in_order():
+    from nightcore_analyzer.engine import _group_bounds
+    for B in (1, 7, 16, 17, 40, 64, 100):
+        g = _group_bounds(B, 16)
+        assert g[0][0] == 0 and g[-1][1] == B
+        assert all(a1 == b0 for (a0, a1), (b0, b1) in zip(g, g[1:]))
+        assert all(b > a for a, b in g)
