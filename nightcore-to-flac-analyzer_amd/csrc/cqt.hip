@@ -73,7 +73,9 @@ __global__ void chroma_plan_kernel(const int64_t* chunk_len, int n, int64_t* oct
 // One workgroup per DEC_OUT outputs; the 2 DEC_OUT + 2K input tile is staged in LDS and the
 // taps are wave-uniform (scalar loads); the zero taps of the half-band (even j - K != 0) are
 // skipped at compile time.
-constexpr int DEC_OUT = 1024;
+constexpr int DEC_OUT = 1024;  // outputs per workgroup: 4 consecutive per thread
+
+__device__ __forceinline__ int dec_pad(int e) { return e + (e >> 3); }  // softens stride-4 bank reuse
 
 __global__ __launch_bounds__(256) void decimate_kernel(const float* sig, const int64_t* chunk_off,
                                                        const int64_t* oct_off, const int64_t* oct_len,
@@ -81,42 +83,60 @@ __global__ __launch_bounds__(256) void decimate_kernel(const float* sig, const i
 #pragma clang fp contract(off)
   constexpr int K = kHalfbandK;       // 23: taps j - K odd (24 of them) plus the centre
   constexpr int H = (K + 1) / 2;      // 12
+  constexpr int W = 4 + 2 * H - 1;    // odd-phase window of 4 consecutive outputs: 27 values
   // in[2m - n] with n = j - K: the centre reads the even phase at m, odd n read the odd
-  // phase at m + c, c = (-n - 1) / 2 in [-H, H - 1].  Both phases are staged in LDS as f64
-  // (deinterleaved: consecutive lanes read consecutive words, no bank conflicts).
-  __shared__ double te[DEC_OUT];
-  __shared__ double to[DEC_OUT + 2 * H];
+  // phase at m + c, c = (-n - 1) / 2 in [-H, H - 1].  Both phases are staged in LDS as f64;
+  // one float2 load fetches one even and one odd sample (coalesced, every input read once).
+  __shared__ double te[DEC_OUT + DEC_OUT / 8];
+  __shared__ double to[DEC_OUT + 2 * H + (DEC_OUT + 2 * H) / 8 + 1];
   const int c = blockIdx.y;
   const int64_t Lin = oct_len[c * 7 + level], Lout = oct_len[c * 7 + level + 1];
   const int64_t m0 = (int64_t)blockIdx.x * DEC_OUT;
   if (m0 >= Lout) return;
   const float* in = level == 0 ? sig + chunk_off[c] : ws_oct + oct_off[c * 7 + level];
   float* out = ws_oct + oct_off[c * 7 + level + 1];
-  for (int u = threadIdx.x; u < DEC_OUT; u += 256) {
-    const int64_t i = 2 * (m0 + u);
-    te[u] = (i < Lin) ? (double)in[i] : 0.0;
-  }
+  // pair p = (in[2p], in[2p + 1]) for p in [m0 - H, m0 + DEC_OUT + H); to[u] = odd phase at m0 - H + u
+  const bool vec = ((reinterpret_cast<uintptr_t>(in) & 7) == 0);
   for (int u = threadIdx.x; u < DEC_OUT + 2 * H; u += 256) {
-    const int64_t i = 2 * (m0 + u - H) + 1;  // odd phase at m0 + u - H
-    to[u] = (i >= 0 && i < Lin) ? (double)in[i] : 0.0;
+    const int64_t pidx = m0 - H + u;
+    const int64_t i = 2 * pidx;
+    double e = 0.0, o = 0.0;
+    if (vec && i >= 0 && i + 1 < Lin) {
+      const float2 v = reinterpret_cast<const float2*>(in)[pidx];
+      e = (double)v.x;
+      o = (double)v.y;
+    } else {
+      if (i >= 0 && i < Lin) e = (double)in[i];
+      if (i + 1 >= 0 && i + 1 < Lin) o = (double)in[i + 1];
+    }
+    if (u >= H && u < H + DEC_OUT) te[dec_pad(u - H)] = e;
+    to[dec_pad(u)] = o;
   }
   __syncthreads();
+  const int l0 = 4 * threadIdx.x;
+  double xo[W], xe[4];
 #pragma unroll
-  for (int q = 0; q < DEC_OUT / 256; ++q) {
-    const int loc = threadIdx.x + 256 * q;
-    const int64_t m = m0 + loc;
-    if (m >= Lout) break;
-    double acc = 0.0;
+  for (int i = 0; i < W; ++i) xo[i] = to[dec_pad(l0 + i)];
 #pragma unroll
-    for (int j = 0; j <= 2 * K; ++j) {  // the oracle's order: ascending j, multiply then add
-      const int n = j - K;
-      if (n == 0) {
-        acc = acc + taps[j] * te[loc];
-      } else if (n & 1) {
-        acc = acc + taps[j] * to[loc + H + (-n - 1) / 2];
-      }
-    }
-    out[m] = (float)(acc * 1.4142135623730951);
+  for (int q = 0; q < 4; ++q) xe[q] = te[dec_pad(l0 + q)];
+  double acc[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+  for (int j = 0; j <= 2 * K; ++j) {  // the oracle's order: ascending j, multiply then add
+    const int n = j - K;
+    if (n != 0 && !(n & 1)) continue;
+    const double h = taps[j];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) acc[q] = acc[q] + h * (n == 0 ? xe[q] : xo[q + H + (-n - 1) / 2]);
+  }
+  const int64_t m = m0 + l0;
+  if (m + 3 < Lout && ((reinterpret_cast<uintptr_t>(out + m) & 15) == 0)) {
+    *reinterpret_cast<float4*>(out + m) =
+        make_float4((float)(acc[0] * 1.4142135623730951), (float)(acc[1] * 1.4142135623730951),
+                    (float)(acc[2] * 1.4142135623730951), (float)(acc[3] * 1.4142135623730951));
+  } else {
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      if (m + q < Lout) out[m + q] = (float)(acc[q] * 1.4142135623730951);
   }
 }
 
@@ -414,17 +434,18 @@ struct CqtArgs {
   const int* tuning_idx;
   const float* ws_oct;
   const int64_t* tf_base;  // partial rows of chunk c start at tf_base[c] / CQ_FR + c
-  int maxnnz;
   const float2* tw;
   const int* cqt_lo;
   const int* cqt_len;
   const int* cqt_off;
   const float2* cqt_w;
   const float* cqt_isl;
-  const int* cqt_plo;      // [tuning][64] lane pieces
+  const int* cqt_plo;      // [tuning][64] lane pieces (nc_tables.cpp)
   const int* cqt_plen;
-  const int* cqt_poff;
-  const int* cqt_partner;  // [tuning][36]
+  const int* cqt_partner;  // [tuning][64]
+  const int* cqt_pfilt;    // [tuning][64]
+  const float2* cqt_wcol;  // [tuning][pmax][64]
+  int pmax;
   int klo, khi;            // FFT bins the rows touch
   double* partial;  // [n][nblk][12]
 };
@@ -433,8 +454,8 @@ constexpr int CQ_SPLIT_R = 2;  // split rounds: 64 * CQ_SPLIT_R >= khi - klo + 1
 
 __host__ __device__ __forceinline__ int cq_al4(int n) { return (n + 3) & ~3; }
 
-size_t cqt_lds_bytes(int maxnnz) {
-  return sizeof(float2) * (cq_al4(CqTw::size) + (size_t)cq_al4(maxnnz)) + sizeof(int) * (3 * 64 + 64) +
+size_t cqt_lds_bytes(int pmax) {
+  return sizeof(float2) * (cq_al4(CqTw::size) + (size_t)pmax * 64) + sizeof(int) * 4 * 64 +
          sizeof(float) * (kCqtBins + CQ_FR * kCqtBins + 2 * CQ_FR * 12) + 16 +
          sizeof(float2) * (size_t)CQ_WAVES * LdsSize<512>::value;
 }
@@ -447,8 +468,8 @@ __global__ __launch_bounds__(CQ_WAVES * 64) void cqt_chroma_kernel(CqtArgs a) {
   if (t0 >= T) return;
   const int tid = threadIdx.x, lane0 = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform (SGPR)
   float2* sh_tw = reinterpret_cast<float2*>(smem);
-  float2* sh_w = sh_tw + cq_al4(CqTw::size);
-  int* sh_desc = reinterpret_cast<int*>(sh_w + cq_al4(a.maxnnz));  // lo[64] len[64] off[64] partner[64]
+  float2* sh_w = sh_tw + cq_al4(CqTw::size);                     // [pmax][64] column-major weights
+  int* sh_desc = reinterpret_cast<int*>(sh_w + a.pmax * 64);      // lo[64] len[64] partner[64] filt[64]
   float* sh_isl = reinterpret_cast<float*>(sh_desc + 4 * 64);
   float* sh_row = sh_isl + kCqtBins;              // [CQ_FR][252]
   float* sh_ch = sh_row + CQ_FR * kCqtBins;       // [CQ_FR][12]
@@ -457,15 +478,13 @@ __global__ __launch_bounds__(CQ_WAVES * 64) void cqt_chroma_kernel(CqtArgs a) {
   const int fft_f = cq_al4((int)(sh_nv + CQ_FR * 12 - reinterpret_cast<float*>(smem)));
   float2* fftbuf = reinterpret_cast<float2*>(reinterpret_cast<float*>(smem) + fft_f) + wave * LdsSize<512>::value;
   const int ti = a.tuning_idx[c];
-  const int woff0 = a.cqt_off[ti * kCqtFilt];
-  const int nnz = a.cqt_off[ti * kCqtFilt + kCqtFilt - 1] + a.cqt_len[ti * kCqtFilt + kCqtFilt - 1] - woff0;
   fill_staged_tw<512>(sh_tw, a.tw, tid, CQ_WAVES * 64);
-  for (int i = tid; i < nnz; i += CQ_WAVES * 64) sh_w[i] = a.cqt_w[woff0 + i];
+  for (int i = tid; i < a.pmax * 64; i += CQ_WAVES * 64) sh_w[i] = a.cqt_wcol[(size_t)ti * a.pmax * 64 + i];
   for (int i = tid; i < 64; i += CQ_WAVES * 64) {
     sh_desc[i] = a.cqt_plo[ti * 64 + i];
     sh_desc[64 + i] = a.cqt_plen[ti * 64 + i];
-    sh_desc[128 + i] = a.cqt_poff[ti * 64 + i];
-    sh_desc[192 + i] = i < kCqtFilt ? a.cqt_partner[ti * kCqtFilt + i] : -1;
+    sh_desc[128 + i] = a.cqt_partner[ti * 64 + i];
+    sh_desc[192 + i] = a.cqt_pfilt[ti * 64 + i];
   }
   for (int i = tid; i < kCqtBins; i += CQ_WAVES * 64) sh_isl[i] = a.cqt_isl[ti * kCqtBins + i];
   __syncthreads();
@@ -517,25 +536,26 @@ __global__ __launch_bounds__(CQ_WAVES * 64) void cqt_chroma_kernel(CqtArgs a) {
     {
       // lane piece of a sparse row (complex64 accumulation in row order), then the
       // row's second half (partner lane) is added to its first half
-      const int lo = sh_desc[lane], len = sh_desc[64 + lane], off = sh_desc[128 + lane];
+      const int lo = sh_desc[lane], len = sh_desc[64 + lane];
       float re = 0.0f, im = 0.0f;
 #pragma unroll 2
       for (int j = 0; j < len; ++j) {
-        const float2 w = sh_w[off + j];
+        const float2 w = sh_w[j * 64 + lane];
         const float2 d = D[lo + j];
         re = fmaf(w.x, d.x, fmaf(-w.y, d.y, re));
         im = fmaf(w.x, d.y, fmaf(w.y, d.x, im));
       }
-      const int partner = sh_desc[192 + lane];
+      const int partner = sh_desc[128 + lane];
       const float re2 = __shfl(re, partner < 0 ? lane : partner, 64);
       const float im2 = __shfl(im, partner < 0 ? lane : partner, 64);
       if (partner >= 0) {
         re += re2;
         im += im2;
       }
-      if (lane >= kCqtFilt) continue;
+      const int filt = sh_desc[192 + lane];
+      if (filt < 0) continue;
       const float oscale = sqrtf((float)(1 << oct));  // fft_basis *= sqrt(sr / my_sr)
-      const int bin = kCqtBins - kCqtFilt * (oct + 1) + lane;
+      const int bin = kCqtBins - kCqtFilt * (oct + 1) + filt;
       sh_row[fl * kCqtBins + bin] = hypotf(re * oscale, im * oscale) * sh_isl[bin];
     }
   }
@@ -717,7 +737,6 @@ int launch_chroma_mean(Context& ctx, const float* sig, const int64_t* chunk_off,
   ca.tuning_idx = w.tuning_idx;
   ca.ws_oct = w.ws_oct;
   ca.tf_base = w.tf_base;
-  ca.maxnnz = ctx.t.cqt_maxnnz;
   ca.tw = ctx.t.tw;
   ca.cqt_lo = ctx.t.cqt_lo;
   ca.cqt_len = ctx.t.cqt_len;
@@ -726,8 +745,10 @@ int launch_chroma_mean(Context& ctx, const float* sig, const int64_t* chunk_off,
   ca.cqt_isl = ctx.t.cqt_inv_sqrt_len;
   ca.cqt_plo = ctx.t.cqt_plo;
   ca.cqt_plen = ctx.t.cqt_plen;
-  ca.cqt_poff = ctx.t.cqt_poff;
   ca.cqt_partner = ctx.t.cqt_partner;
+  ca.cqt_pfilt = ctx.t.cqt_pfilt;
+  ca.cqt_wcol = ctx.t.cqt_wcol;
+  ca.pmax = ctx.t.cqt_pmax;
   ca.klo = ctx.t.cqt_klo;
   ca.khi = ctx.t.cqt_khi;
   if (ca.klo < 1 || ca.khi >= 256 || ca.khi - ca.klo + 1 > 64 * CQ_SPLIT_R) {
@@ -738,7 +759,7 @@ int launch_chroma_mean(Context& ctx, const float* sig, const int64_t* chunk_off,
   const int nblk = (int)((1 + max_chunk_len / 512 + CQ_FR - 1) / CQ_FR);
   {
     KTimer kt_(ctx, "cqt_chroma", st);
-    hipLaunchKernelGGL(cqt_chroma_kernel, dim3(nblk, n), dim3(CQ_WAVES * 64), cqt_lds_bytes(ca.maxnnz), st, ca);
+    hipLaunchKernelGGL(cqt_chroma_kernel, dim3(nblk, n), dim3(CQ_WAVES * 64), cqt_lds_bytes(ca.pmax), st, ca);
   }
   hipLaunchKernelGGL(chroma_finalize_kernel, dim3(n), dim3(64), 0, st, w.partial, w.tf_base, w.n_frames, n,
                      out_chroma);

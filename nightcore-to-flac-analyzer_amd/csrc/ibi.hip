@@ -143,12 +143,17 @@ __global__ __launch_bounds__(TG_KB) void tg_slide_kernel(TgSlideArgs a) {
   for (int i = threadIdx.x; i < t1 - t0 + N; i += TG_KB) sh_x[i] = xf[i];
   for (int i = threadIdx.x; i < t1 - t0; i += TG_KB) sh_r[i] = a.rinv[base + t0 + i];
   __syncthreads();
+  // lags k and N-1-k per thread (two interleaved recurrences, balanced start-up sums)
   const int k = blockIdx.x * TG_KB + threadIdx.x;
-  if (k >= N) return;
+  if (k >= (N + 1) / 2) return;
   auto xl = [&](int i) { return sh_x[i]; };
   auto rl = [&](int t) { return sh_r[t]; };
-  const double acc = slide_lag_sum(xl, rl, N, k, 0, t1 - t0);
-  a.slab[((size_t)f * a.n_tblk + tb) * N + k] = acc;
+  const int kb = N - 1 - k;
+  double sa, sb;
+  slide_lag_sum2(xl, rl, N, k, kb, 0, t1 - t0, sa, sb);
+  double* row = a.slab + ((size_t)f * a.n_tblk + tb) * N;
+  row[k] = sa;
+  if (kb != k) row[kb] = sb;
 }
 
 __global__ void tg_reduce_kernel(const double* slab, const int64_t* frame_base, int n_tblk, int N, double* tg_out) {
@@ -256,7 +261,8 @@ int launch_ibi_tempogram(Context& ctx, const float* onset, const int64_t* frame_
   const size_t lds = TG_TB * sizeof(double) + (size_t)(TG_TB + N) * sizeof(float);
   {
     KTimer kt_(ctx, "tg_slide", st);
-    hipLaunchKernelGGL(tg_slide_kernel, dim3((N + TG_KB - 1) / TG_KB, n_tblk, n_files), dim3(TG_KB), lds, st, a);
+    hipLaunchKernelGGL(tg_slide_kernel, dim3(((N + 1) / 2 + TG_KB - 1) / TG_KB, n_tblk, n_files), dim3(TG_KB), lds, st,
+                     a);
   }
   hipLaunchKernelGGL(tg_reduce_kernel, dim3((N + 255) / 256, n_files), dim3(256), 0, st, slab, frame_base, n_tblk,
                      N, tg_out);

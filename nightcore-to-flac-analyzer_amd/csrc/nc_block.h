@@ -180,14 +180,34 @@ __device__ double block_kth_flagged(const double* vals, const uint8_t* flag, int
       if ((key & mask) == prefix) atomicAdd(&hist[(key >> shift) & 255], 1);
     }
     __syncthreads();
-    if (threadIdx.x == 0) {
-      int kk = k, d = 0;
-      for (; d < 256; ++d) {
-        if (kk < hist[d]) break;
-        kk -= hist[d];
+    if (threadIdx.x < 64) {  // digit pick: 4 bins per lane + a wave prefix scan (no serial walk)
+      const int lane = threadIdx.x;
+      const int h0 = hist[4 * lane], h1 = hist[4 * lane + 1], h2 = hist[4 * lane + 2], h3 = hist[4 * lane + 3];
+      const int sum = h0 + h1 + h2 + h3;
+      int incl = sum;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const int y = __shfl_up(incl, o, 64);
+        if (lane >= o) incl += y;
       }
-      s.l[0] = (long long)d;
-      s.i[0] = kk;
+      const int excl = incl - sum;
+      if (excl <= k && k < incl) {
+        int r = k - excl, d = 4 * lane;
+        if (r >= h0) {
+          r -= h0;
+          ++d;
+          if (r >= h1) {
+            r -= h1;
+            ++d;
+            if (r >= h2) {
+              r -= h2;
+              ++d;
+            }
+          }
+        }
+        s.l[0] = (long long)d;
+        s.i[0] = r;
+      }
     }
     __syncthreads();
     const unsigned long long d = (unsigned long long)s.l[0];

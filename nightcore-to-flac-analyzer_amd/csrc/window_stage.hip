@@ -22,7 +22,22 @@
 
 namespace nc {
 
-constexpr int WT_WAVES = 6;
+// Tuning knobs (compile-time; tools/wtg_variants.sh sweeps them):
+//   NC_WT_SEG   frame segments per window, each an independent set of recurrences
+//   NC_WT_PAIR  lags per thread (1, or 2 = k and acw-1-k interleaved)
+//   NC_WT_SKIP  diagnosis only: 1 skips the sliding sums, 2 also skips onset + normaliser
+#ifndef NC_WT_SEG
+#define NC_WT_SEG 1
+#endif
+#ifndef NC_WT_PAIR
+#define NC_WT_PAIR 2
+#endif
+#ifndef NC_WT_SKIP
+#define NC_WT_SKIP 0
+#endif
+constexpr int WT_SEG = NC_WT_SEG;
+constexpr int WT_PAIR = NC_WT_PAIR;
+constexpr int WT_WAVES = (WT_PAIR == 2 ? 3 : 6) * WT_SEG;  // ceil(344 / WT_PAIR / 64) waves per segment
 constexpr int WT_THREADS = WT_WAVES * 64;
 
 struct WinTgArgs {
@@ -49,7 +64,7 @@ __global__ __launch_bounds__(WT_THREADS) void window_tg_kernel(WinTgArgs a) {
   const int T = a.T, acw = a.acw, p = acw / 2;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   double* sh_rinv = reinterpret_cast<double*>(smem);          // [T]
-  float* sh_x = reinterpret_cast<float*>(sh_rinv + T);        // [T + acw] ramp-padded onset
+  double* sh_x = sh_rinv + T;                                 // [T + acw] ramp-padded onset (f32 values)
   const int64_t g0 = (int64_t)w * T;
 
   // window max (top_db clamp) and energy, fixed-order reductions
@@ -64,36 +79,57 @@ __global__ __launch_bounds__(WT_THREADS) void window_tg_kernel(WinTgArgs a) {
   if (tid == 0) a.energy_out[w] = 20.0 * log10(fmax(sqrt(esum / (double)a.win_len), 1e-10));
   const float c = gmax - 80.0f;
 
-  // onset envelope: one wave per frame, lanes over bands
-  for (int t = wave; t < T; t += WT_WAVES) {
-    float val = 0.0f;
-    if (t >= a.pad_onset) {
-      const float* r0 = a.sdb + (g0 + t - a.pad_onset) * 128;
-      const float* r1 = r0 + 128;
-      const float a0 = fmaxf(r0[lane], c), a1 = fmaxf(r1[lane], c);
-      const float b0 = fmaxf(r0[lane + 64], c), b1 = fmaxf(r1[lane + 64], c);
-      const float part = fmaxf(0.0f, a1 - a0) + fmaxf(0.0f, b1 - b0);
-      val = wave_sum(part) * (1.0f / 128.0f);
-    }
-    if (lane == 0) {
-      sh_x[p + t] = val;
-      a.onset_out[g0 + t] = val;
+  // onset envelope: each wave owns a contiguous run of frames and walks it 8 frames at a
+  // time, loading the 9 S_db rows those frames difference (rows shared between neighbours)
+  // before using any of them, so 18 row loads per lane are in flight instead of 2
+  if (NC_WT_SKIP >= 2) {
+    for (int t = tid; t < T; t += WT_THREADS) sh_x[p + t] = 0.0;
+  } else {
+    constexpr int FB = 8;
+    const int per = (T + WT_WAVES - 1) / WT_WAVES;
+    const int ta = wave * per, tb = min(T, ta + per);
+    for (int t0 = ta; t0 < tb; t0 += FB) {
+      float ra[FB + 1], rb[FB + 1];
+#pragma unroll
+      for (int q = 0; q <= FB; ++q) {
+        const int j = t0 + q - a.pad_onset;  // row j feeds frames j + pad (as j) and j + pad - 1 (as j + 1)
+        const bool ok = j >= 0 && j < T;
+        const float* r = a.sdb + (g0 + (ok ? j : 0)) * 128;
+        ra[q] = ok ? r[lane] : 0.0f;
+        rb[q] = ok ? r[lane + 64] : 0.0f;
+      }
+#pragma unroll
+      for (int q = 0; q < FB; ++q) {
+        const int t = t0 + q;
+        if (t >= tb) break;
+        float val = 0.0f;
+        if (t >= a.pad_onset) {
+          const float a0 = fmaxf(ra[q], c), a1 = fmaxf(ra[q + 1], c);
+          const float b0 = fmaxf(rb[q], c), b1 = fmaxf(rb[q + 1], c);
+          const float part = fmaxf(0.0f, a1 - a0) + fmaxf(0.0f, b1 - b0);
+          val = wave_sum(part) * (1.0f / 128.0f);
+        }
+        if (lane == 0) {
+          sh_x[p + t] = val;
+          a.onset_out[g0 + t] = val;
+        }
+      }
     }
   }
   __syncthreads();
   {  // linear_ramp padding to 0 at both ends (numpy.pad, f64 ramp rounded to f32)
-    const double st0 = (double)sh_x[p] / (double)p, stl = (double)sh_x[p + T - 1] / (double)p;
+    const double st0 = sh_x[p] / (double)p, stl = sh_x[p + T - 1] / (double)p;
     for (int i = tid; i < p; i += WT_THREADS) {
-      sh_x[i] = (float)((double)i * st0);
-      sh_x[p + T + i] = (float)((double)(p - 1 - i) * stl);
+      sh_x[i] = (double)(float)((double)i * st0);
+      sh_x[p + T + i] = (double)(float)((double)(p - 1 - i) * stl);
     }
   }
   __syncthreads();
   // per-frame normaliser 1 / ac_t[0]
   for (int t = tid; t < T; t += WT_THREADS) {
     double s = 0.0;
-    for (int j = 0; j < acw; ++j) {
-      const double v = (double)sh_x[t + j];
+    for (int j = 0; j < (NC_WT_SKIP >= 2 ? 0 : acw); ++j) {
+      const double v = sh_x[t + j];
       s = fma(a.wsq[j], v * v, s);
     }
     sh_rinv[t] = tg_rinv(s);
@@ -101,8 +137,33 @@ __global__ __launch_bounds__(WT_THREADS) void window_tg_kernel(WinTgArgs a) {
   __syncthreads();
   auto xf = [&](int i) { return sh_x[i]; };
   auto rf = [&](int t) { return sh_rinv[t]; };
+  // lags k and acw-1-k per thread: two independent f64 recurrences (latency hiding), and
+  // their start-up sums (acw - k and k + 1 terms) add up to the same work on every thread;
+  // the frames are split into WT_SEG segments, each started by its own direct sums, and
+  // the segment partials are added in segment order
+  double* part = sh_x + (T + acw);  // [WT_SEG][acw]
+  const int seg = tid / (WT_THREADS / WT_SEG), st = tid % (WT_THREADS / WT_SEG);
+  const int ta = T * seg / WT_SEG, tb = T * (seg + 1) / WT_SEG;
+  if (NC_WT_SKIP == 0) {
+    if (WT_PAIR == 2) {
+      for (int i = st; i < (acw + 1) / 2; i += WT_THREADS / WT_SEG) {
+        const int ka = i, kb = acw - 1 - i;
+        double sa, sb;
+        slide_lag_sum2(xf, rf, acw, ka, kb, ta, tb, sa, sb);
+        part[seg * acw + ka] = sa;
+        if (kb != ka) part[seg * acw + kb] = sb;
+      }
+    } else {
+      for (int k = st; k < acw; k += WT_THREADS / WT_SEG) part[seg * acw + k] = slide_lag_sum(xf, rf, acw, k, ta, tb);
+    }
+  } else {
+    for (int k = st; k < acw; k += WT_THREADS / WT_SEG) part[seg * acw + k] = 0.0;
+  }
+  __syncthreads();
   for (int k = tid; k < acw; k += WT_THREADS) {
-    const double acc = slide_lag_sum(xf, rf, acw, k, 0, T);
+    double acc = part[k];
+#pragma unroll
+    for (int q = 1; q < WT_SEG; ++q) acc += part[q * acw + k];
     a.tg_out[(size_t)w * acw + k] = acc / (double)T;
   }
 }
@@ -167,7 +228,7 @@ int launch_window_stage(Context& ctx, const float* sig, const int64_t* win_off, 
   a.onset_out = onset_out;
   a.tg_out = tg_out;
   a.energy_out = energy_out;
-  const size_t lds = (size_t)T * sizeof(double) + (size_t)(T + acw) * sizeof(float);
+  const size_t lds = (size_t)T * sizeof(double) + (size_t)(T + acw + WT_SEG * acw) * sizeof(double);
   if (lds > 64 * 1024) {
     set_error("window stage: window too long for LDS");
     return -2;
