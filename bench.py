@@ -34,6 +34,14 @@ sys.path.insert(0, str(REPO))
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
 WIN_BYTES = 220500 * 4         # algorithmic bytes per 10 s window
 CHUNK_BYTES = 441000 * 4       # algorithmic bytes per 20 s CQT chunk
+VALU_PEAK_TFS = 157.3          # MI355X f32 vector (= f32 MFMA) peak, MI355X_MICROARCH.md
+# Algorithmic FLOPs (a real N-point FFT counted as 2.5 N log2 N):
+#   CQT item (one frame of one octave): rFFT 1024 (25 600) + 36 sparse complex basis rows,
+#   ~600 complex taps x 8 (4 800) -> 30 400; a 20 s chunk has 7 octaves x 862 frames.
+#   STFT->mel frame: rFFT 2048 (56 320) + power (3 075) + Slaney mel, ~2 050 taps x 2 (4 100)
+#   -> 63 495; a 10 s window has 431 frames.
+CHUNK_FLOP = 7 * 862 * 30400
+WIN_FLOP = 431 * 63495
 
 
 def _gen(args):
@@ -172,11 +180,13 @@ def main():
     per = {k: (ms / n, n // ksteps) for k, (ms, n) in timers.items()}
     kper = {k: (ms / n, n / ksteps) for k, (ms, n) in ktimes.items()}
     # algorithmic bytes per launch = SURVEY.md §8d per-unit bytes x units per launch
-    units = {"stft_mel": (win_per_step, WIN_BYTES), "cqt_chroma": (chunks_per_step, CHUNK_BYTES)}
+    units = {"stft_mel": (win_per_step, WIN_BYTES, WIN_FLOP), "cqt_chroma": (chunks_per_step, CHUNK_BYTES, CHUNK_FLOP)}
     dom = max(units, key=lambda k: kper.get(k, (0, 0))[0] * kper.get(k, (0, 0))[1])
     avg_ms, launches = kper[dom]
     alg_per_launch = units[dom][0] / launches * units[dom][1]
     achieved = alg_per_launch / (avg_ms * 1e-3) / 1e9
+    flop_per_launch = units[dom][0] / launches * units[dom][2]
+    tflops = flop_per_launch / (avg_ms * 1e-3) / 1e12
     traffic = _pmc_traffic(dom)
     step_ms = el / args.steps * 1e3
 
@@ -220,7 +230,11 @@ def main():
                          "traffic": traffic["bytes_per_launch"] if traffic else None,
                          "traffic_source": traffic["source"] if traffic else None,
                          "alg_bytes_per_launch": alg_per_launch, "avg_launch_ms": avg_ms,
-                         "launches_per_step": launches},
+                         "launches_per_step": launches,
+                         # the roof that actually binds: f32 VALU, no MFMA on this path
+                         "compute": {"bound": "valu_f32", "achieved": tflops, "peak": VALU_PEAK_TFS,
+                                     "unit": "TFLOP/s", "frac": tflops / VALU_PEAK_TFS,
+                                     "alg_flop_per_launch": flop_per_launch}},
             "kernels_ms_per_step": {k: round(v[0] * v[1], 4) for k, v in kper.items()},
             "entry_points_ms_per_step": {k: round(v[0] * v[1], 4) for k, v in per.items()},
             "check": {"tempo_ratio_pair0": tr, "pitch_ratio_pair0": pr},

@@ -15,7 +15,9 @@
 // position s_r = sum_{q<r} consumed_q; with rare Lemire rejections the
 // positions are found by a fix-point (assume r*m, walk, prefix-sum, repeat until
 // stable) inside one workgroup, each thread jumping to its position with the
-// O(log n) LCG advance.  Medians: the resample's multiset is kept as counts per
+// O(log n) LCG advance.  Since a rejection has probability < n / 2^32 per draw, the
+// common case runs one resample per thread across many workgroups at r*m (counts in
+// LDS) and only a job whose walk met a rejection is redone by the fix-point.  Medians: the resample's multiset is kept as counts per
 // rank of the sorted input, so the k-th smallest is a scan.  Percentiles use
 // numpy's 'linear' method (virtual index (n-1) q, lerp with the t >= 0.5 branch),
 // whose (index, gamma) the host computes with numpy's own formula.
@@ -88,41 +90,93 @@ struct Gen32 {
   }
 };
 
-constexpr int BT = 1024;
+constexpr int BT = 1024;   // rank / finish workgroups
+constexpr int BD = 256;    // draw workgroups: one resample per thread
+constexpr int BD_NV = 96;  // resamples with na + nb <= BD_NV keep their rank counts in LDS
 
 __device__ __forceinline__ double lerp_np(double a, double b, double t) {
   const double d = b - a;
   return t >= 0.5 ? b - d * (1.0 - t) : a + d * t;
 }
 
-__global__ __launch_bounds__(BT) void bootstrap_kernel(BootArgs a) {
-  __shared__ BlockScratch<BT> bs;
-  __shared__ double sorted_boot[2048];
-  __shared__ int sh_changed;
-  const int j = blockIdx.x;
-  const int na = a.a_n[j];
-  const int nb = a.b_n ? a.b_n[j] : 0;
-  const bool hasB = a.b_n != nullptr;
-  if (na < a.min_n || (hasB && nb < a.min_n) || na <= 0) {
-    if (threadIdx.x == 0) {
-      a.point_out[j] = NAN;
-      a.lo_out[j] = NAN;
-      a.hi_out[j] = NAN;
-    }
-    return;
-  }
-  const double* A = a.values + a.a_off[j];
-  const double* B = hasB ? a.values + a.b_off[j] : nullptr;
+// Per-job workspace (bootstrap_job_bytes): rank[na + nb] i32 | sorted[na + nb] f64 |
+// start[n_boot] i64 | boot[n_boot] f64 | flag i32 | counts[n_boot][na + nb] u16 (global path)
+struct JobWs {
+  int* rankA;
+  int* rankB;
+  double* sortedA;
+  double* sortedB;
+  int64_t* start;
+  double* boot;
+  int* flag;
+  uint16_t* cnt;
+};
+
+__device__ __forceinline__ JobWs job_ws(const BootArgs& a, int j, int na) {
   const int cap = a.cap[j];
   char* w = a.ws + a.ws_off[j];
-  int* rankA = reinterpret_cast<int*>(w);
-  int* rankB = rankA + na;
-  double* sortedA = reinterpret_cast<double*>(w + (((size_t)cap * 4 + 15) & ~(size_t)15));
-  double* sortedB = sortedA + na;
-  int64_t* start = reinterpret_cast<int64_t*>(sortedA + cap);
-  uint16_t* cnt = reinterpret_cast<uint16_t*>(start + a.n_boot);  // [n_boot][na + nb]
+  JobWs r;
+  r.rankA = reinterpret_cast<int*>(w);
+  r.rankB = r.rankA + na;
+  r.sortedA = reinterpret_cast<double*>(w + (((size_t)cap * 4 + 15) & ~(size_t)15));
+  r.sortedB = r.sortedA + na;
+  r.start = reinterpret_cast<int64_t*>(r.sortedA + cap);
+  r.boot = reinterpret_cast<double*>(r.start + a.n_boot);
+  r.flag = reinterpret_cast<int*>(r.boot + a.n_boot);
+  r.cnt = reinterpret_cast<uint16_t*>(r.flag + 4);
+  return r;
+}
 
-  // ranks (stable: ties broken by index) and sorted values
+__device__ __forceinline__ bool job_skipped(const BootArgs& a, int j, int& na, int& nb) {
+  na = a.a_n[j];
+  nb = a.b_n ? a.b_n[j] : 0;
+  return na < a.min_n || (a.b_n != nullptr && nb < a.min_n) || na <= 0;
+}
+
+// k-th smallest of a resample held as counts per rank (c[q * stride], q < n)
+__device__ __forceinline__ double kth_count(const uint16_t* c, int stride, int n, int k, const double* srt) {
+  int acc = 0;
+  for (int q = 0; q < n; ++q) {
+    acc += c[q * stride];
+    if (acc > k) return srt[q];
+  }
+  return srt[n - 1];
+}
+__device__ __forceinline__ double med_count(const uint16_t* c, int stride, int n, const double* srt) {
+  if (n & 1) return kth_count(c, stride, n, n / 2, srt);
+  return (kth_count(c, stride, n, n / 2 - 1, srt) + kth_count(c, stride, n, n / 2, srt)) / 2.0;
+}
+
+// One resample's draws (A then B) into counts c[q * stride]; returns the uint32s consumed.
+__device__ __forceinline__ int draw_resample(u128 s0, u128 inc, int64_t start, int na, int nb, bool hasB,
+                                             const int* rankA, const int* rankB, uint16_t* c, int stride) {
+  const int nv = na + nb;
+  for (int q = 0; q < nv; ++q) c[q * stride] = 0;
+  int consumed = 0;
+  const bool draws = (na > 1) || (hasB && nb > 1);
+  Gen32 g;
+  if (draws) g.init(s0, inc, (uint64_t)start);
+  if (na > 1)
+    for (int q = 0; q < na; ++q) c[rankA[g.bounded((uint32_t)na, consumed)] * stride]++;
+  else
+    c[0] += (uint16_t)na;  // n == 1: every draw is index 0, no RNG consumed
+  if (hasB) {
+    if (nb > 1)
+      for (int q = 0; q < nb; ++q) c[(na + rankB[g.bounded((uint32_t)nb, consumed)]) * stride]++;
+    else
+      c[na * stride] += (uint16_t)nb;
+  }
+  return consumed;
+}
+
+// Phase 1 (one workgroup per job): stable ranks and sorted values; clears the job flag.
+__global__ __launch_bounds__(BT) void bootstrap_rank_kernel(BootArgs a) {
+  const int j = blockIdx.x;
+  int na, nb;
+  if (job_skipped(a, j, na, nb)) return;
+  const JobWs w = job_ws(a, j, na);
+  const double* A = a.values + a.a_off[j];
+  const double* B = a.b_n ? a.values + a.b_off[j] : nullptr;
   for (int i = threadIdx.x; i < na; i += BT) {
     const double v = A[i];
     int r = 0;
@@ -130,8 +184,8 @@ __global__ __launch_bounds__(BT) void bootstrap_kernel(BootArgs a) {
       const double u = A[q];
       r += (u < v) || (u == v && q < i);
     }
-    rankA[i] = r;
-    sortedA[r] = v;
+    w.rankA[i] = r;
+    w.sortedA[r] = v;
   }
   for (int i = threadIdx.x; i < nb; i += BT) {
     const double v = B[i];
@@ -140,88 +194,102 @@ __global__ __launch_bounds__(BT) void bootstrap_kernel(BootArgs a) {
       const double u = B[q];
       r += (u < v) || (u == v && q < i);
     }
-    rankB[i] = r;
-    sortedB[r] = v;
+    w.rankB[i] = r;
+    w.sortedB[r] = v;
   }
-  __syncthreads();
+  if (threadIdx.x == 0) *w.flag = 0;
+}
 
+// Phase 2 (grid n_boot / BD x jobs): resample r drawn from uint32 position r * m, the
+// position it has when no Lemire rejection happened before it.  A resample that
+// consumes more than m flags its job; phase 3 then redoes that job exactly.
+__global__ __launch_bounds__(BD) void bootstrap_draw_kernel(BootArgs a) {
+  __shared__ uint16_t cnt_lds[BD_NV * BD];  // [rank][thread]
+  const int j = blockIdx.y;
+  int na, nb;
+  if (job_skipped(a, j, na, nb)) return;
+  const int r = blockIdx.x * BD + threadIdx.x;
+  if (r >= a.n_boot) return;
+  const JobWs w = job_ws(a, j, na);
+  const bool hasB = a.b_n != nullptr;
+  const int nv = na + nb;
+  const int m = (na > 1 ? na : 0) + (nb > 1 ? nb : 0);
   const u128 s0 = ((u128)a.seed[j * 4 + 0] << 64) | (u128)a.seed[j * 4 + 1];
   const u128 inc = ((u128)a.seed[j * 4 + 2] << 64) | (u128)a.seed[j * 4 + 3];
-  const int m = (na > 1 ? na : 0) + (nb > 1 ? nb : 0);  // uint32 draws per resample w/o rejection
-  const int nv = na + nb;
-  for (int r = threadIdx.x; r < a.n_boot; r += BT) start[r] = (int64_t)r * m;
-  __syncthreads();
+  const bool in_lds = nv <= BD_NV;
+  uint16_t* c = in_lds ? cnt_lds + threadIdx.x : w.cnt + (size_t)r * nv;
+  const int stride = in_lds ? BD : 1;
+  const int consumed = draw_resample(s0, inc, (int64_t)r * m, na, nb, hasB, w.rankA, w.rankB, c, stride);
+  if (consumed != m) atomicOr(w.flag, 1);
+  const double ma = med_count(c, stride, na, w.sortedA);
+  w.boot[r] = hasB ? ma / med_count(c + na * stride, stride, nb, w.sortedB) : ma;
+}
 
-  for (int iter = 0; iter < 4096; ++iter) {
-    // walk: consumed count per resample (+ counts as a side effect)
-    int local_cons[(2048 + BT - 1) / BT];
-    int li = 0;
-    for (int r = threadIdx.x; r < a.n_boot; r += BT, ++li) {
-      uint16_t* c = cnt + (size_t)r * nv;
-      for (int q = 0; q < nv; ++q) c[q] = 0;
-      int consumed = 0;
-      if (m > 0) {
-        Gen32 g;
-        g.init(s0, inc, (uint64_t)start[r]);
-        if (na > 1)
-          for (int q = 0; q < na; ++q) c[rankA[g.bounded((uint32_t)na, consumed)]]++;
-        else
-          c[0] += (uint16_t)na;  // n == 1: every draw is index 0, no RNG consumed
-        if (hasB) {
-          if (nb > 1)
-            for (int q = 0; q < nb; ++q) c[na + rankB[g.bounded((uint32_t)nb, consumed)]]++;
-          else
-            c[na] += (uint16_t)nb;
-        }
-      } else {
-        c[0] += (uint16_t)na;
-        if (hasB) c[na] += (uint16_t)nb;
-      }
-      local_cons[li] = consumed;
+// Phase 3 (one workgroup per job): for a flagged job the exact resample positions by a
+// fix-point (assume r * m, walk, prefix-sum the consumed counts, repeat until stable) and
+// the boot values again; then the bitonic sort of the boot values, percentiles, point.
+__global__ __launch_bounds__(BT) void bootstrap_finish_kernel(BootArgs a) {
+  __shared__ BlockScratch<BT> bs;
+  __shared__ double sorted_boot[2048];
+  __shared__ int sh_changed;
+  const int j = blockIdx.x;
+  int na, nb;
+  if (job_skipped(a, j, na, nb)) {
+    if (threadIdx.x == 0) {
+      a.point_out[j] = NAN;
+      a.lo_out[j] = NAN;
+      a.hi_out[j] = NAN;
     }
-    // exclusive scan over resamples (thread-major: r = tid + BT*li)
-    if (threadIdx.x == 0) sh_changed = 0;
+    return;
+  }
+  const JobWs w = job_ws(a, j, na);
+  const bool hasB = a.b_n != nullptr;
+  const int nv = na + nb;
+  if (*w.flag) {  // rare: some resample met a Lemire rejection
+    const u128 s0 = ((u128)a.seed[j * 4 + 0] << 64) | (u128)a.seed[j * 4 + 1];
+    const u128 inc = ((u128)a.seed[j * 4 + 2] << 64) | (u128)a.seed[j * 4 + 3];
+    const int m = (na > 1 ? na : 0) + (nb > 1 ? nb : 0);
+    for (int r = threadIdx.x; r < a.n_boot; r += BT) w.start[r] = (int64_t)r * m;
     __syncthreads();
-    int64_t carry = 0;
-    for (int base = 0, l2 = 0; base < a.n_boot; base += BT, ++l2) {
-      const int r = base + threadIdx.x;
-      const int v = r < a.n_boot ? local_cons[l2] : 0;
-      int tot = 0;
-      const int ex = block_exclusive_scan<BT>(v, tot, bs);
-      if (r < a.n_boot) {
-        const int64_t ns = carry + ex;
-        if (ns != start[r]) {
-          start[r] = ns;
-          sh_changed = 1;
+    for (int iter = 0; iter < 4096; ++iter) {
+      int local_cons[(2048 + BT - 1) / BT];
+      int li = 0;
+      for (int r = threadIdx.x; r < a.n_boot; r += BT, ++li)
+        local_cons[li] = draw_resample(s0, inc, w.start[r], na, nb, hasB, w.rankA, w.rankB,
+                                       w.cnt + (size_t)r * nv, 1);
+      if (threadIdx.x == 0) sh_changed = 0;
+      __syncthreads();
+      int64_t carry = 0;
+      for (int base = 0, l2 = 0; base < a.n_boot; base += BT, ++l2) {
+        const int r = base + threadIdx.x;
+        const int v = r < a.n_boot ? local_cons[l2] : 0;
+        int tot = 0;
+        const int ex = block_exclusive_scan<BT>(v, tot, bs);
+        if (r < a.n_boot) {
+          const int64_t ns = carry + ex;
+          if (ns != w.start[r]) {
+            w.start[r] = ns;
+            sh_changed = 1;
+          }
         }
+        carry += tot;
+        __syncthreads();
       }
-      carry += tot;
+      __syncthreads();
+      if (!sh_changed) break;
       __syncthreads();
     }
-    __syncthreads();
-    if (!sh_changed) break;
+    for (int r = threadIdx.x; r < a.n_boot; r += BT) {
+      const uint16_t* c = w.cnt + (size_t)r * nv;
+      const double ma = med_count(c, 1, na, w.sortedA);
+      w.boot[r] = hasB ? ma / med_count(c + na, 1, nb, w.sortedB) : ma;
+    }
     __syncthreads();
   }
-
-  // medians -> boot values
-  auto kth = [&](const uint16_t* c, int n, int k, const double* srt) {
-    int acc = 0;
-    for (int q = 0; q < n; ++q) {
-      acc += c[q];
-      if (acc > k) return srt[q];
-    }
-    return srt[n - 1];
-  };
-  auto med = [&](const uint16_t* c, int n, const double* srt) {
-    if (n & 1) return kth(c, n, n / 2, srt);
-    return (kth(c, n, n / 2 - 1, srt) + kth(c, n, n / 2, srt)) / 2.0;
-  };
   for (int r = threadIdx.x; r < 2048; r += BT) {
     double v = INFINITY;
     if (r < a.n_boot) {
-      const uint16_t* c = cnt + (size_t)r * nv;
-      const double ma = med(c, na, sortedA);
-      v = hasB ? ma / med(c + na, nb, sortedB) : ma;
+      v = w.boot[r];
       if (a.boot_out) a.boot_out[(size_t)j * a.n_boot + r] = v;
     }
     sorted_boot[r] = v;
@@ -249,16 +317,16 @@ __global__ __launch_bounds__(BT) void bootstrap_kernel(BootArgs a) {
     const int ilp = min(il + 1, a.n_boot - 1), ihp = min(ih + 1, a.n_boot - 1);
     a.lo_out[j] = lerp_np(sorted_boot[il], sorted_boot[ilp], a.g_lo);
     a.hi_out[j] = lerp_np(sorted_boot[ih], sorted_boot[ihp], a.g_hi);
-    const double pa = (na & 1) ? sortedA[na / 2] : (sortedA[na / 2 - 1] + sortedA[na / 2]) / 2.0;
+    const double pa = (na & 1) ? w.sortedA[na / 2] : (w.sortedA[na / 2 - 1] + w.sortedA[na / 2]) / 2.0;
     double pb = 1.0;
-    if (hasB) pb = (nb & 1) ? sortedB[nb / 2] : (sortedB[nb / 2 - 1] + sortedB[nb / 2]) / 2.0;
+    if (hasB) pb = (nb & 1) ? w.sortedB[nb / 2] : (w.sortedB[nb / 2 - 1] + w.sortedB[nb / 2]) / 2.0;
     a.point_out[j] = hasB ? pa / pb : pa;
   }
 }
 
 size_t bootstrap_job_bytes(int cap, int n_boot) {
   size_t b = (((size_t)cap * 4 + 15) & ~(size_t)15);
-  b += (size_t)cap * 8 + (size_t)n_boot * 8 + (size_t)n_boot * cap * 2;
+  b += (size_t)cap * 8 + (size_t)n_boot * 8 + (size_t)n_boot * 8 + 16 + (size_t)n_boot * cap * 2;
   return (b + 255) & ~(size_t)255;
 }
 
@@ -268,7 +336,9 @@ int launch_bootstrap(const BootArgs& a, int n_jobs, hipStream_t st) {
     set_error("bootstrap: n_boot must be in [1, 2048]");
     return -2;
   }
-  hipLaunchKernelGGL(bootstrap_kernel, dim3(n_jobs), dim3(BT), 0, st, a);
+  hipLaunchKernelGGL(bootstrap_rank_kernel, dim3(n_jobs), dim3(BT), 0, st, a);
+  hipLaunchKernelGGL(bootstrap_draw_kernel, dim3((a.n_boot + BD - 1) / BD, n_jobs), dim3(BD), 0, st, a);
+  hipLaunchKernelGGL(bootstrap_finish_kernel, dim3(n_jobs), dim3(BT), 0, st, a);
   NC_HIP(hipGetLastError());
   return 0;
 }

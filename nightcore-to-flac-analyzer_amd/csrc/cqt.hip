@@ -40,18 +40,32 @@ struct ChromaPlan {
   int64_t* tf_base;   // [n+1] prefix of tuning frames
 };
 
-__global__ void chroma_plan_kernel(const int64_t* chunk_len, int n, int64_t* oct_off, int64_t* oct_len,
-                                   int* n_frames, int* n_tframes, int64_t* tf_base) {
-  if (blockIdx.x != 0 || threadIdx.x != 0) return;
-  int64_t acc = 0, tacc = 0;
-  for (int c = 0; c < n; ++c) {
-    int64_t L = chunk_len[c];
-    int hop = 512;
-    int tmin = 0x7fffffff;
+// octave lengths L_{i+1} = ceil(L_i / 2); octave buffers 64-float aligned, laid out chunk-major
+__device__ __forceinline__ int64_t chunk_oct_floats(int64_t L) {
+  int64_t acc = 0;
+  for (int i = 1; i < 7; ++i) {
+    L = (L + 1) / 2;
+    acc += (L + 63) & ~63LL;
+  }
+  return acc;
+}
+
+// one workgroup: per-chunk octave layout and frame counts, two parallel prefix tables
+// (oct_base = octave-buffer base of each chunk, tf_base = tuning-frame base)
+__global__ __launch_bounds__(1024) void chroma_plan_kernel(const int64_t* chunk_len, int n, int64_t* oct_off,
+                                                           int64_t* oct_len, int* n_frames, int* n_tframes,
+                                                           int64_t* tf_base, int64_t* oct_base) {
+  block_prefix_table<1024>(n, oct_base, [&](int c) { return chunk_oct_floats(chunk_len[c]); });
+  block_prefix_table<1024>(n, tf_base, [&](int c) { return 1 + chunk_len[c] / 512; });
+  __syncthreads();
+  for (int c = threadIdx.x; c < n; c += 1024) {
+    int64_t L = chunk_len[c], acc = oct_base[c];
+    int hop = 512, tmin = 0x7fffffff;
     for (int i = 0; i < 7; ++i) {
       oct_len[c * 7 + i] = L;
-      if (i == 0) oct_off[c * 7 + i] = -1;
-      else {
+      if (i == 0) {
+        oct_off[c * 7 + i] = -1;
+      } else {
         oct_off[c * 7 + i] = acc;
         acc += (L + 63) & ~63LL;
       }
@@ -61,10 +75,7 @@ __global__ void chroma_plan_kernel(const int64_t* chunk_len, int n, int64_t* oct
     }
     n_frames[c] = tmin;
     n_tframes[c] = (int)(1 + chunk_len[c] / 512);
-    tf_base[c] = tacc;
-    tacc += n_tframes[c];
   }
-  tf_base[n] = tacc;
 }
 
 // ------------------------------------------------------------------------------ 1. decimation
@@ -636,6 +647,7 @@ struct ChromaWs {
   int* n_frames;
   int* n_tframes;
   int64_t* tf_base;
+  int64_t* oct_base;
   float* ws_oct;
   float* peak_pitch;
   float* peak_mag;
@@ -652,7 +664,7 @@ size_t chroma_ws_bytes(int n, int64_t total_len) {
   size_t b = 0;
   b += al256(sizeof(int64_t) * 7 * n) * 2;
   b += al256(sizeof(int) * n) * 4;
-  b += al256(sizeof(int64_t) * (n + 1));
+  b += al256(sizeof(int64_t) * (n + 1)) * 2;
   b += al256(sizeof(float) * (size_t)(total_len + 64 * 7 * (int64_t)n));
   b += al256(sizeof(float) * (size_t)tfr * kPeakSlots) * 2;
   b += al256(sizeof(double) * (size_t)(tfr / CQ_FR + n + 1) * 12);
@@ -686,13 +698,14 @@ int launch_chroma_mean(Context& ctx, const float* sig, const int64_t* chunk_off,
   w.chunk_npk = reinterpret_cast<int*>(take(sizeof(int) * n));
   w.tuning_idx = out_tuning_idx ? out_tuning_idx : reinterpret_cast<int*>(take(sizeof(int) * n));
   w.tf_base = reinterpret_cast<int64_t*>(take(sizeof(int64_t) * (n + 1)));
+  w.oct_base = reinterpret_cast<int64_t*>(take(sizeof(int64_t) * (n + 1)));
   w.ws_oct = reinterpret_cast<float*>(take(sizeof(float) * (size_t)(total_len + 64 * 7 * (int64_t)n)));
   w.peak_pitch = reinterpret_cast<float*>(take(sizeof(float) * (size_t)tfr * kPeakSlots));
   w.peak_mag = reinterpret_cast<float*>(take(sizeof(float) * (size_t)tfr * kPeakSlots));
   w.partial = reinterpret_cast<double*>(take(sizeof(double) * (size_t)(tfr / CQ_FR + n + 1) * 12));
 
-  hipLaunchKernelGGL(chroma_plan_kernel, dim3(1), dim3(64), 0, st, chunk_len, n, w.oct_off, w.oct_len, w.n_frames,
-                     w.n_tframes, w.tf_base);
+  hipLaunchKernelGGL(chroma_plan_kernel, dim3(1), dim3(1024), 0, st, chunk_len, n, w.oct_off, w.oct_len, w.n_frames,
+                     w.n_tframes, w.tf_base, w.oct_base);
   NC_HIP(hipMemsetAsync(w.chunk_npk, 0, sizeof(int) * n, st));
   // grids are sized by the longest chunk; blocks past a chunk's own length exit
   for (int lvl = 0; lvl < 6; ++lvl) {

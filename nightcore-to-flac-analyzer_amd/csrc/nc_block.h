@@ -114,6 +114,47 @@ __device__ __forceinline__ int block_exclusive_scan(int v, int& total, BlockScra
   return base + incl - v;
 }
 
+// Exclusive prefix sum of one int64 per thread (in thread order) + total; sh holds NT/64
+// int64s of LDS.  Callers walk long lists in tiles of NT, carrying the total.
+template <int NT>
+__device__ __forceinline__ int64_t block_exclusive_scan64(int64_t v, int64_t& total, int64_t* sh) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  int64_t incl = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int64_t y = __shfl_up(incl, o, 64);
+    if (lane >= o) incl += y;
+  }
+  __syncthreads();
+  if (lane == 63) sh[wave] = incl;
+  __syncthreads();
+  int64_t base = 0, tot = 0;
+#pragma unroll
+  for (int i = 0; i < NT / 64; ++i) {
+    if (i < wave) base += sh[i];
+    tot += sh[i];
+  }
+  total = tot;
+  return base + incl - v;
+}
+
+// base[i] = sum_{q<i} count(q) for i in [0, n], one workgroup of NT threads (a parallel
+// replacement of a one-thread prefix loop over files / chunks).
+template <int NT, typename F>
+__device__ __forceinline__ void block_prefix_table(int n, int64_t* base, F count) {
+  __shared__ int64_t sh[NT / 64];
+  int64_t carry = 0;
+  for (int t0 = 0; t0 < n; t0 += NT) {
+    const int i = t0 + (int)threadIdx.x;
+    const int64_t v = i < n ? count(i) : 0;
+    int64_t tot = 0;
+    const int64_t ex = block_exclusive_scan64<NT>(v, tot, sh);
+    if (i < n) base[i] = carry + ex;
+    carry += tot;
+  }
+  if (threadIdx.x == 0) base[n] = carry;
+}
+
 // (value, index) argmax with numpy semantics: NaN wins, ties -> smallest index.
 __device__ __forceinline__ bool np_better(double a, int ia, double b, int ib) {
   const bool na = a != a, nb = b != b;

@@ -23,6 +23,7 @@ from __future__ import annotations
 
 import math
 import threading
+import os
 import time
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional, Sequence, Tuple
@@ -103,6 +104,35 @@ _TORCH_DTYPE = {np.dtype(np.float64).str: torch.float64, np.dtype(np.float32).st
                 np.dtype(np.uint8).str: torch.uint8, np.dtype(np.uint64).str: torch.uint64}
 
 
+class _Arena:
+    """Many small device outputs carved from one byte buffer: one zero-fill on the
+    stream instead of one per tensor, and one D2H copy into one pinned buffer."""
+
+    def __init__(self):
+        self.parts: List[Tuple[str, np.dtype, int]] = []
+
+    def add(self, name: str, n: int, dtype) -> None:
+        self.parts.append((name, np.dtype(dtype), max(1, int(n))))
+
+    def commit(self, dev: torch.device) -> Dict[str, torch.Tensor]:
+        self.offs, total = [], 0
+        for _, dt, n in self.parts:
+            total = (total + 15) & ~15
+            self.offs.append(total)
+            total += n * dt.itemsize
+        self.nbytes = max(16, total)
+        self.buf = torch.zeros(self.nbytes, dtype=torch.uint8, device=dev)
+        return {name: self.buf[o:o + n * dt.itemsize].view(_TORCH_DTYPE[dt.str])
+                for (name, dt, n), o in zip(self.parts, self.offs)}
+
+    def to_host(self) -> Tuple[torch.Tensor, Dict[str, np.ndarray]]:
+        """Queue the D2H copy; the numpy views are valid once the stream reaches it."""
+        host = torch.empty(self.nbytes, dtype=torch.uint8, pin_memory=True)
+        host.copy_(self.buf, non_blocking=True)
+        hb = host.numpy()
+        return host, {name: hb[o:o + n * dt.itemsize].view(dt) for (name, dt, n), o in zip(self.parts, self.offs)}
+
+
 @dataclass
 class DeviceSignals:
     """Signals resident in HBM: one f32 buffer, per-file offset/length (samples)."""
@@ -163,7 +193,9 @@ class Engine:
         self.timers: Optional[Dict[str, list]] = None
         self.host_stats: Optional[Dict[str, float]] = None  # {phase: seconds} when enabled
         # the chroma chain runs on its own stream, concurrently with the window/tempo chain
-        self.chroma_stream = torch.cuda.Stream(self.dev)
+        # (NC_SERIAL_STREAMS=1 queues it on the launch stream instead: isolated per-kernel timings)
+        self.chroma_stream = torch.cuda.current_stream(self.dev) if os.environ.get("NC_SERIAL_STREAMS") == "1" \
+            else torch.cuda.Stream(self.dev)
 
     # -------------------------------------------------------------- plumbing
     def stream(self) -> int:
@@ -402,10 +434,33 @@ class Engine:
         n_chunks = len(chunk_off)
         n_cp = n_chunks // 2
 
+        # bootstrap jobs (tempo: A = nc valid, B = src valid; pitch: A = nc_hz, B = src_hz; shift)
+        n_pitch_jobs = len(pair_chunks)
+        nj = B + n_pitch_jobs
+        TV, PV = max(1, n_win), max(1, 3 * n_cp)   # vals = [tempo values at the window index | shift, nc_hz, src_hz]
+        jobs_a_off = [w0[2 * b] for b in range(B)] + [TV + n_cp + c0 for c0, _ in pair_chunks]
+        jobs_b_off = [w0[2 * b + 1] for b in range(B)] + [TV + 2 * n_cp + c0 for c0, _ in pair_chunks]
+        caps = [max(1, (w1[2 * b] - w0[2 * b]) + (w1[2 * b + 1] - w0[2 * b + 1])) for b in range(B)] + \
+               [2 * (c1 - c0) for c0, c1 in pair_chunks]
+        p_n = [c1 - c0 for c0, c1 in pair_chunks]
+        jb = self.ctx.lib.nc_bootstrap_job_bytes
+        wsoff, tot = [], 0
+        for c in caps:
+            wsoff.append(tot)
+            tot += jb(int(c), C.N_BOOTSTRAP)
+        s_wsoff, s_tot = [], 0
+        for n in p_n:
+            s_wsoff.append(s_tot)
+            s_tot += jb(int(n), C.N_BOOTSTRAP)
+
+        # one H2D copy: plan + bootstrap jobs.  a_n / b_n = [valid counts (written on the
+        # device by nc_collect_valid) | chunk counts of the pitch jobs]
         up = _Upload()
         up.add("win_off", win_abs if n_win else [0], np.int64)
         up.add("w0", w0, np.int32)
         up.add("w1", w1, np.int32)
+        up.add("nc_w0", [w0[2 * b] for b in range(B)], np.int32)
+        up.add("nc_w1", [w1[2 * b] for b in range(B)], np.int32)
         up.add("on_off", np.arange(n_win, dtype=np.int64) * T if n_win else [0], np.int64)
         up.add("on_len", np.full(max(1, n_win), T), np.int32)
         up.add("src_w0", [w0[2 * b + 1] for b in range(B)], np.int32)
@@ -415,6 +470,7 @@ class Engine:
         nc_pair = np.concatenate([np.full(len(starts[2 * b]), b, np.int32) for b in range(B)]) \
             if n_win - n_src_w else np.zeros(1, np.int32)
         up.add("nc_pair", nc_pair, np.int32)
+        up.add("src_pair", np.zeros(max(1, n_src_w), np.int32), np.int32)
         up.add("start120", [120.0], np.float64)
         up.add("chunk_off", chunk_off or [0], np.int64)
         up.add("chunk_len", chunk_len or [0], np.int64)
@@ -422,14 +478,33 @@ class Engine:
         up.add("lag_nc", np.arange(1, n_chunks, 2), np.int32)
         up.add("f_off", f_off, np.int64)
         up.add("f_len", f_len, np.int64)
+        up.add("a_off", jobs_a_off, np.int64)
+        up.add("b_off", jobs_b_off, np.int64)
+        up.add("a_n", [0] * B + p_n, np.int32)
+        up.add("b_n", [0] * B + p_n, np.int32)
+        up.add("seed", seed_state(42) * nj, np.uint64)
+        up.add("wsoff", wsoff, np.int64)
+        up.add("cap", caps, np.int32)
+        up.add("s_off", [TV + c0 for c0, _ in pair_chunks] or [0], np.int64)
+        up.add("s_n", p_n or [0], np.int32)
+        up.add("s_seed", seed_state(0) * max(1, n_pitch_jobs), np.uint64)
+        up.add("s_wsoff", s_wsoff or [0], np.int64)
+        up.add("s_cap", p_n or [1], np.int32)
         d = up.commit(dev)
+
+        # one zero-filled output arena, copied back in one D2H
+        ar = _Arena()
+        for name, n, dt in (("chroma", n_chunks * 12, np.float32), ("tuning", n_chunks, np.float32),
+                            ("clag", n_cp, np.int32), ("vals", TV + PV, np.float64), ("energy", n_win, np.float64),
+                            ("active", n_win, np.uint8), ("bpm", n_win, np.float64), ("lag", n_win, np.int32),
+                            ("nbeats", n_win, np.int32), ("margin", n_win, np.float64), ("prior", B, np.float64),
+                            ("bout", 3 * nj, np.float64), ("sout", 3 * max(1, n_pitch_jobs), np.float64)):
+            ar.add(name, n, dt)
+        o = ar.commit(dev)
+        tvals, pvals = o["vals"][:TV], o["vals"][TV:]
 
         # ---------------------------------------------------------------- 3. chroma (stream 2)
         # runs concurrently with the window/tempo chain; joined before the bootstraps
-        chroma = torch.zeros(max(1, n_chunks * 12), dtype=torch.float32, device=dev)
-        tuning = torch.zeros(max(1, n_chunks), dtype=torch.float32, device=dev)
-        clag = torch.zeros(max(1, n_cp), dtype=torch.int32, device=dev)
-        pvals = torch.zeros(max(1, 3 * n_cp), dtype=torch.float64, device=dev)   # [shift | nc_hz | src_hz]
         s1, s2 = torch.cuda.current_stream(dev), self.chroma_stream
         ev_plan = torch.cuda.Event()
         ev_plan.record(s1)
@@ -441,30 +516,21 @@ class Engine:
             ws_c = self.workspace("chroma", wsb)
             ws_c.record_stream(s2)  # used on stream 2: not reusable until that work is done
             self.call("nc_chroma_mean", signals.buf.data_ptr(), d["chunk_off"].data_ptr(), d["chunk_len"].data_ptr(),
-                      n_chunks, tot_len, int(max(chunk_len)), chroma.data_ptr(), tuning.data_ptr(), None,
+                      n_chunks, tot_len, int(max(chunk_len)), o["chroma"].data_ptr(), o["tuning"].data_ptr(), None,
                       ws_c.data_ptr(), ws_c.numel(), st2)
-            self.call("nc_chroma_lag", chroma.data_ptr(), d["lag_src"].data_ptr(), d["lag_nc"].data_ptr(), n_cp,
-                      clag.data_ptr(), st2)
-            self.call("nc_pitch_hz", clag.data_ptr(), n_cp, pvals[0:n_cp].data_ptr(),
+            self.call("nc_chroma_lag", o["chroma"].data_ptr(), d["lag_src"].data_ptr(), d["lag_nc"].data_ptr(), n_cp,
+                      o["clag"].data_ptr(), st2)
+            self.call("nc_pitch_hz", o["clag"].data_ptr(), n_cp, pvals[0:n_cp].data_ptr(),
                       pvals[n_cp:2 * n_cp].data_ptr(), pvals[2 * n_cp:3 * n_cp].data_ptr(), st2)
         ev_chroma = torch.cuda.Event()
         ev_chroma.record(s2)
 
         # ---------------------------------------------------------------- 4. per-window stage
-        f64 = dict(dtype=torch.float64, device=dev)
-        i32 = dict(dtype=torch.int32, device=dev)
-        onset = torch.empty(max(1, n_win * T), dtype=torch.float32, device=dev)
-        tg = torch.empty(max(1, n_win * acw), **f64)
-        energy = torch.empty(max(1, n_win), **f64)
-        active = torch.empty(max(1, n_win), dtype=torch.uint8, device=dev)
-        bpm = torch.zeros(max(1, n_win), **f64)
-        lag = torch.zeros(max(1, n_win), **i32)
-        nbeats = torch.zeros(max(1, n_win), **i32)
-        margin = torch.zeros(max(1, n_win), **f64)
-        prior = torch.empty(max(1, B), **f64)
-        tvals = torch.zeros(max(1, n_win), **f64)
-        tcount = torch.zeros(nF, **i32)
+        bpm, lag, nbeats, margin, prior = o["bpm"], o["lag"], o["nbeats"], o["margin"], o["prior"]
+        energy, active = o["energy"], o["active"]
         if n_win:
+            onset = torch.empty(n_win * T, dtype=torch.float32, device=dev)
+            tg = torch.empty(n_win * acw, dtype=torch.float64, device=dev)
             wsb = self.ctx.lib.nc_window_stage_workspace_bytes(self.ctx.h, n_win, win_n, HOP_LENGTH)
             ws = self.workspace("win", wsb)
             self.call("nc_window_stage", signals.buf.data_ptr(), d["win_off"].data_ptr(), None, n_win, win_n,
@@ -473,10 +539,9 @@ class Engine:
                       float(p.energy_gate_db), active.data_ptr(), st)
             if n_src_w:
                 self.call("nc_tempo_beats", onset.data_ptr(), d["on_off"].data_ptr(), d["on_len"].data_ptr(),
-                          n_src_w, T, tg.data_ptr(), acw, d["start120"].data_ptr(),
-                          torch.zeros(n_src_w, **i32).data_ptr(), active.data_ptr(), HOP_LENGTH, 1,
-                          bpm.data_ptr(), lag.data_ptr(), nbeats.data_ptr(), margin.data_ptr(), None, 0, None, 0,
-                          st)
+                          n_src_w, T, tg.data_ptr(), acw, d["start120"].data_ptr(), d["src_pair"].data_ptr(),
+                          active.data_ptr(), HOP_LENGTH, 1, bpm.data_ptr(), lag.data_ptr(), nbeats.data_ptr(),
+                          margin.data_ptr(), None, 0, None, 0, st)
             self.call("nc_tempo_prior", bpm.data_ptr(), nbeats.data_ptr(), active.data_ptr(),
                       d["src_w0"].data_ptr(), d["src_w1"].data_ptr(), d["src_len"].data_ptr(),
                       d["nc_len"].data_ptr(), B, prior.data_ptr(), st)
@@ -488,9 +553,11 @@ class Engine:
                           active[n_src_w:].data_ptr(), HOP_LENGTH, 1, bpm[n_src_w:].data_ptr(),
                           lag[n_src_w:].data_ptr(), nbeats[n_src_w:].data_ptr(), margin[n_src_w:].data_ptr(),
                           None, 0, None, 0, st)
-            self.call("nc_collect_valid", bpm.data_ptr(), nbeats.data_ptr(), active.data_ptr(),
-                      d["w0"].data_ptr(), d["w1"].data_ptr(), nF, MIN_BEATS, tvals.data_ptr(),
-                      tcount.data_ptr(), st)
+            # valid-tempo compaction per side: the counts land in the bootstrap jobs' a_n / b_n
+            for side, cnt in (("nc", d["a_n"]), ("src", d["b_n"])):
+                self.call("nc_collect_valid", bpm.data_ptr(), nbeats.data_ptr(), active.data_ptr(),
+                          d[side + "_w0"].data_ptr(), d[side + "_w1"].data_ptr(), B, MIN_BEATS, tvals.data_ptr(),
+                          cnt.data_ptr(), st)
         else:
             prior.fill_(120.0)
 
@@ -498,62 +565,19 @@ class Engine:
         s1.wait_event(ev_chroma)
         n_boot = C.N_BOOTSTRAP
         il, gl, ih, gh = percentile_params(n_boot, C.CI_LEVEL)
-        vals = torch.cat([tvals, pvals])
-        jobs_a_off, jobs_b_off, caps = [], [], []
-        for b in range(B):      # tempo: A = nc valid, B = src valid
-            jobs_a_off.append(w0[2 * b])
-            jobs_b_off.append(w0[2 * b + 1])
-            caps.append(max(1, (w1[2 * b] - w0[2 * b]) + (w1[2 * b + 1] - w0[2 * b + 1])))
-        pbase = tvals.numel()
-        for b in range(len(pair_chunks)):   # pitch: A = nc_hz, B = src_hz
-            c0, c1 = pair_chunks[b]
-            jobs_a_off.append(pbase + n_cp + c0)
-            jobs_b_off.append(pbase + 2 * n_cp + c0)
-            caps.append(2 * (c1 - c0))
-        n_pitch_jobs = len(pair_chunks)
-        nj = B + n_pitch_jobs
-        wsoff, tot = [], 0
-        for c in caps:
-            wsoff.append(tot)
-            tot += self.ctx.lib.nc_bootstrap_job_bytes(int(c), n_boot)
-        # shift bootstrap (pitch.py:143-150, seed 0, log only)
-        s_off, s_caps, s_wsoff, s_tot = [], [], [], 0
-        for b in range(n_pitch_jobs):
-            c0, c1 = pair_chunks[b]
-            s_off.append(pbase + c0)
-            s_caps.append(c1 - c0)
-            s_wsoff.append(s_tot)
-            s_tot += self.ctx.lib.nc_bootstrap_job_bytes(int(c1 - c0), n_boot)
-        up = _Upload()
-        up.add("a_off", jobs_a_off, np.int64)
-        up.add("b_off", jobs_b_off, np.int64)
-        up.add("seed", seed_state(42) * nj, np.uint64)
-        up.add("wsoff", wsoff, np.int64)
-        up.add("cap", caps, np.int32)
-        up.add("p_n", [c1 - c0 for c0, c1 in pair_chunks] or [0], np.int32)
-        up.add("s_off", s_off or [0], np.int64)
-        up.add("s_seed", seed_state(0) * max(1, n_pitch_jobs), np.uint64)
-        up.add("s_wsoff", s_wsoff or [0], np.int64)
-        up.add("s_cap", s_caps or [1], np.int32)
-        db = up.commit(dev)
-        nc_idx = torch.arange(0, nF, 2, dtype=torch.long, device=dev)
-        src_idx = nc_idx + 1
-        a_n = torch.cat([tcount[nc_idx], db["p_n"][:n_pitch_jobs]]).to(torch.int32)
-        b_n = torch.cat([tcount[src_idx], db["p_n"][:n_pitch_jobs]]).to(torch.int32)
-        bout = torch.full((3 * nj,), float("nan"), **f64)
+        bout, sout = o["bout"], o["sout"]
         ws = self.workspace("boot", tot)
-        self.call("nc_bootstrap_ratio", vals.data_ptr(), db["a_off"].data_ptr(), a_n.data_ptr(),
-                  db["b_off"].data_ptr(), b_n.data_ptr(), nj, n_boot, db["seed"].data_ptr(), il, gl, ih, gh,
+        self.call("nc_bootstrap_ratio", o["vals"].data_ptr(), d["a_off"].data_ptr(), d["a_n"].data_ptr(),
+                  d["b_off"].data_ptr(), d["b_n"].data_ptr(), nj, n_boot, d["seed"].data_ptr(), il, gl, ih, gh,
                   C.MIN_VALID, bout[0:nj].data_ptr(), bout[nj:2 * nj].data_ptr(), bout[2 * nj:].data_ptr(), None,
-                  db["wsoff"].data_ptr(), db["cap"].data_ptr(), ws.data_ptr(), ws.numel(), st)
-        sout = torch.full((3 * max(1, n_pitch_jobs),), float("nan"), **f64)
+                  d["wsoff"].data_ptr(), d["cap"].data_ptr(), ws.data_ptr(), ws.numel(), st)
         if n_pitch_jobs:
             ws2 = self.workspace("boot_s", s_tot)
-            self.call("nc_bootstrap_ratio", vals.data_ptr(), db["s_off"].data_ptr(), db["p_n"].data_ptr(), None,
-                      None, n_pitch_jobs, n_boot, db["s_seed"].data_ptr(), il, gl, ih, gh, MIN_CHUNKS,
+            self.call("nc_bootstrap_ratio", o["vals"].data_ptr(), d["s_off"].data_ptr(), d["s_n"].data_ptr(), None,
+                      None, n_pitch_jobs, n_boot, d["s_seed"].data_ptr(), il, gl, ih, gh, MIN_CHUNKS,
                       sout[0:n_pitch_jobs].data_ptr(), sout[n_pitch_jobs:2 * n_pitch_jobs].data_ptr(),
-                      sout[2 * n_pitch_jobs:3 * n_pitch_jobs].data_ptr(), None, db["s_wsoff"].data_ptr(),
-                      db["s_cap"].data_ptr(), ws2.data_ptr(), ws2.numel(), st)
+                      sout[2 * n_pitch_jobs:3 * n_pitch_jobs].data_ptr(), None, d["s_wsoff"].data_ptr(),
+                      d["s_cap"].data_ptr(), ws2.data_ptr(), ws2.numel(), st)
 
         # ---------------------------------------------------------------- 6. IBI pass
         ibi = None
@@ -561,18 +585,19 @@ class Engine:
             ibi = self._ibi_pass(signals, d["f_off"], d["f_len"], f_len, prior, B)
 
         # ---------------------------------------------------------------- 7. async D2H into pinned buffers
-        dev_out = dict(energy=energy, active=active, bpm=bpm, nbeats=nbeats, lag=lag, margin=margin, prior=prior,
-                       tcount=tcount, clag=clag, pvals=pvals, tuning=tuning, chroma=chroma, bout=bout, sout=sout)
+        hbuf, host = ar.to_host()
+        host["pvals"] = host["vals"][TV:]
+        pinned = [hbuf]
         if ibi is not None:
-            dev_out.update({"ibi_" + k: v for k, v in ibi.items() if isinstance(v, torch.Tensor)})
-        host = {}
-        for k, v in dev_out.items():
-            h = torch.empty(v.shape, dtype=v.dtype, pin_memory=True)
-            h.copy_(v, non_blocking=True)
-            host[k] = h
+            for k, v in ibi.items():
+                if isinstance(v, torch.Tensor):
+                    h = torch.empty(v.shape, dtype=v.dtype, pin_memory=True)
+                    h.copy_(v, non_blocking=True)
+                    pinned.append(h)
+                    host["ibi_" + k] = h.numpy()
         ev = torch.cuda.Event()
         ev.record(torch.cuda.current_stream(dev))
-        return dict(p=p, host=host, event=ev, keep=(d, chroma, tuning, clag, pvals), has_ibi=ibi is not None,
+        return dict(p=p, host=host, pinned=pinned, event=ev, keep=(d, o, ar), has_ibi=ibi is not None,
                     starts=starts, w0=w0, w1=w1, f_len=f_len,
                     strip_len=strip_len, lead=lead, trail=trail, intro=intro, win_n=win_n,
                     pair_chunks=pair_chunks, n_cp=n_cp, nj=nj, n_pitch_jobs=n_pitch_jobs, B=B)
@@ -583,7 +608,7 @@ class Engine:
         t0 = time.perf_counter()
         g["event"].synchronize()
         t1 = time.perf_counter()
-        h = {k: v.numpy() for k, v in g["host"].items()}
+        h = dict(g["host"])
         # python-list views for the scalar accesses of the per-pair assembly loops
         for k in ("active", "bpm", "nbeats", "prior", "clag", "pvals", "bout", "sout"):
             h[k + "_l"] = h[k].tolist()
