@@ -11,9 +11,10 @@
 //   1. decimate_kernel x6     y_{i+1} = sqrt(2) * halfband(y_i)[::2]  (soxr_hq replacement)
 //   2. tuning_peaks_kernel    STFT 2048/512 (Hann) -> piptrack peaks, appended per chunk
 //   3. tuning_select_kernel   median(mag) -> residual histogram (0.01 bins) -> tuning index
-//   4. cqt_chroma_kernel      (frame, octave) items per wave: rect-window FFT 1024 ->
-//                             sparse basis[tuning] (LDS) -> |C|/sqrt(len) -> 12-bin chroma ->
-//                             inf-norm -> per-block partial sums (f64)
+//   4. cqt_chroma_kernel      (frame pair, octave) items per wave: two rect 1024 frames as one
+//                             complex FFT 1024, separated in registers -> sparse basis[tuning]
+//                             (register weights) -> |C|/sqrt(len) -> 12-bin chroma -> inf-norm
+//                             -> per-block partial sums (f64)
 //   5. chroma_finalize_kernel mean over frames -> f32[12] per chunk
 //   6. chroma_lag_kernel      argmax_k dot(src, roll(nc, -k)), wrapped to [-5, 6]
 #include <algorithm>
@@ -426,15 +427,39 @@ __global__ __launch_bounds__(NT) void tuning_select_kernel(const float* peak_pit
 }
 
 // ------------------------------------------------------------------------------ 4. CQT + chroma
-// One workgroup per (chunk, CQ_FR frames).  Work items are (frame, octave) pairs, one per
-// wave: rect-window 1024-sample frame of the octave signal -> 512-point complex FFT + real
-// split -> 36 sparse basis rows of the chunk's tuning (staged in LDS once per workgroup)
-// -> |C| sqrt(sr/my_sr) / sqrt(len) into an LDS row tile.  Then per frame the 12-bin chroma
-// (bins 3c-1, 3c, 3c+1 of each octave, in ascending bin order), its inf-norm, and the f64
-// sum over the workgroup's frames.
-constexpr int CQ_WAVES = 8;
-constexpr int CQ_FR = 16;
-using CqTw = StagedTw<512>;
+// One workgroup per (chunk, CQ_FR frames).  Work items are (frame pair, octave), one per
+// wave: the two real 1024-sample rect frames t, t+1 of the octave signal are packed as
+// z = x_t + i x_{t+1} into ONE 1024-point complex FFT (Stockham 16.16 through the wave's
+// LDS slot, then the last radix-4 stage on the lane's butterfly set
+// J = {l, 128-l, 128+l, 256-l} (lane 0: {0, 64, 192, 128}), which holds every output
+// k < 256 together with its mirror 1024 - k, so the two spectra separate in registers:
+//   X_t[k] = (Z[k] + conj Z[N-k]) / 2,   X_{t+1}[k] = (Z[k] - conj Z[N-k]) / 2i.
+// Only the bins the basis rows touch, [klo, khi], are written back (one float4 per bin
+// holding both frames); each lane's piece of a sparse row (weights in registers, loaded
+// once per workgroup for the chunk's tuning) reads them with 16-byte loads.  Per row
+// |C| sqrt(sr/my_sr) / sqrt(len) goes to an LDS row tile; then per frame the 12-bin
+// chroma (bins 3c-1, 3c, 3c+1 of each octave, ascending), its inf-norm and the f64 sum
+// over the workgroup's frames.
+#ifndef NC_CQ_WAVES
+#define NC_CQ_WAVES 16
+#endif
+#ifndef NC_CQ_DIAG  // diagnostic variants only (tools/var_build.sh): 1 no basis, 2 no loads, 4 no chroma tail
+#define NC_CQ_DIAG 0  // 8 no D writes, 16 constant stage-3 twiddles, 32 stage-3 inputs from registers
+#endif
+#ifndef NC_CQ_PREFETCH
+#define NC_CQ_PREFETCH 0
+#endif
+#ifndef NC_CQ_FR
+#define NC_CQ_FR 32
+#endif
+#ifndef NC_CQ_BPW
+#define NC_CQ_BPW 3
+#endif
+constexpr int CQ_WAVES = NC_CQ_WAVES;
+constexpr int CQ_FR = NC_CQ_FR;    // frames per block: CQ_FR / 2 * 7 (frame pair, octave) items
+constexpr int CQ_BPW = NC_CQ_BPW;  // consecutive blocks of one chunk per workgroup (persistent)
+constexpr int CQ_PMAX = 16;          // register-resident taps per lane piece (checked at launch)
+constexpr int CQ_TW2 = 15 * 16;      // stage-2 twiddles W_256^{k r}, [r - 1][k]
 
 struct CqtArgs {
   const float* sig;
@@ -445,11 +470,7 @@ struct CqtArgs {
   const int* tuning_idx;
   const float* ws_oct;
   const int64_t* tf_base;  // partial rows of chunk c start at tf_base[c] / CQ_FR + c
-  const float2* tw;
-  const int* cqt_lo;
-  const int* cqt_len;
-  const int* cqt_off;
-  const float2* cqt_w;
+  const float2* tw;        // exp(-2 pi i m / 8192)
   const float* cqt_isl;
   const int* cqt_plo;      // [tuning][64] lane pieces (nc_tables.cpp)
   const int* cqt_plen;
@@ -461,148 +482,191 @@ struct CqtArgs {
   double* partial;  // [n][nblk][12]
 };
 
-constexpr int CQ_SPLIT_R = 2;  // split rounds: 64 * CQ_SPLIT_R >= khi - klo + 1 (checked at launch)
+// butterfly b of lane l in the last stage: {l, 128-l, 128+l, 256-l}, lane 0 {0, 64, 192, 128}
+__device__ __forceinline__ int Jb(int l, int b) {
+  return b == 0 ? l : b == 1 ? (l ? 128 - l : 64) : b == 2 ? (l ? 128 + l : 192) : (l ? 256 - l : 128);
+}
 
-__host__ __device__ __forceinline__ int cq_al4(int n) { return (n + 3) & ~3; }
-
-size_t cqt_lds_bytes(int pmax) {
-  return sizeof(float2) * (cq_al4(CqTw::size) + (size_t)pmax * 64) + sizeof(int) * 4 * 64 +
-         sizeof(float) * (kCqtBins + CQ_FR * kCqtBins + 2 * CQ_FR * 12) + 16 +
-         sizeof(float2) * (size_t)CQ_WAVES * LdsSize<512>::value;
+// LDS: stage-2 twiddles | per-lane stage-3 twiddles | row tile [CQ_FR][252] | FFT slots (the
+// chroma tail's [CQ_FR][12] scratch reuses the slots once a block's items are done)
+constexpr int CQ_TILE = 7 * 12;  // per frame: octave partials [bin octave][chroma]
+size_t cqt_lds_bytes() {
+  static_assert(2 * CQ_FR * 12 * sizeof(float) <= LdsSize<1024>::value * sizeof(float2), "tail scratch");
+  return sizeof(float2) * (CQ_TW2 + 12 * 64) + sizeof(float) * (CQ_FR * CQ_TILE + CQ_WAVES * 72) + 16 +
+         sizeof(float2) * (size_t)CQ_WAVES * LdsSize<1024>::value;
 }
 
 __global__ __launch_bounds__(CQ_WAVES * 64) void cqt_chroma_kernel(CqtArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int c = blockIdx.y, fb = blockIdx.x;
+  constexpr int NT = CQ_WAVES * 64;
+  const int c = blockIdx.y;
   const int T = a.n_frames[c];
-  const int t0 = fb * CQ_FR;
-  if (t0 >= T) return;
-  const int tid = threadIdx.x, lane0 = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform (SGPR)
+  const int nb = (T + CQ_FR - 1) / CQ_FR;
+  const int fb0 = blockIdx.x * CQ_BPW;
+  if (fb0 >= nb) return;
+  const int fb1 = min(nb, fb0 + CQ_BPW);
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform (SGPR)
   float2* sh_tw = reinterpret_cast<float2*>(smem);
-  float2* sh_w = sh_tw + cq_al4(CqTw::size);                     // [pmax][64] column-major weights
-  int* sh_desc = reinterpret_cast<int*>(sh_w + a.pmax * 64);      // lo[64] len[64] partner[64] filt[64]
-  float* sh_isl = reinterpret_cast<float*>(sh_desc + 4 * 64);
-  float* sh_row = sh_isl + kCqtBins;              // [CQ_FR][252]
-  float* sh_ch = sh_row + CQ_FR * kCqtBins;       // [CQ_FR][12]
-  float* sh_nv = sh_ch + CQ_FR * 12;              // [CQ_FR][12]
-  // 16-byte aligned FFT slots after the tables (index arithmetic keeps the LDS address space)
-  const int fft_f = cq_al4((int)(sh_nv + CQ_FR * 12 - reinterpret_cast<float*>(smem)));
-  float2* fftbuf = reinterpret_cast<float2*>(reinterpret_cast<float*>(smem) + fft_f) + wave * LdsSize<512>::value;
+  float2* sh_tw3 = sh_tw + CQ_TW2;                // [12][64] per-lane stage-3 twiddles
+  float* sh_part = reinterpret_cast<float*>(sh_tw3 + 12 * 64);  // [CQ_FR][7][12] octave chroma partials
+  float* sh_mag = sh_part + CQ_FR * CQ_TILE + wave * 72;         // [2][36] this wave's item rows
+  const int fft_f = (int)(sh_part + CQ_FR * CQ_TILE + CQ_WAVES * 72 - reinterpret_cast<float*>(smem) + 3) & ~3;
+  float2* slots = reinterpret_cast<float2*>(reinterpret_cast<float*>(smem) + fft_f);
+  float2* fftbuf = slots + wave * LdsSize<1024>::value;
+  float* sh_ch = reinterpret_cast<float*>(slots);  // [CQ_FR][12], tail only
+  float* sh_nv = sh_ch + CQ_FR * 12;               // [CQ_FR][12], tail only
   const int ti = a.tuning_idx[c];
-  fill_staged_tw<512>(sh_tw, a.tw, tid, CQ_WAVES * 64);
-  for (int i = tid; i < a.pmax * 64; i += CQ_WAVES * 64) sh_w[i] = a.cqt_wcol[(size_t)ti * a.pmax * 64 + i];
-  for (int i = tid; i < 64; i += CQ_WAVES * 64) {
-    sh_desc[i] = a.cqt_plo[ti * 64 + i];
-    sh_desc[64 + i] = a.cqt_plen[ti * 64 + i];
-    sh_desc[128 + i] = a.cqt_partner[ti * 64 + i];
-    sh_desc[192 + i] = a.cqt_pfilt[ti * 64 + i];
+  for (int i = tid; i < CQ_TW2; i += NT) {
+    const int r = i / 16 + 1, k = i % 16;
+    sh_tw[i] = a.tw[(k * r * 32) & 8191];
   }
-  for (int i = tid; i < kCqtBins; i += CQ_WAVES * 64) sh_isl[i] = a.cqt_isl[ti * kCqtBins + i];
+  const float* isl = a.cqt_isl + ti * kCqtBins;
+  // per-lane constants for the whole workgroup: butterfly set, stage-3 twiddles W_1024^{J r},
+  // the lane's row piece and its weights
+  for (int i = tid; i < 12 * 64; i += NT) {  // sh_tw3[(3 b + r - 1) * 64 + l] = W_1024^{J_b(l) r}
+    const int l = i & 63, br = i >> 6, b = br / 3, r = br % 3 + 1;
+    sh_tw3[i] = a.tw[(Jb(l, b) * r * 8) & 8191];
+  }
+  const int plo = a.cqt_plo[ti * 64 + lane] - a.klo, plen = a.cqt_plen[ti * 64 + lane];
+  const int partner = a.cqt_partner[ti * 64 + lane], pfilt = a.cqt_pfilt[ti * 64 + lane];
+  float2 w[CQ_PMAX];
+#pragma unroll
+  for (int j = 0; j < CQ_PMAX; ++j)
+    w[j] = j < plen ? a.cqt_wcol[((size_t)ti * a.pmax + j) * 64 + lane] : make_float2(0.f, 0.f);
   __syncthreads();
 
+  for (int fb = fb0; fb < fb1; ++fb) {
+  const int t0 = fb * CQ_FR;
   const int nfr = min(CQ_FR, T - t0);
-  for (int it = wave; it < nfr * 7; it += CQ_WAVES) {
-    int lane = lane0;
-    asm volatile("" : "+v"(lane));
-    const int fl = it / 7, oct = it - 7 * fl;
-    const int t = t0 + fl;
+  const int npair = (nfr + 1) >> 1;
+  const int n_items = npair * 7;
+  // the two frames of item `item` in the stage-1 register layout z[l + 64 r]
+  auto load_item = [&](int item, int ln, FftIn<1024>& in) {
+    const int oct = item % 7;
+    const int t = t0 + 2 * (item / 7);
     const float* y = oct == 0 ? a.sig + a.chunk_off[c] : a.ws_oct + a.oct_off[c * 7 + oct];
     const int64_t Ly = a.oct_len[c * 7 + oct];
     const int hop = 512 >> oct;
-    const int64_t s0 = (int64_t)t * hop - 512;
-    FftIn<512> in;
-    if (s0 >= 0 && s0 + 1024 <= Ly && ((reinterpret_cast<uintptr_t>(y) & 7) == 0)) {
-      const float2* y2 = reinterpret_cast<const float2*>(y + s0);
+    const int64_t sA = (int64_t)t * hop - 512, sB = sA + hop;
+    if (NC_CQ_DIAG & 2) {
 #pragma unroll
-      for (int r = 0; r < 8; ++r) in[0][r] = y2[lane + 64 * r];
+      for (int r = 0; r < 16; ++r) in[0][r] = make_float2((float)(ln + r), (float)(item - r));
+    } else if (sA >= 0 && sB + 1024 <= Ly) {
+      const float* pa = y + (sA + ln);  // 64 r floats = immediate offsets of one base address
+      const float* pb = pa + hop;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) in[0][r] = make_float2(pa[64 * r], pb[64 * r]);
     } else {
 #pragma unroll
-      for (int r = 0; r < 8; ++r) {
-        const int n = lane + 64 * r;
-        const int64_t i0 = s0 + 2 * n;
-        const float x0 = (i0 >= 0 && i0 < Ly) ? y[i0] : 0.0f;
-        const float x1 = (i0 + 1 >= 0 && i0 + 1 < Ly) ? y[i0 + 1] : 0.0f;
-        in[0][r] = make_float2(x0, x1);
+      for (int r = 0; r < 16; ++r) {
+        const int64_t ia = sA + ln + 64 * r, ib = sB + ln + 64 * r;
+        in[0][r] = make_float2((ia >= 0 && ia < Ly) ? y[ia] : 0.0f, (ib >= 0 && ib < Ly) ? y[ib] : 0.0f);
       }
     }
-    wave_fft<512, 0>(in, fftbuf, sh_tw, lane);
-    // real split for the bins the rows touch only: X[k], k in [klo, khi] (all < 256)
-    float2 xk[CQ_SPLIT_R];
-    const int nk = a.khi - a.klo + 1;
+  };
+  FftIn<1024> in;
+  if (NC_CQ_PREFETCH && wave < n_items) load_item(wave, lane, in);
+  for (int it = wave; it < n_items; it += CQ_WAVES) {
+    // opaque lane id: per-lane addresses are recomputed per item instead of being hoisted
+    // out of the loop into registers (which would spill)
+    int ln = lane;
+    asm volatile("" : "+v"(ln));
+    const int pr = it / 7, oct = it - 7 * pr;
+    const int fl = 2 * pr;
+    if (!NC_CQ_PREFETCH) load_item(it, ln, in);
+    stockham_stage_regs<1024, 16, 1, 64, false, 0, 0>(in, fftbuf, sh_tw, ln);
+    // with NC_CQ_PREFETCH the next item's samples stream in while this one finishes
+    if (NC_CQ_PREFETCH && it + CQ_WAVES < n_items) load_item(it + CQ_WAVES, ln, in);
+    stockham_stage<1024, 16, 16, 64, false, 0, 0>(fftbuf, sh_tw, ln);
+    float2 v[4][4];
 #pragma unroll
-    for (int m = 0; m < CQ_SPLIT_R; ++m) {
-      const int k = a.klo + lane + 64 * m;
-      if (lane + 64 * m < nk) {
-        const float2 za = fftbuf[lpad(k)];
-        const float2 zb = cconj(fftbuf[lpad(512 - k)]);
-        const float2 E = cscale(cadd(za, zb), 0.5f);
-        const float2 O = cmul_mi(cscale(csub(za, zb), 0.5f));
-        xk[m] = cadd(E, cmul(sh_tw[CqTw::split + k], O));
+    for (int b = 0; b < 4; ++b)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        v[b][r] = (NC_CQ_DIAG & 32) ? make_float2(in[0][4 * b + r].y, in[0][(4 * b + r + 1) & 15].x)
+                                    : fftbuf[lpad(Jb(ln, b) + 256 * r)];
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+#pragma unroll
+      for (int r = 1; r < 4; ++r)
+        v[b][r] = cmul(v[b][r], (NC_CQ_DIAG & 16) ? make_float2(0.7f, 0.3f * r) : sh_tw3[(3 * b + r - 1) * 64 + ln]);
+      DFT<4>::run(v[b]);
+    }
+    // v[b][r] = Z[J[b] + 256 r]; the mirror of k = J[b] is Z[(256 - J[b]) + 768]
+    float4* D = reinterpret_cast<float4*>(fftbuf);  // D[k - klo] = (X_t[k], X_{t+1}[k]); all reads above precede
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+      const int k = Jb(ln, b);
+      if (!(NC_CQ_DIAG & 8) && k >= a.klo && k <= a.khi) {
+        const float2 m = b == 0 ? v[3][3] : b == 1 ? v[2][3] : b == 2 ? v[1][3] : (ln ? v[0][3] : v[3][3]);
+        const float2 za = v[b][0], zb = cconj(m);
+        const float2 s = csub(za, zb);
+        D[k - a.klo] = make_float4(0.5f * (za.x + zb.x), 0.5f * (za.y + zb.y), 0.5f * s.y, -0.5f * s.x);
       }
     }
-    float2* D = fftbuf;  // reuse as D[k] unpadded (all Z reads above precede these writes)
+    // lane piece of a sparse row (complex64 accumulation in row order) for both frames; the
+    // row's second half (partner lane) is then added to its first half
+    float ar = 0.0f, ai = 0.0f, br = 0.0f, bi = 0.0f;
 #pragma unroll
-    for (int m = 0; m < CQ_SPLIT_R; ++m)
-      if (lane + 64 * m < nk) D[a.klo + lane + 64 * m] = xk[m];
-    {
-      // lane piece of a sparse row (complex64 accumulation in row order), then the
-      // row's second half (partner lane) is added to its first half
-      const int lo = sh_desc[lane], len = sh_desc[64 + lane];
-      float re = 0.0f, im = 0.0f;
-#pragma unroll 2
-      for (int j = 0; j < len; ++j) {
-        const float2 w = sh_w[j * 64 + lane];
-        const float2 d = D[lo + j];
-        re = fmaf(w.x, d.x, fmaf(-w.y, d.y, re));
-        im = fmaf(w.x, d.y, fmaf(w.y, d.x, im));
+    for (int j = 0; j < CQ_PMAX; ++j) {
+      if (!(NC_CQ_DIAG & 1) && j < plen) {
+        const float4 d = D[plo + j];
+        ar = fmaf(w[j].x, d.x, fmaf(-w[j].y, d.y, ar));
+        ai = fmaf(w[j].x, d.y, fmaf(w[j].y, d.x, ai));
+        br = fmaf(w[j].x, d.z, fmaf(-w[j].y, d.w, br));
+        bi = fmaf(w[j].x, d.w, fmaf(w[j].y, d.z, bi));
       }
-      const int partner = sh_desc[128 + lane];
-      const float re2 = __shfl(re, partner < 0 ? lane : partner, 64);
-      const float im2 = __shfl(im, partner < 0 ? lane : partner, 64);
-      if (partner >= 0) {
-        re += re2;
-        im += im2;
-      }
-      const int filt = sh_desc[192 + lane];
-      if (filt < 0) continue;
+    }
+    const int src = partner < 0 ? ln : partner;
+    const float ar2 = __shfl(ar, src, 64), ai2 = __shfl(ai, src, 64);
+    const float br2 = __shfl(br, src, 64), bi2 = __shfl(bi, src, 64);
+    if (partner >= 0) {
+      ar += ar2;
+      ai += ai2;
+      br += br2;
+      bi += bi2;
+    }
+    if (pfilt >= 0) {
       const float oscale = sqrtf((float)(1 << oct));  // fft_basis *= sqrt(sr / my_sr)
-      const int bin = kCqtBins - kCqtFilt * (oct + 1) + filt;
-      sh_row[fl * kCqtBins + bin] = hypotf(re * oscale, im * oscale) * sh_isl[bin];
+      const float il = isl[kCqtBins - kCqtFilt * (oct + 1) + pfilt];
+      sh_mag[pfilt] = hypotf(ar * oscale, ai * oscale) * il;
+      sh_mag[36 + pfilt] = hypotf(br * oscale, bi * oscale) * il;
+    }
+    // this octave's share of the 12 chroma bins of both frames: bins 3c-1, 3c, 3c+1 (mod 36),
+    // in ascending order (c = 0: 0, 1, 35); tile row = bin octave 6 - oct (ascending bins)
+    if (ln < 24) {
+      const int f = ln >= 12, cc = ln - 12 * f;
+      const float* m = sh_mag + 36 * f;
+      const float p = cc == 0 ? (m[0] + m[1]) + m[35] : (m[3 * cc - 1] + m[3 * cc]) + m[3 * cc + 1];
+      if (fl + f < nfr) sh_part[(fl + f) * CQ_TILE + (6 - oct) * 12 + cc] = p;
     }
   }
   __syncthreads();
-  // chroma c <- CQT bins with (j mod 36) in {3c-1, 3c, 3c+1} (mod 36): octave-major, ascending
-  if (tid < nfr * 12) {
-    const int fl = tid / 12, cc = tid - 12 * fl;
-    const float* row = sh_row + fl * kCqtBins;
+  if (NC_CQ_DIAG & 4) continue;
+  // chroma c = sum over the 7 octaves (ascending bins) of the octave partials
+  for (int q = tid; q < nfr * 12; q += NT) {
+    const int fl = q / 12, cc = q - 12 * fl;
+    const float* pt = sh_part + fl * CQ_TILE + cc;
     float ch = 0.0f;
-    for (int o = 0; o < 7; ++o) {
-      const int b = 36 * o;
-      if (cc == 0) {
-        ch += row[b];
-        ch += row[b + 1];
-        ch += row[b + 35];
-      } else {
-        ch += row[b + 3 * cc - 1];
-        ch += row[b + 3 * cc];
-        ch += row[b + 3 * cc + 1];
-      }
-    }
-    sh_ch[tid] = ch;
+#pragma unroll
+    for (int o = 0; o < 7; ++o) ch += pt[12 * o];
+    sh_ch[q] = ch;
   }
   __syncthreads();
-  if (tid < nfr * 12) {
-    const int fl = tid / 12;
+  for (int q = tid; q < nfr * 12; q += NT) {
+    const int fl = q / 12;
     float mx = 0.0f;
     for (int j = 0; j < 12; ++j) mx = fmaxf(mx, fabsf(sh_ch[fl * 12 + j]));
     const double len = (mx < 1.17549435e-38f) ? 1.0 : (double)mx;
-    sh_nv[tid] = (float)((double)sh_ch[tid] / len);
+    sh_nv[q] = (float)((double)sh_ch[q] / len);
   }
   __syncthreads();
   if (tid < 12) {
     double acc = 0.0;
     for (int fl = 0; fl < nfr; ++fl) acc += (double)sh_nv[fl * 12 + tid];
     a.partial[(a.tf_base[c] / CQ_FR + c + fb) * 12 + tid] = acc;
+  }
+  __syncthreads();  // the slots are reused by the next block's items
   }
 }
 
@@ -751,10 +815,6 @@ int launch_chroma_mean(Context& ctx, const float* sig, const int64_t* chunk_off,
   ca.ws_oct = w.ws_oct;
   ca.tf_base = w.tf_base;
   ca.tw = ctx.t.tw;
-  ca.cqt_lo = ctx.t.cqt_lo;
-  ca.cqt_len = ctx.t.cqt_len;
-  ca.cqt_off = ctx.t.cqt_off;
-  ca.cqt_w = ctx.t.cqt_w;
   ca.cqt_isl = ctx.t.cqt_inv_sqrt_len;
   ca.cqt_plo = ctx.t.cqt_plo;
   ca.cqt_plen = ctx.t.cqt_plen;
@@ -764,15 +824,17 @@ int launch_chroma_mean(Context& ctx, const float* sig, const int64_t* chunk_off,
   ca.pmax = ctx.t.cqt_pmax;
   ca.klo = ctx.t.cqt_klo;
   ca.khi = ctx.t.cqt_khi;
-  if (ca.klo < 1 || ca.khi >= 256 || ca.khi - ca.klo + 1 > 64 * CQ_SPLIT_R) {
-    set_error("chroma: CQT basis bin range outside the split schedule");
+  // the mirror pairs (k, 1024 - k) of the packed FFT cover k in [1, 255]; D must fit a slot
+  if (ca.klo < 1 || ca.khi > 255 || ca.pmax > CQ_PMAX ||
+      (size_t)(ca.khi - ca.klo + 1) * sizeof(float4) > LdsSize<1024>::value * sizeof(float2)) {
+    set_error("chroma: CQT basis bin range / piece length outside the kernel's schedule");
     return -2;
   }
   ca.partial = w.partial;
   const int nblk = (int)((1 + max_chunk_len / 512 + CQ_FR - 1) / CQ_FR);
   {
     KTimer kt_(ctx, "cqt_chroma", st);
-    hipLaunchKernelGGL(cqt_chroma_kernel, dim3(nblk, n), dim3(CQ_WAVES * 64), cqt_lds_bytes(ca.pmax), st, ca);
+    hipLaunchKernelGGL(cqt_chroma_kernel, dim3((nblk + CQ_BPW - 1) / CQ_BPW, n), dim3(CQ_WAVES * 64), cqt_lds_bytes(), st, ca);
   }
   hipLaunchKernelGGL(chroma_finalize_kernel, dim3(n), dim3(64), 0, st, w.partial, w.tf_base, w.n_frames, n,
                      out_chroma);
