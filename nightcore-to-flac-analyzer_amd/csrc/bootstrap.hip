@@ -90,7 +90,7 @@ struct Gen32 {
   }
 };
 
-constexpr int BT = 1024;   // rank / finish workgroups
+constexpr int BT = 256;    // rank / finish workgroups (small: they share CUs with the other stream)
 constexpr int BD = 256;    // draw workgroups: one resample per thread
 constexpr int BD_NV = 96;  // resamples with na + nb <= BD_NV keep their rank counts in LDS
 

@@ -53,13 +53,13 @@ __device__ __forceinline__ int64_t chunk_oct_floats(int64_t L) {
 
 // one workgroup: per-chunk octave layout and frame counts, two parallel prefix tables
 // (oct_base = octave-buffer base of each chunk, tf_base = tuning-frame base)
-__global__ __launch_bounds__(1024) void chroma_plan_kernel(const int64_t* chunk_len, int n, int64_t* oct_off,
+__global__ __launch_bounds__(256) void chroma_plan_kernel(const int64_t* chunk_len, int n, int64_t* oct_off,
                                                            int64_t* oct_len, int* n_frames, int* n_tframes,
                                                            int64_t* tf_base, int64_t* oct_base) {
-  block_prefix_table<1024>(n, oct_base, [&](int c) { return chunk_oct_floats(chunk_len[c]); });
-  block_prefix_table<1024>(n, tf_base, [&](int c) { return 1 + chunk_len[c] / 512; });
+  block_prefix_table<256>(n, oct_base, [&](int c) { return chunk_oct_floats(chunk_len[c]); });
+  block_prefix_table<256>(n, tf_base, [&](int c) { return 1 + chunk_len[c] / 512; });
   __syncthreads();
-  for (int c = threadIdx.x; c < n; c += 1024) {
+  for (int c = threadIdx.x; c < n; c += 256) {
     int64_t L = chunk_len[c], acc = oct_base[c];
     int hop = 512, tmin = 0x7fffffff;
     for (int i = 0; i < 7; ++i) {
@@ -224,30 +224,20 @@ __global__ __launch_bounds__(TP_WAVES * 64) void tuning_peaks_kernel(PeakArgs a)
         in[0][r] = make_float2(x0 * a.hann2048[2 * n], x1 * a.hann2048[2 * n + 1]);
       }
     }
-    wave_fft<1024, 0>(in, fftbuf, sh_tw, lane);
-    float m1[9], m2[9];
-    const int pa = lpad(lane), pb = lpad(1024 - lane);
-#pragma unroll
-    for (int m = 0; m < 9; ++m) {
-      const int k = lane + 64 * m;
-      if (k <= 512) {
-        float2 X, XN;
-        rfft_split_m<1024, 0, TpTw::split>(fftbuf, sh_tw, lane, m, pa, pb, X, XN);
-        m1[m] = hypotf(X.x, X.y);
-        m2[m] = hypotf(XN.x, XN.y);
-      }
-    }
-    float* S = reinterpret_cast<float*>(fftbuf);
+    // stages 1-2 through LDS, the last stage on mirror-paired butterflies, then the real split
+    // and |X| straight from registers (stft_mel structure)
+    stockham_stage_regs<1024, 16, 1, 64, false, 0, 0>(in, fftbuf, sh_tw, lane);
+    stockham_stage<1024, 16, 16, 64, false, 0, 0>(fftbuf, sh_tw, lane);
+    float2 v[4][4];
+    fft1024_last_mirror<TpTw::s3>(fftbuf, sh_tw, lane, v);
+    float* S = reinterpret_cast<float*>(fftbuf);  // |X[k]|, k in [0, 1024] (all Z reads precede)
     float mx = 0.0f;
-#pragma unroll
-    for (int m = 0; m < 9; ++m) {
-      const int k = lane + 64 * m;
-      if (k <= 512) {
-        S[k] = m1[m];
-        S[1024 - k] = m2[m];
-        mx = fmaxf(mx, fmaxf(m1[m], m2[m]));
-      }
-    }
+    rsplit_mirror<TpTw::split>(v, sh_tw, lane, [&](int k, float2 X, float2 XN) {
+      const float m1 = __fsqrt_rn(fmaf(X.x, X.x, X.y * X.y)), m2 = __fsqrt_rn(fmaf(XN.x, XN.x, XN.y * XN.y));
+      S[k] = m1;
+      S[1024 - k] = m2;
+      mx = fmaxf(mx, fmaxf(m1, m2));
+    });
     mx = wave_max(mx);
     const float ref = 0.1f * mx;
     // bins inside [150, 4000) Hz: k * 22050 / 2048 -> 14..371 (6 rounds of 64 lanes)
@@ -768,7 +758,7 @@ int launch_chroma_mean(Context& ctx, const float* sig, const int64_t* chunk_off,
   w.peak_mag = reinterpret_cast<float*>(take(sizeof(float) * (size_t)tfr * kPeakSlots));
   w.partial = reinterpret_cast<double*>(take(sizeof(double) * (size_t)(tfr / CQ_FR + n + 1) * 12));
 
-  hipLaunchKernelGGL(chroma_plan_kernel, dim3(1), dim3(1024), 0, st, chunk_len, n, w.oct_off, w.oct_len, w.n_frames,
+  hipLaunchKernelGGL(chroma_plan_kernel, dim3(1), dim3(256), 0, st, chunk_len, n, w.oct_off, w.oct_len, w.n_frames,
                      w.n_tframes, w.tf_base, w.oct_base);
   NC_HIP(hipMemsetAsync(w.chunk_npk, 0, sizeof(int) * n, st));
   // grids are sized by the longest chunk; blocks past a chunk's own length exit
@@ -803,7 +793,7 @@ int launch_chroma_mean(Context& ctx, const float* sig, const int64_t* chunk_off,
       hipLaunchKernelGGL(tuning_peaks_kernel, dim3(grid), dim3(TP_WAVES * 64), lds, st, pa);
     }
   }
-  hipLaunchKernelGGL((tuning_select_kernel<1024>), dim3(n), dim3(1024), 0, st, w.peak_pitch, w.peak_mag,
+  hipLaunchKernelGGL((tuning_select_kernel<256>), dim3(n), dim3(256), 0, st, w.peak_pitch, w.peak_mag,
                      w.chunk_npk, w.tf_base, w.tuning_idx, out_tuning);
   CqtArgs ca;
   ca.sig = sig;

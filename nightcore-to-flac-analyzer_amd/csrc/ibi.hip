@@ -19,9 +19,9 @@
 namespace nc {
 
 // ------------------------------------------------------------------------------ frame indexing
-__global__ __launch_bounds__(1024) void ibi_plan_kernel(const int64_t* file_len, int n_files, int hop,
+__global__ __launch_bounds__(256) void ibi_plan_kernel(const int64_t* file_len, int n_files, int hop,
                                                         int64_t* frame_base) {
-  block_prefix_table<1024>(n_files, frame_base, [&](int f) { return 1 + file_len[f] / hop; });
+  block_prefix_table<256>(n_files, frame_base, [&](int f) { return 1 + file_len[f] / hop; });
 }
 
 __device__ __forceinline__ int find_file(const int64_t* base, int n, int64_t g) {
@@ -186,7 +186,7 @@ int launch_ibi_onset(Context& ctx, const float* sig, const int64_t* file_off, co
   float* fmax_ = reinterpret_cast<float*>(p);
   p += a256(sizeof(float) * (size_t)total_frames);
   float* sdb = reinterpret_cast<float*>(p);
-  hipLaunchKernelGGL(ibi_plan_kernel, dim3(1), dim3(1024), 0, st, file_len, n_files, hop, fb);
+  hipLaunchKernelGGL(ibi_plan_kernel, dim3(1), dim3(256), 0, st, file_len, n_files, hop, fb);
   StftMelArgs s{};
   s.sig = sig;
   s.seq_off = file_off;

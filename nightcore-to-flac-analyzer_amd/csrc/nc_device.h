@@ -319,4 +319,55 @@ __device__ __forceinline__ void rfft_split(const float2* lds, const float2* __re
   XNk = cconj(csub(E, WO));
 }
 
+
+// ------------------------------------------------------------------ mirror-paired last stage
+// Last radix-4 stage (NS = 256) of the 1024-point plan 16.16.4 done on the lane's butterfly
+// set J = {l, 128-l, 128+l, 256-l} (lane 0: {0, 64, 192, 128}) instead of j = l + 64 b.  The
+// set is closed under j -> 256 - j, so every output Z[k] sits in the same lane as its mirror
+// Z[1024 - k]: real-input splits need neither a final LDS write nor a cross-lane read.
+// v[b][r] = Z[J_b + 256 r].  STW3 = offset of the stage-3 table W_1024^{j r} at [r - 1][j].
+__device__ __forceinline__ int mirror_J(int l, int b) {
+  return b == 0 ? l : b == 1 ? (l ? 128 - l : 64) : b == 2 ? (l ? 128 + l : 192) : (l ? 256 - l : 128);
+}
+
+template <int STW3>
+__device__ __forceinline__ void fft1024_last_mirror(const float2* lds, const float2* tw, int l, float2 (&v)[4][4]) {
+#pragma unroll
+  for (int b = 0; b < 4; ++b)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) v[b][r] = lds[lpad(mirror_J(l, b) + 256 * r)];
+#pragma unroll
+  for (int b = 0; b < 4; ++b) {
+#pragma unroll
+    for (int r = 1; r < 4; ++r) v[b][r] = cmul(v[b][r], tw[STW3 + (r - 1) * 256 + mirror_J(l, b)]);
+    DFT<4>::run(v[b]);
+  }
+}
+
+// Real-FFT split of a 2048-sample real frame packed as z[n] = x[2n] + i x[2n+1] from the
+// mirror-paired outputs: f(k, X[k], X[1024 - k]) for the lane's 8 pairs (9 on lane 0),
+// k <= 512, together covering X[0..1024] once (X[512] twice on lane 0).  Same arithmetic as
+// rfft_split_m; SPLIT = offset of W_2048^k in tw.
+template <int SPLIT, class F>
+__device__ __forceinline__ void rsplit_mirror(const float2 (&v)[4][4], const float2* tw, int l, F&& f) {
+  const bool l0 = l == 0;
+  const int J1 = l0 ? 64 : 128 - l, J2 = l0 ? 192 : 128 + l, J3 = l0 ? 128 : 256 - l;
+  auto pair = [&](float2 za, float2 zm, int k) {
+    const float2 b = cconj(zm);
+    const float2 E = cscale(cadd(za, b), 0.5f);
+    const float2 O = cmul_mi(cscale(csub(za, b), 0.5f));  // (a-b)/(2i)
+    const float2 WO = cmul(tw[SPLIT + k], O);
+    f(k, cadd(E, WO), cconj(csub(E, WO)));
+  };
+  pair(v[0][0], l0 ? v[0][0] : v[3][3], l);
+  pair(v[0][1], l0 ? v[0][3] : v[3][2], l + 256);
+  pair(l0 ? v[0][2] : v[3][1], v[0][2], l0 ? 512 : J3 + 256);
+  pair(v[3][0], l0 ? v[3][3] : v[0][3], J3);
+  pair(v[1][0], v[2][3], J1);
+  pair(v[1][1], v[2][2], J1 + 256);
+  pair(v[2][1], v[1][2], J2 + 256);
+  pair(v[2][0], v[1][3], J2);
+  if (l0) pair(v[3][1], v[3][2], 384);
+}
+
 }  // namespace nc

@@ -146,6 +146,32 @@ void build_tables(Context& ctx) {
     t.mel_off = upload(offs);
     t.mel_w = upload(wts);
     t.mel_nnz = (int)wts.size();
+    // lane slots: lane l owns bands l (short) and 127 - l (long)
+    std::vector<int> lo4(128), nj4(128);
+    int jmax[2] = {0, 0};
+    for (int sl = 0; sl < 2; ++sl)
+      for (int l = 0; l < 64; ++l) {
+        const int b = sl ? 127 - l : l;
+        lo4[sl * 64 + l] = lo[b] & ~3;
+        nj4[sl * 64 + l] = (lo[b] - (lo[b] & ~3) + len[b] + 3) / 4;
+        jmax[sl] = std::max(jmax[sl], nj4[sl * 64 + l]);
+      }
+    t.mel_j0 = jmax[0];
+    t.mel_j1 = jmax[1];
+    std::vector<float4> w4((size_t)(jmax[0] + jmax[1]) * 64, make_float4(0.f, 0.f, 0.f, 0.f));
+    for (int sl = 0; sl < 2; ++sl)
+      for (int l = 0; l < 64; ++l) {
+        const int b = sl ? 127 - l : l;
+        for (int j = 0; j < 4 * nj4[sl * 64 + l]; ++j) {
+          const int k = lo4[sl * 64 + l] + j;
+          const float wv = (k >= lo[b] && k < lo[b] + len[b]) ? wts[offs[b] + k - lo[b]] : 0.0f;
+          float* q = reinterpret_cast<float*>(&w4[(size_t)((sl ? jmax[0] : 0) + j / 4) * 64 + l]);
+          q[j % 4] = wv;
+        }
+      }
+    t.mel_w4 = upload(w4);
+    t.mel_lo4 = upload(lo4);
+    t.mel_nj4 = upload(nj4);
   }
 
   // half-band decimator (oracle/ncref.py halfband_taps): 0.5 sinc(n/2) kaiser(n; 11), unit DC
@@ -341,7 +367,7 @@ void free_tables(Context& ctx) {
   Tables& t = ctx.t;
   void* ptrs[] = {t.tw, t.hann2048, t.hann_ac512, t.hann_ac64, t.wsq512, t.wsq64, t.mel_lo,  t.mel_len, t.mel_off,
                   t.mel_w,  t.cqt_lo,   t.cqt_len,    t.cqt_off,  t.cqt_w,   t.cqt_inv_sqrt_len, t.halfband,
-                  t.cqt_plo, t.cqt_plen, t.cqt_partner, t.cqt_pfilt, t.cqt_wcol};
+                  t.cqt_plo, t.cqt_plen, t.cqt_partner, t.cqt_pfilt, t.cqt_wcol, t.mel_w4, t.mel_lo4, t.mel_nj4};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   t = Tables();

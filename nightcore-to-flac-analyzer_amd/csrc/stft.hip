@@ -38,28 +38,21 @@ __device__ __forceinline__ int seq_of_frame(const int64_t* base, int n, int64_t 
 
 __host__ __device__ __forceinline__ int al4(int n) { return (n + 3) & ~3; }
 
-size_t stft_mel_lds_bytes(int mel_nnz) {
-  return (size_t)al4(SmTw::size) * sizeof(float2) + (size_t)al4(mel_nnz) * sizeof(float) + 3 * 128 * sizeof(int) +
+size_t stft_mel_lds_bytes(int mel_j) {
+  return (size_t)al4(SmTw::size) * sizeof(float2) + (size_t)mel_j * 64 * sizeof(float4) +
          (size_t)SM_WAVES * LdsSize<1024>::value * sizeof(float2);
 }
 
 __global__ __launch_bounds__(SM_THREADS) void stft_mel_kernel(StftMelArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   float2* sh_tw = reinterpret_cast<float2*>(smem);
-  float* sh_melw = reinterpret_cast<float*>(sh_tw + al4(SmTw::size));
-  int* sh_mel = reinterpret_cast<int*>(sh_melw + al4(a.mel_nnz));  // lo[128] len[128] off[128]
+  float4* sh_w4 = reinterpret_cast<float4*>(sh_tw + al4(SmTw::size));  // [mel_j0 + mel_j1][64]
   const int lane0 = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform (SGPR)
-  float2* fftbuf = reinterpret_cast<float2*>(sh_mel + 3 * 128) + wave * LdsSize<1024>::value;
+  float2* fftbuf = reinterpret_cast<float2*>(sh_w4 + (a.mel_j0 + a.mel_j1) * 64) + wave * LdsSize<1024>::value;
 
   fill_staged_tw<1024>(sh_tw, a.tw, threadIdx.x, SM_THREADS);
-  for (int i = threadIdx.x; i < a.mel_nnz; i += SM_THREADS) sh_melw[i] = a.mel_w[i];
-  for (int i = threadIdx.x; i < 128; i += SM_THREADS) {
-    sh_mel[i] = a.mel_lo[i];
-    sh_mel[128 + i] = a.mel_len[i];
-    sh_mel[256 + i] = a.mel_off[i];
-  }
+  for (int i = threadIdx.x; i < (a.mel_j0 + a.mel_j1) * 64; i += SM_THREADS) sh_w4[i] = a.mel_w4[i];
   __syncthreads();
-  // lane l owns bands l and 127 - l (short low band + long high band)
 
   const int64_t n_groups = (a.total_frames + SM_WAVES - 1) / SM_WAVES;
   const int64_t gb = n_groups * blockIdx.x / gridDim.x, ge = n_groups * (blockIdx.x + 1) / gridDim.x;
@@ -84,8 +77,7 @@ __global__ __launch_bounds__(SM_THREADS) void stft_mel_kernel(StftMelArgs a) {
     const int64_t s0 = t * a.hop - 1024;
 
     // Opaque lane id: every per-lane address and table load is recomputed each
-    // frame instead of being hoisted out of the loop (~140 extra VGPRs, which
-    // would cap occupancy at 2 waves/SIMD).
+    // frame instead of being hoisted out of the loop (which would cost occupancy).
     int lane = lane0;
     asm volatile("" : "+v"(lane));
     const float2* twl = sh_tw;
@@ -130,36 +122,39 @@ __global__ __launch_bounds__(SM_THREADS) void stft_mel_kernel(StftMelArgs a) {
       e = wave_sum(e);
       if (lane == 0) a.frame_energy[g] = e;
     }
-    wave_fft<1024, 0>(in, fftbuf, twl, lane);
-    float p1[9], p2[9];
-    const int pa = lpad(lane), pb = lpad(1024 - lane);
-#pragma unroll
-    for (int m = 0; m < 9; ++m) {
-      const int k = lane + 64 * m;
-      if (k <= 512) {
-        float2 X, XN;
-        rfft_split_m<1024, 0, SmTw::split>(fftbuf, twl, lane, m, pa, pb, X, XN);
-        p1[m] = fmaf(X.x, X.x, X.y * X.y);
-        p2[m] = fmaf(XN.x, XN.x, XN.y * XN.y);
-      }
-    }
-    float* pw = reinterpret_cast<float*>(fftbuf);
-#pragma unroll
-    for (int m = 0; m < 9; ++m) {
-      const int k = lane + 64 * m;
-      if (k <= 512) {
-        pw[k] = p1[m];
-        pw[1024 - k] = p2[m];
-      }
-    }
-    // lane l owns bands l and 127 - l (short low band + long high band)
-    const int lo0 = sh_mel[lane], len0 = sh_mel[128 + lane], off0 = sh_mel[256 + lane];
-    const int lo1 = sh_mel[127 - lane], len1 = sh_mel[255 - lane], off1 = sh_mel[383 - lane];
+    // 1024-point complex FFT of the packed frame: stages 1-2 through LDS, the last stage on
+    // mirror-paired butterflies, then the real split and |X|^2 straight from registers
+    stockham_stage_regs<1024, 16, 1, 64, false, 0, 0>(in, fftbuf, twl, lane);
+    stockham_stage<1024, 16, 16, 64, false, 0, 0>(fftbuf, twl, lane);
+    float2 v[4][4];
+    fft1024_last_mirror<SmTw::s3>(fftbuf, twl, lane, v);
+    float* pw = reinterpret_cast<float*>(fftbuf);  // power P[k], k in [0, 1024] (all Z reads precede)
+    rsplit_mirror<SmTw::split>(v, twl, lane, [&](int k, float2 X, float2 XN) {
+      pw[k] = fmaf(X.x, X.x, X.y * X.y);
+      pw[1024 - k] = fmaf(XN.x, XN.x, XN.y * XN.y);
+    });
+    // Slaney mel: lane l owns bands l and 127 - l, read as float4 steps from a 16-byte aligned
+    // first bin with zero-padded weights (fmaf chain in bin order, as the CSR form)
     float acc0 = 0.0f, acc1 = 0.0f;
-#pragma unroll 4
-    for (int j = 0; j < len0; ++j) acc0 = fmaf(sh_melw[off0 + j], pw[lo0 + j], acc0);
-#pragma unroll 4
-    for (int j = 0; j < len1; ++j) acc1 = fmaf(sh_melw[off1 + j], pw[lo1 + j], acc1);
+    {
+      const int lo = a.mel_lo4[lane], nj = a.mel_nj4[lane];
+      for (int j = 0; j < a.mel_j0; ++j)
+        if (j < nj) {
+          const float4 p = *reinterpret_cast<const float4*>(pw + lo + 4 * j);
+          const float4 w = sh_w4[j * 64 + lane];
+          acc0 = fmaf(w.w, p.w, fmaf(w.z, p.z, fmaf(w.y, p.y, fmaf(w.x, p.x, acc0))));
+        }
+    }
+    {
+      const int lo = a.mel_lo4[64 + lane], nj = a.mel_nj4[64 + lane];
+      const float4* w1 = sh_w4 + a.mel_j0 * 64;
+      for (int j = 0; j < a.mel_j1; ++j)
+        if (j < nj) {
+          const float4 p = *reinterpret_cast<const float4*>(pw + lo + 4 * j);
+          const float4 w = w1[j * 64 + lane];
+          acc1 = fmaf(w.w, p.w, fmaf(w.z, p.z, fmaf(w.y, p.y, fmaf(w.x, p.x, acc1))));
+        }
+    }
     const float db0 = 10.0f * log10f(fmaxf(1e-10f, acc0));
     const float db1 = 10.0f * log10f(fmaxf(1e-10f, acc1));
     float* row = a.sdb + g * 128;
@@ -180,11 +175,16 @@ int launch_stft_mel(Context& ctx, const StftMelArgs& args, hipStream_t st) {
   a.mel_off = ctx.t.mel_off;
   a.mel_w = ctx.t.mel_w;
   a.mel_nnz = ctx.t.mel_nnz;
+  a.mel_w4 = ctx.t.mel_w4;
+  a.mel_lo4 = ctx.t.mel_lo4;
+  a.mel_nj4 = ctx.t.mel_nj4;
+  a.mel_j0 = ctx.t.mel_j0;
+  a.mel_j1 = ctx.t.mel_j1;
   if (a.hop <= 0 || a.hop > 512 || (a.hop & 1)) {
     set_error("stft_mel: hop must be even and <= 512");
     return -2;
   }
-  const size_t lds = stft_mel_lds_bytes(a.mel_nnz);
+  const size_t lds = stft_mel_lds_bytes(a.mel_j0 + a.mel_j1);
   const int64_t n_groups = (a.total_frames + SM_WAVES - 1) / SM_WAVES;
   const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(n_groups, (int64_t)ctx.num_cu * (lds <= 80 * 1024 ? 2 : 1)));
   {

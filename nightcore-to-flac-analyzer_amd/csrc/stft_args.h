@@ -28,6 +28,10 @@ struct StftMelArgs {
   const int* mel_off;
   const float* mel_w;
   int mel_nnz;
+  const float4* mel_w4;
+  const int* mel_lo4;
+  const int* mel_nj4;
+  int mel_j0, mel_j1;
 };
 
 int launch_stft_mel(Context& ctx, const StftMelArgs& args, hipStream_t st);

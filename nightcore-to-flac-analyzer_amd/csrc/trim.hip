@@ -110,8 +110,8 @@ size_t trim_ws_bytes(const int64_t* host_file_len, int n_files) {
 }
 
 // frame_base is computed on the device from file_len (parallel exclusive scan, one block)
-__global__ __launch_bounds__(1024) void frame_base_kernel(const int64_t* file_len, int n_files, int64_t* frame_base) {
-  block_prefix_table<1024>(n_files, frame_base, [&](int f) { return 1 + file_len[f] / 512; });
+__global__ __launch_bounds__(256) void frame_base_kernel(const int64_t* file_len, int n_files, int64_t* frame_base) {
+  block_prefix_table<256>(n_files, frame_base, [&](int f) { return 1 + file_len[f] / 512; });
 }
 
 int launch_trim(Context& ctx, const float* sig, const int64_t* file_off, const int64_t* file_len, int n_files,
@@ -127,7 +127,7 @@ int launch_trim(Context& ctx, const float* sig, const int64_t* file_off, const i
   }
   int64_t* frame_base = static_cast<int64_t*>(ws);
   double* blk = reinterpret_cast<double*>(frame_base + n_files + 1);
-  hipLaunchKernelGGL(frame_base_kernel, dim3(1), dim3(1024), 0, st, file_len, n_files, frame_base);
+  hipLaunchKernelGGL(frame_base_kernel, dim3(1), dim3(256), 0, st, file_len, n_files, frame_base);
   const int64_t blocks = (max_frames + 3) / 4;
   {
     KTimer kt_(ctx, "trim_blocks", st);

@@ -72,6 +72,15 @@ def analyze(path, steps=5):
           f"({100 * busy / span:.1f} %), kernels {len(sel) // steps}/step")
     for k, v in sorted(per.items(), key=lambda x: -x[1])[:16]:
         print(f"  {k:48s} {v / steps / 1e6:7.3f} ms/step")
+    # one step in detail: start / end (us from the step start) and queue of every kernel
+    n1 = len(sel) // steps
+    q = "Queue_Id" if "Queue_Id" in sel[0] else ("Stream_Id" if "Stream_Id" in sel[0] else None)
+    t00 = int(sel[0]["Start_Timestamp"])
+    print("step 0 detail (us):")
+    for r in sel[:n1]:
+        k = r["Kernel_Name"].split("(")[0].replace("void ", "")[:40]
+        print(f"  q{r.get(q, '?') if q else '?':>3} {(int(r['Start_Timestamp']) - t00) / 1e3:9.1f} "
+              f"{(int(r['End_Timestamp']) - t00) / 1e3:9.1f}  {k}")
 
 
 if __name__ == "__main__":
