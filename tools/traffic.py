@@ -1,0 +1,67 @@
+#!/usr/bin/env python3
+"""Per-launch HBM traffic of the bench kernels from the two counter passes of
+tools/pmc_traffic.sh, corrected per MI355X_MICROARCH.md (FETCH_SIZE reports half the
+bytes of a wide coalesced read on gfx950: hbm = 2 x FETCH_SIZE + WRITE_SIZE, KiB -> B),
+written to profiles/r1_traffic.json for bench.py's roofline.traffic.
+    python3 tools/traffic.py OUTDIR"""
+import collections
+import csv
+import json
+import subprocess
+import sys
+from pathlib import Path
+
+REPO = Path(__file__).resolve().parents[1]
+TAGS = {"cqt_chroma_kernel": "cqt_chroma", "stft_mel_kernel": "stft_mel", "tuning_peaks_kernel": "tuning_peaks",
+        "trim_blocks_kernel": "trim_blocks", "window_tg_kernel": "window_tg", "decimate_kernel": "decimate"}
+# algorithmic bytes per step of the config-3 bench: 3968 windows x 882 000 B,
+# 896 chunks x 1 764 000 B, 64 pairs of 3 969 000 + 3 175 200 samples x 4 B for the trim pass
+ALG_STEP = {"cqt_chroma": 896 * 1764000, "stft_mel": 3968 * 882000, "trim_blocks": 64 * (3969000 + 3175200) * 4}
+
+
+def per_dispatch(d: Path, counter: str):
+    vals = collections.defaultdict(list)
+    for f in d.rglob("*counter_collection.csv"):
+        acc = collections.defaultdict(float)
+        for r in csv.DictReader(open(f)):
+            if r["Counter_Name"] != counter:
+                continue
+            name = r["Kernel_Name"].split("(")[0].split("::")[-1].split("<")[0]
+            if name in TAGS:
+                acc[(TAGS[name], r["Dispatch_Id"])] += float(r["Counter_Value"])
+        for (tag, _), v in acc.items():
+            vals[tag].append(v)
+    return vals
+
+
+def main(out):
+    out = Path(out)
+    fetch = per_dispatch(out / "FETCH_SIZE", "FETCH_SIZE")
+    write = per_dispatch(out / "WRITE_SIZE", "WRITE_SIZE")
+    commit = subprocess.run(["git", "rev-parse", "--short", "HEAD"], cwd=REPO, capture_output=True,
+                            text=True).stdout.strip() or "unknown"
+    kern = {}
+    for tag in sorted(set(fetch) | set(write)):
+        f = sum(fetch.get(tag, [0])) / max(1, len(fetch.get(tag, [])))
+        w = sum(write.get(tag, [0])) / max(1, len(write.get(tag, [])))
+        k = {"launches": len(fetch.get(tag, [])), "fetch_size_kib_raw": round(f, 2), "write_size_kib": round(w, 2),
+             "hbm_bytes_per_launch": int(round((2 * f + w) * 1024))}
+        if tag in ALG_STEP and fetch.get(tag):
+            # the profiled run does warmup + 2 timed + kernel-timer steps; launches per step from the count
+            steps = {"trim_blocks": 1}.get(tag, 5)
+            k["alg_bytes_per_launch"] = ALG_STEP[tag] // steps
+        kern[tag] = k
+    doc = {"workload": "config3-64pairs", "commit": commit,
+           "command": "tools/pmc_traffic.sh: rocprofv3 --pmc FETCH_SIZE, then a separate --pmc WRITE_SIZE pass, "
+                      "--output-format csv -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-ibi "
+                      "(means over every launch; groups of 16,16,16,8,8 pairs per step)",
+           "correction": "hbm_bytes = 2 x FETCH_SIZE + WRITE_SIZE (KiB -> bytes): on gfx950 FETCH_SIZE reports half "
+                         "the bytes of a wide coalesced read (MI355X_MICROARCH.md; calibrated with "
+                         "tools/calib_fetch.hip: a 1 GiB stream read reports 0.500 GiB)",
+           "kernels": kern}
+    (REPO / "profiles" / "r1_traffic.json").write_text(json.dumps(doc, indent=1) + "\n")
+    print(json.dumps(doc, indent=1))
+
+
+if __name__ == "__main__":
+    main(sys.argv[1])
