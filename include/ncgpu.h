@@ -221,6 +221,29 @@ int nc_xcorr_search(nc_ctx* ctx, const float* sig, const int64_t* item_a, const 
                     const int64_t* pb, const int64_t* exp_pb, int n_jobs, double* ratio_out,
                     double* quality_out, void* stream);
 
+/* ---------------------------------------------------------------------------
+ * intro offset of pipeline.run(auto_align=True) — xcorr.find_content_offset
+ * (xcorr.py:165-259; called at pipeline.py:111-125) for n_pairs (src, nc)
+ * pairs of 22050 Hz signals (sig[src_off[p] ..], src_len[p] samples; likewise
+ * nc): 2:1 resample to 11025 Hz, RMS envelopes (frame 2048, hop 512), for each
+ * of n_speeds candidate speeds (device f64, the reference's np.linspace(1.03,
+ * 1.5, 30)) the nc envelope stretched to int(len / speed) frames by np.interp
+ * and correlated with the first max_offset_frames + 1 lags of the src envelope
+ * (int(120 / (512 / 11025)) = 2583 in the reference); the cosine score of each
+ * speed's first argmax decides, first best wins.  Outputs per pair: peak lag
+ * (offset_sec = peak * 512 / 11025), speed index (-1: no speed searchable,
+ * the reference then returns (0.0, (lo + hi) / 2)) and the score.
+ * total_len = sum of all 2 n_pairs lengths, max_len = the longest (grid and
+ * workspace sizing); size ws with nc_align_workspace_bytes.
+ * ------------------------------------------------------------------------- */
+size_t nc_align_workspace_bytes(const nc_ctx* ctx, int n_pairs, int n_speeds, int64_t total_len,
+                                int64_t max_len, int max_offset_frames);
+int nc_align_offsets(nc_ctx* ctx, const float* sig, const int64_t* src_off, const int64_t* src_len,
+                     const int64_t* nc_off, const int64_t* nc_len, int n_pairs, const double* speeds,
+                     int n_speeds, int max_offset_frames, int64_t total_len, int64_t max_len,
+                     int* peak_out, int* speed_idx_out, double* score_out, void* ws, size_t ws_bytes,
+                     void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -20,6 +20,7 @@
 #include <algorithm>
 
 #include "nc_block.h"
+#include "nc_decim.h"
 #include "nc_engine.h"
 
 namespace nc {
@@ -80,76 +81,16 @@ __global__ __launch_bounds__(256) void chroma_plan_kernel(const int64_t* chunk_l
 }
 
 // ------------------------------------------------------------------------------ 1. decimation
-// out[m] = sqrt(2) * sum_{j=0}^{2K} h[j] in[2m - (j - K)]  (zero outside), accumulated in f64
-// in the oracle's order (ascending j, separate multiply and add: oracle/ncref.py decimate2).
-// One workgroup per DEC_OUT outputs; the 2 DEC_OUT + 2K input tile is staged in LDS and the
-// taps are wave-uniform (scalar loads); the zero taps of the half-band (even j - K != 0) are
-// skipped at compile time.
-constexpr int DEC_OUT = 1024;  // outputs per workgroup: 4 consecutive per thread
-
-__device__ __forceinline__ int dec_pad(int e) { return e + (e >> 3); }  // softens stride-4 bank reuse
-
+// y_{i+1} = sqrt(2) * halfband(y_i)[::2] per chunk and level (nc_decim.h)
 __global__ __launch_bounds__(256) void decimate_kernel(const float* sig, const int64_t* chunk_off,
                                                        const int64_t* oct_off, const int64_t* oct_len,
                                                        float* ws_oct, int level, const double* __restrict__ taps) {
-#pragma clang fp contract(off)
-  constexpr int K = kHalfbandK;       // 23: taps j - K odd (24 of them) plus the centre
-  constexpr int H = (K + 1) / 2;      // 12
-  constexpr int W = 4 + 2 * H - 1;    // odd-phase window of 4 consecutive outputs: 27 values
-  // in[2m - n] with n = j - K: the centre reads the even phase at m, odd n read the odd
-  // phase at m + c, c = (-n - 1) / 2 in [-H, H - 1].  Both phases are staged in LDS as f64;
-  // one float2 load fetches one even and one odd sample (coalesced, every input read once).
-  __shared__ double te[DEC_OUT + DEC_OUT / 8];
-  __shared__ double to[DEC_OUT + 2 * H + (DEC_OUT + 2 * H) / 8 + 1];
   const int c = blockIdx.y;
   const int64_t Lin = oct_len[c * 7 + level], Lout = oct_len[c * 7 + level + 1];
   const int64_t m0 = (int64_t)blockIdx.x * DEC_OUT;
   if (m0 >= Lout) return;
   const float* in = level == 0 ? sig + chunk_off[c] : ws_oct + oct_off[c * 7 + level];
-  float* out = ws_oct + oct_off[c * 7 + level + 1];
-  // pair p = (in[2p], in[2p + 1]) for p in [m0 - H, m0 + DEC_OUT + H); to[u] = odd phase at m0 - H + u
-  const bool vec = ((reinterpret_cast<uintptr_t>(in) & 7) == 0);
-  for (int u = threadIdx.x; u < DEC_OUT + 2 * H; u += 256) {
-    const int64_t pidx = m0 - H + u;
-    const int64_t i = 2 * pidx;
-    double e = 0.0, o = 0.0;
-    if (vec && i >= 0 && i + 1 < Lin) {
-      const float2 v = reinterpret_cast<const float2*>(in)[pidx];
-      e = (double)v.x;
-      o = (double)v.y;
-    } else {
-      if (i >= 0 && i < Lin) e = (double)in[i];
-      if (i + 1 >= 0 && i + 1 < Lin) o = (double)in[i + 1];
-    }
-    if (u >= H && u < H + DEC_OUT) te[dec_pad(u - H)] = e;
-    to[dec_pad(u)] = o;
-  }
-  __syncthreads();
-  const int l0 = 4 * threadIdx.x;
-  double xo[W], xe[4];
-#pragma unroll
-  for (int i = 0; i < W; ++i) xo[i] = to[dec_pad(l0 + i)];
-#pragma unroll
-  for (int q = 0; q < 4; ++q) xe[q] = te[dec_pad(l0 + q)];
-  double acc[4] = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-  for (int j = 0; j <= 2 * K; ++j) {  // the oracle's order: ascending j, multiply then add
-    const int n = j - K;
-    if (n != 0 && !(n & 1)) continue;
-    const double h = taps[j];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) acc[q] = acc[q] + h * (n == 0 ? xe[q] : xo[q + H + (-n - 1) / 2]);
-  }
-  const int64_t m = m0 + l0;
-  if (m + 3 < Lout && ((reinterpret_cast<uintptr_t>(out + m) & 15) == 0)) {
-    *reinterpret_cast<float4*>(out + m) =
-        make_float4((float)(acc[0] * 1.4142135623730951), (float)(acc[1] * 1.4142135623730951),
-                    (float)(acc[2] * 1.4142135623730951), (float)(acc[3] * 1.4142135623730951));
-  } else {
-#pragma unroll
-    for (int q = 0; q < 4; ++q)
-      if (m + q < Lout) out[m + q] = (float)(acc[q] * 1.4142135623730951);
-  }
+  halfband_tile<true>(in, Lin, ws_oct + oct_off[c * 7 + level + 1], Lout, m0, taps);
 }
 
 // ------------------------------------------------------------------------------ 2. tuning peaks

@@ -52,6 +52,11 @@ int launch_ibi_tempogram(Context& ctx, const float* onset, const int64_t* frame_
                          int64_t total_frames, int max_frames, int hop,
                          double* tg_out, void* ws, size_t ws_bytes, hipStream_t st);
 
+size_t align_ws_bytes(int n_pairs, int n_speeds, int64_t total_len, int64_t max_len, int max_off_frames);
+int launch_align_offsets(Context& ctx, const float* sig, const int64_t* src_off, const int64_t* src_len,
+                         const int64_t* nc_off, const int64_t* nc_len, int n_pairs, const double* speeds,
+                         int n_speeds, int max_off_frames, int64_t total_len, int64_t max_len, int* out_peak,
+                         int* out_speed, double* out_score, void* ws, size_t ws_bytes, hipStream_t st);
 int launch_xcorr(const float* sig, const int64_t* ia, const int64_t* ib, int n_items, int win, double* dot,
                  double* sqb, const int* w0, const int* w1, const int* sw, const int* c0, const int* c1,
                  const int64_t* pa, const int64_t* pbv, const int64_t* exp_pb, int n_jobs, double* ratio_out,
@@ -332,6 +337,23 @@ int nc_xcorr_search(nc_ctx* ctx, const float* sig, const int64_t* item_a, const 
   SET_DEVICE(ctx);
   return nc::launch_xcorr(sig, item_a, item_b, n_items, win, dot, sqb, w0, w1, win_self, cand0, cand1, pa, pb,
                           exp_pb, n_jobs, ratio_out, quality_out, (hipStream_t)stream);
+}
+
+size_t nc_align_workspace_bytes(const nc_ctx* ctx, int n_pairs, int n_speeds, int64_t total_len, int64_t max_len,
+                                int max_offset_frames) {
+  (void)ctx;
+  return nc::align_ws_bytes(n_pairs, n_speeds, total_len, max_len, max_offset_frames);
+}
+
+int nc_align_offsets(nc_ctx* ctx, const float* sig, const int64_t* src_off, const int64_t* src_len,
+                     const int64_t* nc_off, const int64_t* nc_len, int n_pairs, const double* speeds, int n_speeds,
+                     int max_offset_frames, int64_t total_len, int64_t max_len, int* peak_out, int* speed_idx_out,
+                     double* score_out, void* ws, size_t ws_bytes, void* stream) {
+  CHECK_CTX(ctx);
+  SET_DEVICE(ctx);
+  return nc::launch_align_offsets(ctx->c, sig, src_off, src_len, nc_off, nc_len, n_pairs, speeds, n_speeds,
+                                  max_offset_frames, total_len, max_len, peak_out, speed_idx_out, score_out, ws,
+                                  ws_bytes, (hipStream_t)stream);
 }
 
 }  // extern "C"

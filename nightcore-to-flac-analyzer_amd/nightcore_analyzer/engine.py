@@ -41,6 +41,9 @@ MIN_BEATS = 4
 CHUNK_SEC = 20.0
 MIN_CHUNKS = 3
 REF_HZ = 440.0
+ALIGN_SR, ALIGN_HOP = 11025, 512                                   # xcorr.py:45-46
+ALIGN_SPEED_LO, ALIGN_SPEED_HI, ALIGN_N_SPEEDS = 1.03, 1.50, 30    # xcorr.py:47-49
+ALIGN_MAX_OFFSET, ALIGN_MIN_OFFSET = 120.0, 1.0                   # xcorr.py:50-51
 _ALIGN = 64
 
 
@@ -309,6 +312,50 @@ class Engine:
         o = out.cpu().numpy()
         return [(float(o[i]), (float(o[n + i]), float(o[2 * n + i]))) for i in range(n)]
 
+    # -------------------------------------------------------------- auto-align (xcorr.py:165-259)
+    def align_offsets(self, buf: torch.Tensor, src_off, src_len, nc_off, nc_len, sr: int = SR,
+                      speed_lo: float = ALIGN_SPEED_LO, speed_hi: float = ALIGN_SPEED_HI,
+                      n_speeds: int = ALIGN_N_SPEEDS, max_offset_sec: float = ALIGN_MAX_OFFSET):
+        """xcorr.find_content_offset for every (src, nc) pair of signals already in ``buf``
+        (sample offsets / lengths): [(offset_sec, speed_est)] (one host sync)."""
+        if sr != 2 * ALIGN_SR:
+            raise NotImplementedError("the device resampler is 2:1 (sr 22050 -> 11025) only")
+        n = len(src_off)
+        if n == 0:
+            return []
+        speeds = np.linspace(speed_lo, speed_hi, n_speeds)            # xcorr.py:220
+        hop_sec = ALIGN_HOP / ALIGN_SR                                   # xcorr.py:213
+        max_frames = int(max_offset_sec / hop_sec)                       # xcorr.py:214
+        lens = np.concatenate([np.asarray(src_len, np.int64), np.asarray(nc_len, np.int64)])
+        up = _Upload()
+        up.add("src_off", src_off, np.int64)
+        up.add("src_len", src_len, np.int64)
+        up.add("nc_off", nc_off, np.int64)
+        up.add("nc_len", nc_len, np.int64)
+        up.add("speeds", speeds, np.float64)
+        d = up.commit(self.dev)
+        ar = _Arena()
+        ar.add("peak", n, np.int32)
+        ar.add("speed", n, np.int32)
+        ar.add("score", n, np.float64)
+        o = ar.commit(self.dev)
+        tot, mx = int(lens.sum()), int(max(1, lens.max()))
+        ws = self.workspace("align", self.ctx.lib.nc_align_workspace_bytes(self.ctx.h, n, n_speeds, tot, mx,
+                                                                           max_frames))
+        self.call("nc_align_offsets", buf.data_ptr(), d["src_off"].data_ptr(), d["src_len"].data_ptr(),
+                  d["nc_off"].data_ptr(), d["nc_len"].data_ptr(), n, d["speeds"].data_ptr(), n_speeds, max_frames,
+                  tot, mx, o["peak"].data_ptr(), o["speed"].data_ptr(), o["score"].data_ptr(), ws.data_ptr(),
+                  ws.numel(), self.stream())
+        hbuf, h = ar.to_host()
+        torch.cuda.current_stream(self.dev).synchronize()
+        out = []
+        for p_, s_ in zip(h["peak"].tolist(), h["speed"].tolist()):
+            if s_ < 0:
+                out.append((0.0, (speed_lo + speed_hi) / 2.0))
+            else:
+                out.append((p_ * hop_sec, float(speeds[s_])))
+        return out
+
     # -------------------------------------------------------------- batched pipeline
     def analyze(self, pairs: Optional[Sequence[Tuple[np.ndarray, np.ndarray]]] = None, params: Params = None,
                 signals: Optional[DeviceSignals] = None, group_pairs: int = 16) -> List[PairOutcome]:
@@ -322,8 +369,6 @@ class Engine:
         back asynchronously) before the host assembles the results of group g-1,
         so host assembly overlaps device work."""
         p = params or Params()
-        if p.auto_align and p.src_trim_sec == 0.0:
-            raise NotImplementedError("auto_align (xcorr.find_content_offset) is not on the MI355X path yet")
         if signals is None:
             flat = []
             for nc, src in pairs:
@@ -333,6 +378,10 @@ class Engine:
         hs = self.host_stats
         t0 = time.perf_counter()
         start, end = self._trim_all(signals, p)
+        align = None
+        if p.auto_align and p.src_trim_sec == 0.0:      # pipeline.py:111-125 (manual trim has priority)
+            align = self.align_offsets(signals.buf, signals.off[1::2] + start[1::2], end[1::2] - start[1::2],
+                                       signals.off[0::2] + start[0::2], end[0::2] - start[0::2])
         if hs is not None:
             hs["trim"] = hs.get("trim", 0.0) + time.perf_counter() - t0
         outs: List[PairOutcome] = []
@@ -341,7 +390,8 @@ class Engine:
             sl = slice(2 * g0, 2 * g1)
             sub = DeviceSignals(signals.buf, signals.off[sl], signals.length[sl])
             t0 = time.perf_counter()
-            nxt = self._launch_group(sub, p, start[sl].copy(), end[sl].copy())
+            nxt = self._launch_group(sub, p, start[sl].copy(), end[sl].copy(),
+                                     align[g0:g1] if align is not None else None)
             if hs is not None:
                 hs["launch"] = hs.get("launch", 0.0) + time.perf_counter() - t0
             if pending is not None:
@@ -371,7 +421,8 @@ class Engine:
         se_h = se.cpu().numpy()
         return se_h[:nF].copy(), se_h[nF:].copy()
 
-    def _launch_group(self, signals: DeviceSignals, p: Params, start: np.ndarray, end: np.ndarray) -> dict:
+    def _launch_group(self, signals: DeviceSignals, p: Params, start: np.ndarray, end: np.ndarray,
+                      align: Optional[List[Tuple[float, float]]] = None) -> dict:
         """Queue the whole device pipeline of one group of pairs; returns the pending group."""
         dev, st = self.dev, self.stream()
         nF = signals.n_files
@@ -390,6 +441,14 @@ class Engine:
                 f_off[f] += cut
                 f_len[f] -= cut
                 intro[b] = p.src_trim_sec
+        elif align is not None:
+            for b, (raw, _) in enumerate(align):
+                if raw >= ALIGN_MIN_OFFSET:                  # pipeline.py:114-116
+                    f = 2 * b + 1
+                    cut = min(int(raw * SR), int(f_len[f]))
+                    f_off[f] += cut
+                    f_len[f] -= cut
+                    intro[b] = raw
 
         # ---------------------------------------------------------------- 2. plan
         win_n, hop_n = int(p.window_sec * SR), int(p.hop_sec * SR)
@@ -597,7 +656,7 @@ class Engine:
                     host["ibi_" + k] = h.numpy()
         ev = torch.cuda.Event()
         ev.record(torch.cuda.current_stream(dev))
-        return dict(p=p, host=host, pinned=pinned, event=ev, keep=(d, o, ar), has_ibi=ibi is not None,
+        return dict(p=p, host=host, pinned=pinned, event=ev, keep=(d, o, ar), has_ibi=ibi is not None, align=align,
                     starts=starts, w0=w0, w1=w1, f_len=f_len,
                     strip_len=strip_len, lead=lead, trail=trail, intro=intro, win_n=win_n,
                     pair_chunks=pair_chunks, n_cp=n_cp, nj=nj, n_pitch_jobs=n_pitch_jobs, B=B)
@@ -617,7 +676,7 @@ class Engine:
         ibi = {k[4:]: v for k, v in h.items() if k.startswith("ibi_")} if g["has_ibi"] else None
         out = [self._assemble_pair(b, g["p"], h, ibi, g["starts_l"], g["w0"], g["w1"], g["f_len"], g["strip_len"],
                                    g["lead"], g["trail"], g["intro"][b], g["win_n"], g["pair_chunks"], g["n_cp"],
-                                   g["nj"], g["n_pitch_jobs"])
+                                   g["nj"], g["n_pitch_jobs"], g["align"][b] if g["align"] else None)
                for b in range(g["B"])]
         if hs is not None:
             hs["wait"] = hs.get("wait", 0.0) + t1 - t0
@@ -701,7 +760,7 @@ class Engine:
 
     # -------------------------------------------------------------- host assembly + logs
     def _assemble_pair(self, b, p: Params, h, ibi, starts, w0, w1, f_len, strip_len, lead, trail, intro,
-                       win_n, pair_chunks, n_cp, nj, n_pitch_jobs) -> PairOutcome:
+                       win_n, pair_chunks, n_cp, nj, n_pitch_jobs, align=None) -> PairOutcome:
         out = PairOutcome()
         L = out.logs.append
         fn, fs = 2 * b, 2 * b + 1
@@ -714,6 +773,13 @@ class Engine:
               f"  →  {strip_len[fs] / SR:.1f} s")
         if p.src_trim_sec > 0.0:
             L(f"Manual source trim: skipping {p.src_trim_sec:.2f}s from source start")
+        elif align is not None:                              # pipeline.py:111-125
+            raw, spd = align
+            L("Detecting intro offset (RMS envelope alignment)…")
+            if raw >= ALIGN_MIN_OFFSET:
+                L(f"  Intro detected — trimming {raw:.2f}s from source start  (speed hint: {spd:.4f}×)")
+            else:
+                L(f"  No significant intro offset detected  (raw: {raw:.2f}s < {ALIGN_MIN_OFFSET:.1f}s threshold)")
         L(f"Slicing into {p.window_sec:.0f} s windows (hop {p.hop_sec:.0f} s)…")
         L(f"  nightcore: {len(starts[fn])} windows  |  source: {len(starts[fs])} windows")
         L(f"Energy gating (threshold {p.energy_gate_db} dB below peak)…")

@@ -67,7 +67,7 @@ analyze = run
 def run_batch(pairs: Sequence[Tuple[PathOrArray, PathOrArray]], *, window_sec: float = WINDOW_SEC,
               hop_sec: float = HOP_SEC, energy_gate_db: float = ENERGY_GATE_DB,
               silence_strip_db: Optional[float] = SILENCE_STRIP_DB, src_trim_sec: float = 0.0,
-              compute_pitch: bool = True, compute_ibi: bool = True,
+              auto_align: bool = False, compute_pitch: bool = True, compute_ibi: bool = True,
               log: Optional[Callable[[str], None]] = None) -> List[Union[AnalysisResult, BaseException]]:
     """Analyse many (nightcore, source) pairs in one GPU batch.  Returns, per
     pair, the AnalysisResult or the exception ``run`` would have raised."""
@@ -75,7 +75,7 @@ def run_batch(pairs: Sequence[Tuple[PathOrArray, PathOrArray]], *, window_sec: f
     arrays = [(_load(n, quiet, "nightcore"), _load(s, quiet, "source")) for n, s in pairs]
     from .engine import get_engine
     outs = get_engine().analyze(arrays, _params(window_sec, hop_sec, energy_gate_db, silence_strip_db,
-                                                src_trim_sec, False, compute_pitch, compute_ibi))
+                                                src_trim_sec, auto_align, compute_pitch, compute_ibi))
     res = []
     for i, o in enumerate(outs):
         if log is not None:

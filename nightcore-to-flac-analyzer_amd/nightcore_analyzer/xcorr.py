@@ -5,8 +5,10 @@ reference's nightcore_analyzer/xcorr.py).
 decisions run on the MI355X (``nc_xcorr_search``); the reference's integer
 geometry (edge trim, linspace window positions, stride candidates) is planned
 on the host exactly as the reference computes it.
-``find_content_offset`` (xcorr.py:165-259) is the next row of the build
- and is not on the device path yet.
+``find_content_offset`` (xcorr.py:165-259, the intro search of
+``pipeline.run(auto_align=True)``): 2:1 resample, RMS envelopes, the 30-speed
+stretch / correlate / cosine-score search, all on the MI355X
+(``nc_align_offsets``); a batch of pairs is searched at once by the engine.
 """
 from __future__ import annotations
 
@@ -52,10 +54,16 @@ def estimate_speed_xcorr(path_a: Union[str, Path], path_b: Union[str, Path], sr:
     return estimate_speed_xcorr_arrays(ya, yb, sr, n_windows, window_sec, search_range, skip_edges)
 
 
-def find_content_offset(src_audio, nc_audio, sr, *, speed_lo=ALIGN_SPEED_LO, speed_hi=ALIGN_SPEED_HI,
-                        n_speeds=ALIGN_N_SPEEDS, max_offset_sec=ALIGN_MAX_OFFSET):
-    raise NotImplementedError("find_content_offset (auto_align) is the next row of the MI355X build "
-                              "(SURVEY.md §8f); pass src_trim_sec instead")
+def find_content_offset(src_audio: np.ndarray, nc_audio: np.ndarray, sr: int, *, speed_lo: float = ALIGN_SPEED_LO,
+                        speed_hi: float = ALIGN_SPEED_HI, n_speeds: int = ALIGN_N_SPEEDS,
+                        max_offset_sec: float = ALIGN_MAX_OFFSET) -> Tuple[float, float]:
+    """(offset_sec, speed_est): seconds of src_audio before the content that matches the
+    start of nc_audio, and the speed of the best (speed, lag) envelope match."""
+    from .engine import get_engine
+    eng = get_engine()
+    sig = eng.upload_signals([np.asarray(src_audio, np.float32), np.asarray(nc_audio, np.float32)])
+    return eng.align_offsets(sig.buf, sig.off[:1], sig.length[:1], sig.off[1:], sig.length[1:], sr,
+                             speed_lo, speed_hi, n_speeds, max_offset_sec)[0]
 
 
 def quality_label(quality: float) -> str:

@@ -415,6 +415,23 @@ def decimate2(y: np.ndarray, taps: np.ndarray | None = None) -> np.ndarray:
     return (out * np.sqrt(2.0)).astype(np.float32)
 
 
+def resample_half(y: np.ndarray, taps: np.ndarray | None = None) -> np.ndarray:
+    """librosa.resample(y, orig_sr=2 sr', target_sr=sr', res_type='soxr_hq') with the
+    default scale=False, restated with ``halfband_taps`` (decimate2 without the sqrt(2))."""
+    if taps is None:
+        taps = halfband_taps()
+    K = (len(taps) - 1) // 2
+    y = np.asarray(y, dtype=np.float32).astype(np.float64)
+    M = (len(y) + 1) // 2
+    yp = np.pad(y, (K, K + 1))
+    out = np.zeros(M, dtype=np.float64)
+    for j, n in enumerate(range(-K, K + 1)):
+        if taps[j] == 0.0:
+            continue
+        out += taps[j] * yp[K - n: K - n + 2 * M: 2][:M]
+    return out.astype(np.float32)
+
+
 def interval_frequencies(n_bins, fmin, bins_per_octave):
     ratios = 2.0 ** (np.arange(0, bins_per_octave, dtype=float) / bins_per_octave)
     n_oct = int(np.ceil(n_bins / len(ratios)))

@@ -27,6 +27,9 @@ CHUNK_SEC, MIN_CHUNKS = 20.0, 3          # pitch.py:44-45
 REF_HZ = 440.0                           # pitch.py:50
 N_BOOTSTRAP, CI_LEVEL, MIN_VALID = 2000, 0.95, 3   # consensus.py:52-55
 PURE_NC_TOLERANCE = 0.02                 # consensus.py:54
+ALIGN_SR, ALIGN_HOP = 11025, 512         # xcorr.py:45-46
+ALIGN_SPEED_LO, ALIGN_SPEED_HI, ALIGN_N_SPEEDS = 1.03, 1.50, 30   # xcorr.py:47-49
+ALIGN_MAX_OFFSET, ALIGN_MIN_OFFSET = 120.0, 1.0                  # xcorr.py:50-51
 
 
 # ------------------------------------------------------------------ io.py
@@ -219,7 +222,7 @@ def build_result(src_p, nc_p, src_t, nc_t, nc_duration=None, src_duration=None) 
 # ------------------------------------------------------------------ pipeline.py
 def run_arrays(nc_audio, src_audio, sr=SR, *, window_sec=WINDOW_SEC, hop_sec=HOP_SEC,
                energy_gate_db=ENERGY_GATE_DB, silence_strip_db=SILENCE_STRIP_DB,
-               src_trim_sec=0.0, compute_pitch=True, compute_ibi=True) -> dict:
+               src_trim_sec=0.0, auto_align=False, compute_pitch=True, compute_ibi=True) -> dict:
     """pipeline.py:23-216 on decoded arrays (load_audio is out of scope)."""
     nc_audio = np.asarray(nc_audio, np.float32)
     src_audio = np.asarray(src_audio, np.float32)
@@ -230,6 +233,11 @@ def run_arrays(nc_audio, src_audio, sr=SR, *, window_sec=WINDOW_SEC, hop_sec=HOP
     if src_trim_sec > 0.0:                                             # :106-110
         src_audio = src_audio[int(src_trim_sec * sr):]
         intro = src_trim_sec
+    elif auto_align:                                                   # :111-125
+        raw_offset, _ = find_content_offset(src_audio, nc_audio, sr)
+        if raw_offset >= ALIGN_MIN_OFFSET:
+            src_audio = src_audio[int(raw_offset * sr):]
+            intro = raw_offset
     ncw = energy_gate(slice_windows(nc_audio, sr, window_sec, hop_sec), energy_gate_db)
     srw = energy_gate(slice_windows(src_audio, sr, window_sec, hop_sec), energy_gate_db)
     if not ncw or not srw:                                             # :142-146
@@ -305,6 +313,44 @@ def estimate_speed_xcorr_arrays(ya, yb, sr=SR, n_windows=20, window_sec=3.0,
     a = np.array([c[0] for c in corr], dtype=float)
     b = np.array([c[1] for c in corr], dtype=float)
     return float(np.polyfit(a, b, 1)[0]), float(np.median(qual))
+
+
+def find_content_offset(src_audio, nc_audio, sr=SR, *, speed_lo=ALIGN_SPEED_LO, speed_hi=ALIGN_SPEED_HI,
+                        n_speeds=ALIGN_N_SPEEDS, max_offset_sec=ALIGN_MAX_OFFSET, detail=False):
+    """xcorr.py:165-259: RMS-envelope cross-correlation over a grid of nightcore speeds.
+    Returns (offset_sec, speed); with detail=True also (peak_idx, speed_idx, score) of the
+    winner (speed_idx -1 when no speed is searchable)."""
+    if sr != 2 * ALIGN_SR:
+        raise NotImplementedError("the restated resampler is 2:1 (sr 22050 -> 11025) only")
+    src_env = ncref.rms_frames(ncref.resample_half(src_audio), 2048, ALIGN_HOP).astype(np.float64)  # :205-211
+    nc_env = ncref.rms_frames(ncref.resample_half(nc_audio), 2048, ALIGN_HOP).astype(np.float64)
+    hop_sec = ALIGN_HOP / ALIGN_SR                                     # :213
+    max_offset_frames = int(max_offset_sec / hop_sec)                  # :214
+    best_score, best_offset, best_speed = -1.0, 0.0, (speed_lo + speed_hi) / 2.0
+    best = (0, -1, -1.0)
+    for si, speed in enumerate(np.linspace(speed_lo, speed_hi, n_speeds)):   # :220
+        n_st = int(len(nc_env) / speed)
+        if n_st < 4 or n_st >= len(src_env):
+            continue
+        stretched = np.interp(np.linspace(0.0, 1.0, n_st), np.linspace(0.0, 1.0, len(nc_env)), nc_env)
+        search_len = min(max_offset_frames, len(src_env) - n_st)       # :237
+        if search_len <= 0:
+            continue
+        corr = np.correlate(src_env[:search_len + n_st], stretched, mode="valid")[:search_len + 1]
+        if len(corr) == 0:
+            continue
+        peak_idx = int(np.argmax(corr))
+        peak_val = float(corr[peak_idx])
+        win_energy = float(np.sum(src_env[peak_idx:peak_idx + n_st] ** 2))   # :252-254
+        query_energy = float(np.sum(stretched ** 2))
+        denom = np.sqrt(win_energy * query_energy)
+        score = peak_val / denom if denom > 1e-12 else 0.0
+        if score > best_score:                                         # :257
+            best_score, best_offset, best_speed = score, peak_idx * hop_sec, speed
+            best = (peak_idx, si, score)
+    if detail:
+        return best_offset, float(best_speed), best
+    return best_offset, float(best_speed)
 
 
 def rubberband_pitch_st(pitch_ratio):     # consensus.py:355

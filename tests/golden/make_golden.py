@@ -137,6 +137,13 @@ def _make_librosa_shim():
     def chroma_cqt(y=None, sr=22050, bins_per_octave=36, hop_length=512, **kw):
         return ncref.chroma_cqt(y, sr, hop_length, bins_per_octave)
 
+    def resample(y, orig_sr=22050, target_sr=11025, res_type="soxr_hq", scale=False, **kw):
+        assert orig_sr == 2 * target_sr and not scale, (orig_sr, target_sr, scale)
+        return ncref.resample_half(y)
+
+    def rms(y=None, frame_length=2048, hop_length=512, **kw):
+        return ncref.rms_frames(y, frame_length, hop_length)[np.newaxis, :]
+
     lib.load = load
     lib.effects.trim = trim
     lib.onset.onset_strength = onset_strength
@@ -144,6 +151,8 @@ def _make_librosa_shim():
     lib.feature.tempogram = tempogram
     lib.feature.tempo = tempo
     lib.feature.chroma_cqt = chroma_cqt
+    lib.feature.rms = rms
+    lib.resample = resample
     lib.frames_to_time = frames_to_time
     sys.modules["librosa"] = lib
     return lib
@@ -198,7 +207,7 @@ def _result_fields(r) -> dict:
 
 # ----------------------------------------------------------------------------- cases
 sys.path.insert(0, str(OUT))
-from cases import PIPELINE_CASES, edit as _edit  # noqa: E402
+from cases import ALIGN_CASES, PIPELINE_CASES, edit as _edit, make_align_pair  # noqa: E402
 
 
 def gen_pipeline(mods, names=None):
@@ -210,7 +219,7 @@ def gen_pipeline(mods, names=None):
             continue
         nc, src = synth.make_pair(secs, seed, kind)
         if edit:
-            nc, src = _edit(nc, src, edit, seed)
+            nc, src = _edit(nc, src, edit, seed, synth, secs)
         ncp, srp = tmp / f"{name}_nc.wav", tmp / f"{name}_src.wav"
         ncp.write_bytes(b"x")
         srp.write_bytes(b"x")
@@ -347,6 +356,14 @@ def gen_units(mods, pkg):
                         "rb": cons._rubberband_params(tr, pr, ncd, srd)}
                        for tr, pr, ncd, srd in [(1.25, 1.08, 143.9, 179.9), (1.2, 1.2, None, None),
                                                 (0.9, 1.0, 100.0, 90.0)]]
+    # xcorr.find_content_offset (xcorr.py:165-259) on intro pairs (inputs from cases.ALIGN_CASES)
+    al = []
+    for secs, seed, intro, up, down in ALIGN_CASES:
+        nc, src = make_align_pair(synth, secs, seed, intro, up, down)
+        off, spd = mods["xcorr"].find_content_offset(src, nc, 22050)
+        al.append({"seconds": secs, "seed": seed, "intro": intro, "up": up, "down": down,
+                   "src_sha256": _sha(src), "nc_sha256": _sha(nc), "offset": off, "speed": float(spd)})
+    g["find_content_offset"] = al
     # tempo.estimate_tempo agreement branch is driven by beat_track/tempo; record one window
     nc, src = synth.make_pair(12.0, 1004, "chords")
     w = io.AudioWindow(src[:220500], 22050, 0.0, 10.0, 0.0)

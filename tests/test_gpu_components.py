@@ -90,6 +90,27 @@ def test_xcorr_speed_matches_oracle(eng, speed):
     assert xcorr.estimate_speed_xcorr_arrays(np.zeros(500_000, np.float32), yb) == (1.0, 0.0)
 
 
+def test_find_content_offset_matches_reference(eng, golden_units):
+    """The device intro search reproduces the reference's find_content_offset goldens, one
+    pair at a time (the drop-in) and as one batch (the engine path of run(auto_align))."""
+    from golden.cases import make_align_pair
+    pairs, exp = [], []
+    for c in golden_units["find_content_offset"]:
+        nc, src = make_align_pair(synth, c["seconds"], c["seed"], c["intro"], c["up"], c["down"])
+        assert xcorr.find_content_offset(src, nc, 22050) == (c["offset"], c["speed"])
+        pairs.append((src, nc))
+        exp.append((c["offset"], c["speed"]))
+    sig = eng.upload_signals([a for p in pairs for a in p])
+    got = eng.align_offsets(sig.buf, sig.off[0::2], sig.length[0::2], sig.off[1::2], sig.length[1::2])
+    assert got == exp
+    # a 60-min source against a 48-min nightcore: the device search matches the oracle
+    rng = np.random.default_rng(5)
+    g = np.repeat(rng.uniform(0.25, 1.0, 3601), 22050).astype(np.float32)
+    src = (np.resize(synth.make_source(60.0, 1013), 3600 * 22050) * g[:3600 * 22050]).astype(np.float32)
+    nc = scipy.signal.resample_poly(src[30 * 22050:], 4, 5).astype(np.float32)
+    assert xcorr.find_content_offset(src, nc, 22050) == refglue.find_content_offset(src, nc, 22050)
+
+
 def test_full_size_pair_properties(eng):
     """BASELINE config 2 (one 3-min pair): exact window counts and duration ratio,
     tempo on the expected grid lags (21 / 17), chroma lag +4 on every chunk, IBI ~1.25."""

@@ -77,7 +77,18 @@ def test_classify_grid(golden_units):
         assert refglue.classify(c["tr"], c["pr"], tuple(c["tci"]), tuple(c["pci"])) == c["cls"]
 
 
-@pytest.mark.parametrize("name,ibi", [("sweep30", True), ("chords60_gate", False), ("chords75_silence", False)])
+def test_find_content_offset_matches_reference(golden_units):
+    """xcorr.find_content_offset (xcorr.py:165-259) of the reference, run on the same
+    primitives: identical (offset, speed) on every intro / no-intro / too-short case."""
+    from golden.cases import make_align_pair
+    for c in golden_units["find_content_offset"]:
+        nc, src = make_align_pair(synth, c["seconds"], c["seed"], c["intro"], c["up"], c["down"])
+        assert _sha(src) == c["src_sha256"] and _sha(nc) == c["nc_sha256"]
+        assert refglue.find_content_offset(src, nc, 22050) == (c["offset"], c["speed"])
+
+
+@pytest.mark.parametrize("name,ibi", [("sweep30", True), ("chords60_gate", False), ("chords75_silence", False),
+                                      ("chords60_intro", False)])
 def test_run_arrays_matches_reference_pipeline(golden_pipeline, name, ibi):
     """The oracle's pipeline restatement reproduces the reference's pipeline.run
     (run with the same primitives) on every decision and number."""
