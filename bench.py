@@ -118,6 +118,7 @@ def main():
     ap.add_argument("--seconds", type=float, default=180.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-ibi", action="store_true")
+    ap.add_argument("--no-config5", action="store_true", help="skip the 60-min pair (BASELINE configs[4]) timing")
     ap.add_argument("--cpu-workers", type=int, default=8, help="CPU baseline processes (one pair each)")
     ap.add_argument("--workers", type=int, default=min(16, os.cpu_count() or 1))
     args = ap.parse_args()
@@ -207,6 +208,29 @@ def main():
         ibi = {"pairs": 2, "seconds_per_pair": (t_ibi - t_no) / 2, "hop64_frames_per_s": frames / max(1e-9, t_ibi - t_no),
                "ibi_ratio_pair0": o2[0].result.ibi_ratio}
 
+    # BASELINE configs[4]: one 60-min pair, the whole run() incl. the hop-64 IBI pass, plus the
+    # waveform xcorr verification search (xcorr.estimate_speed_xcorr) over the same signals
+    cfg5 = None
+    if not args.no_config5 and rank == 0 and world == 1:
+        from nightcore_analyzer import xcorr as X
+        nc5, src5 = make_pairs(1, 3600.0, 5000, 1)[0]
+        sig5 = eng.upload_signals([nc5, src5])
+        eng.analyze(signals=sig5, params=E.Params(compute_ibi=True))
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        o5, = eng.analyze(signals=sig5, params=E.Params(compute_ibi=True))
+        torch.cuda.synchronize()
+        t_run = time.perf_counter() - t1
+        t1 = time.perf_counter()
+        xr = X.estimate_speed_xcorr_arrays(src5, src5)
+        t_x = time.perf_counter() - t1
+        cfg5 = {"workload": "config 5: one 60-min pair (src 3600 s, nc = resample_poly(src, 4, 5)), run() with "
+                            "the hop-64 IBI pass; xcorr search src vs src (host upload included)",
+                "seconds_run": t_run, "seconds_xcorr": t_x,
+                "hop64_frames": int((1 + len(nc5) // 64) + (1 + len(src5) // 64)),
+                "windows": int(o5.detail["energy_src"].size + o5.detail["energy_nc"].size),
+                "tempo_ratio": o5.result.tempo_ratio, "ibi_ratio": o5.result.ibi_ratio, "xcorr_ratio": xr[0]}
+
     if rank == 0:
         line = {
             "metric": "10 s windows/sec (CQT+onset, 22.05 kHz mono) at 1/2/4/8 GPUs; % HBM roofline",
@@ -241,6 +265,8 @@ def main():
         }
         if ibi is not None:
             line["ibi_pass"] = ibi
+        if cfg5 is not None:
+            line["config5"] = cfg5
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(args.seconds, 1000, args.cpu_workers)
         print(json.dumps(line), flush=True)

@@ -150,10 +150,26 @@ class DeviceSignals:
 
 @dataclass
 class PairOutcome:
+    """One pair's result (or the exception run() raises) and its log lines.  Lines are
+    recorded as strings or zero-argument callables and rendered on first access of
+    ``logs`` (same text, formatted only if somebody reads it)."""
     result: Optional[C.AnalysisResult] = None
     error: Optional[BaseException] = None
-    logs: List[str] = field(default_factory=list)
+    _log_ops: list = field(default_factory=list)
     detail: dict = field(default_factory=dict)
+
+    @property
+    def logs(self) -> List[str]:
+        if any(not isinstance(x, str) for x in self._log_ops):
+            lines: List[str] = []
+            for x in self._log_ops:
+                if isinstance(x, str):
+                    lines.append(x)
+                else:
+                    r = x()
+                    lines.extend(r) if isinstance(r, list) else lines.append(r)
+            self._log_ops = lines
+        return self._log_ops
 
 
 @dataclass
@@ -762,15 +778,15 @@ class Engine:
     def _assemble_pair(self, b, p: Params, h, ibi, starts, w0, w1, f_len, strip_len, lead, trail, intro,
                        win_n, pair_chunks, n_cp, nj, n_pitch_jobs, align=None) -> PairOutcome:
         out = PairOutcome()
-        L = out.logs.append
+        L = out._log_ops.append   # str, or a callable rendering the line(s) when logs are read
         fn, fs = 2 * b, 2 * b + 1
         nc_len, src_len = int(f_len[fn]), int(f_len[fs])
         if p.silence_strip_db is not None:
-            L(f"Stripping silence (top_db={p.silence_strip_db} dB)…")
-            L(f"  nightcore: −{lead[fn]:.2f}s leading, −{trail[fn]:.2f}s trailing"
-              f"  →  {strip_len[fn] / SR:.1f} s")
-            L(f"  source:    −{lead[fs]:.2f}s leading, −{trail[fs]:.2f}s trailing"
-              f"  →  {strip_len[fs] / SR:.1f} s")
+            L(lambda: [f"Stripping silence (top_db={p.silence_strip_db} dB)…",
+                       f"  nightcore: −{lead[fn]:.2f}s leading, −{trail[fn]:.2f}s trailing"
+                       f"  →  {strip_len[fn] / SR:.1f} s",
+                       f"  source:    −{lead[fs]:.2f}s leading, −{trail[fs]:.2f}s trailing"
+                       f"  →  {strip_len[fs] / SR:.1f} s"])
         if p.src_trim_sec > 0.0:
             L(f"Manual source trim: skipping {p.src_trim_sec:.2f}s from source start")
         elif align is not None:                              # pipeline.py:111-125
@@ -780,13 +796,13 @@ class Engine:
                 L(f"  Intro detected — trimming {raw:.2f}s from source start  (speed hint: {spd:.4f}×)")
             else:
                 L(f"  No significant intro offset detected  (raw: {raw:.2f}s < {ALIGN_MIN_OFFSET:.1f}s threshold)")
-        L(f"Slicing into {p.window_sec:.0f} s windows (hop {p.hop_sec:.0f} s)…")
-        L(f"  nightcore: {len(starts[fn])} windows  |  source: {len(starts[fs])} windows")
-        L(f"Energy gating (threshold {p.energy_gate_db} dB below peak)…")
+        L(lambda: [f"Slicing into {p.window_sec:.0f} s windows (hop {p.hop_sec:.0f} s)…",
+                   f"  nightcore: {len(starts[fn])} windows  |  source: {len(starts[fs])} windows",
+                   f"Energy gating (threshold {p.energy_gate_db} dB below peak)…"])
         act = h["active_l"]
         src_w = [w for w in range(w0[fs], w1[fs]) if act[w]]
         nc_w = [w for w in range(w0[fn], w1[fn]) if act[w]]
-        L(f"  after gating — nightcore: {len(nc_w)} windows  |  source: {len(src_w)} windows")
+        L(lambda: f"  after gating — nightcore: {len(nc_w)} windows  |  source: {len(src_w)} windows")
         out.detail.update(energy_src=h["energy"][w0[fs]:w1[fs]].copy(), energy_nc=h["energy"][w0[fn]:w1[fn]].copy(),
                           n_src_windows=len(src_w), n_nc_windows=len(nc_w),
                           nc_duration=nc_len / SR, src_duration=src_len / SR)
@@ -814,8 +830,8 @@ class Engine:
                 lo_st = hi_st = point_st
                 L(f"    Only {n} chunk(s) available (need ≥ {MIN_CHUNKS}) — "
                   "pitch CI is degenerate; estimate may be less reliable.")
-            L(f"    Chroma xcorr: {point_st:+.3f} st  95% CI [{lo_st:+.3f}, {hi_st:+.3f}] st"
-              f"  ({n} chunk{'s' if n != 1 else ''})")
+            L(lambda: f"    Chroma xcorr: {point_st:+.3f} st  95% CI [{lo_st:+.3f}, {hi_st:+.3f}] st"
+                      f"  ({n} chunk{'s' if n != 1 else ''})")
             L("    essentia not available — skipping MELODIA refinement")
             L("  Pitch method: chroma_xcorr")
             method = "chroma_xcorr"
@@ -838,19 +854,21 @@ class Engine:
             f = fs if side == "src" else fn
             st_f, base = starts[f], w0[f]
             bpm_l, nb_l, nws = h["bpm_l"], h["nbeats_l"], len(ws_)
-            for i, w in enumerate(ws_):
-                s0 = st_f[w - base]
-                L(f"    tempo window {i + 1}/{nws}  [{s0 / SR:.1f}–{(s0 + win_n) / SR:.1f} s]")
-                vals.append(bpm_l[w] if nb_l[w] >= MIN_BEATS else None)
-            L(f"    {sum(1 for v in vals if v is not None)}/{len(ws_)} windows yielded a confident tempo estimate")
+            L(lambda st_f=st_f, base=base, ws_=ws_, nws=nws: [
+                f"    tempo window {i + 1}/{nws}  [{st_f[w - base] / SR:.1f}–{(st_f[w - base] + win_n) / SR:.1f} s]"
+                for i, w in enumerate(ws_)])
+            vals = [bpm_l[w] if nb_l[w] >= MIN_BEATS else None for w in ws_]
+            L(lambda vals=vals, n=nws:
+              f"    {sum(1 for v in vals if v is not None)}/{n} windows yielded a confident tempo estimate")
             tempos[side] = vals
             if side == "src":
                 valid_src = [t for t in vals if t is not None]
                 nc_dur, src_dur = nc_len / SR, src_len / SR
                 if valid_src and nc_dur > 0 and src_dur > 0:
                     med = C._median(valid_src)
-                    L(f"  NC tempo prior: {h['prior_l'][b]:.1f} BPM  "
-                      f"(src median {med:.1f} BPM × dur ratio {src_dur / nc_dur:.4f})")
+                    pr_ = h['prior_l'][b]
+                    L(lambda: f"  NC tempo prior: {pr_:.1f} BPM  "
+                              f"(src median {med:.1f} BPM × dur ratio {src_dur / nc_dur:.4f})")
                 L("  ← nightcore →")
         out.detail.update(src_tempos=tempos["src"], nc_tempos=tempos["nc"], nc_start_bpm=h["prior_l"][b],
                           tempo_margin_src=h["margin"][src_w].copy(), tempo_margin_nc=h["margin"][nc_w].copy())
@@ -873,7 +891,7 @@ class Engine:
                 o = ibi["out"]
                 res.ibi_ratio = float(o[b])
                 res.ibi_ci = (float(o[Bn + b]), float(o[2 * Bn + b]))
-                L(f"  IBI ratio: {res.ibi_ratio:.6f}×  95% CI [{res.ibi_ci[0]:.6f}, {res.ibi_ci[1]:.6f}]")
+                L(lambda: f"  IBI ratio: {res.ibi_ratio:.6f}×  95% CI [{res.ibi_ci[0]:.6f}, {res.ibi_ci[1]:.6f}]")
             else:
                 L("  IBI ratio: insufficient beats — skipped")
             out.detail.update(ibi_nbeats=(int(ibi["nbeats"][2 * b]), int(ibi["nbeats"][2 * b + 1])),

@@ -12,6 +12,6 @@ timeout -k 10 120 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smo
 tail -1 $O/smoke.log
 timeout -k 10 300 python -u bench.py > $O/bench.json 2> $O/bench.err || { echo "bench failed"; tail -20 $O/bench.err; exit 1; }
 cat $O/bench.json
-cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/$O/prof -o run --output-format csv -- python3 $GRAFT_REPO_ROOT/bench.py --no-cpu-baseline --no-ibi > $GRAFT_REPO_ROOT/$O/prof_bench.json 2> $GRAFT_REPO_ROOT/$O/prof.err || { echo "rocprof failed"; tail -20 $GRAFT_REPO_ROOT/$O/prof.err; exit 1; }
+cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/$O/prof -o run --output-format csv -- python3 $GRAFT_REPO_ROOT/bench.py --no-cpu-baseline --no-ibi --no-config5 > $GRAFT_REPO_ROOT/$O/prof_bench.json 2> $GRAFT_REPO_ROOT/$O/prof.err || { echo "rocprof failed"; tail -20 $GRAFT_REPO_ROOT/$O/prof.err; exit 1; }
 cat $GRAFT_REPO_ROOT/$O/prof_bench.json
 find $GRAFT_REPO_ROOT/$O/prof -name '*kernel_stats.csv' | head -3

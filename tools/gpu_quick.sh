@@ -12,6 +12,6 @@ tail -1 $O/pytest_gpu.log
 for t in chroma windows; do
   cd /tmp && timeout -k 10 120 rocprofv3 --kernel-trace --stats -d $R/$O/$t -o run --output-format csv -- python3 $R/tools/prof_kernels.py $t > $R/$O/$t.log 2>&1 || { echo "stats $t failed"; tail -5 $R/$O/$t.log; exit 1; }
 done
-cd $R && timeout -k 10 300 python -u bench.py --no-cpu-baseline > $O/bench.json 2> $O/bench.err || { echo "bench failed"; tail -20 $O/bench.err; exit 1; }
+cd $R && timeout -k 10 300 python -u bench.py --no-cpu-baseline --no-config5 > $O/bench.json 2> $O/bench.err || { echo "bench failed"; tail -20 $O/bench.err; exit 1; }
 python3 tools/pmc_report.py $O/chroma $O/windows
 python3 -c "import json; d=json.load(open('$O/bench.json')); print('value', round(d['value']), 'ms', round(d['ms_per_step'],3), d['kernels_ms_per_step'])"
