@@ -88,8 +88,8 @@ __global__ __launch_bounds__(WT_THREADS) void window_tg_kernel(WinTgArgs a) {
     constexpr int FB = 8;
     const int per = (T + WT_WAVES - 1) / WT_WAVES;
     const int ta = wave * per, tb = min(T, ta + per);
-    for (int t0 = ta; t0 < tb; t0 += FB) {
-      float ra[FB + 1], rb[FB + 1];
+    // rows of batch t0 + FB are requested before batch t0 is differenced (software pipeline)
+    auto load_rows = [&](int t0, float (&ra)[FB + 1], float (&rb)[FB + 1]) {
 #pragma unroll
       for (int q = 0; q <= FB; ++q) {
         const int j = t0 + q - a.pad_onset;  // row j feeds frames j + pad (as j) and j + pad - 1 (as j + 1)
@@ -98,6 +98,11 @@ __global__ __launch_bounds__(WT_THREADS) void window_tg_kernel(WinTgArgs a) {
         ra[q] = ok ? r[lane] : 0.0f;
         rb[q] = ok ? r[lane + 64] : 0.0f;
       }
+    };
+    float ra[FB + 1], rb[FB + 1], na[FB + 1], nb[FB + 1];
+    if (ta < tb) load_rows(ta, ra, rb);
+    for (int t0 = ta; t0 < tb; t0 += FB) {
+      if (t0 + FB < tb) load_rows(t0 + FB, na, nb);
 #pragma unroll
       for (int q = 0; q < FB; ++q) {
         const int t = t0 + q;
@@ -114,6 +119,11 @@ __global__ __launch_bounds__(WT_THREADS) void window_tg_kernel(WinTgArgs a) {
           a.onset_out[g0 + t] = val;
         }
       }
+#pragma unroll
+      for (int q = 0; q <= FB; ++q) {
+        ra[q] = na[q];
+        rb[q] = nb[q];
+      }
     }
   }
   __syncthreads();
@@ -125,14 +135,27 @@ __global__ __launch_bounds__(WT_THREADS) void window_tg_kernel(WinTgArgs a) {
     }
   }
   __syncthreads();
-  // per-frame normaliser 1 / ac_t[0]
+  // per-frame normaliser 1 / ac_t[0] = 1 / sum_j hann[j]^2 x[t+j]^2: Hann^2 staged in LDS,
+  // four interleaved partial sums per frame (independent FMA chains), joined in a fixed order
+  double* sh_wsq = sh_x + (T + acw) + WT_SEG * acw;
+  for (int j = tid; j < acw; j += WT_THREADS) sh_wsq[j] = a.wsq[j];
+  __syncthreads();
   for (int t = tid; t < T; t += WT_THREADS) {
-    double s = 0.0;
-    for (int j = 0; j < (NC_WT_SKIP >= 2 ? 0 : acw); ++j) {
-      const double v = sh_x[t + j];
-      s = fma(a.wsq[j], v * v, s);
+    double s4[4] = {0.0, 0.0, 0.0, 0.0};
+    const int n = NC_WT_SKIP >= 2 ? 0 : acw;
+    int j = 0;
+    for (; j + 4 <= n; j += 4) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const double v = sh_x[t + j + q];
+        s4[q] = fma(sh_wsq[j + q], v * v, s4[q]);
+      }
     }
-    sh_rinv[t] = tg_rinv(s);
+    for (; j < n; ++j) {
+      const double v = sh_x[t + j];
+      s4[0] = fma(sh_wsq[j], v * v, s4[0]);
+    }
+    sh_rinv[t] = tg_rinv((s4[0] + s4[1]) + (s4[2] + s4[3]));
   }
   __syncthreads();
   auto xf = [&](int i) { return sh_x[i]; };
@@ -228,7 +251,7 @@ int launch_window_stage(Context& ctx, const float* sig, const int64_t* win_off, 
   a.onset_out = onset_out;
   a.tg_out = tg_out;
   a.energy_out = energy_out;
-  const size_t lds = (size_t)T * sizeof(double) + (size_t)(T + acw + WT_SEG * acw) * sizeof(double);
+  const size_t lds = (size_t)T * sizeof(double) + (size_t)(T + acw + WT_SEG * acw + acw) * sizeof(double);
   if (lds > 64 * 1024) {
     set_error("window stage: window too long for LDS");
     return -2;

@@ -184,14 +184,40 @@ class Params:
     compute_ibi: bool = True
 
 
-def _group_bounds(B: int, group_pairs: int) -> List[Tuple[int, int]]:
+def _group_bounds(B: int, group_pairs, ) -> List[Tuple[int, int]]:
     """Pair groups of about group_pairs; the last one is halved so that the host
-    assembly left exposed after the final device work stays short."""
-    gp = max(1, int(group_pairs))
-    sizes = [gp] * (B // gp) + ([B % gp] if B % gp else [])
-    if len(sizes) > 1 and sizes[-1] >= 8:
-        last = sizes.pop()
-        sizes += [last - last // 2, last // 2]
+    assembly left exposed after the final device work stays short.  A list of sizes
+    gives the schedule explicitly (repeated from its start if it does not cover B)."""
+    if isinstance(group_pairs, (list, tuple)):
+        sizes, left, i = [], B, 0
+        while left > 0:
+            n = min(left, max(1, int(group_pairs[i % len(group_pairs)])))
+            sizes.append(n)
+            left -= n
+            i += 1
+    elif group_pairs is None:
+        # default: a 16-pair group to start the device early, 32-pair groups (fewer, fuller
+        # launches of the latency-bound per-window kernels), a 16-pair group at the end to
+        # keep the exposed host assembly short (tools/group_sweep.py)
+        sizes, left = [], B
+        if left > 16:
+            sizes.append(16)
+            left -= 16
+        while left > 48:
+            sizes.append(32)
+            left -= 32
+        if left > 32:
+            sizes += [left - 16, 16]
+        elif left > 16:
+            sizes += [left - left // 2, left // 2]
+        elif left > 0:
+            sizes.append(left)
+    else:
+        gp = max(1, int(group_pairs))
+        sizes = [gp] * (B // gp) + ([B % gp] if B % gp else [])
+        if len(sizes) > 1 and sizes[-1] >= 8:
+            last = sizes.pop()
+            sizes += [last - last // 2, last // 2]
     out, g0 = [], 0
     for n in sizes:
         out.append((g0, g0 + n))
@@ -374,7 +400,7 @@ class Engine:
 
     # -------------------------------------------------------------- batched pipeline
     def analyze(self, pairs: Optional[Sequence[Tuple[np.ndarray, np.ndarray]]] = None, params: Params = None,
-                signals: Optional[DeviceSignals] = None, group_pairs: int = 16) -> List[PairOutcome]:
+                signals: Optional[DeviceSignals] = None, group_pairs=None) -> List[PairOutcome]:
         """Run pipeline.run's analysis for every (nc, src) pair.  ``signals``
         (files ordered nc_0, src_0, nc_1, src_1, ...) may be passed already
         resident in HBM; otherwise ``pairs`` are uploaded.
