@@ -13,47 +13,70 @@
 
 namespace nc {
 
-// f64 sum of x^2 over each 512-sample block b = [512 b, 512 b + 512) of each file (one
-// wave per block, every sample read once); block b of file f at blk[frame_base[f] + b].
+// f64 sum of x^2 over each 512-sample block b = [512 b, 512 b + 512) of each file, every
+// sample read once; block b of file f at blk[frame_base[f] + b].  One workgroup per tile of
+// TR_BPG blocks of one file (tile_base[f] = first tile of file f: one search per workgroup,
+// not per wave); each wave sums TR_BPW consecutive blocks with all their 16-byte loads in flight.
+constexpr int TR_BPW = 4;                  // blocks per wave
+constexpr int TR_BPG = 4 * TR_BPW;         // blocks per workgroup (4 waves)
+
 __global__ __launch_bounds__(256) void trim_blocks_kernel(const float* sig, const int64_t* file_off,
                                                           const int64_t* file_len, const int64_t* frame_base,
-                                                          int n_files, int64_t total_frames, double* blk) {
+                                                          const int64_t* tile_base, int n_files, double* blk) {
   const int lane = threadIdx.x & 63;
-  const int64_t gw = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (gw >= total_frames) return;
+  const int64_t tile = blockIdx.x;
+  if (tile >= tile_base[n_files]) return;
   int lo = 0, hi = n_files - 1;
   while (lo < hi) {
     const int mid = (lo + hi + 1) >> 1;
-    if (frame_base[mid] <= gw) lo = mid;
+    if (tile_base[mid] <= tile) lo = mid;
     else hi = mid - 1;
   }
-  const int f = lo;
-  const int64_t b = gw - frame_base[f];
-  const int64_t off = file_off[f];
+  const int f = __builtin_amdgcn_readfirstlane(lo);
   const int64_t N = file_len[f];
-  const int64_t s0 = b * 512;
-  double acc = 0.0;
-  if (s0 + 512 <= N && ((off + s0) & 3) == 0) {
-    const float4* x4 = reinterpret_cast<const float4*>(sig + off + s0);
+  const int64_t nblk = (N + 511) / 512;
+  const int64_t b0 = (tile - tile_base[f]) * TR_BPG + (threadIdx.x >> 6) * TR_BPW;
+  if (b0 >= nblk) return;
+  const int64_t off = file_off[f];
+  double acc[TR_BPW];
+  if ((b0 + TR_BPW) * 512 <= N && ((off + b0 * 512) & 3) == 0) {
+    const float4* x4 = reinterpret_cast<const float4*>(sig + off + b0 * 512);
+    float4 v[TR_BPW][2];
 #pragma unroll
-    for (int q = 0; q < 2; ++q) {
-      const float4 v = x4[lane + 64 * q];
-      acc = fma((double)v.x, (double)v.x, acc);
-      acc = fma((double)v.y, (double)v.y, acc);
-      acc = fma((double)v.z, (double)v.z, acc);
-      acc = fma((double)v.w, (double)v.w, acc);
+    for (int i = 0; i < TR_BPW; ++i)
+#pragma unroll
+      for (int q = 0; q < 2; ++q) v[i][q] = x4[i * 128 + lane + 64 * q];
+#pragma unroll
+    for (int i = 0; i < TR_BPW; ++i) {
+      double a = 0.0;
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        a = fma((double)v[i][q].x, (double)v[i][q].x, a);
+        a = fma((double)v[i][q].y, (double)v[i][q].y, a);
+        a = fma((double)v[i][q].z, (double)v[i][q].z, a);
+        a = fma((double)v[i][q].w, (double)v[i][q].w, a);
+      }
+      acc[i] = a;
     }
   } else {
     const float* x = sig + off;
 #pragma unroll
-    for (int q = 0; q < 8; ++q) {
-      const int64_t i = s0 + lane + 64 * q;
-      const double v = i < N ? (double)x[i] : 0.0;
-      acc = fma(v, v, acc);
+    for (int i = 0; i < TR_BPW; ++i) {
+      double a = 0.0;
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const int64_t j = (b0 + i) * 512 + lane + 64 * q;
+        const double v = j < N ? (double)x[j] : 0.0;
+        a = fma(v, v, a);
+      }
+      acc[i] = a;
     }
   }
-  acc = wave_sum(acc);
-  if (lane == 0) blk[gw] = acc;
+#pragma unroll
+  for (int i = 0; i < TR_BPW; ++i) {
+    const double a = wave_sum(acc[i]);
+    if (lane == 0 && b0 + i < nblk) blk[frame_base[f] + b0 + i] = a;
+  }
 }
 
 // ms[t] = mean of x^2 over the centred 2048-sample frame t = blocks t-2 .. t+1 (zero outside)
@@ -106,12 +129,15 @@ __global__ __launch_bounds__(256) void trim_bounds_kernel(const double* blk_all,
 size_t trim_ws_bytes(const int64_t* host_file_len, int n_files) {
   size_t frames = 0;
   for (int f = 0; f < n_files; ++f) frames += 1 + host_file_len[f] / 512;
-  return frames * sizeof(double) + (size_t)(n_files + 1) * sizeof(int64_t) + 256;
+  return frames * sizeof(double) + 2 * (size_t)(n_files + 1) * sizeof(int64_t) + 256;
 }
 
 // frame_base is computed on the device from file_len (parallel exclusive scan, one block)
-__global__ __launch_bounds__(256) void frame_base_kernel(const int64_t* file_len, int n_files, int64_t* frame_base) {
+__global__ __launch_bounds__(256) void frame_base_kernel(const int64_t* file_len, int n_files, int64_t* frame_base,
+                                                         int64_t* tile_base) {
   block_prefix_table<256>(n_files, frame_base, [&](int f) { return 1 + file_len[f] / 512; });
+  block_prefix_table<256>(n_files, tile_base,
+                          [&](int f) { return ((file_len[f] + 511) / 512 + TR_BPG - 1) / TR_BPG; });
 }
 
 int launch_trim(Context& ctx, const float* sig, const int64_t* file_off, const int64_t* file_len, int n_files,
@@ -120,19 +146,21 @@ int launch_trim(Context& ctx, const float* sig, const int64_t* file_off, const i
   (void)ctx;
   if (n_files <= 0) return 0;
   // max_frames = total frames over all files (host knows the lengths)
-  const size_t need = (size_t)max_frames * sizeof(double) + (size_t)(n_files + 1) * sizeof(int64_t);
+  const size_t need = (size_t)max_frames * sizeof(double) + 2 * (size_t)(n_files + 1) * sizeof(int64_t);
   if (ws_bytes < need) {
     set_error("trim: workspace too small");
     return -3;
   }
   int64_t* frame_base = static_cast<int64_t*>(ws);
-  double* blk = reinterpret_cast<double*>(frame_base + n_files + 1);
-  hipLaunchKernelGGL(frame_base_kernel, dim3(1), dim3(256), 0, st, file_len, n_files, frame_base);
-  const int64_t blocks = (max_frames + 3) / 4;
+  int64_t* tile_base = frame_base + n_files + 1;
+  double* blk = reinterpret_cast<double*>(tile_base + n_files + 1);
+  hipLaunchKernelGGL(frame_base_kernel, dim3(1), dim3(256), 0, st, file_len, n_files, frame_base, tile_base);
+  // tiles <= sum over files of ceil(blocks / TR_BPG) <= max_frames / TR_BPG + n_files
+  const int64_t tiles = max_frames / TR_BPG + n_files + 1;
   {
     KTimer kt_(ctx, "trim_blocks", st);
-    hipLaunchKernelGGL(trim_blocks_kernel, dim3((unsigned)blocks), dim3(256), 0, st, sig, file_off, file_len,
-                       frame_base, n_files, max_frames, blk);
+    hipLaunchKernelGGL(trim_blocks_kernel, dim3((unsigned)tiles), dim3(256), 0, st, sig, file_off, file_len,
+                       frame_base, tile_base, n_files, blk);
   }
   hipLaunchKernelGGL(trim_bounds_kernel, dim3(n_files), dim3(256), 0, st, blk, frame_base, file_len, top_db,
                      out_start, out_end);
