@@ -41,20 +41,23 @@ def main(out):
     commit = subprocess.run(["git", "rev-parse", "--short", "HEAD"], cwd=REPO, capture_output=True,
                             text=True).stdout.strip() or "unknown"
     kern = {}
+    # one trim pass per analyze call: the profiled run's call count, hence launches per step of
+    # every kernel (the pair-group schedule sets how many launches one step makes)
+    calls = max(1, len(fetch.get("trim_blocks", [])))
     for tag in sorted(set(fetch) | set(write)):
         f = sum(fetch.get(tag, [0])) / max(1, len(fetch.get(tag, [])))
         w = sum(write.get(tag, [0])) / max(1, len(write.get(tag, [])))
         k = {"launches": len(fetch.get(tag, [])), "fetch_size_kib_raw": round(f, 2), "write_size_kib": round(w, 2),
              "hbm_bytes_per_launch": int(round((2 * f + w) * 1024))}
+        k["launches_per_step"] = round(k["launches"] / calls, 3)
         if tag in ALG_STEP and fetch.get(tag):
-            # the profiled run does warmup + 2 timed + kernel-timer steps; launches per step from the count
-            steps = {"trim_blocks": 1}.get(tag, 5)
-            k["alg_bytes_per_launch"] = ALG_STEP[tag] // steps
+            # mean over launches of unequal groups: per-step bytes / launches per step
+            k["alg_bytes_per_launch"] = int(ALG_STEP[tag] * calls / len(fetch[tag]))
         kern[tag] = k
-    doc = {"workload": "config3-64pairs", "commit": commit,
+    doc = {"workload": "config3-64pairs", "commit": commit, "analyze_calls": calls,
            "command": "tools/pmc_traffic.sh: rocprofv3 --pmc FETCH_SIZE, then a separate --pmc WRITE_SIZE pass, "
                       "--output-format csv -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-ibi "
-                      "(means over every launch; groups of 16,16,16,8,8 pairs per step)",
+                      "--no-config5 (means over every launch; the engine's default pair-group schedule)",
            "correction": "hbm_bytes = 2 x FETCH_SIZE + WRITE_SIZE (KiB -> bytes): on gfx950 FETCH_SIZE reports half "
                          "the bytes of a wide coalesced read (MI355X_MICROARCH.md; calibrated with "
                          "tools/calib_fetch.hip: a 1 GiB stream read reports 0.500 GiB)",
