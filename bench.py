@@ -119,6 +119,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-ibi", action="store_true")
     ap.add_argument("--no-config5", action="store_true", help="skip the 60-min pair (BASELINE configs[4]) timing")
+    ap.add_argument("--no-spectral", action="store_true", help="skip the spectral.analyze (SURVEY.md §8f) timing")
     ap.add_argument("--cpu-workers", type=int, default=8, help="CPU baseline processes (one pair each)")
     ap.add_argument("--workers", type=int, default=min(16, os.cpu_count() or 1))
     args = ap.parse_args()
@@ -231,6 +232,54 @@ def main():
                 "windows": int(o5.detail["energy_src"].size + o5.detail["energy_nc"].size),
                 "tempo_ratio": o5.result.tempo_ratio, "ibi_ratio": o5.result.ibi_ratio, "xcorr_ratio": xr[0]}
 
+    # spectral.analyze statistics of every resident file of the batch in one
+    # call (spectral.py:52-94); per-kernel HIP events on the launch stream, the oracle beside it
+    spec = None
+    if not args.no_spectral and rank == 0:
+        srs = [22050] * signals.n_files
+        ev, h, keep = eng.spectral_frames(signals.buf, signals.off, signals.length, srs)
+        ev.synchronize()
+        reps = 3
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        for _ in range(reps):
+            ev, h, keep = eng.spectral_frames(signals.buf, signals.off, signals.length, srs)
+            ev.synchronize()
+            res = eng.spectral_finish(h)
+        t_spec = (time.perf_counter() - t1) / reps
+        eng.kernel_profile(True)
+        for _ in range(reps):
+            eng.spectral_frames(signals.buf, signals.off, signals.length, srs)[0].synchronize()
+        sk = {k: (ms / n, n / reps) for k, (ms, n) in eng.kernel_times().items()}
+        eng.kernel_profile(False)
+        frames = int(h["T"].sum())
+        fr_ms = sk["spectral_frames"][0]
+        bins_ms = sk["spectral_bins"][0]
+        spec = {"workload": f"spectral.analyze of the {signals.n_files} resident 3-min files (22.05 kHz), one call",
+                "files": signals.n_files, "frames": frames, "ms_per_call": t_spec * 1e3,
+                "frames_per_s": frames / t_spec, "files_per_s": signals.n_files / t_spec,
+                "kernels_ms_per_call": {k: round(v[0] * v[1], 4) for k, v in sk.items()},
+                # spectral_frames: each input sample read once (512 x 4 B per frame hop);
+                # spectral_bins: the dB rows streamed once (1025 x 4 B per frame)
+                "roofline_frames": {"bound": "hbm", "achieved": frames * 2048 / (fr_ms * 1e-3) / 1e9,
+                                    "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                                    "frac": frames * 2048 / (fr_ms * 1e-3) / 1e9 / HBM_PEAK_GBS},
+                "roofline_bins": {"bound": "hbm", "achieved": frames * 4100 / (bins_ms * 1e-3) / 1e9,
+                                  "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                                  "frac": frames * 4100 / (bins_ms * 1e-3) / 1e9 / HBM_PEAK_GBS},
+                "check": {"centroid_file0": res[0]["centroid"],
+                          "effective_bandwidth_hz_file0": res[0]["effective_bandwidth_hz"]}}
+        if world == 1 and not args.no_cpu_baseline:
+            sys.path.insert(0, str(REPO))
+            from oracle import refglue
+            y0 = pairs[0][1]
+            t1 = time.perf_counter()
+            refglue.spectral_analyze(y0, 22050)
+            t_cpu = time.perf_counter() - t1
+            spec["cpu_baseline"] = {"value": (1 + len(y0) // 512) / t_cpu, "unit": "frames/s", "cores": 1,
+                                    "kind": "port", "sample": "oracle/refglue.spectral_analyze of file 1 "
+                                                              "(one 3-min src), numpy, 1 process"}
+
     if rank == 0:
         line = {
             "metric": "10 s windows/sec (CQT+onset, 22.05 kHz mono) at 1/2/4/8 GPUs; % HBM roofline",
@@ -267,6 +316,8 @@ def main():
             line["ibi_pass"] = ibi
         if cfg5 is not None:
             line["config5"] = cfg5
+        if spec is not None:
+            line["spectral"] = spec
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(args.seconds, 1000, args.cpu_workers)
         print(json.dumps(line), flush=True)

@@ -53,7 +53,7 @@ int nc_num_cu(const nc_ctx* ctx);
  * nc_profile_read(tag) waits for the recorded launches, returns their summed
  * duration and count, and resets the tag.  Tags: "stft_mel", "window_tg",
  * "tuning_peaks", "decimate", "cqt_chroma", "trim_blocks", "tempo_beat",
- * "tg_slide".  Enabling (or disabling) discards pending records. */
+ * "tg_slide", "spectral_frames", "spectral_bins".  Enabling (or disabling) discards pending records. */
 int nc_profile_enable(nc_ctx* ctx, int on);
 int nc_profile_read(nc_ctx* ctx, const char* tag, double* total_ms, int* launches);
 
@@ -243,6 +243,32 @@ int nc_align_offsets(nc_ctx* ctx, const float* sig, const int64_t* src_off, cons
                      int n_speeds, int max_offset_frames, int64_t total_len, int64_t max_len,
                      int* peak_out, int* speed_idx_out, double* score_out, void* ws, size_t ws_bytes,
                      void* stream);
+
+/* ---------------------------------------------------------------------------
+ * S1  spectral statistics — replaces, inside spectral.analyze (spectral.py:38-103),
+ *     librosa.feature.spectral_centroid (:54), spectral_rolloff(roll_percent) (:55-57),
+ *     feature.rms (:59, :76), the |stft| band means (:63-74) and
+ *     amplitude_to_db(|stft|, ref=np.max) averaged over time (:87-88).
+ * File f = file_len[f] samples at sig + file_off[f], at its own sample rate (the
+ * reference loads with sr=None, :52).  STFT 2048 / hop 512, periodic Hann, centred,
+ * zero pad: T_f = 1 + file_len[f] / 512 frames, frame_base[f] = sum_{q<f} T_q
+ * (device, n_files + 1 entries; total_frames = frame_base[n_files], max_frames =
+ * max T_f).  bin_hz[f] = np.fft.rfftfreq(2048, 1/sr)[1] (f64, device);
+ * band_bins[f*10 + 2b], [f*10 + 2b + 1] = the [lo, hi) bins of band b's mask
+ * (freqs >= lo_hz) & (freqs < hi_hz) for the bands 20-80, 80-250, 250-2000,
+ * 2000-6000, 6000-20000 Hz.
+ * Outputs: rms_out[frame_base[f] + t] = frame RMS (f32); stats_out[f*12 + i] =
+ * {sum_t centroid_t, sum_t rolloff_t (Hz), 5 x sum_t sum_{k in band} |S|, max |S|,
+ * mean(rms), var(rms), np.percentile(rms, 75), mean(diff(rms[rms > p75]))};
+ * bin_db_out[f*1025 + k] = sum_t max(dB(|S|^2) - dB(ref^2), -80).  The host
+ * divides by T_f (and by the band bin counts) and thresholds the bin means.
+ * Size ws with nc_spectral_workspace_bytes.
+ * ------------------------------------------------------------------------- */
+size_t nc_spectral_workspace_bytes(int64_t total_frames, int n_files, int64_t max_frames);
+int nc_spectral_stats(nc_ctx* ctx, const float* sig, const int64_t* file_off, const int64_t* file_len,
+                      const int64_t* frame_base, const double* bin_hz, const int* band_bins, int n_files,
+                      int64_t total_frames, int64_t max_frames, float roll_percent, float* rms_out,
+                      double* stats_out, double* bin_db_out, void* ws, size_t ws_bytes, void* stream);
 
 #ifdef __cplusplus
 }

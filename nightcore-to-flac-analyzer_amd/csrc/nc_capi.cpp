@@ -62,6 +62,12 @@ int launch_xcorr(const float* sig, const int64_t* ia, const int64_t* ib, int n_i
                  const int64_t* pa, const int64_t* pbv, const int64_t* exp_pb, int n_jobs, double* ratio_out,
                  double* quality_out, hipStream_t st);
 
+size_t spectral_ws_bytes(int64_t total_frames, int n_files, int64_t max_frames);
+int launch_spectral(Context& ctx, const float* sig, const int64_t* file_off, const int64_t* file_len,
+                    const int64_t* frame_base, const double* bin_hz, const int* band_bins, int n_files,
+                    int64_t total_frames, int64_t max_frames, float roll_percent, float* rms_out,
+                    double* stats_out, double* bin_db_out, void* ws, size_t ws_bytes, hipStream_t st);
+
 int launch_energy_gate(const double* energy, const int* w0, const int* w1, int n_groups, double gate_db,
                        uint8_t* active, hipStream_t st);
 int launch_collect_valid(const double* bpm, const int* nbeats, const uint8_t* active, const int* w0, const int* w1,
@@ -354,6 +360,21 @@ int nc_align_offsets(nc_ctx* ctx, const float* sig, const int64_t* src_off, cons
   return nc::launch_align_offsets(ctx->c, sig, src_off, src_len, nc_off, nc_len, n_pairs, speeds, n_speeds,
                                   max_offset_frames, total_len, max_len, peak_out, speed_idx_out, score_out, ws,
                                   ws_bytes, (hipStream_t)stream);
+}
+
+size_t nc_spectral_workspace_bytes(int64_t total_frames, int n_files, int64_t max_frames) {
+  return nc::spectral_ws_bytes(total_frames, n_files, max_frames);
+}
+
+int nc_spectral_stats(nc_ctx* ctx, const float* sig, const int64_t* file_off, const int64_t* file_len,
+                      const int64_t* frame_base, const double* bin_hz, const int* band_bins, int n_files,
+                      int64_t total_frames, int64_t max_frames, float roll_percent, float* rms_out,
+                      double* stats_out, double* bin_db_out, void* ws, size_t ws_bytes, void* stream) {
+  CHECK_CTX(ctx);
+  SET_DEVICE(ctx);
+  return nc::launch_spectral(ctx->c, sig, file_off, file_len, frame_base, bin_hz, band_bins, n_files, total_frames,
+                             max_frames, roll_percent, rms_out, stats_out, bin_db_out, ws, ws_bytes,
+                             (hipStream_t)stream);
 }
 
 }  // extern "C"

@@ -276,7 +276,7 @@ class Engine:
         return out
 
     KERNEL_TAGS = ("stft_mel", "window_tg", "tuning_peaks", "decimate", "cqt_chroma", "trim_blocks", "tempo_beat",
-                   "tg_slide")
+                   "tg_slide", "spectral_frames", "spectral_bins")
 
     def kernel_profile(self, on: bool) -> None:
         """Enable/disable the library's per-kernel HIP-event timers (nc_profile_enable)."""
@@ -399,6 +399,91 @@ class Engine:
         return out
 
     # -------------------------------------------------------------- batched pipeline
+    # -------------------------------------------------------------- spectral (spectral.py:38-103)
+    SPECTRAL_BANDS = ((20, 80), (80, 250), (250, 2000), (2000, 6000), (6000, 20000))   # spectral.py:70-74
+
+    def spectral_frames(self, buf: torch.Tensor, off, length, srs, roll_percent: float = 0.85,
+                        frame_rms: bool = False):
+        """nc_spectral_stats over signals already in ``buf`` (sample offsets / lengths, each at
+        its own rate srs[f]).  Queues the launch and the D2H copy of the per-file sums (and,
+        with frame_rms, of the frame RMS); returns (event, host views, keep-alive).
+        ``spectral_finish`` turns the views into per-file statistics."""
+        off = np.asarray(off, np.int64)
+        length = np.asarray(length, np.int64)
+        n = len(off)
+        T = 1 + length // 512                                              # centred frames
+        base = np.zeros(n + 1, np.int64)
+        base[1:] = np.cumsum(T)
+        bands = np.zeros((n, len(self.SPECTRAL_BANDS), 2), np.int32)
+        hz = np.zeros(n, np.float64)
+        for f, sr in enumerate(srs):
+            freqs = np.fft.rfftfreq(2048, 1.0 / sr)                        # librosa.fft_frequencies
+            hz[f] = freqs[1]
+            for b, (lo, hi) in enumerate(self.SPECTRAL_BANDS):
+                idx = np.flatnonzero((freqs >= lo) & (freqs < hi))
+                if idx.size:
+                    bands[f, b] = (idx[0], idx[-1] + 1)
+        up = _Upload()
+        up.add("off", off, np.int64)
+        up.add("len", length, np.int64)
+        up.add("base", base, np.int64)
+        up.add("hz", hz, np.float64)
+        up.add("bands", bands, np.int32)
+        d = up.commit(self.dev)
+        ar = _Arena()
+        ar.add("stats", 12 * n, np.float64)
+        ar.add("bins", 1025 * n, np.float64)
+        o = ar.commit(self.dev)
+        rms = torch.empty(int(base[-1]), dtype=torch.float32, device=self.dev)
+        tot, mx = int(base[-1]), int(T.max())
+        ws = self.workspace("spectral", self.ctx.lib.nc_spectral_workspace_bytes(tot, n, mx))
+        self.call("nc_spectral_stats", buf.data_ptr(), d["off"].data_ptr(), d["len"].data_ptr(),
+                  d["base"].data_ptr(), d["hz"].data_ptr(), d["bands"].data_ptr(), n, tot, mx,
+                  float(roll_percent), rms.data_ptr(), o["stats"].data_ptr(), o["bins"].data_ptr(),
+                  ws.data_ptr(), ws.numel(), self.stream())
+        hbuf, h = ar.to_host()
+        if frame_rms:
+            hr = torch.empty(rms.numel(), dtype=torch.float32, pin_memory=True)
+            hr.copy_(rms, non_blocking=True)
+            h["rms"] = hr.numpy()
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(self.dev))
+        h.update(base=base, T=T, bands=bands, hz=hz, length=length, srs=list(srs))
+        return ev, h, (d, o, hbuf, rms)
+
+    @staticmethod
+    def spectral_finish(h) -> List[dict]:
+        """Per-file SpectralStats fields from the device sums (spectral.py:54-94): means over
+        the T_f frames and band bins, the effective bandwidth from the per-bin dB means."""
+        n = len(h["srs"])
+        st = h["stats"].reshape(n, 12)
+        T = h["T"].astype(np.float64)
+        nb = (h["bands"][:, :, 1] - h["bands"][:, :, 0]).astype(np.float64)
+        band = np.where(nb > 0, st[:, 2:7] / (np.maximum(nb, 1.0) * T[:, None]), 0.0)
+        favg = h["bins"].reshape(n, 1025) / T[:, None]
+        sig = favg > favg.max(axis=1, keepdims=True) - 60.0
+        last = np.where(sig.any(axis=1), 1024 - np.argmax(sig[:, ::-1], axis=1), 1024)
+        names = ("sub_bass", "bass", "midrange", "presence", "brilliance")
+        out = []
+        for f in range(n):
+            r = {"centroid": float(st[f, 0] / T[f]), "rolloff": float(st[f, 1] / T[f]),
+                 "rms_mean": float(st[f, 8]), "rms_variance": float(st[f, 9])}
+            r.update({name: float(band[f, b]) for b, name in enumerate(names)})
+            r["decay_rate"] = float(st[f, 11])
+            r["duration"] = float(h["length"][f]) / h["srs"][f]            # librosa.get_duration
+            r["effective_bandwidth_hz"] = float(int(last[f]) * h["hz"][f])
+            out.append(r)
+        return out
+
+    def spectral(self, signals: Sequence[Tuple[np.ndarray, int]]) -> List[dict]:
+        """spectral.analyze statistics for decoded (signal, native rate) pairs, one batch."""
+        if not signals:
+            return []
+        sig = self.upload_signals([np.asarray(y, np.float32) for y, _ in signals])
+        ev, h, keep = self.spectral_frames(sig.buf, sig.off, sig.length, [int(sr) for _, sr in signals])
+        ev.synchronize()
+        return self.spectral_finish(h)
+
     def analyze(self, pairs: Optional[Sequence[Tuple[np.ndarray, np.ndarray]]] = None, params: Params = None,
                 signals: Optional[DeviceSignals] = None, group_pairs=None) -> List[PairOutcome]:
         """Run pipeline.run's analysis for every (nc, src) pair.  ``signals``

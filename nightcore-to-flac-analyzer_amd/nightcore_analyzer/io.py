@@ -16,7 +16,7 @@ from __future__ import annotations
 import wave
 from dataclasses import dataclass
 from pathlib import Path
-from typing import List
+from typing import List, Optional
 
 import numpy as np
 
@@ -64,11 +64,13 @@ def _read_wav(path: Path):
     return x.reshape(-1, ch).mean(axis=1).astype(np.float32), sr
 
 
-def load_audio(path: str, sr: int = SAMPLE_RATE) -> tuple[np.ndarray, int]:
-    """Decode *path* to mono float32 at *sr* Hz (io.py:44-55; decode stays on the CPU)."""
+def load_audio(path: str, sr: Optional[int] = SAMPLE_RATE) -> tuple[np.ndarray, int]:
+    """Decode *path* to mono float32 at *sr* Hz (io.py:44-55; decode stays on the CPU).
+    ``sr=None`` keeps the file's own rate (librosa.load(sr=None), spectral.py:52); a .npy
+    file carries no rate and is taken to be at SAMPLE_RATE."""
     p = Path(path)
     if p.suffix.lower() == ".npy":
-        y, file_sr = np.load(p, allow_pickle=False).astype(np.float32), sr
+        y, file_sr = np.load(p, allow_pickle=False).astype(np.float32), sr or SAMPLE_RATE
         if y.ndim > 1:
             y = y.mean(axis=0).astype(np.float32)
     elif p.suffix.lower() == ".wav":
@@ -85,6 +87,8 @@ def load_audio(path: str, sr: int = SAMPLE_RATE) -> tuple[np.ndarray, int]:
         raise NotImplementedError(
             f"{p.suffix} decoding is outside the engine (the reference uses librosa.load/soundfile, "
             "not installed here); convert to WAV or .npy first")
+    if sr is None:
+        sr = file_sr
     if file_sr != sr:
         import math
         import scipy.signal

@@ -20,6 +20,8 @@ Reference call sites served (file:line under /root/reference/nightcore_analyzer)
   tempo.py:58,63     librosa.feature.tempogram / tempo  -> tempogram_mean(), tempo_from_tg()
   tempo.py:168       librosa.frames_to_time             -> frames_to_time()
   pitch.py:58        librosa.feature.chroma_cqt         -> chroma_cqt()
+  spectral.py:54-88  feature.spectral_centroid / spectral_rolloff / rms, stft, fft_frequencies,
+                     amplitude_to_db, get_duration     -> spectral_*(), stft_mag(), ...
 """
 from __future__ import annotations
 
@@ -381,8 +383,63 @@ def trim(y, top_db=60.0, frame_length=2048, hop=512):
     return y[start:end], (start, end)
 
 
+# --------------------------------------------------------------------------- spectral features
+# spectral.py:52-94 calls these librosa functions on a file at its native rate (sr=None).
+def fft_frequencies(sr=22050, n_fft=2048) -> np.ndarray:
+    """librosa.fft_frequencies = np.fft.rfftfreq(n_fft, 1/sr) (f64): k * (1 / (n_fft * (1/sr)))."""
+    return np.fft.rfftfreq(n=n_fft, d=1.0 / sr)
+
+
+def stft_mag(y, n_fft=2048, hop=512) -> np.ndarray:
+    """np.abs(librosa.stft(y)) -> f32 (1 + n_fft//2, T).  librosa allocates the STFT matrix in
+    Fortran order, so reductions over time run frame by frame (kept here for the same
+    summation order)."""
+    return np.asfortranarray(np.abs(stft(y, n_fft, hop)))
+
+
+def normalize_l1(S: np.ndarray) -> np.ndarray:
+    """librosa.util.normalize(S, norm=1, axis=-2): f64 magnitude sums, columns whose sum is
+    below tiny(S) are left unscaled, the result is stored back in S's dtype."""
+    length = np.sum(np.abs(S).astype(np.float64), axis=-2, keepdims=True)
+    length[length < np.finfo(S.dtype).tiny] = 1.0
+    out = np.empty_like(S)
+    out[:] = S / length
+    return out
+
+
+def spectral_centroid(y=None, sr=22050, S=None, n_fft=2048, hop=512) -> np.ndarray:
+    """librosa.feature.spectral_centroid -> f64 (1, T): sum_k f_k * S_k / sum_k S_k."""
+    S = stft_mag(y, n_fft, hop) if S is None else S
+    freq = fft_frequencies(sr, n_fft)[:, None]
+    return np.sum(freq * normalize_l1(S), axis=-2, keepdims=True)
+
+
+def spectral_rolloff(y=None, sr=22050, S=None, n_fft=2048, hop=512, roll_percent=0.85) -> np.ndarray:
+    """librosa.feature.spectral_rolloff -> f64 (1, T): the lowest bin frequency at which the
+    f32 running sum of |S| reaches roll_percent of the frame total."""
+    S = stft_mag(y, n_fft, hop) if S is None else S
+    freq = fft_frequencies(sr, n_fft)[:, None]
+    total = np.cumsum(S, axis=-2)
+    thr = np.expand_dims(roll_percent * total[-1, :], axis=-2)
+    ind = np.where(total < thr, np.nan, 1)
+    return np.nanmin(ind * freq, axis=-2, keepdims=True)
+
+
+def amplitude_to_db(S, ref=np.max, amin=1e-5, top_db=80.0) -> np.ndarray:
+    """librosa.amplitude_to_db = power_to_db(|S|^2, ref=ref(|S|)^2, amin=amin^2, top_db)."""
+    mag = np.abs(np.asarray(S))
+    ref_value = ref(mag) if callable(ref) else np.abs(ref)
+    power = np.square(mag, out=mag)
+    return power_to_db(power, amin=amin ** 2, top_db=top_db, ref=ref_value ** 2)
+
+
+def get_duration(y, sr=22050) -> float:
+    """librosa.get_duration(y=y, sr=sr) = samples / sr."""
+    return float(np.asarray(y).shape[-1]) / sr
+
+
 # --------------------------------------------------------------------------- CQT chroma
-C1_HZ = 440.0 * 2.0 ** ((24 - 69) / 12.0)       # note_to_hz('C1')
+C1_HZ =440.0 * 2.0 ** ((24 - 69) / 12.0)       # note_to_hz('C1')
 WINDOW_BANDWIDTH_HANN = 1.50018310546875
 
 

@@ -355,3 +355,35 @@ def find_content_offset(src_audio, nc_audio, sr=SR, *, speed_lo=ALIGN_SPEED_LO, 
 
 def rubberband_pitch_st(pitch_ratio):     # consensus.py:355
     return -12.0 * math.log2(pitch_ratio)
+
+
+# ------------------------------------------------------------------ spectral.py
+SPECTRAL_BANDS = (("sub_bass", 20, 80), ("bass", 80, 250), ("midrange", 250, 2000),   # spectral.py:70-74
+                  ("presence", 2000, 6000), ("brilliance", 6000, 20000))
+
+
+def spectral_analyze(y, sr, detail=False):
+    """spectral.py:38-103 on an already-decoded mono f32 signal at its native rate (the
+    reference loads with sr=None, :52).  Returns the SpectralStats fields as a dict; with
+    detail=True also the per-frame / per-bin intermediates the engine is checked on."""
+    y = np.asarray(y, dtype=np.float32)
+    S = ncref.stft_mag(y)                                               # :63 (shared by :54-57)
+    cen = ncref.spectral_centroid(S=S, sr=sr)[0]                        # :54
+    rol = ncref.spectral_rolloff(S=S, sr=sr, roll_percent=0.85)[0]      # :55-57
+    rms = ncref.rms_frames(y)                                           # :59 and :76 (same call)
+    freqs = ncref.fft_frequencies(sr)                                   # :64
+    out = {"centroid": float(np.mean(cen)), "rolloff": float(np.mean(rol)),
+           "rms_mean": float(np.mean(rms)), "rms_variance": float(np.var(rms))}
+    for name, lo, hi in SPECTRAL_BANDS:                                 # :66-74
+        mask = (freqs >= lo) & (freqs < hi)
+        out[name] = float(np.mean(S[mask, :])) if mask.any() else 0.0
+    loud = rms[rms > np.percentile(rms, 75)]                            # :77-78
+    out["decay_rate"] = float(np.mean(np.diff(loud))) if len(loud) > 1 else 0.0
+    out["duration"] = ncref.get_duration(y, sr)                         # :80
+    db = ncref.amplitude_to_db(S, ref=np.max)                           # :87-94
+    favg = np.mean(db, axis=1)
+    sig = favg > (np.max(favg) - 60.0)
+    out["effective_bandwidth_hz"] = float(freqs[np.where(sig)[0][-1]]) if sig.any() else float(freqs[-1])
+    if detail:
+        return out, {"centroid": cen, "rolloff": rol, "rms": rms, "bin_db_mean": favg, "S": S}
+    return out

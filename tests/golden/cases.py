@@ -55,3 +55,71 @@ def make_case(synth, name):
                 nc, src = edit(nc, src, ed, seed, synth, secs)
             return nc, src, kw
     raise KeyError(name)
+
+
+# spectral.analyze cases (spectral.py:38-103): name -> (seconds, seed, native sample rate, edit)
+SPECTRAL_CASES = [
+    ("chords30_22k", 30.0, 1000, 22050, "plain"),
+    ("chords30_44k", 30.0, 1001, 44100, "full"),          # broadband content up to 22 kHz
+    ("chords30_44k_lp16k", 30.0, 1001, 44100, "lp16k"),   # same content, MP3-128k-like cutoff
+    ("chords30_44k_dark", 30.0, 1001, 44100, "dark"),     # low-passed + compressed + reverb tail
+    ("sweep20_48k", 20.0, 1002, 48000, "sweep"),
+    ("tone20_22k", 20.0, 1003, 22050, "tone"),
+    ("intro25_22k", 25.0, 1004, 22050, "intro"),
+    ("silence", 0.25, 1005, 22050, "zeros"),
+    ("short", 0.07, 1006, 22050, "noise"),
+]
+
+# compare_and_print pairs: (ref case, other case, label_ref, label_other, ref_path, other_path)
+SPECTRAL_COMPARE = [
+    ("chords30_44k", "chords30_44k_lp16k", "HQ", "NCOG", "hq.flac", "ncog.flac"),
+    ("chords30_44k", "chords30_44k_dark", "REFERENCE", "OTHER", "a.wav", "b.mp3"),
+    ("chords30_44k_dark", "chords30_44k", "HQNC", "NCOG", "x.mp3", "y.flac"),
+    ("chords30_22k", "intro25_22k", "REFERENCE", "OTHER", None, None),
+    ("chords30_44k_lp16k", "chords30_44k_lp16k", "A", "B", "a.aiff", "b.wav"),
+    ("sweep20_48k", "chords30_44k", "S", "C", "s.mp3", "c.ogg"),
+]
+
+
+def make_spectral_signal(synth, name):
+    """(mono f32 signal, native sample rate) of a SPECTRAL_CASES entry."""
+    from scipy.signal import butter, resample_poly, sosfilt
+    for n, secs, seed, sr, how in SPECTRAL_CASES:
+        if n != name:
+            continue
+        rng = np.random.default_rng(seed)
+        if how == "zeros":
+            return np.zeros(int(secs * sr), np.float32), sr
+        if how == "noise":
+            return (rng.standard_normal(int(secs * sr)) * 0.1).astype(np.float32), sr
+        if how == "tone":
+            k0 = 93
+            t = np.arange(int(secs * sr))
+            return (0.5 * np.sin(2 * np.pi * k0 * sr / 2048 * t / sr)).astype(np.float32), sr
+        if how == "sweep":
+            src = synth.make_pair(secs, seed, "sweep")[1].astype(np.float64)
+        elif how in ("full", "lp16k", "dark"):                        # sustained chords, no kick
+            src = synth._chords(int(secs * 22050), np.random.default_rng(seed)).astype(np.float64)
+        else:
+            src = synth.make_source(secs, seed).astype(np.float64)
+        if sr != 22050:
+            g = np.gcd(sr, 22050)
+            src = resample_poly(src, sr // g, 22050 // g)
+        if how in ("full", "lp16k"):                                  # mastered: limited peaks
+            src = np.tanh(3.0 * src) / 3.0
+        if how in ("full", "lp16k", "dark", "sweep"):
+            hiss = rng.standard_normal(len(src)) * 0.01               # broadband air / cymbal noise
+            src = src + sosfilt(butter(4, 5000, "highpass", fs=sr, output="sos"), hiss)
+        if how == "lp16k":                                            # brick-wall, as an MP3 encoder
+            X = np.fft.rfft(src)
+            X[np.fft.rfftfreq(len(src), 1.0 / sr) >= 16000.0] = 0.0
+            src = np.fft.irfft(X, len(src))
+        elif how == "dark":
+            src = sosfilt(butter(6, 3000, "lowpass", fs=sr, output="sos"), src)
+            src = np.tanh(4.0 * src) / 4.0
+            tail = np.exp(-np.arange(int(0.4 * sr)) / (0.12 * sr)) * rng.standard_normal(int(0.4 * sr)) * 0.02
+            src = np.convolve(src, np.concatenate([[1.0], tail]))[:len(src)]
+        elif how == "intro":
+            src[:5 * sr] *= 10 ** (-30 / 20)
+        return src.astype(np.float32), sr
+    raise KeyError(name)

@@ -89,6 +89,7 @@ class _RefFinder(importlib.abc.MetaPathFinder):
 
 # ----------------------------------------------------------------------------- librosa shim
 _AUDIO: dict[str, np.ndarray] = {}
+_NATIVE_SR: dict[str, int] = {}          # spectral cases: the file's own rate (load(sr=None))
 
 
 def _make_librosa_shim():
@@ -98,6 +99,8 @@ def _make_librosa_shim():
         sys.modules["librosa." + sub] = getattr(lib, sub)
 
     def load(path, sr=22050, mono=True, dtype=np.float32, **kw):
+        if sr is None:
+            return np.asarray(_AUDIO[str(path)], dtype=dtype).copy(), _NATIVE_SR[str(path)]
         return np.asarray(_AUDIO[str(path)], dtype=dtype).copy(), sr
 
     def trim(y, top_db=60, **kw):
@@ -144,7 +147,22 @@ def _make_librosa_shim():
     def rms(y=None, frame_length=2048, hop_length=512, **kw):
         return ncref.rms_frames(y, frame_length, hop_length)[np.newaxis, :]
 
+    def spectral_centroid(y=None, sr=22050, **kw):
+        return ncref.spectral_centroid(y, sr)
+
+    def spectral_rolloff(y=None, sr=22050, roll_percent=0.85, **kw):
+        return ncref.spectral_rolloff(y, sr, roll_percent=roll_percent)
+
+    def stft(y, n_fft=2048, hop_length=512, **kw):
+        return np.asfortranarray(ncref.stft(y, n_fft, hop_length))
+
     lib.load = load
+    lib.feature.spectral_centroid = spectral_centroid
+    lib.feature.spectral_rolloff = spectral_rolloff
+    lib.stft = stft
+    lib.fft_frequencies = lambda sr=22050, n_fft=2048: ncref.fft_frequencies(sr, n_fft)
+    lib.amplitude_to_db = lambda S, ref=1.0, amin=1e-5, top_db=80.0: ncref.amplitude_to_db(S, ref, amin, top_db)
+    lib.get_duration = lambda y=None, sr=22050, **kw: ncref.get_duration(y, sr)
     lib.effects.trim = trim
     lib.onset.onset_strength = onset_strength
     lib.beat.beat_track = beat_track
@@ -164,7 +182,7 @@ def load_reference():
     import importlib
     pkg = importlib.import_module("_refpkg")
     mods = {m: importlib.import_module("_refpkg." + m)
-            for m in ("io", "tempo", "pitch", "consensus", "pipeline", "export", "cli", "xcorr")}
+            for m in ("io", "tempo", "pitch", "consensus", "pipeline", "export", "cli", "xcorr", "spectral")}
     return pkg, mods
 
 
@@ -207,7 +225,8 @@ def _result_fields(r) -> dict:
 
 # ----------------------------------------------------------------------------- cases
 sys.path.insert(0, str(OUT))
-from cases import ALIGN_CASES, PIPELINE_CASES, edit as _edit, make_align_pair  # noqa: E402
+from cases import (ALIGN_CASES, PIPELINE_CASES, SPECTRAL_CASES, SPECTRAL_COMPARE,  # noqa: E402
+                   edit as _edit, make_align_pair, make_spectral_signal)
 
 
 def gen_pipeline(mods, names=None):
@@ -372,13 +391,46 @@ def gen_units(mods, pkg):
     return g
 
 
+def gen_spectral(mods):
+    """spectral.analyze (spectral.py:38-103) on every SPECTRAL_CASES signal, and the
+    compare_and_print report (spectral.py:113-249) for the SPECTRAL_COMPARE pairs."""
+    import contextlib
+    import dataclasses
+    import io as _io
+    spec = mods["spectral"]
+    tmp = Path(tempfile.mkdtemp())
+    stats, out = {}, {"cases": {}, "compare": []}
+    for name, secs, seed, sr, how in SPECTRAL_CASES:
+        y, sr = make_spectral_signal(synth, name)
+        path = tmp / f"{name}.wav"
+        path.write_bytes(b"x")
+        _AUDIO[str(path)], _NATIVE_SR[str(path)] = y, sr
+        buf = _io.StringIO()
+        with contextlib.redirect_stdout(buf):
+            st = spec.analyze(str(path), label=name.upper())
+        stats[name] = st
+        out["cases"][name] = {"seconds": secs, "seed": seed, "sr": sr, "edit": how, "n": len(y),
+                              "sha256": _sha(y), "stdout": buf.getvalue(),
+                              "stats": dataclasses.asdict(st)}
+        print(name, "done", dataclasses.asdict(st))
+    for a, b, la, lb, pa, pb in SPECTRAL_COMPARE:
+        buf = _io.StringIO()
+        with contextlib.redirect_stdout(buf):
+            spec.compare_and_print(stats[a], stats[b], la, lb, pa, pb)
+        out["compare"].append({"ref": a, "other": b, "label_ref": la, "label_other": lb,
+                               "ref_path": pa, "other_path": pb, "text": buf.getvalue()})
+    return out
+
+
 def main(argv=None):
     argv = argv if argv is not None else sys.argv[1:]
     pkg, mods = load_reference()
     if not argv or "units" in argv:
         _dump("units.json", gen_units(mods, pkg))
+    if not argv or "spectral" in argv:
+        _dump("spectral.json", gen_spectral(mods))
     if not argv or "pipeline" in argv:
-        names = [a for a in argv if a not in ("units", "pipeline")] or None
+        names = [a for a in argv if a not in ("units", "pipeline", "spectral")] or None
         _dump("pipeline.json", gen_pipeline(mods, names))
 
 
