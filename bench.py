@@ -24,6 +24,7 @@ import json
 import os
 import sys
 import time
+import numpy as np
 from concurrent.futures import ProcessPoolExecutor
 from pathlib import Path
 
@@ -120,6 +121,7 @@ def main():
     ap.add_argument("--no-ibi", action="store_true")
     ap.add_argument("--no-config5", action="store_true", help="skip the 60-min pair (BASELINE configs[4]) timing")
     ap.add_argument("--no-spectral", action="store_true", help="skip the spectral.analyze (SURVEY.md §8f) timing")
+    ap.add_argument("--no-resample", action="store_true", help="skip the load-time resampler (SURVEY.md §8f) timing")
     ap.add_argument("--cpu-workers", type=int, default=8, help="CPU baseline processes (one pair each)")
     ap.add_argument("--workers", type=int, default=min(16, os.cpu_count() or 1))
     args = ap.parse_args()
@@ -280,6 +282,49 @@ def main():
                                     "kind": "port", "sample": "oracle/refglue.spectral_analyze of file 1 "
                                                               "(one 3-min src), numpy, 1 process"}
 
+    # the load-time resampler (io.py:54) on 44.1 kHz copies of the batch's
+    # src files, resident in HBM (nc_resample_poly, bit-identical to scipy.signal.resample_poly)
+    rsmp = None
+    if not args.no_resample and rank == 0:
+        import scipy.signal
+        from nightcore_analyzer.ops import poly_plan
+        n_files = min(16, len(pairs))
+        x44 = [scipy.signal.resample_poly(pairs[i][1], 2, 1).astype(np.float32) for i in range(n_files)]
+        sig44 = eng.upload_signals(x44)
+        up_, down_, hh, pre = poly_plan(1, 2, int(sig44.length.max()))
+        n_out = np.array([-(-int(n) * up_ // down_) for n in sig44.length], np.int64)
+        o_off = np.concatenate([[0], np.cumsum(n_out)[:-1]]).astype(np.int64)
+        dev = eng.dev
+        tens = {k: torch.from_numpy(np.asarray(v)).to(dev) for k, v in
+                (("in_off", sig44.off), ("in_len", sig44.length), ("out_off", o_off), ("out_len", n_out), ("h", hh))}
+        yout = torch.empty(int(n_out.sum()), dtype=torch.float32, device=dev)
+
+        def _rs():
+            eng.call("nc_resample_poly", sig44.buf.data_ptr(), tens["in_off"].data_ptr(), tens["in_len"].data_ptr(),
+                     n_files, yout.data_ptr(), tens["out_off"].data_ptr(), tens["out_len"].data_ptr(),
+                     int(n_out.max()), tens["h"].data_ptr(), len(hh), up_, down_, pre, eng.stream())
+        _rs()
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(10):
+            _rs()
+        e1.record()
+        torch.cuda.synchronize()
+        ms = e0.elapsed_time(e1) / 10
+        n_in = int(sig44.length.sum())
+        alg = n_in * 4 + int(n_out.sum()) * 4          # every input sample read once, every output written once
+        rsmp = {"workload": f"{n_files} x 3-min 44.1 kHz files -> 22.05 kHz (resample_poly 1/2, 42-tap f64 FIR)",
+                "ms_per_call": ms, "input_samples_per_s": n_in / (ms * 1e-3),
+                "roofline": {"bound": "hbm", "achieved": alg / (ms * 1e-3) / 1e9, "peak": HBM_PEAK_GBS,
+                             "unit": "GB/s", "frac": alg / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS}}
+        if world == 1 and not args.no_cpu_baseline:
+            t1 = time.perf_counter()
+            scipy.signal.resample_poly(x44[0].astype(np.float64), 1, 2)
+            rsmp["cpu_baseline"] = {"value": len(x44[0]) / (time.perf_counter() - t1), "unit": "input samples/s",
+                                    "cores": 1, "kind": "port",
+                                    "sample": "scipy.signal.resample_poly of one 3-min 44.1 kHz file, 1 process"}
+
     if rank == 0:
         line = {
             "metric": "10 s windows/sec (CQT+onset, 22.05 kHz mono) at 1/2/4/8 GPUs; % HBM roofline",
@@ -318,6 +363,8 @@ def main():
             line["config5"] = cfg5
         if spec is not None:
             line["spectral"] = spec
+        if rsmp is not None:
+            line["resample"] = rsmp
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(args.seconds, 1000, args.cpu_workers)
         print(json.dumps(line), flush=True)

@@ -270,6 +270,23 @@ int nc_spectral_stats(nc_ctx* ctx, const float* sig, const int64_t* file_off, co
                       int64_t total_frames, int64_t max_frames, float roll_percent, float* rms_out,
                       double* stats_out, double* bin_db_out, void* ws, size_t ws_bytes, void* stream);
 
+/* ---------------------------------------------------------------------------
+ * R1  load-time resampler — replaces the resample inside io.load_audio
+ *     (io.py:44-55: librosa.load(path, sr=22050) -> soxr_hq) for files that are
+ *     not at 22 050 Hz.  libsoxr is absent and cannot be bit-matched; the engine's
+ *     stand-in is scipy.signal.resample_poly(x, up, down) (Kaiser(5.0) FIR,
+ *     constant zero padding), reproduced bit for bit in f64.  For each file f:
+ *     y[out_off[f] + m] = upfirdn(h, x[in_off[f] ..], up, down)[m + pre_remove]
+ *     (float), m < out_len[f] = ceil(in_len[f] up / down); max_out = max out_len.
+ *     h (device f64, h_len = a multiple of up) is resample_poly's filter:
+ *     firwin(20 max(up,down) + 1, 1/max(up,down), ('kaiser', 5)) * up, with its
+ *     leading / trailing zero padding; pre_remove = resample_poly's n_pre_remove.
+ *     All files of one call share (up, down, h).
+ * ------------------------------------------------------------------------- */
+int nc_resample_poly(nc_ctx* ctx, const float* x, const int64_t* in_off, const int64_t* in_len, int n_files,
+                     float* y, const int64_t* out_off, const int64_t* out_len, int64_t max_out,
+                     const double* h, int h_len, int up, int down, int64_t pre_remove, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -68,6 +68,10 @@ int launch_spectral(Context& ctx, const float* sig, const int64_t* file_off, con
                     int64_t total_frames, int64_t max_frames, float roll_percent, float* rms_out,
                     double* stats_out, double* bin_db_out, void* ws, size_t ws_bytes, hipStream_t st);
 
+int launch_resample_poly(const float* x, const int64_t* in_off, const int64_t* in_len, int n_files,
+                         float* y, const int64_t* out_off, const int64_t* out_len, int64_t max_out,
+                         const double* h, int h_len, int up, int down, int64_t pre_remove, hipStream_t st);
+
 int launch_energy_gate(const double* energy, const int* w0, const int* w1, int n_groups, double gate_db,
                        uint8_t* active, hipStream_t st);
 int launch_collect_valid(const double* bpm, const int* nbeats, const uint8_t* active, const int* w0, const int* w1,
@@ -375,6 +379,15 @@ int nc_spectral_stats(nc_ctx* ctx, const float* sig, const int64_t* file_off, co
   return nc::launch_spectral(ctx->c, sig, file_off, file_len, frame_base, bin_hz, band_bins, n_files, total_frames,
                              max_frames, roll_percent, rms_out, stats_out, bin_db_out, ws, ws_bytes,
                              (hipStream_t)stream);
+}
+
+int nc_resample_poly(nc_ctx* ctx, const float* x, const int64_t* in_off, const int64_t* in_len, int n_files,
+                     float* y, const int64_t* out_off, const int64_t* out_len, int64_t max_out, const double* h,
+                     int h_len, int up, int down, int64_t pre_remove, void* stream) {
+  CHECK_CTX(ctx);
+  SET_DEVICE(ctx);
+  return nc::launch_resample_poly(x, in_off, in_len, n_files, y, out_off, out_len, max_out, h, h_len, up, down,
+                                  pre_remove, (hipStream_t)stream);
 }
 
 }  // extern "C"

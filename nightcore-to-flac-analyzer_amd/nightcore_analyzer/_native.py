@@ -60,6 +60,7 @@ SIGNATURES = {
     "nc_align_offsets": (I32, [P, P, P, P, P, P, I32, P, I32, I32, I64, I64, P, P, P, P, SZ, P]),
     "nc_spectral_workspace_bytes": (SZ, [I64, I32, I64]),
     "nc_spectral_stats": (I32, [P, P, P, P, P, P, P, I32, I64, I64, F32, P, P, P, P, SZ, P]),
+    "nc_resample_poly": (I32, [P, P, P, P, I32, P, P, P, I64, P, I32, I32, I32, I64, P]),
 }
 
 

@@ -4,8 +4,9 @@
 * ``load_audio`` (io.py:44-55) decodes on the CPU — file decode is out of the
   engine's scope (north_star); WAV (PCM 8/16/24/32-bit, float) and ``.npy`` are
   read with the standard library / numpy, down-mixed to mono float32 and, if
-  the file is not at 22 050 Hz, resampled with scipy's polyphase filter (the
-  reference uses librosa.load's soxr_hq; not bit-identical — see DESIGN.md).
+  the file is not at 22 050 Hz, resampled on the GPU by ``nc_resample_poly``
+  (bit-identical to scipy.signal.resample_poly; the reference uses librosa.load's
+  soxr_hq, which is absent here — see DESIGN.md).
 * ``strip_silence`` (io.py:58-79) runs ``nc_trim_bounds`` on the GPU.
 * ``slice_windows`` (io.py:82-112) returns views like the reference, with the
   window energies computed by ``nc_window_energy`` on the GPU.
@@ -89,11 +90,12 @@ def load_audio(path: str, sr: Optional[int] = SAMPLE_RATE) -> tuple[np.ndarray, 
             "not installed here); convert to WAV or .npy first")
     if sr is None:
         sr = file_sr
-    if file_sr != sr:
+    if file_sr != sr:                   # io.py:54 resamples at load: on the GPU (nc_resample_poly)
         import math
-        import scipy.signal
+        from .engine import get_engine
+        from .ops import resample_poly
         g = math.gcd(int(sr), int(file_sr))
-        y = scipy.signal.resample_poly(y.astype(np.float64), sr // g, file_sr // g).astype(np.float32)
+        y, = resample_poly(get_engine(), [y], int(sr) // g, int(file_sr) // g)
     return np.ascontiguousarray(y, dtype=np.float32), sr
 
 

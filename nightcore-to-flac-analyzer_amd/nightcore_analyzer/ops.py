@@ -198,3 +198,58 @@ def shift_bootstrap(eng: Engine, shifts: np.ndarray) -> Tuple[float, float]:
     """pitch.py:143-150: CI of the median chunk shift, rng = default_rng(0)."""
     (_, ci), = eng.bootstrap([(np.asarray(shifts, np.float64), None)], seed=0)
     return ci
+
+
+# ------------------------------------------------------------------ load-time resampler
+def poly_plan(up: int, down: int, max_in: int):
+    """scipy.signal.resample_poly's filter and offsets for ratio up/down (reduced), sized for
+    inputs up to max_in samples: (up, down, h padded to a multiple of up (f64), pre_remove).
+    Trailing zero taps beyond what a shorter input needs leave every sum unchanged."""
+    import math
+    from scipy.signal import firwin
+    g = math.gcd(int(up), int(down))
+    up, down = int(up) // g, int(down) // g
+    max_rate = max(up, down)
+    half_len = 10 * max_rate
+    h = firwin(2 * half_len + 1, 1.0 / max_rate, window=("kaiser", 5.0)) * up
+    n_pre_pad = down - half_len % down
+    pre_remove = (half_len + n_pre_pad) // down
+    n_out = -(-max_in * up // down)
+
+    def out_len(len_h, n_in):        # scipy.signal._upfirdn_apply._output_len
+        n = n_in + (len_h + (-len_h % up)) // up - 1
+        return -(-n * up // down)
+    post = 0
+    while out_len(len(h) + n_pre_pad + post, max_in) < n_out + pre_remove:
+        post += 1
+    h = np.concatenate([np.zeros(n_pre_pad), h, np.zeros(post)])
+    h = np.concatenate([h, np.zeros(-len(h) % up)])
+    return up, down, h, pre_remove
+
+
+def resample_poly(eng: Engine, arrays: Sequence[np.ndarray], up: int, down: int) -> List[np.ndarray]:
+    """float32(scipy.signal.resample_poly(float64(x), up, down)) for each array, on the GPU
+    (nc_resample_poly; bit-identical to scipy).  The load-time resampler of io.load_audio."""
+    arrays = [np.asarray(a, np.float32) for a in arrays]
+    if not arrays:
+        return []
+    up, down, h, pre = poly_plan(up, down, max(len(a) for a in arrays))
+    if up == down == 1:
+        return [a.copy() for a in arrays]
+    sig = eng.upload_signals(arrays)
+    n_out = np.array([-(-len(a) * up // down) for a in arrays], np.int64)
+    o_off = np.zeros(len(arrays), np.int64)
+    o_off[1:] = np.cumsum(n_out)[:-1]
+    up_ = _Upload()
+    up_.add("in_off", sig.off, np.int64)
+    up_.add("in_len", sig.length, np.int64)
+    up_.add("out_off", o_off, np.int64)
+    up_.add("out_len", n_out, np.int64)
+    up_.add("h", h, np.float64)
+    d = up_.commit(eng.dev)
+    y = torch.empty(max(1, int(n_out.sum())), dtype=torch.float32, device=eng.dev)
+    eng.call("nc_resample_poly", sig.buf.data_ptr(), d["in_off"].data_ptr(), d["in_len"].data_ptr(), len(arrays),
+             y.data_ptr(), d["out_off"].data_ptr(), d["out_len"].data_ptr(), int(n_out.max()), d["h"].data_ptr(),
+             len(h), up, down, pre, eng.stream())
+    hy = y.cpu().numpy()
+    return [hy[o:o + n].copy() for o, n in zip(o_off, n_out)]

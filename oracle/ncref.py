@@ -438,6 +438,33 @@ def get_duration(y, sr=22050) -> float:
     return float(np.asarray(y).shape[-1]) / sr
 
 
+# --------------------------------------------------------------------------- load-time resample
+# io.py:54 (librosa.load(sr=22050) -> soxr_hq, absent here): the engine's stand-in is
+# scipy.signal.resample_poly; this is its upfirdn sum restated term by term (scipy 1.15
+# signal/_upfirdn_apply.pyx _apply_impl), the order the GPU kernel reproduces.
+def resample_poly_terms(x, up, down, h, pre_remove, n_out):
+    """y[m'] = sum over i = hpp-1..0 of x[x_idx - i] * h[p + i up] for m = m' + pre_remove,
+    x_idx = m down // up, p = m down % up (oldest sample first, separate rounding of
+    products and sums); left out-of-range taps are skipped while x_idx < len(x), every
+    tap (zero samples included) is added once x_idx >= len(x)."""
+    x = np.asarray(x, np.float64)
+    h = np.asarray(h, np.float64)
+    hpp = len(h) // up
+    m = np.arange(n_out, dtype=np.int64) + pre_remove
+    x_idx = m * down // up
+    ph = m * down % up
+    flush = x_idx >= len(x)
+    acc = np.zeros(n_out)
+    xp = np.concatenate([x, [0.0]])
+    for i in range(hpp - 1, -1, -1):
+        xi = x_idx - i
+        inside = (xi >= 0) & (xi < len(x))
+        xv = xp[np.where(inside, xi, len(x))]
+        take = flush | (xi >= 0)
+        acc = np.where(take, acc + xv * h[ph + i * up], acc)
+    return acc
+
+
 # --------------------------------------------------------------------------- CQT chroma
 C1_HZ =440.0 * 2.0 ** ((24 - 69) / 12.0)       # note_to_hz('C1')
 WINDOW_BANDWIDTH_HANN = 1.50018310546875
