@@ -171,18 +171,26 @@ __global__ __launch_bounds__(TP_WAVES * 64) void tuning_peaks_kernel(PeakArgs a)
     stockham_stage<1024, 16, 16, 64, false, 0, 0>(fftbuf, sh_tw, lane);
     float2 v[4][4];
     fft1024_last_mirror<TpTw::s3>(fftbuf, sh_tw, lane, v);
-    float* S = reinterpret_cast<float*>(fftbuf);  // |X[k]|, k in [0, 1024] (all Z reads precede)
-    float mx = 0.0f;
+    // |X|^2 into LDS only where the peak stencil reads it (bins klo-1 .. khi+1); the frame max
+    // of |X| is sqrt(max |X|^2) (the correctly rounded sqrt is monotonic), so the other 2/3 of
+    // the bins need no square root at all
+    constexpr int klo = 14, khi = 371, NR = (khi - klo + 64) / 64;  // [150, 4000) Hz: k 22050 / 2048
+    float* S = reinterpret_cast<float*>(fftbuf);  // (all Z reads precede)
+    float pmax = 0.0f;
     rsplit_mirror<TpTw::split>(v, sh_tw, lane, [&](int k, float2 X, float2 XN) {
-      const float m1 = __fsqrt_rn(fmaf(X.x, X.x, X.y * X.y)), m2 = __fsqrt_rn(fmaf(XN.x, XN.x, XN.y * XN.y));
-      S[k] = m1;
-      S[1024 - k] = m2;
-      mx = fmaxf(mx, fmaxf(m1, m2));
+      const float p1 = fmaf(X.x, X.x, X.y * X.y), p2 = fmaf(XN.x, XN.x, XN.y * XN.y);
+      if (k >= klo - 1 && k <= khi + 1) S[k] = p1;
+      if (1024 - k <= khi + 1) S[1024 - k] = p2;
+      pmax = fmaxf(pmax, fmaxf(p1, p2));
     });
-    mx = wave_max(mx);
+    const float mx = __fsqrt_rn(wave_max(pmax));
     const float ref = 0.1f * mx;
-    // bins inside [150, 4000) Hz: k * 22050 / 2048 -> 14..371 (6 rounds of 64 lanes)
-    constexpr int klo = 14, khi = 371, NR = (khi - klo + 64) / 64;
+    // |X| over the stencil's bins, in place (6 per lane)
+#pragma unroll
+    for (int q = 0; q < (khi - klo + 3 + 63) / 64; ++q) {
+      const int k = klo - 1 + 64 * q + lane;
+      if (k <= khi + 1) S[k] = __fsqrt_rn(S[k]);
+    }
     float pitch[NR], mag[NR];
     unsigned long long bal[NR];
     int cnt = 0;
@@ -702,7 +710,9 @@ int launch_chroma_mean(Context& ctx, const float* sig, const int64_t* chunk_off,
   hipLaunchKernelGGL(chroma_plan_kernel, dim3(1), dim3(256), 0, st, chunk_len, n, w.oct_off, w.oct_len, w.n_frames,
                      w.n_tframes, w.tf_base, w.oct_base);
   NC_HIP(hipMemsetAsync(w.chunk_npk, 0, sizeof(int) * n, st));
-  // grids are sized by the longest chunk; blocks past a chunk's own length exit
+  // grids are sized by the longest chunk; blocks past a chunk's own length exit.  (Forking
+  // the decimation onto a second stream, concurrent with the tuning estimate, measured no
+  // gain: the chip is already full with the window chain on the caller's other stream.)
   for (int lvl = 0; lvl < 6; ++lvl) {
     const int64_t mo = (max_chunk_len >> (lvl + 1)) + 1;
     dim3 grid((unsigned)((mo + DEC_OUT - 1) / DEC_OUT), (unsigned)n);

@@ -8,7 +8,9 @@
 namespace nc {
 
 // out[m] = s * sum_{j=0}^{2K} h[j] in[2m - (j - K)]  (zero outside), accumulated in f64
-// in the oracle's order (ascending j, separate multiply and add: oracle/ncref.py decimate2),
+// in the oracle's order (ascending j: oracle/ncref.py decimate2) with one fused multiply-add
+// per tap (the oracle rounds product and sum separately: < 1e-16 relative, below the f32
+// the octave signals are stored in; half the f64 VALU work of the unfused form),
 // s = sqrt(2) or 1.  One workgroup of 256 threads per DEC_OUT outputs; the 2 DEC_OUT + 2K
 // input tile is staged in LDS and the taps are wave-uniform (scalar loads); the zero taps
 // of the half-band (even j - K != 0) are skipped at compile time.
@@ -19,8 +21,7 @@ __device__ __forceinline__ int dec_pad(int e) { return e + (e >> 3); }  // softe
 template <bool SQRT2>
 __device__ __forceinline__ void halfband_tile(const float* in, int64_t Lin, float* out, int64_t Lout, int64_t m0,
                                               const double* __restrict__ taps) {
-#pragma clang fp contract(off)
-  constexpr int K = kHalfbandK;       // 23: taps j - K odd (24 of them) plus the centre
+  constexpr int K = kHalfbandK;      // 23: taps j - K odd (24 of them) plus the centre
   constexpr int H = (K + 1) / 2;      // 12
   constexpr int W = 4 + 2 * H - 1;    // odd-phase window of 4 consecutive outputs: 27 values
   // in[2m - n] with n = j - K: the centre reads the even phase at m, odd n read the odd
@@ -54,12 +55,12 @@ __device__ __forceinline__ void halfband_tile(const float* in, int64_t Lin, floa
   for (int q = 0; q < 4; ++q) xe[q] = te[dec_pad(l0 + q)];
   double acc[4] = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-  for (int j = 0; j <= 2 * K; ++j) {  // the oracle's order: ascending j, multiply then add
+  for (int j = 0; j <= 2 * K; ++j) {  // the oracle's order (ascending j), one f64 FMA per tap
     const int n = j - K;
     if (n != 0 && !(n & 1)) continue;
     const double h = taps[j];
 #pragma unroll
-    for (int q = 0; q < 4; ++q) acc[q] = acc[q] + h * (n == 0 ? xe[q] : xo[q + H + (-n - 1) / 2]);
+    for (int q = 0; q < 4; ++q) acc[q] = fma(h, n == 0 ? xe[q] : xo[q + H + (-n - 1) / 2], acc[q]);
   }
   float r[4];
 #pragma unroll

@@ -196,22 +196,18 @@ def _group_bounds(B: int, group_pairs, ) -> List[Tuple[int, int]]:
             left -= n
             i += 1
     elif group_pairs is None:
-        # default: a 16-pair group to start the device early, 32-pair groups (fewer, fuller
-        # launches of the latency-bound per-window kernels), a 16-pair group at the end to
-        # keep the exposed host assembly short (tools/group_sweep.py)
-        sizes, left = [], B
-        if left > 16:
-            sizes.append(16)
-            left -= 16
-        while left > 48:
-            sizes.append(32)
-            left -= 32
-        if left > 32:
-            sizes += [left - 16, 16]
-        elif left > 16:
-            sizes += [left - left // 2, left // 2]
-        elif left > 0:
-            sizes.append(left)
+        # default: an 8-pair group to start the device early (its host plan is the only one
+        # exposed), 24-pair groups (fuller launches of the latency-bound per-window kernels),
+        # an 8-pair group at the end to keep the exposed host assembly and the chroma tail
+        # short (tools/group_sweep.py: 8,24,24,8 is the fastest schedule for 64 pairs)
+        if B <= 16:
+            sizes = [B] if B else []
+        else:
+            sizes, left = [8], B - 8
+            while left > 32:
+                sizes.append(24)
+                left -= 24
+            sizes += [left - 8, 8] if left > 16 else [left]
     else:
         gp = max(1, int(group_pairs))
         sizes = [gp] * (B // gp) + ([B % gp] if B % gp else [])
@@ -240,6 +236,11 @@ class Engine:
         # the chroma chain runs on its own stream, concurrently with the window/tempo chain
         # (NC_SERIAL_STREAMS=1 queues it on the launch stream instead: isolated per-kernel timings)
         self.chroma_stream = torch.cuda.current_stream(self.dev) if os.environ.get("NC_SERIAL_STREAMS") == "1" \
+            else torch.cuda.Stream(self.dev)
+        # consensus tail (bootstraps + D2H of a group) on a third stream: the window chain of the
+        # next group starts as soon as this group's window chain is done, instead of queueing
+        # behind a bootstrap that waits for this group's (longer) chroma chain
+        self.tail_stream = torch.cuda.current_stream(self.dev) if os.environ.get("NC_SERIAL_STREAMS") == "1" \
             else torch.cuda.Stream(self.dev)
 
     # -------------------------------------------------------------- plumbing
@@ -492,9 +493,9 @@ class Engine:
 
         After one trim pass over all files (the only blocking read-back), pairs
         are processed in groups of ``group_pairs``: the whole device pipeline of
-        group g is queued (plans uploaded through pinned memory, results copied
-        back asynchronously) before the host assembles the results of group g-1,
-        so host assembly overlaps device work."""
+        every group is queued (plans uploaded through pinned memory, results copied
+        back asynchronously) before the host assembles the results of group 0, so
+        host assembly overlaps the device work of the later groups."""
         p = params or Params()
         if signals is None:
             flat = []
@@ -511,21 +512,21 @@ class Engine:
                                        signals.off[0::2] + start[0::2], end[0::2] - start[0::2])
         if hs is not None:
             hs["trim"] = hs.get("trim", 0.0) + time.perf_counter() - t0
+        # every group is queued before the host waits for any: the window stream never idles
+        # behind the host assembly of an earlier group, and the assembly of group g overlaps
+        # the device work of the groups after it
         outs: List[PairOutcome] = []
-        pending = None
+        pending = []
         for g0, g1 in _group_bounds(B, group_pairs):
             sl = slice(2 * g0, 2 * g1)
             sub = DeviceSignals(signals.buf, signals.off[sl], signals.length[sl])
             t0 = time.perf_counter()
-            nxt = self._launch_group(sub, p, start[sl].copy(), end[sl].copy(),
-                                     align[g0:g1] if align is not None else None)
+            pending.append(self._launch_group(sub, p, start[sl].copy(), end[sl].copy(),
+                                              align[g0:g1] if align is not None else None))
             if hs is not None:
                 hs["launch"] = hs.get("launch", 0.0) + time.perf_counter() - t0
-            if pending is not None:
-                outs += self._finish_group(pending)
-            pending = nxt
-        if pending is not None:
-            outs += self._finish_group(pending)
+        for g in pending:
+            outs += self._finish_group(g)
         return outs
 
     def _trim_all(self, signals: DeviceSignals, p: Params) -> Tuple[np.ndarray, np.ndarray]:
@@ -747,43 +748,54 @@ class Engine:
         else:
             prior.fill_(120.0)
 
-        # ---------------------------------------------------------------- 5. bootstraps (tempo + pitch, seed 42)
-        s1.wait_event(ev_chroma)
+        # ---------------------------------------------------------------- 5. IBI pass (window stream)
+        ibi = None
+        if p.compute_ibi:
+            ibi = self._ibi_pass(signals, d["f_off"], d["f_len"], f_len, prior, B)
+        ev_window = torch.cuda.Event()
+        ev_window.record(s1)
+
+        # ---------------------------------------------------------------- 6. bootstraps (tempo + pitch, seed 42)
+        # on the tail stream once both chains of this group are done; the window stream is free
+        # for the next group's window chain meanwhile
+        s3 = self.tail_stream
+        s3.wait_event(ev_window)
+        s3.wait_event(ev_chroma)
+        st3 = s3.cuda_stream
         n_boot = C.N_BOOTSTRAP
         il, gl, ih, gh = percentile_params(n_boot, C.CI_LEVEL)
         bout, sout = o["bout"], o["sout"]
         ws = self.workspace("boot", tot)
+        ws.record_stream(s3)
         self.call("nc_bootstrap_ratio", o["vals"].data_ptr(), d["a_off"].data_ptr(), d["a_n"].data_ptr(),
                   d["b_off"].data_ptr(), d["b_n"].data_ptr(), nj, n_boot, d["seed"].data_ptr(), il, gl, ih, gh,
                   C.MIN_VALID, bout[0:nj].data_ptr(), bout[nj:2 * nj].data_ptr(), bout[2 * nj:].data_ptr(), None,
-                  d["wsoff"].data_ptr(), d["cap"].data_ptr(), ws.data_ptr(), ws.numel(), st)
+                  d["wsoff"].data_ptr(), d["cap"].data_ptr(), ws.data_ptr(), ws.numel(), st3)
         if n_pitch_jobs:
             ws2 = self.workspace("boot_s", s_tot)
+            ws2.record_stream(s3)
             self.call("nc_bootstrap_ratio", o["vals"].data_ptr(), d["s_off"].data_ptr(), d["s_n"].data_ptr(), None,
                       None, n_pitch_jobs, n_boot, d["s_seed"].data_ptr(), il, gl, ih, gh, MIN_CHUNKS,
                       sout[0:n_pitch_jobs].data_ptr(), sout[n_pitch_jobs:2 * n_pitch_jobs].data_ptr(),
                       sout[2 * n_pitch_jobs:3 * n_pitch_jobs].data_ptr(), None, d["s_wsoff"].data_ptr(),
-                      d["s_cap"].data_ptr(), ws2.data_ptr(), ws2.numel(), st)
-
-        # ---------------------------------------------------------------- 6. IBI pass
-        ibi = None
-        if p.compute_ibi:
-            ibi = self._ibi_pass(signals, d["f_off"], d["f_len"], f_len, prior, B)
+                      d["s_cap"].data_ptr(), ws2.data_ptr(), ws2.numel(), st3)
 
         # ---------------------------------------------------------------- 7. async D2H into pinned buffers
-        hbuf, host = ar.to_host()
-        host["pvals"] = host["vals"][TV:]
-        pinned = [hbuf]
-        if ibi is not None:
-            for k, v in ibi.items():
-                if isinstance(v, torch.Tensor):
-                    h = torch.empty(v.shape, dtype=v.dtype, pin_memory=True)
-                    h.copy_(v, non_blocking=True)
-                    pinned.append(h)
-                    host["ibi_" + k] = h.numpy()
-        ev = torch.cuda.Event()
-        ev.record(torch.cuda.current_stream(dev))
-        return dict(p=p, host=host, pinned=pinned, event=ev, keep=(d, o, ar), has_ibi=ibi is not None, align=align,
+        with torch.cuda.stream(s3):
+            hbuf, host = ar.to_host()
+            host["pvals"] = host["vals"][TV:]
+            pinned = [hbuf]
+            if ibi is not None:
+                for k, v in ibi.items():
+                    if isinstance(v, torch.Tensor):
+                        h = torch.empty(v.shape, dtype=v.dtype, pin_memory=True)
+                        h.copy_(v, non_blocking=True)
+                        pinned.append(h)
+                        host["ibi_" + k] = h.numpy()
+            ev = torch.cuda.Event()
+            ev.record(s3)
+        return dict(p=p, host=host, pinned=pinned, event=ev, keep=(d, o, ar, ibi), has_ibi=ibi is not None,
+                    align=align,
                     starts=starts, w0=w0, w1=w1, f_len=f_len,
                     strip_len=strip_len, lead=lead, trail=trail, intro=intro, win_n=win_n,
                     pair_chunks=pair_chunks, n_cp=n_cp, nj=nj, n_pitch_jobs=n_pitch_jobs, B=B)
