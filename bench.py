@@ -193,6 +193,22 @@ def main():
     tflops = flop_per_launch / (avg_ms * 1e-3) / 1e12
     traffic = _pmc_traffic(dom)
     step_ms = el / args.steps * 1e3
+    # the same kernel launched alone (streams serialized for one more untimed step): its own
+    # speed, where the launches above share the chip with the other stream's chain
+    eng.set_serial(True)
+    eng.kernel_profile(True)
+    eng.analyze(signals=signals, params=params)
+    iso = eng.kernel_times()
+    eng.kernel_profile(False)
+    eng.set_serial(False)
+    iso_ms = iso[dom][0] / iso[dom][1] if dom in iso else None
+    isolated = None
+    if iso_ms:
+        a_iso = units[dom][0] / iso[dom][1] * units[dom][1] / (iso_ms * 1e-3) / 1e9
+        f_iso = units[dom][0] / iso[dom][1] * units[dom][2] / (iso_ms * 1e-3) / 1e12
+        isolated = {"avg_launch_ms": iso_ms, "achieved": a_iso, "frac": a_iso / HBM_PEAK_GBS,
+                    "compute_achieved": f_iso, "compute_frac": f_iso / VALU_PEAK_TFS,
+                    "kernels_ms_per_step": {k: round(v[0], 4) for k, v in iso.items()}}
 
     ibi = None
     if not args.no_ibi and rank == 0:
@@ -352,7 +368,11 @@ def main():
                          # the roof that actually binds: f32 VALU, no MFMA on this path
                          "compute": {"bound": "valu_f32", "achieved": tflops, "peak": VALU_PEAK_TFS,
                                      "unit": "TFLOP/s", "frac": tflops / VALU_PEAK_TFS,
-                                     "alg_flop_per_launch": flop_per_launch}},
+                                     "alg_flop_per_launch": flop_per_launch},
+                         # achieved/avg_launch_ms above: launches as they run in the step, sharing
+                         # the chip with the concurrent chain (what rocprofv3 --stats averages);
+                         # isolated: the same kernel with the other streams idle
+                         "isolated": isolated},
             "kernels_ms_per_step": {k: round(v[0] * v[1], 4) for k, v in kper.items()},
             "entry_points_ms_per_step": {k: round(v[0] * v[1], 4) for k, v in per.items()},
             "check": {"tempo_ratio_pair0": tr, "pitch_ratio_pair0": pr},

@@ -243,6 +243,17 @@ class Engine:
         self.tail_stream = torch.cuda.current_stream(self.dev) if os.environ.get("NC_SERIAL_STREAMS") == "1" \
             else torch.cuda.Stream(self.dev)
 
+    def set_serial(self, on: bool) -> None:
+        """Queue the chroma chain and the consensus tail on the launch stream too (on=True):
+        every kernel then runs alone, so per-kernel timers measure its isolated speed rather
+        than its share of a concurrently loaded chip.  Measurement only (bench.py)."""
+        if on:
+            self._streams = (self.chroma_stream, self.tail_stream)
+            self.chroma_stream = self.tail_stream = torch.cuda.current_stream(self.dev)
+        elif getattr(self, "_streams", None):
+            self.chroma_stream, self.tail_stream = self._streams
+            self._streams = None
+
     # -------------------------------------------------------------- plumbing
     def stream(self) -> int:
         return torch.cuda.current_stream(self.dev).cuda_stream
