@@ -134,6 +134,33 @@ size_t nc_chroma_workspace_bytes(const nc_ctx* ctx, int n_chunks, int64_t total_
 int nc_chroma_mean(nc_ctx* ctx, const float* sig, const int64_t* chunk_off, const int64_t* chunk_len,
                    int n_chunks, int64_t total_len, int64_t max_chunk_len, float* out_chroma,
                    float* out_tuning, int* out_tuning_idx, void* ws, size_t ws_bytes, void* stream);
+
+/* ---------------------------------------------------------------------------
+ * K9-K11 with shared tuning frames (optional fusion; same results as the pair
+ * nc_window_stage + nc_chroma_mean).  The first tp_frames tuning frames (2048 / 512,
+ * centred) of a 20 s chunk that starts where a 10 s window starts are that window's
+ * own STFT frames: same samples, same zero padding on the left, none on the right
+ * while t * 512 + 1024 <= win_len (tp_frames = 429 for 10 s windows).
+ * nc_window_stage_tuning = nc_window_stage that also runs estimate_tuning's piptrack
+ * (pitch.py:58 -> librosa.estimate_tuning) on those frames: win_chunk[w] = the chunk
+ * window w starts (or -1), chunk_tf_base[c] = sum_{q<c} (1 + chunk_len[q] / 512) (the
+ * chunk's slot base in the peak lists, in units of 192 slots), peak_pitch / peak_mag =
+ * chunk_tf_base[n] * 192 floats each, chunk_npk[n] zeroed by the caller.  If
+ * stft_done_event (a hipEvent_t) is given it is recorded once the peaks are written.
+ * nc_chroma_mean_shared = nc_chroma_mean on the same peak lists: tuning frames
+ * t < tf_skip[c] are not recomputed (tf_skip_total = sum of tf_skip, host value), the
+ * counts are not zeroed, and the stream waits for wait_event before the tuning select.
+ * ------------------------------------------------------------------------- */
+int nc_window_stage_tuning(nc_ctx* ctx, const float* sig, const int64_t* win_off, const uint8_t* active,
+                           int n_win, int win_len, int hop, float* onset_out, double* tg_out,
+                           double* energy_out, const int* win_chunk, const int64_t* chunk_tf_base,
+                           int tp_frames, float* peak_pitch, float* peak_mag, int* chunk_npk,
+                           void* stft_done_event, void* ws, size_t ws_bytes, void* stream);
+int nc_chroma_mean_shared(nc_ctx* ctx, const float* sig, const int64_t* chunk_off, const int64_t* chunk_len,
+                          int n_chunks, int64_t total_len, int64_t max_chunk_len, float* out_chroma,
+                          float* out_tuning, int* out_tuning_idx, const int* tf_skip, int64_t tf_skip_total,
+                          float* peak_pitch, float* peak_mag, int* chunk_npk, void* wait_event, void* ws,
+                          size_t ws_bytes, void* stream);
 /* pitch._cyclic_xcorr_peak (pitch.py:67-85): lag_out[p] = wrapped argmax_k
  * dot(chroma[src_idx[p]], roll(chroma[nc_idx[p]], -k)), in [-5, 6]. */
 int nc_chroma_lag(nc_ctx* ctx, const float* chroma, const int* src_idx, const int* nc_idx, int n_pairs,

@@ -22,10 +22,10 @@
 #include "nc_block.h"
 #include "nc_decim.h"
 #include "nc_engine.h"
+#include "nc_piptrack.h"
 
 namespace nc {
 
-constexpr int kPeakSlots = 192;  // >= max piptrack peaks per frame (bins 14..371 -> <= 179)
 
 // ------------------------------------------------------------------------------ plan
 // per chunk: octave i signal at oct_off[c*7+i] (i=0 -> the chunk itself inside sig, flagged by
@@ -56,9 +56,12 @@ __device__ __forceinline__ int64_t chunk_oct_floats(int64_t L) {
 // (oct_base = octave-buffer base of each chunk, tf_base = tuning-frame base)
 __global__ __launch_bounds__(256) void chroma_plan_kernel(const int64_t* chunk_len, int n, int64_t* oct_off,
                                                            int64_t* oct_len, int* n_frames, int* n_tframes,
-                                                           int64_t* tf_base, int64_t* oct_base) {
+                                                           int64_t* tf_base, int64_t* oct_base,
+                                                           const int* tf_skip, int64_t* tp_base) {
   block_prefix_table<256>(n, oct_base, [&](int c) { return chunk_oct_floats(chunk_len[c]); });
   block_prefix_table<256>(n, tf_base, [&](int c) { return 1 + chunk_len[c] / 512; });
+  // tuning frames the tuning kernel itself computes (all but the skipped leading ones)
+  block_prefix_table<256>(n, tp_base, [&](int c) { return 1 + chunk_len[c] / 512 - (tf_skip ? tf_skip[c] : 0); });
   __syncthreads();
   for (int c = threadIdx.x; c < n; c += 256) {
     int64_t L = chunk_len[c], acc = oct_base[c];
@@ -109,13 +112,15 @@ struct PeakArgs {
   const int64_t* chunk_len;
   const int* n_tframes;
   const int64_t* tf_base;
+  const int64_t* tp_base;  // [n + 1] prefix of the frames this kernel computes per chunk
   int n_chunks;
-  int64_t total_tframes;  // upper bound of tf_base[n]
+  int64_t total_tframes;  // upper bound of tp_base[n]
   const float2* tw;
   const float* hann2048;
   float* peak_pitch;      // chunk c region starts at tf_base[c] * kPeakSlots
   float* peak_mag;
-  int* chunk_npk;         // [n] zeroed by the launcher
+  int* chunk_npk;         // [n] zeroed by the launcher (or by the caller, with tf_skip)
+  const int* tf_skip;     // nullable [n]: leading tuning frames whose peaks the window stage appended
 };
 
 __global__ __launch_bounds__(TP_WAVES * 64) void tuning_peaks_kernel(PeakArgs a) {
@@ -133,11 +138,13 @@ __global__ __launch_bounds__(TP_WAVES * 64) void tuning_peaks_kernel(PeakArgs a)
     int lo = 0, hi = a.n_chunks - 1;
     while (lo < hi) {
       const int mid = (lo + hi + 1) >> 1;
-      if (a.tf_base[mid] <= gf) lo = mid;
+      if (a.tp_base[mid] <= gf) lo = mid;
       else hi = mid - 1;
     }
     const int c = lo;
-    const int t = (int)(gf - a.tf_base[c]);
+    // frames [0, tf_skip[c]) of the chunk were done by the window stage: the work list is
+    // the remaining frames only, so the persistent workgroups stay balanced
+    const int t = (int)(gf - a.tp_base[c]) + (a.tf_skip ? a.tf_skip[c] : 0);
     if (t >= a.n_tframes[c]) continue;
     int lane = lane0;
     asm volatile("" : "+v"(lane));
@@ -171,69 +178,26 @@ __global__ __launch_bounds__(TP_WAVES * 64) void tuning_peaks_kernel(PeakArgs a)
     stockham_stage<1024, 16, 16, 64, false, 0, 0>(fftbuf, sh_tw, lane);
     float2 v[4][4];
     fft1024_last_mirror<TpTw::s3>(fftbuf, sh_tw, lane, v);
-    // |X|^2 into LDS only where the peak stencil reads it (bins klo-1 .. khi+1); the frame max
-    // of |X| is sqrt(max |X|^2) (the correctly rounded sqrt is monotonic), so the other 2/3 of
-    // the bins need no square root at all
-    constexpr int klo = 14, khi = 371, NR = (khi - klo + 64) / 64;  // [150, 4000) Hz: k 22050 / 2048
+    // |X|^2 into LDS only where the peak stencil reads it (bins kPipLo-1 .. kPipHi+1); the frame
+    // max of |X| is sqrt(max |X|^2) (the correctly rounded sqrt is monotonic), so the other
+    // 2/3 of the bins need no square root at all
     float* S = reinterpret_cast<float*>(fftbuf);  // (all Z reads precede)
     float pmax = 0.0f;
     rsplit_mirror<TpTw::split>(v, sh_tw, lane, [&](int k, float2 X, float2 XN) {
       const float p1 = fmaf(X.x, X.x, X.y * X.y), p2 = fmaf(XN.x, XN.x, XN.y * XN.y);
-      if (k >= klo - 1 && k <= khi + 1) S[k] = p1;
-      if (1024 - k <= khi + 1) S[1024 - k] = p2;
+      if (k >= kPipLo - 1 && k <= kPipHi + 1) S[k] = p1;
+      if (1024 - k <= kPipHi + 1) S[1024 - k] = p2;
       pmax = fmaxf(pmax, fmaxf(p1, p2));
     });
     const float mx = __fsqrt_rn(wave_max(pmax));
-    const float ref = 0.1f * mx;
     // |X| over the stencil's bins, in place (6 per lane)
 #pragma unroll
-    for (int q = 0; q < (khi - klo + 3 + 63) / 64; ++q) {
-      const int k = klo - 1 + 64 * q + lane;
-      if (k <= khi + 1) S[k] = __fsqrt_rn(S[k]);
+    for (int q = 0; q < (kPipHi - kPipLo + 3 + 63) / 64; ++q) {
+      const int k = kPipLo - 1 + 64 * q + lane;
+      if (k <= kPipHi + 1) S[k] = __fsqrt_rn(S[k]);
     }
-    float pitch[NR], mag[NR];
-    unsigned long long bal[NR];
-    int cnt = 0;
-#pragma unroll
-    for (int q = 0; q < NR; ++q) {
-      const int k = klo + 64 * q + lane;
-      bool pk = false;
-      pitch[q] = 0.0f;
-      mag[q] = 0.0f;
-      if (k <= khi) {
-        const float sm = S[k - 1], s = S[k], sp = S[k + 1];
-        const float zm = sm > ref ? sm : 0.0f, z = s > ref ? s : 0.0f, zp = sp > ref ? sp : 0.0f;
-        pk = (z > zm) && (z >= zp);
-        if (pk) {
-          // parabolic shift (librosa numba stencil, f64 arithmetic, stored f32)
-          const double aa = (double)(sp + sm) - 2.0 * (double)s;  // f32 add, then f64 (numba typing)
-          const double bb = (double)(sp - sm) / 2.0;
-          const float shift = (fabs(bb) >= fabs(aa)) ? 0.0f : (float)(-bb / aa);
-          const float avg = (sp - sm) / 2.0f;
-          const float dskew = (0.5f * avg) * shift;
-          pitch[q] = (float)((((double)k + (double)shift) * 22050.0) / 2048.0);
-          mag[q] = s + dskew;
-        }
-      }
-      bal[q] = __ballot(pk);
-      cnt += __popcll(bal[q]);
-    }
-    if (cnt == 0) continue;
-    int pos = 0;
-    if (lane == 0) pos = atomicAdd(&a.chunk_npk[c], cnt);
-    pos = __shfl(pos, 0, 64);
-    float* pp = a.peak_pitch + a.tf_base[c] * kPeakSlots;
-    float* pm = a.peak_mag + a.tf_base[c] * kPeakSlots;
-    const unsigned long long below = (1ull << lane) - 1ull;
-#pragma unroll
-    for (int q = 0; q < NR; ++q) {
-      if ((bal[q] >> lane) & 1ull) {
-        const int i = pos + __popcll(bal[q] & below);
-        pp[i] = pitch[q];
-        pm[i] = mag[q];
-      }
-      pos += __popcll(bal[q]);
-    }
+    piptrack_append([&](int k) { return S[k]; }, mx, lane, &a.chunk_npk[c],
+                    a.peak_pitch + a.tf_base[c] * kPeakSlots, a.peak_mag + a.tf_base[c] * kPeakSlots);
   }
 }
 
@@ -671,13 +635,20 @@ size_t chroma_ws_bytes(int n, int64_t total_len) {
   b += al256(sizeof(float) * (size_t)(total_len + 64 * 7 * (int64_t)n));
   b += al256(sizeof(float) * (size_t)tfr * kPeakSlots) * 2;
   b += al256(sizeof(double) * (size_t)(tfr / CQ_FR + n + 1) * 12);
+  b += al256(sizeof(int64_t) * (n + 1));
   return b + 4096;
 }
 
 int launch_chroma_mean(Context& ctx, const float* sig, const int64_t* chunk_off, const int64_t* chunk_len, int n,
                        int64_t total_len, int64_t max_chunk_len, float* out_chroma, float* out_tuning,
-                       int* out_tuning_idx, void* ws, size_t ws_bytes, hipStream_t st) {
+                       int* out_tuning_idx, const int* tf_skip, int64_t tf_skip_total, float* ext_pitch,
+                       float* ext_mag, int* ext_npk, void* wait_event, void* ws, size_t ws_bytes, hipStream_t st) {
   if (n <= 0) return 0;
+  const bool ext = ext_pitch && ext_mag && ext_npk;
+  if ((tf_skip && !ext) || tf_skip_total < 0) {
+    set_error("chroma: tf_skip needs the caller's peak lists (ext_pitch / ext_mag / ext_npk)");
+    return -2;
+  }
   if (ws_bytes < chroma_ws_bytes(n, total_len)) {
     set_error("chroma: workspace too small");
     return -3;
@@ -706,10 +677,16 @@ int launch_chroma_mean(Context& ctx, const float* sig, const int64_t* chunk_off,
   w.peak_pitch = reinterpret_cast<float*>(take(sizeof(float) * (size_t)tfr * kPeakSlots));
   w.peak_mag = reinterpret_cast<float*>(take(sizeof(float) * (size_t)tfr * kPeakSlots));
   w.partial = reinterpret_cast<double*>(take(sizeof(double) * (size_t)(tfr / CQ_FR + n + 1) * 12));
+  int64_t* tp_base = reinterpret_cast<int64_t*>(take(sizeof(int64_t) * (n + 1)));
+  if (ext) {  // the caller's lists (zeroed counts): the window stage appends to them too
+    w.peak_pitch = ext_pitch;
+    w.peak_mag = ext_mag;
+    w.chunk_npk = ext_npk;
+  }
 
   hipLaunchKernelGGL(chroma_plan_kernel, dim3(1), dim3(256), 0, st, chunk_len, n, w.oct_off, w.oct_len, w.n_frames,
-                     w.n_tframes, w.tf_base, w.oct_base);
-  NC_HIP(hipMemsetAsync(w.chunk_npk, 0, sizeof(int) * n, st));
+                     w.n_tframes, w.tf_base, w.oct_base, tf_skip, tp_base);
+  if (!ext) NC_HIP(hipMemsetAsync(w.chunk_npk, 0, sizeof(int) * n, st));
   // grids are sized by the longest chunk; blocks past a chunk's own length exit.  (Forking
   // the decimation onto a second stream, concurrent with the tuning estimate, measured no
   // gain: the chip is already full with the window chain on the caller's other stream.)
@@ -728,8 +705,10 @@ int launch_chroma_mean(Context& ctx, const float* sig, const int64_t* chunk_off,
   pa.chunk_len = chunk_len;
   pa.n_tframes = w.n_tframes;
   pa.tf_base = w.tf_base;
+  pa.tp_base = tp_base;
+  pa.tf_skip = tf_skip;
   pa.n_chunks = n;
-  pa.total_tframes = tfr;  // upper bound; frames past tf_base[n] are skipped
+  pa.total_tframes = tfr - tf_skip_total;  // upper bound of tp_base[n]; frames past it are idle
   pa.tw = ctx.t.tw;
   pa.hann2048 = ctx.t.hann2048;
   pa.peak_pitch = w.peak_pitch;
@@ -737,13 +716,15 @@ int launch_chroma_mean(Context& ctx, const float* sig, const int64_t* chunk_off,
   pa.chunk_npk = w.chunk_npk;
   {
     const size_t lds = (((TpTw::size + 1) & ~1) + (size_t)TP_WAVES * LdsSize<1024>::value) * sizeof(float2);
-    const int64_t groups = (tfr + TP_WAVES - 1) / TP_WAVES;
+    const int64_t groups = (pa.total_tframes + TP_WAVES - 1) / TP_WAVES;
     const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(groups, ctx.num_cu));
     {
       KTimer kt_(ctx, "tuning_peaks", st);
       hipLaunchKernelGGL(tuning_peaks_kernel, dim3(grid), dim3(TP_WAVES * 64), lds, st, pa);
     }
   }
+  // the window stage's share of the peaks (tf_skip) must have landed before the select
+  if (wait_event) NC_HIP(hipStreamWaitEvent(st, static_cast<hipEvent_t>(wait_event), 0));
   hipLaunchKernelGGL((tuning_select_kernel<256>), dim3(n), dim3(256), 0, st, w.peak_pitch, w.peak_mag,
                      w.chunk_npk, w.tf_base, w.tuning_idx, out_tuning);
   CqtArgs ca;

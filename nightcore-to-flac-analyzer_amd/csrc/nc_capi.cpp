@@ -17,7 +17,9 @@ struct BeatArgs;
 size_t window_stage_ws_bytes(const Context& ctx, int n_win, int T);
 int launch_window_stage(Context& ctx, const float* sig, const int64_t* win_off, const uint8_t* active,
                         int n_win, int win_len, int hop, float* onset_out, double* tg_out,
-                        double* energy_out, void* ws, size_t ws_bytes, hipStream_t st);
+                        double* energy_out, const int* win_chunk, const int64_t* chunk_tf_base, int tp_frames,
+                        float* peak_pitch, float* peak_mag, int* chunk_npk, void* stft_done,
+                        void* ws, size_t ws_bytes, hipStream_t st);
 int launch_tempo_beats_c(Context& ctx, const float* onset, const int64_t* off, const int* len, int n_seq,
                          int max_len, const double* tg, int acw, const double* start_bpm,
                          const int* prior_idx, const uint8_t* active, int hop, int trim, double* bpm_out,
@@ -36,7 +38,8 @@ int launch_trim(Context& ctx, const float* sig, const int64_t* file_off, const i
 size_t chroma_ws_bytes(int n, int64_t total_len);
 int launch_chroma_mean(Context& ctx, const float* sig, const int64_t* chunk_off, const int64_t* chunk_len, int n,
                        int64_t total_len, int64_t max_chunk_len, float* out_chroma, float* out_tuning,
-                       int* out_tuning_idx, void* ws, size_t ws_bytes, hipStream_t st);
+                       int* out_tuning_idx, const int* tf_skip, int64_t tf_skip_total, float* ext_pitch,
+                       float* ext_mag, int* ext_npk, void* wait_event, void* ws, size_t ws_bytes, hipStream_t st);
 int launch_chroma_lag(const float* chroma, const int* src_idx, const int* nc_idx, int n_pairs, int* lag_out,
                       hipStream_t st);
 
@@ -191,7 +194,20 @@ int nc_window_stage(nc_ctx* ctx, const float* sig, const int64_t* win_off, const
   CHECK_CTX(ctx);
   SET_DEVICE(ctx);
   return nc::launch_window_stage(ctx->c, sig, win_off, active, n_win, win_len, hop, onset_out, tg_out,
-                                 energy_out, ws, ws_bytes, (hipStream_t)stream);
+                                 energy_out, nullptr, nullptr, 0, nullptr, nullptr, nullptr, nullptr, ws, ws_bytes,
+                                 (hipStream_t)stream);
+}
+
+int nc_window_stage_tuning(nc_ctx* ctx, const float* sig, const int64_t* win_off, const uint8_t* active, int n_win,
+                           int win_len, int hop, float* onset_out, double* tg_out, double* energy_out,
+                           const int* win_chunk, const int64_t* chunk_tf_base, int tp_frames, float* peak_pitch,
+                           float* peak_mag, int* chunk_npk, void* stft_done_event, void* ws, size_t ws_bytes,
+                           void* stream) {
+  CHECK_CTX(ctx);
+  SET_DEVICE(ctx);
+  return nc::launch_window_stage(ctx->c, sig, win_off, active, n_win, win_len, hop, onset_out, tg_out,
+                                 energy_out, win_chunk, chunk_tf_base, tp_frames, peak_pitch, peak_mag, chunk_npk,
+                                 stft_done_event, ws, ws_bytes, (hipStream_t)stream);
 }
 
 size_t nc_tempo_beats_workspace_bytes(int64_t total_frames) {
@@ -238,7 +254,20 @@ int nc_chroma_mean(nc_ctx* ctx, const float* sig, const int64_t* chunk_off, cons
   CHECK_CTX(ctx);
   SET_DEVICE(ctx);
   return nc::launch_chroma_mean(ctx->c, sig, chunk_off, chunk_len, n_chunks, total_len, max_chunk_len, out_chroma,
-                                out_tuning, out_tuning_idx, ws, ws_bytes, (hipStream_t)stream);
+                                out_tuning, out_tuning_idx, nullptr, 0, nullptr, nullptr, nullptr, nullptr, ws,
+                                ws_bytes, (hipStream_t)stream);
+}
+
+int nc_chroma_mean_shared(nc_ctx* ctx, const float* sig, const int64_t* chunk_off, const int64_t* chunk_len,
+                          int n_chunks, int64_t total_len, int64_t max_chunk_len, float* out_chroma,
+                          float* out_tuning, int* out_tuning_idx, const int* tf_skip, int64_t tf_skip_total,
+                          float* peak_pitch, float* peak_mag, int* chunk_npk, void* wait_event, void* ws,
+                          size_t ws_bytes, void* stream) {
+  CHECK_CTX(ctx);
+  SET_DEVICE(ctx);
+  return nc::launch_chroma_mean(ctx->c, sig, chunk_off, chunk_len, n_chunks, total_len, max_chunk_len, out_chroma,
+                                out_tuning, out_tuning_idx, tf_skip, tf_skip_total, peak_pitch, peak_mag, chunk_npk,
+                                wait_event, ws, ws_bytes, (hipStream_t)stream);
 }
 
 int nc_chroma_lag(nc_ctx* ctx, const float* chroma, const int* src_idx, const int* nc_idx, int n_pairs, int* lag_out,

@@ -18,6 +18,7 @@
 
 #include "nc_block.h"
 #include "nc_engine.h"
+#include "nc_piptrack.h"
 #include "stft_args.h"
 
 namespace nc {
@@ -133,6 +134,21 @@ __global__ __launch_bounds__(SM_THREADS) void stft_mel_kernel(StftMelArgs a) {
       pw[k] = fmaf(X.x, X.x, X.y * X.y);
       pw[1024 - k] = fmaf(XN.x, XN.x, XN.y * XN.y);
     });
+    // a leading frame of a window that starts a 20 s chunk is also that chunk's tuning frame
+    // t (same samples, padding and FFT): estimate_tuning's piptrack runs here, on the same
+    // |X| values tuning_peaks_kernel would compute (nc_piptrack.h)
+    if (a.win_chunk && t < a.tp_frames) {
+      const int c = uniform32(a.win_chunk[s]);
+      if (c >= 0) {
+        float pm = pw[1024];
+#pragma unroll
+        for (int j = 0; j < 16; ++j) pm = fmaxf(pm, pw[lane + 64 * j]);
+        const float mx = __fsqrt_rn(wave_max(pm));
+        const int64_t base = uniform64(a.chunk_tf_base[c]) * kPeakSlots;
+        piptrack_append([&](int k) { return __fsqrt_rn(pw[k]); }, mx, lane, &a.chunk_npk[c], a.peak_pitch + base,
+                        a.peak_mag + base);
+      }
+    }
     // Slaney mel: lane l owns bands l and 127 - l, read as float4 steps from a 16-byte aligned
     // first bin with zero-padded weights (fmaf chain in bin order, as the CSR form)
     float acc0 = 0.0f, acc1 = 0.0f;

@@ -32,6 +32,15 @@ struct StftMelArgs {
   const int* mel_lo4;
   const int* mel_nj4;
   int mel_j0, mel_j1;
+  // shared tuning frames (nullable win_chunk): frames t < tp_frames of sequence s with
+  // win_chunk[s] = c >= 0 are also tuning frames t of chunk c; their piptrack peaks are
+  // appended to chunk c's list (peak_*[chunk_tf_base[c] * kPeakSlots ..], count chunk_npk[c])
+  const int* win_chunk;
+  const int64_t* chunk_tf_base;
+  int tp_frames;
+  float* peak_pitch;
+  float* peak_mag;
+  int* chunk_npk;
 };
 
 int launch_stft_mel(Context& ctx, const StftMelArgs& args, hipStream_t st);

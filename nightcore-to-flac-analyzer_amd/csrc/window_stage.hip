@@ -200,7 +200,9 @@ size_t window_stage_ws_bytes(const Context&, int n_win, int T) {
 
 int launch_window_stage(Context& ctx, const float* sig, const int64_t* win_off, const uint8_t* active,
                         int n_win, int win_len, int hop, float* onset_out, double* tg_out,
-                        double* energy_out, void* ws, size_t ws_bytes, hipStream_t st) {
+                        double* energy_out, const int* win_chunk, const int64_t* chunk_tf_base, int tp_frames,
+                        float* peak_pitch, float* peak_mag, int* chunk_npk, void* stft_done,
+                        void* ws, size_t ws_bytes, hipStream_t st) {
   if (n_win <= 0) return 0;
   if (hop != 512) {
     set_error("window stage: only hop_length=512 is supported (tempo.py:24)");
@@ -234,8 +236,24 @@ int launch_window_stage(Context& ctx, const float* sig, const int64_t* win_off, 
   s.sdb = sdb;
   s.frame_max = fmax_;
   s.frame_energy = fen;
+  if (win_chunk) {
+    // a shared frame must see no right-edge padding of the window: t hop + n_fft / 2 <= win_len
+    if (!chunk_tf_base || !peak_pitch || !peak_mag || !chunk_npk || tp_frames < 0 || tp_frames > T ||
+        (tp_frames > 0 && (int64_t)(tp_frames - 1) * hop + kNFFT / 2 > win_len)) {
+      set_error("window stage: shared tuning frames need chunk bases, peak lists and frames inside the window");
+      return -2;
+    }
+    s.win_chunk = win_chunk;
+    s.chunk_tf_base = chunk_tf_base;
+    s.tp_frames = tp_frames;
+    s.peak_pitch = peak_pitch;
+    s.peak_mag = peak_mag;
+    s.chunk_npk = chunk_npk;
+  }
   int rc = launch_stft_mel(ctx, s, st);
   if (rc) return rc;
+  // the shared tuning peaks are complete here: a chroma chain on another stream may go on
+  if (stft_done) NC_HIP(hipEventRecord(static_cast<hipEvent_t>(stft_done), st));
 
   WinTgArgs a;
   a.sdb = sdb;

@@ -74,6 +74,9 @@ def percentile_params(n_boot: int, ci: float) -> Tuple[float, float, float, floa
     return tuple(out)
 
 
+PEAK_SLOTS = 192   # piptrack peak slots per tuning frame (csrc/nc_piptrack.h kPeakSlots)
+
+
 class _Upload:
     """Packs many small host arrays into one H2D copy; returns device views."""
 
@@ -242,6 +245,9 @@ class Engine:
         # behind a bootstrap that waits for this group's (longer) chroma chain
         self.tail_stream = torch.cuda.current_stream(self.dev) if os.environ.get("NC_SERIAL_STREAMS") == "1" \
             else torch.cuda.Stream(self.dev)
+        # leading tuning frames of a chunk computed inside the window STFT (nc_window_stage_tuning);
+        # NC_SHARE_TUNING=0 runs every tuning frame in the chroma chain instead (same results)
+        self.share_tuning = os.environ.get("NC_SHARE_TUNING", "1") != "0"
 
     def set_serial(self, on: bool) -> None:
         """Queue the chroma chain and the consensus tail on the launch stream too (on=True):
@@ -632,6 +638,30 @@ class Engine:
         n_chunks = len(chunk_off)
         n_cp = n_chunks // 2
 
+        # shared tuning frames: a standard 20 s chunk that starts where a window of the same file
+        # starts has its first tp tuning frames in that window's STFT (nc_window_stage_tuning)
+        tp = (win_n - 1024) // HOP_LENGTH + 1 if win_n >= 1024 else 0
+        share = tp > 0 and n_win > 0 and n_chunks > 0 and self.share_tuning
+        win_chunk = np.full(max(1, n_win), -1, np.int32)
+        tf_skip = np.zeros(max(1, n_chunks), np.int32)
+        if share:
+            cn = int(CHUNK_SEC * SR)
+            for b, (c0, c1) in enumerate(pair_chunks):
+                for f, side in ((2 * b + 1, 0), (2 * b, 1)):
+                    st_f = starts[f]
+                    for i in range(c1 - c0):
+                        c = 2 * (c0 + i) + side
+                        if chunk_len[c] != cn or (i * cn) % hop_n:
+                            continue
+                        k = i * cn // hop_n
+                        if k < len(st_f) and st_f[k] == i * cn:
+                            win_chunk[w0[f] + k] = c
+                            tf_skip[c] = tp
+            share = bool(tf_skip.any())
+        chunk_tf_base = np.zeros(max(1, n_chunks) + 1, np.int64)
+        if n_chunks:
+            chunk_tf_base[1:n_chunks + 1] = np.cumsum(1 + np.asarray(chunk_len, np.int64) // HOP_LENGTH)
+
         # bootstrap jobs (tempo: A = nc valid, B = src valid; pitch: A = nc_hz, B = src_hz; shift)
         n_pitch_jobs = len(pair_chunks)
         nj = B + n_pitch_jobs
@@ -688,6 +718,9 @@ class Engine:
         up.add("s_seed", seed_state(0) * max(1, n_pitch_jobs), np.uint64)
         up.add("s_wsoff", s_wsoff or [0], np.int64)
         up.add("s_cap", p_n or [1], np.int32)
+        up.add("win_chunk", win_chunk, np.int32)
+        up.add("tf_skip", tf_skip, np.int32)
+        up.add("tf_base", chunk_tf_base, np.int64)
         d = up.commit(dev)
 
         # one zero-filled output arena, copied back in one D2H
@@ -696,32 +729,30 @@ class Engine:
                             ("clag", n_cp, np.int32), ("vals", TV + PV, np.float64), ("energy", n_win, np.float64),
                             ("active", n_win, np.uint8), ("bpm", n_win, np.float64), ("lag", n_win, np.int32),
                             ("nbeats", n_win, np.int32), ("margin", n_win, np.float64), ("prior", B, np.float64),
-                            ("bout", 3 * nj, np.float64), ("sout", 3 * max(1, n_pitch_jobs), np.float64)):
+                            ("bout", 3 * nj, np.float64), ("sout", 3 * max(1, n_pitch_jobs), np.float64),
+                            ("npk", n_chunks, np.int32)):
             ar.add(name, n, dt)
         o = ar.commit(dev)
         tvals, pvals = o["vals"][:TV], o["vals"][TV:]
 
-        # ---------------------------------------------------------------- 3. chroma (stream 2)
-        # runs concurrently with the window/tempo chain; joined before the bootstraps
+        # ---------------------------------------------------------------- 3. plan ready -> stream 2
+        # the chroma chain runs on stream 2, concurrently with the window/tempo chain; the
+        # consensus tail joins them.  With shared tuning frames the window stage appends the
+        # leading frames' piptrack peaks to this group's peak lists (its own, zeroed in the
+        # arena) and the chroma chain waits for them before the tuning select.
         s1, s2 = torch.cuda.current_stream(dev), self.chroma_stream
+        peaks = None
+        ev_stft = None
+        if share:
+            n_slots = int(chunk_tf_base[n_chunks]) * PEAK_SLOTS
+            peaks = (torch.empty(n_slots, dtype=torch.float32, device=dev),
+                     torch.empty(n_slots, dtype=torch.float32, device=dev))
+            ev_stft = torch.cuda.Event()
+            ev_stft.record(s1)          # creates the event; the window stage re-records it after the STFT
         ev_plan = torch.cuda.Event()
         ev_plan.record(s1)
         s2.wait_event(ev_plan)
         st2 = s2.cuda_stream
-        if n_chunks:
-            tot_len = int(np.sum(chunk_len))
-            wsb = self.ctx.lib.nc_chroma_workspace_bytes(self.ctx.h, n_chunks, tot_len)
-            ws_c = self.workspace("chroma", wsb)
-            ws_c.record_stream(s2)  # used on stream 2: not reusable until that work is done
-            self.call("nc_chroma_mean", signals.buf.data_ptr(), d["chunk_off"].data_ptr(), d["chunk_len"].data_ptr(),
-                      n_chunks, tot_len, int(max(chunk_len)), o["chroma"].data_ptr(), o["tuning"].data_ptr(), None,
-                      ws_c.data_ptr(), ws_c.numel(), st2)
-            self.call("nc_chroma_lag", o["chroma"].data_ptr(), d["lag_src"].data_ptr(), d["lag_nc"].data_ptr(), n_cp,
-                      o["clag"].data_ptr(), st2)
-            self.call("nc_pitch_hz", o["clag"].data_ptr(), n_cp, pvals[0:n_cp].data_ptr(),
-                      pvals[n_cp:2 * n_cp].data_ptr(), pvals[2 * n_cp:3 * n_cp].data_ptr(), st2)
-        ev_chroma = torch.cuda.Event()
-        ev_chroma.record(s2)
 
         # ---------------------------------------------------------------- 4. per-window stage
         bpm, lag, nbeats, margin, prior = o["bpm"], o["lag"], o["nbeats"], o["margin"], o["prior"]
@@ -731,8 +762,41 @@ class Engine:
             tg = torch.empty(n_win * acw, dtype=torch.float64, device=dev)
             wsb = self.ctx.lib.nc_window_stage_workspace_bytes(self.ctx.h, n_win, win_n, HOP_LENGTH)
             ws = self.workspace("win", wsb)
-            self.call("nc_window_stage", signals.buf.data_ptr(), d["win_off"].data_ptr(), None, n_win, win_n,
-                      HOP_LENGTH, onset.data_ptr(), tg.data_ptr(), energy.data_ptr(), ws.data_ptr(), ws.numel(), st)
+            if share:
+                self.call("nc_window_stage_tuning", signals.buf.data_ptr(), d["win_off"].data_ptr(), None, n_win,
+                          win_n, HOP_LENGTH, onset.data_ptr(), tg.data_ptr(), energy.data_ptr(),
+                          d["win_chunk"].data_ptr(), d["tf_base"].data_ptr(), tp, peaks[0].data_ptr(),
+                          peaks[1].data_ptr(), o["npk"].data_ptr(), ev_stft.cuda_event, ws.data_ptr(), ws.numel(), st)
+            else:
+                self.call("nc_window_stage", signals.buf.data_ptr(), d["win_off"].data_ptr(), None, n_win, win_n,
+                          HOP_LENGTH, onset.data_ptr(), tg.data_ptr(), energy.data_ptr(), ws.data_ptr(), ws.numel(),
+                          st)
+
+        # ---------------------------------------------------------------- 3b. chroma (stream 2)
+        if n_chunks:
+            tot_len = int(np.sum(chunk_len))
+            wsb = self.ctx.lib.nc_chroma_workspace_bytes(self.ctx.h, n_chunks, tot_len)
+            ws_c = self.workspace("chroma", wsb)
+            ws_c.record_stream(s2)  # used on stream 2: not reusable until that work is done
+            if share:
+                self.call("nc_chroma_mean_shared", signals.buf.data_ptr(), d["chunk_off"].data_ptr(),
+                          d["chunk_len"].data_ptr(), n_chunks, tot_len, int(max(chunk_len)), o["chroma"].data_ptr(),
+                          o["tuning"].data_ptr(), None, d["tf_skip"].data_ptr(), int(tf_skip.sum()),
+                          peaks[0].data_ptr(), peaks[1].data_ptr(), o["npk"].data_ptr(), ev_stft.cuda_event,
+                          ws_c.data_ptr(), ws_c.numel(), st2)
+            else:
+                self.call("nc_chroma_mean", signals.buf.data_ptr(), d["chunk_off"].data_ptr(),
+                          d["chunk_len"].data_ptr(), n_chunks, tot_len, int(max(chunk_len)), o["chroma"].data_ptr(),
+                          o["tuning"].data_ptr(), None, ws_c.data_ptr(), ws_c.numel(), st2)
+            self.call("nc_chroma_lag", o["chroma"].data_ptr(), d["lag_src"].data_ptr(), d["lag_nc"].data_ptr(), n_cp,
+                      o["clag"].data_ptr(), st2)
+            self.call("nc_pitch_hz", o["clag"].data_ptr(), n_cp, pvals[0:n_cp].data_ptr(),
+                      pvals[n_cp:2 * n_cp].data_ptr(), pvals[2 * n_cp:3 * n_cp].data_ptr(), st2)
+        ev_chroma = torch.cuda.Event()
+        ev_chroma.record(s2)
+
+        # ---------------------------------------------------------------- 4b. tempo (window stream)
+        if n_win:
             self.call("nc_energy_gate", energy.data_ptr(), d["w0"].data_ptr(), d["w1"].data_ptr(), nF,
                       float(p.energy_gate_db), active.data_ptr(), st)
             if n_src_w:
@@ -805,7 +869,7 @@ class Engine:
                         host["ibi_" + k] = h.numpy()
             ev = torch.cuda.Event()
             ev.record(s3)
-        return dict(p=p, host=host, pinned=pinned, event=ev, keep=(d, o, ar, ibi), has_ibi=ibi is not None,
+        return dict(p=p, host=host, pinned=pinned, event=ev, keep=(d, o, ar, ibi, peaks), has_ibi=ibi is not None,
                     align=align,
                     starts=starts, w0=w0, w1=w1, f_len=f_len,
                     strip_len=strip_len, lead=lead, trail=trail, intro=intro, win_n=win_n,
