@@ -21,9 +21,10 @@ The host never touches audio samples after the upload; there is no CPU path.
 """
 from __future__ import annotations
 
+import gc
 import math
-import threading
 import os
+import threading
 import time
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional, Sequence, Tuple
@@ -199,18 +200,19 @@ def _group_bounds(B: int, group_pairs, ) -> List[Tuple[int, int]]:
             left -= n
             i += 1
     elif group_pairs is None:
-        # default: an 8-pair group to start the device early (its host plan is the only one
-        # exposed), 24-pair groups (fuller launches of the latency-bound per-window kernels),
-        # an 8-pair group at the end to keep the exposed host assembly and the chroma tail
-        # short (tools/group_sweep.py: 8,24,24,8 is the fastest schedule for 64 pairs)
+        # default: a 6-pair group to start the device early (its host plan is the only one
+        # exposed), 26-pair groups (fuller launches of the latency-bound per-window kernels),
+        # a 6-pair group at the end to keep the exposed host assembly and the chroma tail
+        # short (tools/group_sweep.py, tools/sched_probe.py: 6,26,26,6 is the fastest
+        # schedule measured for 64 pairs, 2 % ahead of 8,24,24,8)
         if B <= 16:
             sizes = [B] if B else []
         else:
-            sizes, left = [8], B - 8
+            sizes, left = [6], B - 6
             while left > 32:
-                sizes.append(24)
-                left -= 24
-            sizes += [left - 8, 8] if left > 16 else [left]
+                sizes.append(26)
+                left -= 26
+            sizes += [left - 6, 6] if left > 12 else [left]
     else:
         gp = max(1, int(group_pairs))
         sizes = [gp] * (B // gp) + ([B % gp] if B % gp else [])
@@ -292,6 +294,8 @@ class Engine:
         out = {k: (sum(a.elapsed_time(b) for a, b in v), len(v)) for k, v in (self.timers or {}).items()}
         self.timers = None
         return out
+
+    GROUPS_IN_FLIGHT = 3    # pair groups queued ahead of the host's oldest wait (analyze)
 
     KERNEL_TAGS = ("stft_mel", "window_tg", "tuning_peaks", "decimate", "cqt_chroma", "trim_blocks", "tempo_beat",
                    "tg_slide", "spectral_frames", "spectral_bins")
@@ -510,9 +514,24 @@ class Engine:
 
         After one trim pass over all files (the only blocking read-back), pairs
         are processed in groups of ``group_pairs``: the whole device pipeline of
-        every group is queued (plans uploaded through pinned memory, results copied
-        back asynchronously) before the host assembles the results of group 0, so
-        host assembly overlaps the device work of the later groups."""
+        up to GROUPS_IN_FLIGHT groups is queued (plans uploaded through pinned memory,
+        results copied back asynchronously) before the host assembles the results of
+        the oldest, so host assembly overlaps the device work of the later groups.
+
+        Python's cyclic garbage collector is paused for the call: a generation-2 pass
+        over the host's live objects costs ~10 ms, as long as several groups of device
+        work, and lands at a random point of the pipeline.  The call creates no reference
+        cycles (everything it allocates is freed by reference counting), and the
+        collector's previous state is restored on return."""
+        gc_was_enabled = gc.isenabled()
+        gc.disable()
+        try:
+            return self._analyze(pairs, params, signals, group_pairs)
+        finally:
+            if gc_was_enabled:
+                gc.enable()
+
+    def _analyze(self, pairs, params, signals, group_pairs) -> List[PairOutcome]:
         p = params or Params()
         if signals is None:
             flat = []
@@ -529,11 +548,12 @@ class Engine:
                                        signals.off[0::2] + start[0::2], end[0::2] - start[0::2])
         if hs is not None:
             hs["trim"] = hs.get("trim", 0.0) + time.perf_counter() - t0
-        # every group is queued before the host waits for any: the window stream never idles
-        # behind the host assembly of an earlier group, and the assembly of group g overlaps
-        # the device work of the groups after it
+        # up to GROUPS_IN_FLIGHT groups are queued before the host waits for the oldest: the
+        # window stream never idles behind the host assembly of an earlier group, the assembly
+        # of group g overlaps the device work of the groups after it, and the depth of the
+        # device queues (and the memory held by queued groups) stays bounded for long batches
         outs: List[PairOutcome] = []
-        pending = []
+        pending: List[dict] = []
         for g0, g1 in _group_bounds(B, group_pairs):
             sl = slice(2 * g0, 2 * g1)
             sub = DeviceSignals(signals.buf, signals.off[sl], signals.length[sl])
@@ -542,6 +562,8 @@ class Engine:
                                               align[g0:g1] if align is not None else None))
             if hs is not None:
                 hs["launch"] = hs.get("launch", 0.0) + time.perf_counter() - t0
+            if len(pending) > self.GROUPS_IN_FLIGHT:
+                outs += self._finish_group(pending.pop(0))
         for g in pending:
             outs += self._finish_group(g)
         return outs
@@ -557,7 +579,9 @@ class Engine:
         up.add("len", signals.length, np.int64)
         d0 = up.commit(dev)
         tot_frames = int(np.sum(1 + signals.length // 512))
-        wsb = self.ctx.lib.nc_trim_workspace_bytes(signals.length.ctypes.data_as(_native.P), nF)
+        lens = np.ascontiguousarray(signals.length, np.int64)
+        # a plain address (ndarray.ctypes.data_as would build a ctypes.cast reference cycle)
+        wsb = self.ctx.lib.nc_trim_workspace_bytes(lens.ctypes.data, nF)
         ws = self.workspace("trim", wsb)
         se = torch.empty(2 * nF, dtype=torch.int64, device=dev)
         self.call("nc_trim_bounds", signals.buf.data_ptr(), d0["off"].data_ptr(), d0["len"].data_ptr(), nF,
@@ -744,9 +768,15 @@ class Engine:
         peaks = None
         ev_stft = None
         if share:
+            # peak lists from a ring of GROUPS_IN_FLIGHT + 1 workspaces: a slot comes back only
+            # after the host has waited for the group that used it (analyze's in-flight bound),
+            # so no large per-group allocation reaches the caching allocator
             n_slots = int(chunk_tf_base[n_chunks]) * PEAK_SLOTS
-            peaks = (torch.empty(n_slots, dtype=torch.float32, device=dev),
-                     torch.empty(n_slots, dtype=torch.float32, device=dev))
+            self._peak_ring = (getattr(self, "_peak_ring", -1) + 1) % (self.GROUPS_IN_FLIGHT + 1)
+            pk = self.workspace(f"peaks{self._peak_ring}", 8 * n_slots)
+            for s_ in (s1, self.chroma_stream):
+                pk.record_stream(s_)
+            peaks = (pk[:4 * n_slots].view(torch.float32), pk[4 * n_slots:8 * n_slots].view(torch.float32))
             ev_stft = torch.cuda.Event()
             ev_stft.record(s1)          # creates the event; the window stage re-records it after the STFT
         ev_plan = torch.cuda.Event()

@@ -25,8 +25,8 @@ def trim_bounds(eng: Engine, audios: Sequence[np.ndarray], top_db: float) -> Lis
     d = up.commit(eng.dev)
     n = sig.n_files
     tot = int(np.sum(1 + sig.length // 512))
-    ws = eng.workspace("trim", eng.ctx.lib.nc_trim_workspace_bytes(sig.length.ctypes.data_as(
-        __import__("ctypes").c_void_p), n))
+    lens = np.ascontiguousarray(sig.length, np.int64)
+    ws = eng.workspace("trim", eng.ctx.lib.nc_trim_workspace_bytes(lens.ctypes.data, n))
     se = torch.empty(2 * n, dtype=torch.int64, device=eng.dev)
     eng.call("nc_trim_bounds", sig.buf.data_ptr(), d["off"].data_ptr(), d["len"].data_ptr(), n, tot,
              float(top_db), se[:n].data_ptr(), se[n:].data_ptr(), ws.data_ptr(), ws.numel(), eng.stream())

@@ -54,3 +54,21 @@ def test_shared_tuning_with_trim_and_offsets(eng):
         b = _run(eng, pairs, True, **kw)[0]
         assert np.array_equal(a.detail["tuning"], b.detail["tuning"])
         assert str(a.result) == str(b.result)
+
+
+def test_analyze_leaves_no_reference_cycles(eng):
+    """analyze() pauses the cyclic collector; everything it allocates must be freed by
+    reference counting, or garbage would pile up between collections."""
+    import gc
+    pairs = [synth.make_pair(45.0, 1001), synth.make_pair(12.0, 1007)]
+    eng.analyze(pairs, E.Params(compute_ibi=True))
+    gc.collect()
+    gc.disable()
+    try:
+        outs = eng.analyze(pairs, E.Params(compute_ibi=True))
+        _ = [str(o.result) for o in outs if o.result is not None] + [o.logs for o in outs]
+        del outs, _
+        found = gc.collect()
+    finally:
+        gc.enable()
+    assert found == 0, f"{found} objects in reference cycles"
