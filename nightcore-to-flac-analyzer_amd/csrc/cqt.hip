@@ -84,7 +84,7 @@ __global__ __launch_bounds__(256) void chroma_plan_kernel(const int64_t* chunk_l
 }
 
 // ------------------------------------------------------------------------------ 1. decimation
-// y_{i+1} = sqrt(2) * halfband(y_i)[::2] per chunk and level (nc_decim.h)
+// y_{i+1} = sqrt(2) * halfband(y_i)[::2] per chunk and level (nc_decim.h, f32 accumulation)
 __global__ __launch_bounds__(256) void decimate_kernel(const float* sig, const int64_t* chunk_off,
                                                        const int64_t* oct_off, const int64_t* oct_len,
                                                        float* ws_oct, int level, const double* __restrict__ taps) {
@@ -93,7 +93,7 @@ __global__ __launch_bounds__(256) void decimate_kernel(const float* sig, const i
   const int64_t m0 = (int64_t)blockIdx.x * DEC_OUT;
   if (m0 >= Lout) return;
   const float* in = level == 0 ? sig + chunk_off[c] : ws_oct + oct_off[c * 7 + level];
-  halfband_tile<true>(in, Lin, ws_oct + oct_off[c * 7 + level + 1], Lout, m0, taps);
+  halfband_tile<true, float>(in, Lin, ws_oct + oct_off[c * 7 + level + 1], Lout, m0, taps);
 }
 
 // ------------------------------------------------------------------------------ 2. tuning peaks
