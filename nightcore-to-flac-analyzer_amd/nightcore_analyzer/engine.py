@@ -540,12 +540,25 @@ class Engine:
             signals = self.upload_signals(flat)
         B = signals.n_files // 2
         hs = self.host_stats
+        groups = _group_bounds(B, group_pairs)
         t0 = time.perf_counter()
-        start, end = self._trim_all(signals, p)
         align = None
-        if p.auto_align and p.src_trim_sec == 0.0:      # pipeline.py:111-125 (manual trim has priority)
-            align = self.align_offsets(signals.buf, signals.off[1::2] + start[1::2], end[1::2] - start[1::2],
-                                       signals.off[0::2] + start[0::2], end[0::2] - start[0::2])
+        rest = None
+        if p.silence_strip_db is not None and len(groups) > 1 and not (p.auto_align and p.src_trim_sec == 0.0):
+            # io.strip_silence bounds in two launches: the first group's files alone (the only
+            # blocking read-back before the device has work), the others on the tail stream,
+            # read back while the first group runs
+            nF, f1 = signals.n_files, 2 * groups[0][1]
+            first = self._trim_launch(signals, 0, f1, p, torch.cuda.current_stream(self.dev), "trim0")
+            rest = self._trim_launch(signals, f1, nF, p, self.tail_stream, "trim1")
+            start = np.zeros(nF, np.int64)
+            end = np.zeros(nF, np.int64)
+            start[:f1], end[:f1] = self._trim_wait(first)
+        else:
+            start, end = self._trim_all(signals, p)
+            if p.auto_align and p.src_trim_sec == 0.0:      # pipeline.py:111-125 (manual trim has priority)
+                align = self.align_offsets(signals.buf, signals.off[1::2] + start[1::2], end[1::2] - start[1::2],
+                                           signals.off[0::2] + start[0::2], end[0::2] - start[0::2])
         if hs is not None:
             hs["trim"] = hs.get("trim", 0.0) + time.perf_counter() - t0
         # up to GROUPS_IN_FLIGHT groups are queued before the host waits for the oldest: the
@@ -554,7 +567,10 @@ class Engine:
         # device queues (and the memory held by queued groups) stays bounded for long batches
         outs: List[PairOutcome] = []
         pending: List[dict] = []
-        for g0, g1 in _group_bounds(B, group_pairs):
+        for gi, (g0, g1) in enumerate(groups):
+            if gi == 1 and rest is not None:
+                f1 = 2 * groups[0][1]
+                start[f1:], end[f1:] = self._trim_wait(rest)
             sl = slice(2 * g0, 2 * g1)
             sub = DeviceSignals(signals.buf, signals.off[sl], signals.length[sl])
             t0 = time.perf_counter()
@@ -567,6 +583,44 @@ class Engine:
         for g in pending:
             outs += self._finish_group(g)
         return outs
+
+    def _trim_launch(self, signals: DeviceSignals, f0: int, f1: int, p: Params, stream, ws_name: str):
+        """Queue nc_trim_bounds for files [f0, f1) on `stream` and the async copy of the bounds
+        into pinned memory; returns (event, pinned bounds, keep-alive)."""
+        dev = self.dev
+        off, length = signals.off[f0:f1], signals.length[f0:f1]
+        n = f1 - f0
+        lens = np.ascontiguousarray(length, np.int64)
+        launch = torch.cuda.current_stream(dev)
+        if stream != launch:          # the signals may still be in flight on the launch stream
+            ev_in = torch.cuda.Event()
+            ev_in.record(launch)
+            stream.wait_event(ev_in)
+        with torch.cuda.stream(stream):
+            up = _Upload()
+            up.add("off", off, np.int64)
+            up.add("len", lens, np.int64)
+            d0 = up.commit(dev)
+            wsb = self.ctx.lib.nc_trim_workspace_bytes(lens.ctypes.data, n)
+            ws = self.workspace(ws_name, wsb)
+            ws.record_stream(stream)
+            se = torch.empty(2 * n, dtype=torch.int64, device=dev)
+            self.call("nc_trim_bounds", signals.buf.data_ptr(), d0["off"].data_ptr(), d0["len"].data_ptr(), n,
+                      int(np.sum(1 + lens // 512)), float(p.silence_strip_db), se[:n].data_ptr(),
+                      se[n:].data_ptr(), ws.data_ptr(), ws.numel(), stream.cuda_stream)
+            host = torch.empty(2 * n, dtype=torch.int64, pin_memory=True)
+            host.copy_(se, non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record(stream)
+        return ev, host, (d0, se)
+
+    @staticmethod
+    def _trim_wait(launched) -> Tuple[np.ndarray, np.ndarray]:
+        ev, host, _ = launched
+        ev.synchronize()
+        h = host.numpy()
+        n = len(h) // 2
+        return h[:n].copy(), h[n:].copy()
 
     def _trim_all(self, signals: DeviceSignals, p: Params) -> Tuple[np.ndarray, np.ndarray]:
         """io.strip_silence bounds of every file (sync 1)."""
