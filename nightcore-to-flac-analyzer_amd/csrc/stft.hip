@@ -23,7 +23,13 @@
 
 namespace nc {
 
-constexpr int SM_WAVES = 14;
+#ifndef NC_SM_WAVES
+#define NC_SM_WAVES 14
+#endif
+#ifndef NC_SM_MEL_GLOBAL  // 1: mel lane weights read through L1 instead of staged in LDS
+#define NC_SM_MEL_GLOBAL 0
+#endif
+constexpr int SM_WAVES = NC_SM_WAVES;
 constexpr int SM_THREADS = SM_WAVES * 64;
 using SmTw = StagedTw<1024>;  // per-stage twiddle table in LDS (conflict-free reads)
 
@@ -40,7 +46,7 @@ __device__ __forceinline__ int seq_of_frame(const int64_t* base, int n, int64_t 
 __host__ __device__ __forceinline__ int al4(int n) { return (n + 3) & ~3; }
 
 size_t stft_mel_lds_bytes(int mel_j) {
-  return (size_t)al4(SmTw::size) * sizeof(float2) + (size_t)mel_j * 64 * sizeof(float4) +
+  return (size_t)al4(SmTw::size) * sizeof(float2) + (NC_SM_MEL_GLOBAL ? 0 : (size_t)mel_j * 64 * sizeof(float4)) +
          (size_t)SM_WAVES * LdsSize<1024>::value * sizeof(float2);
 }
 
@@ -49,10 +55,13 @@ __global__ __launch_bounds__(SM_THREADS) void stft_mel_kernel(StftMelArgs a) {
   float2* sh_tw = reinterpret_cast<float2*>(smem);
   float4* sh_w4 = reinterpret_cast<float4*>(sh_tw + al4(SmTw::size));  // [mel_j0 + mel_j1][64]
   const int lane0 = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform (SGPR)
-  float2* fftbuf = reinterpret_cast<float2*>(sh_w4 + (a.mel_j0 + a.mel_j1) * 64) + wave * LdsSize<1024>::value;
+  float2* fftbuf = reinterpret_cast<float2*>(sh_w4 + (NC_SM_MEL_GLOBAL ? 0 : (a.mel_j0 + a.mel_j1) * 64)) +
+                   wave * LdsSize<1024>::value;
 
   fill_staged_tw<1024>(sh_tw, a.tw, threadIdx.x, SM_THREADS);
-  for (int i = threadIdx.x; i < (a.mel_j0 + a.mel_j1) * 64; i += SM_THREADS) sh_w4[i] = a.mel_w4[i];
+  if (!NC_SM_MEL_GLOBAL)
+    for (int i = threadIdx.x; i < (a.mel_j0 + a.mel_j1) * 64; i += SM_THREADS) sh_w4[i] = a.mel_w4[i];
+  const float4* mw4 = NC_SM_MEL_GLOBAL ? a.mel_w4 : sh_w4;
   __syncthreads();
 
   const int64_t n_groups = (a.total_frames + SM_WAVES - 1) / SM_WAVES;
@@ -157,13 +166,13 @@ __global__ __launch_bounds__(SM_THREADS) void stft_mel_kernel(StftMelArgs a) {
       for (int j = 0; j < a.mel_j0; ++j)
         if (j < nj) {
           const float4 p = *reinterpret_cast<const float4*>(pw + lo + 4 * j);
-          const float4 w = sh_w4[j * 64 + lane];
+          const float4 w = mw4[j * 64 + lane];
           acc0 = fmaf(w.w, p.w, fmaf(w.z, p.z, fmaf(w.y, p.y, fmaf(w.x, p.x, acc0))));
         }
     }
     {
       const int lo = a.mel_lo4[64 + lane], nj = a.mel_nj4[64 + lane];
-      const float4* w1 = sh_w4 + a.mel_j0 * 64;
+      const float4* w1 = mw4 + a.mel_j0 * 64;
       for (int j = 0; j < a.mel_j1; ++j)
         if (j < nj) {
           const float4 p = *reinterpret_cast<const float4*>(pw + lo + 4 * j);
