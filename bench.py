@@ -113,8 +113,8 @@ def cpu_baseline(seconds, base_seed, workers):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=5)
-    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--pairs", type=int, default=64, help="pairs per GPU (config 3: 64)")
     ap.add_argument("--seconds", type=float, default=180.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
