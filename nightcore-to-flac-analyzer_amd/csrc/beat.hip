@@ -9,10 +9,11 @@
 // One workgroup per sequence.  The DP (cumscore[i] = ls[i] + max_d cum[i-d] -
 // pen[d], d in [round(P/2), 2P]) is serial in i but every frame of a block of
 // round(P/2) consecutive frames depends only on frames before the block, so a
-// block is evaluated in parallel (waves over frames, lanes over candidates) with
-// one barrier per block: 43 barriers for a 431-frame window, 738 for a 3-min
-// hop-64 signal.  Short sequences keep every array in LDS; long ones (hop-64
-// IBI pass) use a global workspace that stays L2 resident.
+// block is scored at once: threads split (frame, candidate chunk) pairs, the
+// per-chunk winners meet in LDS and one thread per frame folds them — two
+// barriers per block, no cross-lane shuffle chains.  Short sequences keep every
+// array in LDS; long ones (hop-64 IBI pass) keep ls/cum/back in a global
+// workspace and the last cumulative scores in an LDS ring.
 //
 // Decision arithmetic is float64 throughout (as librosa's numba kernels), with
 // FMA contraction disabled where librosa adds separately rounded products.
@@ -45,9 +46,26 @@ struct BeatArgs {
   uint8_t* ws_marks;
   int max_len;          // SMALL: LDS capacity in frames
   int tab_cap;          // doubles for the window / penalty table
+  int ring_cap;         // !SMALL: LDS ring of the last ring_cap cumulative scores (power of 2)
 };
 
 __host__ __device__ __forceinline__ size_t al16(size_t n) { return (n + 15) & ~(size_t)15; }
+
+// Workgroup barrier for LDS-only hand-offs: waits for this wave's LDS traffic but not for
+// its outstanding global loads/stores (which __syncthreads' fence would drain every block).
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+#ifdef NC_BEAT_PROF
+#define NC_BEAT_T(k) \
+  do { __syncthreads(); if (threadIdx.x == 0) prof_t[k] = wall_clock64(); } while (0)
+#define NC_BEAT_DUMP() \
+  do { if (threadIdx.x == 0 && blockIdx.x == 0) printf("beatprof SMALL=%d N=%d P=%d: %ld %ld %ld %ld %ld %ld\n", (int)SMALL, N, Pi, \
+       (long)(prof_t[1]-prof_t[0]), (long)(prof_t[2]-prof_t[1]), (long)(prof_t[3]-prof_t[2]), (long)(prof_t[4]-prof_t[3]), \
+       (long)(prof_t[5]-prof_t[4]), (long)(prof_t[6]-prof_t[5])); } while (0)
+#else
+#define NC_BEAT_T(k) do {} while (0)
+#define NC_BEAT_DUMP() do {} while (0)
+#endif
 
 template <int NT, bool SMALL>
 __global__ __launch_bounds__(NT) void tempo_beat_kernel(BeatArgs a) {
@@ -56,9 +74,12 @@ __global__ __launch_bounds__(NT) void tempo_beat_kernel(BeatArgs a) {
   __shared__ BlockScratch<NT> bs;
   __shared__ int hist[256];
   __shared__ int sh_int[4];
+  __shared__ double dp_best[NT];
+  __shared__ int dp_d[NT];
+#ifdef NC_BEAT_PROF
+  __shared__ long long prof_t[8];
+#endif
   const int s = blockIdx.x;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  constexpr int NW = NT / 64;
 
   if (a.active && !a.active[s]) {
     if (threadIdx.x == 0) {
@@ -105,6 +126,7 @@ __global__ __launch_bounds__(NT) void tempo_beat_kernel(BeatArgs a) {
   }
 
   // ------------------------------------------------------------ tempo: prior-weighted argmax
+  NC_BEAT_T(0);
   const double fs = (double)a.sr;
   const double start = a.prior_idx ? a.start_bpm[a.prior_idx[s]] : a.start_bpm[s];
   const double lstart = log2(start);
@@ -161,6 +183,7 @@ __global__ __launch_bounds__(NT) void tempo_beat_kernel(BeatArgs a) {
   const int Pi = (int)P;
 
   // ------------------------------------------------------------ normalise + local score
+  NC_BEAT_T(1);
   double sx = 0.0;
   for (int i = threadIdx.x; i < N; i += NT) sx += (double)onset[i];
   sx = block_sum<NT>(sx, bs);
@@ -178,12 +201,17 @@ __global__ __launch_bounds__(NT) void tempo_beat_kernel(BeatArgs a) {
     const double v = ((double)(k - Pi) * 32.0) / P;
     tab[k] = exp(-0.5 * (v * v));
   }
+  // onset / norm once per frame (the same f32 quotient the per-tap form computed), kept in
+  // cum's storage until the DP overwrites it
+  float* onn = reinterpret_cast<float*>(cum);
+  for (int i = threadIdx.x; i < N; i += NT) onn[i] = onset[i] / norm;
   __syncthreads();
   double lmax = -INFINITY;
   for (int i = threadIdx.x; i < N; i += NT) {
     const int klo = max(0, i + Pi - N + 1), khi = min(i + Pi, K - 1);
+    const float* on = onn + i + Pi;
     double acc = 0.0;
-    for (int k = klo; k <= khi; ++k) acc = acc + tab[k] * (double)(onset[i + Pi - k] / norm);
+    for (int k = klo; k <= khi; ++k) acc = acc + tab[k] * (double)on[-k];
     ls[i] = acc;
     lmax = fmax(lmax, acc);
   }
@@ -195,6 +223,7 @@ __global__ __launch_bounds__(NT) void tempo_beat_kernel(BeatArgs a) {
   const int i0 = block_min_i<NT>(first, bs);
 
   // ------------------------------------------------------------ DP
+  NC_BEAT_T(2);
   const int dmin = (int)rint(P / 2.0);
   const int dmax = 2 * Pi;
   const double lP = log(P);
@@ -205,39 +234,89 @@ __global__ __launch_bounds__(NT) void tempo_beat_kernel(BeatArgs a) {
     tab[d] = tight * (t * t);
   }
   __syncthreads();
-  const int B = max(dmin, 1);
+  // Frames [b0, b0 + B) with B <= dmin only read cum[] before b0, so a block of B frames is
+  // scored at once: thread t takes frame t % B and the t / B-th of Gn consecutive chunks of
+  // the candidate range [dmin, dmax]; per-chunk winners (ties: smaller d, as the ascending
+  // scan) go to LDS and the B frame threads fold them in ascending chunk order.
+  const int B = max(1, min(dmin, NT / 2));
+  const int D = dmax - dmin + 1;
+  // chunk length and fold length both ~sqrt(D): the scan and the fold are serial per thread
+  const int Gn = max(1, min(NT / B, (int)ceil(sqrt((double)D))));
+  const int C = (D + Gn - 1) / Gn;
+  // long sequences: the DP reads cum[i - d] for d in [dmin, dmax] only, so the last ring_cap
+  // (>= dmax + B) scores are kept in an LDS ring instead of being re-read from L2 per candidate
+  double* ring = SMALL ? cum : reinterpret_cast<double*>(smem + al16((size_t)a.tab_cap * sizeof(double)));
+  const int RM = SMALL ? 0x7fffffff : a.ring_cap - 1;
+  if (!SMALL && dmax + B > a.ring_cap) {
+    if (threadIdx.x == 0) a.nbeats_out[s] = -1;  // capacity error (cannot happen for P <= acw - 1)
+    return;
+  }
+  const int f = threadIdx.x % B, g = threadIdx.x / B;
+  const int dlo = dmin + g * C, dend = min(dmax + 1, dlo + C);
+  // ls[] two blocks ahead (long sequences: a global read whose latency would otherwise
+  // sit inside every block)
+  const bool fthr = threadIdx.x < B;
+  double ls_n1 = (fthr && f < N) ? ls[f] : 0.0;
+  double ls_n2 = (fthr && B + f < N) ? ls[B + f] : 0.0;
   for (int b0 = 0; b0 < N; b0 += B) {
-    const int b1 = min(N, b0 + B);
-    for (int i = b0 + wave; i < b1; i += NW) {
-      const int dhi = min(dmax, i);
+    const int i = b0 + f;
+    const bool own = fthr && i < N;
+    const double lsi = ls_n1;
+    ls_n1 = ls_n2;
+    ls_n2 = (fthr && i + 2 * B < N) ? ls[i + 2 * B] : 0.0;
+    if (g < Gn) {
       double best = -INFINITY;
       int bd = 0x7fffffff;
-      for (int d = dmin + lane; d <= dhi; d += 64) {
-        const double sc = cum[i - d] - tab[d];
-        if (sc > best || (sc == best && d < bd)) {
-          best = sc;
+      if (i < N) {
+        const int dh = min(dend, i + 1);
+        int d = dlo;
+        for (; d + 3 < dh; d += 4) {
+          double sc[4];
+#pragma unroll
+          for (int u = 0; u < 4; ++u) sc[u] = ring[(i - d - u) & RM] - tab[d + u];
+#pragma unroll
+          for (int u = 0; u < 4; ++u)
+            if (sc[u] > best) {
+              best = sc[u];
+              bd = d + u;
+            }
+        }
+        for (; d < dh; ++d) {
+          const double sc = ring[(i - d) & RM] - tab[d];
+          if (sc > best) {
+            best = sc;
+            bd = d;
+          }
+        }
+      }
+      dp_best[threadIdx.x] = best;
+      dp_d[threadIdx.x] = bd;
+    }
+    lds_barrier();
+    if (own) {
+      double best = -INFINITY;
+      int bd = 0x7fffffff;
+#pragma unroll 4
+      for (int q = 0; q < Gn; ++q) {
+        const double v = dp_best[q * B + f];
+        const int d = dp_d[q * B + f];
+        if (v > best || (v == best && d < bd)) {
+          best = v;
           bd = d;
         }
       }
-#pragma unroll
-      for (int o = 32; o > 0; o >>= 1) {
-        const double ov = __shfl_xor(best, o, 64);
-        const int od = __shfl_xor(bd, o, 64);
-        if (ov > best || (ov == best && od < bd)) {
-          best = ov;
-          bd = od;
-        }
-      }
-      if (lane == 0) {
-        const bool found = (dhi >= dmin) && (best > -INFINITY);
-        cum[i] = found ? ls[i] + best : ls[i];
-        back[i] = (i < i0 || !found) ? -1 : i - bd;
-      }
+      const bool found = (i >= dmin) && (best > -INFINITY);
+      const double v = found ? lsi + best : lsi;
+      cum[i] = v;
+      if (!SMALL) ring[i & RM] = v;
+      back[i] = (i < i0 || !found) ? -1 : i - bd;
     }
-    __syncthreads();
+    lds_barrier();
   }
+  __syncthreads();  // cum / back global stores (long sequences) visible to the whole workgroup
 
   // ------------------------------------------------------------ last beat
+  NC_BEAT_T(3);
   for (int i = threadIdx.x; i < N; i += NT) {
     const double x = cum[i];
     const bool left = i > 0 ? (x > cum[i - 1]) : false;
@@ -266,6 +345,7 @@ __global__ __launch_bounds__(NT) void tempo_beat_kernel(BeatArgs a) {
   }
 
   // ------------------------------------------------------------ backtrack
+  NC_BEAT_T(4);
   __syncthreads();
   for (int i = threadIdx.x; i < N; i += NT) marks[i] = 0;
   __syncthreads();
@@ -291,6 +371,7 @@ __global__ __launch_bounds__(NT) void tempo_beat_kernel(BeatArgs a) {
   __syncthreads();
 
   // ------------------------------------------------------------ trim (0.5 RMS of smoothed beat scores)
+  NC_BEAT_T(5);
   double thr3 = 0.0;
   if (a.trim) {
     double e2 = 0.0;
@@ -334,6 +415,8 @@ __global__ __launch_bounds__(NT) void tempo_beat_kernel(BeatArgs a) {
   if (threadIdx.x == 0) a.nbeats_out[s] = nkeep;
   if (a.beats_out)
     for (int j = threadIdx.x; j < nkeep; j += NT) a.beats_out[off + j] = back[kfirst + j];
+  NC_BEAT_T(6);
+  NC_BEAT_DUMP();
   (void)sh_int;
 }
 
@@ -431,13 +514,18 @@ int launch_tempo_beats(Context& ctx, BeatArgs a, int n_seq, int max_len, hipStre
       set_error("tempo_beats: long sequences need the global workspace");
       return -3;
     }
-    if (tab > 120 * 1024) {
+    // LDS ring of cumulative scores: >= dmax + B = 2P + round(P/2) frames, P <= acw - 1
+    int ring = 1;
+    while (ring < (a.tab_cap / 2) * 5 / 2 + 2) ring <<= 1;
+    a.ring_cap = ring;
+    const size_t lds = tab + (size_t)ring * sizeof(double);
+    if (lds > 150 * 1024) {
       set_error("tempo_beats: tempogram window too long");
       return -2;
     }
     {
       KTimer kt_(ctx, "tempo_beat", st);
-      hipLaunchKernelGGL((tempo_beat_kernel<1024, false>), dim3(n_seq), dim3(1024), tab, st, a);
+      hipLaunchKernelGGL((tempo_beat_kernel<1024, false>), dim3(n_seq), dim3(1024), lds, st, a);
     }
   }
   NC_HIP(hipGetLastError());

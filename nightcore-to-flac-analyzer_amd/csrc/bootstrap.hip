@@ -12,13 +12,17 @@
 // bounded 32-bit draw on next_uint32(), which returns the LOW then the HIGH half
 // of each 64-bit output with the spare half buffered in the bit generator (so it
 // carries across calls); n == 1 consumes nothing.  Resample r starts at uint32
-// position s_r = sum_{q<r} consumed_q; with rare Lemire rejections the
-// positions are found by a fix-point (assume r*m, walk, prefix-sum, repeat until
-// stable) inside one workgroup, each thread jumping to its position with the
-// O(log n) LCG advance.  Since a rejection has probability < n / 2^32 per draw, the
-// common case runs one resample per thread across many workgroups at r*m (counts in
-// LDS) and only a job whose walk met a rejection is redone by the fix-point.  Medians: the resample's multiset is kept as counts per
-// rank of the sorted input, so the k-th smallest is a scan.  Percentiles use
+// position s_r = sum_{q<r} consumed_q.  A Lemire rejection (probability < n / 2^32 per
+// draw) is a property of the stream position and the bound alone, so the exact positions
+// come from the sparse list of positions a bound-n draw would reject: the draw pass runs
+// one resample per thread at r*m (counts in LDS for short jobs); a job where some resample
+// consumed more than m has its stream range scanned for rejecting positions across many
+// workgroups, one thread walks the resample boundaries over the sorted lists, and the
+// job's resamples are drawn again from the exact starts.  The old fix-point (assume r*m,
+// walk, prefix-sum, repeat until stable, inside one workgroup) remains as the fallback
+// for a job whose rejection list overflows.
+// Medians: the resample's multiset is kept as counts per rank of the sorted input, so
+// the k-th smallest is a scan.  Percentiles use
 // numpy's 'linear' method (virtual index (n-1) q, lerp with the t >= 0.5 branch),
 // whose (index, gamma) the host computes with numpy's own formula.
 #include "nc_block.h"
@@ -100,7 +104,20 @@ __device__ __forceinline__ double lerp_np(double a, double b, double t) {
 }
 
 // Per-job workspace (bootstrap_job_bytes): rank[na + nb] i32 | sorted[na + nb] f64 |
-// start[n_boot] i64 | boot[n_boot] f64 | flag i32 | counts[n_boot][na + nb] u16 (global path)
+// start[n_boot] i64 | boot[n_boot] f64 | JobCtl | rejA[REJ_CAP] i64 | rejB[REJ_CAP] i64 |
+// counts[n_boot][na + nb] u16 (global path)
+constexpr int REJ_CAP = 512;          // rejecting positions kept per bound (expected: ~40 for n = 7000)
+constexpr int64_t REJ_SLACK = 65536;  // stream positions scanned beyond n_boot * m
+constexpr int SCAN_WG = 64;           // scan workgroups per job
+
+struct JobCtl {
+  int flag;    // bit 0: some resample consumed != m (set by the draw pass)
+  int nrejA, nrejB;
+  int status;  // 0: exact starts valid; 1: list overflow / range short; 2: redraw mismatch
+  int64_t end; // stream position after the last resample
+  int64_t pad;
+};
+
 struct JobWs {
   int* rankA;
   int* rankB;
@@ -108,7 +125,10 @@ struct JobWs {
   double* sortedB;
   int64_t* start;
   double* boot;
+  JobCtl* ctl;
   int* flag;
+  int64_t* rejA;
+  int64_t* rejB;
   uint16_t* cnt;
 };
 
@@ -122,8 +142,11 @@ __device__ __forceinline__ JobWs job_ws(const BootArgs& a, int j, int na) {
   r.sortedB = r.sortedA + na;
   r.start = reinterpret_cast<int64_t*>(r.sortedA + cap);
   r.boot = reinterpret_cast<double*>(r.start + a.n_boot);
-  r.flag = reinterpret_cast<int*>(r.boot + a.n_boot);
-  r.cnt = reinterpret_cast<uint16_t*>(r.flag + 4);
+  r.ctl = reinterpret_cast<JobCtl*>(r.boot + a.n_boot);
+  r.flag = &r.ctl->flag;
+  r.rejA = reinterpret_cast<int64_t*>(r.ctl + 1);
+  r.rejB = r.rejA + REJ_CAP;
+  r.cnt = reinterpret_cast<uint16_t*>(r.rejB + REJ_CAP);
   return r;
 }
 
@@ -169,40 +192,58 @@ __device__ __forceinline__ int draw_resample(u128 s0, u128 inc, int64_t start, i
   return consumed;
 }
 
-// Phase 1 (one workgroup per job): stable ranks and sorted values; clears the job flag.
+// Phase 1 (grid RANK_SPLIT x jobs): stable ranks and sorted values; clears the job flag.
+// Element i's rank counts the values before it in sorted order, scanning the array in LDS
+// tiles (every thread of a workgroup reads the same value: a broadcast), so long jobs (the
+// hop-64 IBI lists of a 60-min pair, ~7 000 values) spread over RANK_SPLIT workgroups.
+constexpr int RANK_SPLIT = 16;
+constexpr int RANK_TILE = 2048;
+
+__device__ __forceinline__ void rank_array(const double* X, int n, int* rank, double* sorted, double* tile) {
+  const int stride = RANK_SPLIT * BT;
+  for (int i0 = blockIdx.x * BT; i0 < n; i0 += stride) {
+    const int i = i0 + threadIdx.x;
+    const double v = i < n ? X[i] : 0.0;
+    int r = 0;
+    for (int t0 = 0; t0 < n; t0 += RANK_TILE) {
+      const int tn = min(RANK_TILE, n - t0);
+      __syncthreads();
+      for (int q = threadIdx.x; q < tn; q += BT) tile[q] = X[t0 + q];
+      __syncthreads();
+      for (int q = 0; q < tn; ++q) {
+        const double u = tile[q];
+        r += (u < v) || (u == v && t0 + q < i);
+      }
+    }
+    if (i < n) {
+      rank[i] = r;
+      sorted[r] = v;
+    }
+  }
+}
+
 __global__ __launch_bounds__(BT) void bootstrap_rank_kernel(BootArgs a) {
-  const int j = blockIdx.x;
+  __shared__ double tile[RANK_TILE];
+  const int j = blockIdx.y;
   int na, nb;
   if (job_skipped(a, j, na, nb)) return;
   const JobWs w = job_ws(a, j, na);
-  const double* A = a.values + a.a_off[j];
-  const double* B = a.b_n ? a.values + a.b_off[j] : nullptr;
-  for (int i = threadIdx.x; i < na; i += BT) {
-    const double v = A[i];
-    int r = 0;
-    for (int q = 0; q < na; ++q) {
-      const double u = A[q];
-      r += (u < v) || (u == v && q < i);
-    }
-    w.rankA[i] = r;
-    w.sortedA[r] = v;
+  rank_array(a.values + a.a_off[j], na, w.rankA, w.sortedA, tile);
+  if (a.b_n) rank_array(a.values + a.b_off[j], nb, w.rankB, w.sortedB, tile);
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    w.ctl->flag = 0;
+    w.ctl->nrejA = 0;
+    w.ctl->nrejB = 0;
+    w.ctl->status = 0;
   }
-  for (int i = threadIdx.x; i < nb; i += BT) {
-    const double v = B[i];
-    int r = 0;
-    for (int q = 0; q < nb; ++q) {
-      const double u = B[q];
-      r += (u < v) || (u == v && q < i);
-    }
-    w.rankB[i] = r;
-    w.sortedB[r] = v;
-  }
-  if (threadIdx.x == 0) *w.flag = 0;
 }
 
 // Phase 2 (grid n_boot / BD x jobs): resample r drawn from uint32 position r * m, the
 // position it has when no Lemire rejection happened before it.  A resample that
-// consumes more than m flags its job; phase 3 then redoes that job exactly.
+// consumes more than m flags its job.  EXACT: the pass again for flagged jobs only, from
+// the starts phase 2c found; a resample whose consumption disagrees marks the job for the
+// fix-point fallback.
+template <bool EXACT>
 __global__ __launch_bounds__(BD) void bootstrap_draw_kernel(BootArgs a) {
   __shared__ uint16_t cnt_lds[BD_NV * BD];  // [rank][thread]
   const int j = blockIdx.y;
@@ -211,6 +252,7 @@ __global__ __launch_bounds__(BD) void bootstrap_draw_kernel(BootArgs a) {
   const int r = blockIdx.x * BD + threadIdx.x;
   if (r >= a.n_boot) return;
   const JobWs w = job_ws(a, j, na);
+  if (EXACT && (!w.ctl->flag || w.ctl->status)) return;
   const bool hasB = a.b_n != nullptr;
   const int nv = na + nb;
   const int m = (na > 1 ? na : 0) + (nb > 1 ? nb : 0);
@@ -219,10 +261,120 @@ __global__ __launch_bounds__(BD) void bootstrap_draw_kernel(BootArgs a) {
   const bool in_lds = nv <= BD_NV;
   uint16_t* c = in_lds ? cnt_lds + threadIdx.x : w.cnt + (size_t)r * nv;
   const int stride = in_lds ? BD : 1;
-  const int consumed = draw_resample(s0, inc, (int64_t)r * m, na, nb, hasB, w.rankA, w.rankB, c, stride);
-  if (consumed != m) atomicOr(w.flag, 1);
+  const int64_t st = EXACT ? w.start[r] : (int64_t)r * m;
+  const int consumed = draw_resample(s0, inc, st, na, nb, hasB, w.rankA, w.rankB, c, stride);
+  if (EXACT) {
+    const int64_t nxt = r + 1 < a.n_boot ? w.start[r + 1] : w.ctl->end;
+    if (st + consumed != nxt) atomicOr(&w.ctl->status, 2);
+  } else if (consumed != m) {
+    atomicOr(w.flag, 1);
+  }
   const double ma = med_count(c, stride, na, w.sortedA);
   w.boot[r] = hasB ? ma / med_count(c + na * stride, stride, nb, w.sortedB) : ma;
+}
+
+__device__ __forceinline__ uint32_t lemire_thr(uint32_t n) { return (uint32_t)((0xFFFFFFFFu - (n - 1)) % n); }
+
+// Phase 2b (grid SCAN_WG x jobs, flagged jobs only): every stream position p in
+// [0, n_boot * m + REJ_SLACK) at which a bound-na (bound-nb) draw would be rejected:
+// low32(u_p * n) < (2^32 - n) mod n.  Each thread walks a contiguous run of positions.
+__global__ __launch_bounds__(BT) void bootstrap_rejscan_kernel(BootArgs a) {
+  const int j = blockIdx.y;
+  int na, nb;
+  if (job_skipped(a, j, na, nb)) return;
+  const JobWs w = job_ws(a, j, na);
+  if (!w.ctl->flag) return;
+  const bool hasB = a.b_n != nullptr;
+  const bool ra = na > 1, rb = hasB && nb > 1;
+  const int m = (ra ? na : 0) + (rb ? nb : 0);
+  const int64_t total = (int64_t)a.n_boot * m + REJ_SLACK;
+  const int64_t nthreads = (int64_t)SCAN_WG * BT;
+  const int64_t per = ((total + nthreads - 1) / nthreads + 1) & ~(int64_t)1;
+  const int64_t p0 = ((int64_t)blockIdx.x * BT + threadIdx.x) * per;
+  const int64_t p1 = min(total, p0 + per);
+  if (p0 >= p1) return;
+  const u128 s0 = ((u128)a.seed[j * 4 + 0] << 64) | (u128)a.seed[j * 4 + 1];
+  const u128 inc = ((u128)a.seed[j * 4 + 2] << 64) | (u128)a.seed[j * 4 + 3];
+  const uint32_t thA = ra ? lemire_thr((uint32_t)na) : 0u, thB = rb ? lemire_thr((uint32_t)nb) : 0u;
+  Gen32 g;
+  g.init(s0, inc, (uint64_t)p0);
+  for (int64_t p = p0; p < p1; ++p) {
+    const uint32_t v = g.next();
+    if (ra && (uint32_t)((uint64_t)v * (uint32_t)na) < thA) {
+      const int k = atomicAdd(&w.ctl->nrejA, 1);
+      if (k < REJ_CAP) w.rejA[k] = p;
+    }
+    if (rb && (uint32_t)((uint64_t)v * (uint32_t)nb) < thB) {
+      const int k = atomicAdd(&w.ctl->nrejB, 1);
+      if (k < REJ_CAP) w.rejB[k] = p;
+    }
+  }
+}
+
+// sorts list[0, n) (n <= REJ_CAP, distinct values) in LDS by rank
+__device__ void sort_rejections(int64_t* list, int n, int64_t* tmp) {
+  for (int i = threadIdx.x; i < n; i += BT) tmp[i] = list[i];
+  __syncthreads();
+  for (int i = threadIdx.x; i < n; i += BT) {
+    const int64_t v = tmp[i];
+    int r = 0;
+    for (int q = 0; q < n; ++q) r += tmp[q] < v;
+    list[r] = v;
+  }
+  __syncthreads();
+}
+
+// Phase 2c (one workgroup per flagged job): sort the lists, then one thread walks the
+// resample boundaries: a bound-n phase starting at p ends at the first e with
+// e - p - (rejections in [p, e)) = n.
+__global__ __launch_bounds__(BT) void bootstrap_walk_kernel(BootArgs a) {
+  __shared__ int64_t tmp[REJ_CAP];
+  __shared__ int64_t la[REJ_CAP], lb[REJ_CAP];
+  const int j = blockIdx.x;
+  int na, nb;
+  if (job_skipped(a, j, na, nb)) return;
+  const JobWs w = job_ws(a, j, na);
+  if (!w.ctl->flag) return;
+  const int ca = w.ctl->nrejA, cb = w.ctl->nrejB;
+  if (ca > REJ_CAP || cb > REJ_CAP) {
+    if (threadIdx.x == 0) w.ctl->status = 1;
+    return;
+  }
+  sort_rejections(w.rejA, ca, tmp);
+  sort_rejections(w.rejB, cb, tmp);
+  for (int i = threadIdx.x; i < ca; i += BT) la[i] = w.rejA[i];
+  for (int i = threadIdx.x; i < cb; i += BT) lb[i] = w.rejB[i];
+  __syncthreads();
+  if (threadIdx.x != 0) return;
+  const bool hasB = a.b_n != nullptr;
+  const bool ra = na > 1, rb = hasB && nb > 1;
+  const int m = (ra ? na : 0) + (rb ? nb : 0);
+  const int64_t total = (int64_t)a.n_boot * m + REJ_SLACK;
+  int64_t p = 0;
+  int ia = 0, ib = 0;
+  for (int r = 0; r < a.n_boot; ++r) {
+    w.start[r] = p;
+    if (ra) {
+      while (ia < ca && la[ia] < p) ++ia;
+      int64_t e = p + na;
+      while (ia < ca && la[ia] < e) {
+        ++e;
+        ++ia;
+      }
+      p = e;
+    }
+    if (rb) {
+      while (ib < cb && lb[ib] < p) ++ib;
+      int64_t e = p + nb;
+      while (ib < cb && lb[ib] < e) {
+        ++e;
+        ++ib;
+      }
+      p = e;
+    }
+  }
+  w.ctl->end = p;
+  if (p > total) w.ctl->status = 1;  // the scan did not cover the whole walk
 }
 
 // Phase 3 (one workgroup per job): for a flagged job the exact resample positions by a
@@ -245,7 +397,7 @@ __global__ __launch_bounds__(BT) void bootstrap_finish_kernel(BootArgs a) {
   const JobWs w = job_ws(a, j, na);
   const bool hasB = a.b_n != nullptr;
   const int nv = na + nb;
-  if (*w.flag) {  // rare: some resample met a Lemire rejection
+  if (w.ctl->flag && w.ctl->status) {  // fallback: the exact-start pass could not be used
     const u128 s0 = ((u128)a.seed[j * 4 + 0] << 64) | (u128)a.seed[j * 4 + 1];
     const u128 inc = ((u128)a.seed[j * 4 + 2] << 64) | (u128)a.seed[j * 4 + 3];
     const int m = (na > 1 ? na : 0) + (nb > 1 ? nb : 0);
@@ -326,7 +478,8 @@ __global__ __launch_bounds__(BT) void bootstrap_finish_kernel(BootArgs a) {
 
 size_t bootstrap_job_bytes(int cap, int n_boot) {
   size_t b = (((size_t)cap * 4 + 15) & ~(size_t)15);
-  b += (size_t)cap * 8 + (size_t)n_boot * 8 + (size_t)n_boot * 8 + 16 + (size_t)n_boot * cap * 2;
+  b += (size_t)cap * 8 + (size_t)n_boot * 8 + (size_t)n_boot * 8 + sizeof(JobCtl) + 2 * REJ_CAP * 8 +
+       (size_t)n_boot * cap * 2;
   return (b + 255) & ~(size_t)255;
 }
 
@@ -336,8 +489,12 @@ int launch_bootstrap(const BootArgs& a, int n_jobs, hipStream_t st) {
     set_error("bootstrap: n_boot must be in [1, 2048]");
     return -2;
   }
-  hipLaunchKernelGGL(bootstrap_rank_kernel, dim3(n_jobs), dim3(BT), 0, st, a);
-  hipLaunchKernelGGL(bootstrap_draw_kernel, dim3((a.n_boot + BD - 1) / BD, n_jobs), dim3(BD), 0, st, a);
+  hipLaunchKernelGGL(bootstrap_rank_kernel, dim3(RANK_SPLIT, n_jobs), dim3(BT), 0, st, a);
+  const dim3 gd((a.n_boot + BD - 1) / BD, n_jobs);
+  hipLaunchKernelGGL(bootstrap_draw_kernel<false>, gd, dim3(BD), 0, st, a);
+  hipLaunchKernelGGL(bootstrap_rejscan_kernel, dim3(SCAN_WG, n_jobs), dim3(BT), 0, st, a);
+  hipLaunchKernelGGL(bootstrap_walk_kernel, dim3(n_jobs), dim3(BT), 0, st, a);
+  hipLaunchKernelGGL(bootstrap_draw_kernel<true>, gd, dim3(BD), 0, st, a);
   hipLaunchKernelGGL(bootstrap_finish_kernel, dim3(n_jobs), dim3(BT), 0, st, a);
   NC_HIP(hipGetLastError());
   return 0;

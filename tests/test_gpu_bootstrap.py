@@ -37,7 +37,7 @@ def _numpy_boots(a, b, seed, n_boot=2000):
     return out
 
 
-def _device_boots(eng, a, b, seed):
+def _device_boots(eng, a, b, seed, ctl_out=None):
     """Run nc_bootstrap_ratio with boot_out to compare every resample."""
     from nightcore_analyzer.engine import _Upload, percentile_params, seed_state
     vals = np.concatenate([a, b]) if b is not None else a
@@ -61,6 +61,10 @@ def _device_boots(eng, a, b, seed):
              1, 2000, d["seed"].data_ptr(), il, gl, ih, gh, 1, out[0:1].data_ptr(), out[1:2].data_ptr(),
              out[2:3].data_ptr(), boots.data_ptr(), d["wsoff"].data_ptr(), d["cap"].data_ptr(), ws.data_ptr(),
              ws.numel(), eng.stream())
+    if ctl_out is not None:  # JobCtl (bootstrap.hip): after rank/sorted/start/boot
+        o = ((cap * 4 + 15) & ~15) + cap * 8 + 2000 * 16
+        ctl_out.extend(ws[o:o + 24].cpu().numpy().view(np.int32)[:4].tolist())
+        ctl_out.append(int(ws[o + 16:o + 24].cpu().numpy().view(np.int64)[0]))
     return boots.cpu().numpy(), out.cpu().numpy()
 
 
@@ -75,3 +79,17 @@ def test_every_resample_bit_exact(eng, na, nb, seed):
     ref = _numpy_boots(a, b, seed)
     np.testing.assert_array_equal(got, ref)
     assert pt[1] == np.percentile(ref, 2.5) and pt[2] == np.percentile(ref, 97.5)
+
+
+def test_rejections_resolved_by_exact_starts(eng):
+    """A large job meets Lemire rejections (flag set); the sparse rejection scan + walk gives
+    exact starts (status 0: no fix-point fallback) and every resample stays bit-exact."""
+    rng = np.random.default_rng(5)
+    a = np.round(rng.random(3000) * 100 + 50, 1)
+    b = np.round(rng.random(2500) * 100 + 50, 1)
+    ctl = []
+    got, _ = _device_boots(eng, a, b, 42, ctl)
+    flag, nrej_a, nrej_b, status, end = ctl
+    assert flag == 1 and status == 0
+    assert nrej_a + nrej_b > 0 and end > 2000 * 5500
+    np.testing.assert_array_equal(got, _numpy_boots(a, b, 42))
