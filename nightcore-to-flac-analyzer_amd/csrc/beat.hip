@@ -47,6 +47,7 @@ struct BeatArgs {
   int max_len;          // SMALL: LDS capacity in frames
   int tab_cap;          // doubles for the window / penalty table
   int ring_cap;         // !SMALL: LDS ring of the last ring_cap cumulative scores (power of 2)
+  int phase;            // !SMALL: 0 one launch, 1 up to the normalised onset, 2 from the local score
 };
 
 __host__ __device__ __forceinline__ size_t al16(size_t n) { return (n + 15) & ~(size_t)15; }
@@ -66,6 +67,45 @@ __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(
 #define NC_BEAT_T(k) do {} while (0)
 #define NC_BEAT_DUMP() do {} while (0)
 #endif
+
+// beat_track's local score: the onset envelope (normalised) convolved with a Gaussian
+// window of 2P + 1 taps, exp(-0.5 ((k - P) 32 / P)^2), summed in ascending tap order
+__device__ __forceinline__ double beat_window(int k, int Pi, double P) {
+#pragma clang fp contract(off)
+  const double v = ((double)(k - Pi) * 32.0) / P;
+  return exp(-0.5 * (v * v));
+}
+__device__ __forceinline__ double beat_local_score(const float* onn, const double* tab, int i, int N, int Pi, int K) {
+#pragma clang fp contract(off)
+  const int klo = max(0, i + Pi - N + 1), khi = min(i + Pi, K - 1);
+  const float* on = onn + i + Pi;
+  double acc = 0.0;
+  for (int k = klo; k <= khi; ++k) acc = acc + tab[k] * (double)on[-k];
+  return acc;
+}
+
+// Long sequences, between phase 1 and phase 2 of tempo_beat_kernel<1024, false>: the local
+// score of every frame, one frame per thread over the whole chip (a hop-64 60-min signal has
+// ~1M frames x 2P + 1 taps, which one workgroup took ~27 ms over).
+template <int NT>
+__global__ __launch_bounds__(NT) void beat_localscore_kernel(BeatArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  double* ltab = reinterpret_cast<double*>(smem);
+  const int s = blockIdx.y;
+  if (a.active && !a.active[s]) return;
+  const int N = a.len[s];
+  if (N < 4 || (int64_t)blockIdx.x * NT >= N) return;
+  const int64_t off = a.off[s];
+  const int* meta = a.ws_back + off;
+  if (meta[3] != 1) return;
+  const int Pi = meta[0], K = 2 * Pi + 1;
+  for (int k = threadIdx.x; k < K; k += NT) ltab[k] = beat_window(k, Pi, (double)Pi);
+  __syncthreads();
+  const int i = blockIdx.x * NT + threadIdx.x;
+  if (i < N) a.ws_ls[off + i] = beat_local_score(reinterpret_cast<const float*>(a.ws_cum + off), ltab, i, N, Pi, K);
+}
+
+constexpr int kBeatWin = 1024;  // long-sequence DP window (frames staged per global round trip)
 
 template <int NT, bool SMALL>
 __global__ __launch_bounds__(NT) void tempo_beat_kernel(BeatArgs a) {
@@ -109,6 +149,7 @@ __global__ __launch_bounds__(NT) void tempo_beat_kernel(BeatArgs a) {
     cum = a.ws_cum + off;
     back = a.ws_back + off;
     marks = a.ws_marks + off;
+    if (a.phase == 1 && N >= 4 && threadIdx.x == 0) back[3] = 0;  // local-score meta: not ready
   }
 
   // ------------------------------------------------------------ any onset?
@@ -184,36 +225,45 @@ __global__ __launch_bounds__(NT) void tempo_beat_kernel(BeatArgs a) {
 
   // ------------------------------------------------------------ normalise + local score
   NC_BEAT_T(1);
-  double sx = 0.0;
-  for (int i = threadIdx.x; i < N; i += NT) sx += (double)onset[i];
-  sx = block_sum<NT>(sx, bs);
-  const float mean32 = (float)(sx / (double)N);
-  double sq = 0.0;
-  for (int i = threadIdx.x; i < N; i += NT) {
-    const double d = (double)(onset[i] - mean32);
-    sq += d * d;
-  }
-  sq = block_sum<NT>(sq, bs);
-  const float std32 = (float)sqrt(sq / (double)(N - 1));
-  const float norm = std32 + 1.17549435e-38f;
-
-  for (int k = threadIdx.x; k < K; k += NT) {
-    const double v = ((double)(k - Pi) * 32.0) / P;
-    tab[k] = exp(-0.5 * (v * v));
-  }
-  // onset / norm once per frame (the same f32 quotient the per-tap form computed), kept in
-  // cum's storage until the DP overwrites it
-  float* onn = reinterpret_cast<float*>(cum);
-  for (int i = threadIdx.x; i < N; i += NT) onn[i] = onset[i] / norm;
-  __syncthreads();
+  // Long sequences split this section over three launches (launch_tempo_beats): phase 1
+  // stops after the normalised onset (meta in back[0..3]: P, -, -, ready), beat_localscore_kernel
+  // fills ls[] across the chip, phase 2 starts from ls[].
+  const bool split = !SMALL && a.phase != 0 && N >= 4;
   double lmax = -INFINITY;
-  for (int i = threadIdx.x; i < N; i += NT) {
-    const int klo = max(0, i + Pi - N + 1), khi = min(i + Pi, K - 1);
-    const float* on = onn + i + Pi;
-    double acc = 0.0;
-    for (int k = klo; k <= khi; ++k) acc = acc + tab[k] * (double)on[-k];
-    ls[i] = acc;
-    lmax = fmax(lmax, acc);
+  if (!split || a.phase == 1) {
+    double sx = 0.0;
+    for (int i = threadIdx.x; i < N; i += NT) sx += (double)onset[i];
+    sx = block_sum<NT>(sx, bs);
+    const float mean32 = (float)(sx / (double)N);
+    double sq = 0.0;
+    for (int i = threadIdx.x; i < N; i += NT) {
+      const double d = (double)(onset[i] - mean32);
+      sq += d * d;
+    }
+    sq = block_sum<NT>(sq, bs);
+    const float std32 = (float)sqrt(sq / (double)(N - 1));
+    const float norm = std32 + 1.17549435e-38f;
+
+    // onset / norm once per frame (the same f32 quotient the per-tap form computed), kept in
+    // cum's storage until the DP overwrites it
+    float* onn = reinterpret_cast<float*>(cum);
+    for (int i = threadIdx.x; i < N; i += NT) onn[i] = onset[i] / norm;
+    if (split) {  // phase 1 ends here
+      if (threadIdx.x == 0) {
+        back[0] = Pi;
+        back[3] = 1;
+      }
+      return;
+    }
+    for (int k = threadIdx.x; k < K; k += NT) tab[k] = beat_window(k, Pi, P);
+    __syncthreads();
+    for (int i = threadIdx.x; i < N; i += NT) {
+      const double acc = beat_local_score(onn, tab, i, N, Pi, K);
+      ls[i] = acc;
+      lmax = fmax(lmax, acc);
+    }
+  } else {
+    for (int i = threadIdx.x; i < N; i += NT) lmax = fmax(lmax, ls[i]);
   }
   lmax = block_max<NT>(lmax, bs);
   const double thr = 0.01 * lmax;
@@ -241,77 +291,95 @@ __global__ __launch_bounds__(NT) void tempo_beat_kernel(BeatArgs a) {
   const int B = max(1, min(dmin, NT / 2));
   const int D = dmax - dmin + 1;
   // chunk length and fold length both ~sqrt(D): the scan and the fold are serial per thread
-  const int Gn = max(1, min(NT / B, (int)ceil(sqrt((double)D))));
+#ifndef NC_BEAT_GCAP
+#define NC_BEAT_GCAP 64
+#endif
+  const int Gn = max(1, min(min(NT / B, NC_BEAT_GCAP), (int)ceil(sqrt((double)D))));
   const int C = (D + Gn - 1) / Gn;
   // long sequences: the DP reads cum[i - d] for d in [dmin, dmax] only, so the last ring_cap
   // (>= dmax + B) scores are kept in an LDS ring instead of being re-read from L2 per candidate
   double* ring = SMALL ? cum : reinterpret_cast<double*>(smem + al16((size_t)a.tab_cap * sizeof(double)));
   const int RM = SMALL ? 0x7fffffff : a.ring_cap - 1;
-  if (!SMALL && dmax + B > a.ring_cap) {
+  if (!SMALL && (dmax + B > a.ring_cap || kBeatWin > a.ring_cap)) {
     if (threadIdx.x == 0) a.nbeats_out[s] = -1;  // capacity error (cannot happen for P <= acw - 1)
     return;
   }
   const int f = threadIdx.x % B, g = threadIdx.x / B;
   const int dlo = dmin + g * C, dend = min(dmax + 1, dlo + C);
-  // ls[] two blocks ahead (long sequences: a global read whose latency would otherwise
-  // sit inside every block)
+  // Long sequences run the DP in windows of FW frames (a multiple of B): ls of the window is
+  // staged into LDS first, back[] collects in LDS, and cum / back go to global memory once
+  // per window (from the ring, which still holds the window: FW <= ring_cap).  The blocks
+  // themselves touch LDS only, so no block waits on a global round trip.  Short sequences
+  // hold everything in LDS already: one window.
   const bool fthr = threadIdx.x < B;
-  double ls_n1 = (fthr && f < N) ? ls[f] : 0.0;
-  double ls_n2 = (fthr && B + f < N) ? ls[B + f] : 0.0;
-  for (int b0 = 0; b0 < N; b0 += B) {
-    const int i = b0 + f;
-    const bool own = fthr && i < N;
-    const double lsi = ls_n1;
-    ls_n1 = ls_n2;
-    ls_n2 = (fthr && i + 2 * B < N) ? ls[i + 2 * B] : 0.0;
-    if (g < Gn) {
-      double best = -INFINITY;
-      int bd = 0x7fffffff;
-      if (i < N) {
-        const int dh = min(dend, i + 1);
-        int d = dlo;
-        for (; d + 3 < dh; d += 4) {
-          double sc[4];
+  const int FW = SMALL ? N : max(B, (kBeatWin / B) * B);
+  double* lsw = SMALL ? ls : ring + a.ring_cap;
+  int* bkw = SMALL ? back : reinterpret_cast<int*>(lsw + kBeatWin);
+  for (int w0 = 0; w0 < N; w0 += FW) {
+    const int w1 = min(N, w0 + FW);
+    if (!SMALL) {
+      for (int q = threadIdx.x; q < w1 - w0; q += NT) lsw[q] = ls[w0 + q];
+      __syncthreads();
+    }
+    for (int b0 = w0; b0 < w1; b0 += B) {
+      const int i = b0 + f;
+      const bool own = fthr && i < w1;
+      const double lsi = own ? lsw[i - w0] : 0.0;
+      if (g < Gn) {
+        double best = -INFINITY;
+        int bd = 0x7fffffff;
+        if (i < w1) {
+          const int dh = min(dend, i + 1);
+          int d = dlo;
+          for (; d + 3 < dh; d += 4) {
+            double sc[4];
 #pragma unroll
-          for (int u = 0; u < 4; ++u) sc[u] = ring[(i - d - u) & RM] - tab[d + u];
+            for (int u = 0; u < 4; ++u) sc[u] = ring[(i - d - u) & RM] - tab[d + u];
 #pragma unroll
-          for (int u = 0; u < 4; ++u)
-            if (sc[u] > best) {
-              best = sc[u];
-              bd = d + u;
+            for (int u = 0; u < 4; ++u)
+              if (sc[u] > best) {
+                best = sc[u];
+                bd = d + u;
+              }
+          }
+          for (; d < dh; ++d) {
+            const double sc = ring[(i - d) & RM] - tab[d];
+            if (sc > best) {
+              best = sc;
+              bd = d;
             }
+          }
         }
-        for (; d < dh; ++d) {
-          const double sc = ring[(i - d) & RM] - tab[d];
-          if (sc > best) {
-            best = sc;
+        dp_best[threadIdx.x] = best;
+        dp_d[threadIdx.x] = bd;
+      }
+      lds_barrier();
+      if (own) {
+        double best = -INFINITY;
+        int bd = 0x7fffffff;
+#pragma unroll 4
+        for (int q = 0; q < Gn; ++q) {
+          const double v = dp_best[q * B + f];
+          const int d = dp_d[q * B + f];
+          if (v > best || (v == best && d < bd)) {
+            best = v;
             bd = d;
           }
         }
+        const bool found = (i >= dmin) && (best > -INFINITY);
+        const double v = found ? lsi + best : lsi;
+        ring[i & RM] = v;  // = cum[i] for short sequences
+        bkw[i - w0] = (i < i0 || !found) ? -1 : i - bd;
       }
-      dp_best[threadIdx.x] = best;
-      dp_d[threadIdx.x] = bd;
+      lds_barrier();
     }
-    lds_barrier();
-    if (own) {
-      double best = -INFINITY;
-      int bd = 0x7fffffff;
-#pragma unroll 4
-      for (int q = 0; q < Gn; ++q) {
-        const double v = dp_best[q * B + f];
-        const int d = dp_d[q * B + f];
-        if (v > best || (v == best && d < bd)) {
-          best = v;
-          bd = d;
-        }
+    if (!SMALL) {
+      for (int q = threadIdx.x; q < w1 - w0; q += NT) {
+        cum[w0 + q] = ring[(w0 + q) & RM];
+        back[w0 + q] = bkw[q];
       }
-      const bool found = (i >= dmin) && (best > -INFINITY);
-      const double v = found ? lsi + best : lsi;
-      cum[i] = v;
-      if (!SMALL) ring[i & RM] = v;
-      back[i] = (i < i0 || !found) ? -1 : i - bd;
+      lds_barrier();  // the next window restages lsw / bkw
     }
-    lds_barrier();
   }
   __syncthreads();  // cum / back global stores (long sequences) visible to the whole workgroup
 
@@ -518,13 +586,18 @@ int launch_tempo_beats(Context& ctx, BeatArgs a, int n_seq, int max_len, hipStre
     int ring = 1;
     while (ring < (a.tab_cap / 2) * 5 / 2 + 2) ring <<= 1;
     a.ring_cap = ring;
-    const size_t lds = tab + (size_t)ring * sizeof(double);
+    const size_t lds = tab + (size_t)ring * sizeof(double) + (size_t)kBeatWin * (sizeof(double) + sizeof(int));
     if (lds > 150 * 1024) {
       set_error("tempo_beats: tempogram window too long");
       return -2;
     }
     {
       KTimer kt_(ctx, "tempo_beat", st);
+      a.phase = 1;
+      hipLaunchKernelGGL((tempo_beat_kernel<1024, false>), dim3(n_seq), dim3(1024), lds, st, a);
+      hipLaunchKernelGGL((beat_localscore_kernel<256>), dim3((unsigned)((max_len + 255) / 256), n_seq), dim3(256),
+                         (size_t)a.tab_cap * sizeof(double), st, a);
+      a.phase = 2;
       hipLaunchKernelGGL((tempo_beat_kernel<1024, false>), dim3(n_seq), dim3(1024), lds, st, a);
     }
   }
