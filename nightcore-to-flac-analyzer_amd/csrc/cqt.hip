@@ -8,7 +8,7 @@
 // and oracle/refglue.py (cyclic_xcorr_peak).
 //
 // Pipeline per chunk (one launch each, all chunks of the batch at once):
-//   1. decimate_kernel x6     y_{i+1} = sqrt(2) * halfband(y_i)[::2]  (soxr_hq replacement)
+//   1. decimate3_kernel x2    y_{i+1} = sqrt(2) * halfband(y_i)[::2], three levels per launch
 //   2. tuning_peaks_kernel    STFT 2048/512 (Hann) -> piptrack peaks, appended per chunk
 //   3. tuning_select_kernel   median(mag) -> residual histogram (0.01 bins) -> tuning index
 //   4. cqt_chroma_kernel      (frame pair, octave) items per wave: two rect 1024 frames as one
@@ -84,16 +84,129 @@ __global__ __launch_bounds__(256) void chroma_plan_kernel(const int64_t* chunk_l
 }
 
 // ------------------------------------------------------------------------------ 1. decimation
-// y_{i+1} = sqrt(2) * halfband(y_i)[::2] per chunk and level (nc_decim.h, f32 accumulation)
-__global__ __launch_bounds__(256) void decimate_kernel(const float* sig, const int64_t* chunk_off,
-                                                       const int64_t* oct_off, const int64_t* oct_len,
-                                                       float* ws_oct, int level, const double* __restrict__ taps) {
+// y_{i+1} = sqrt(2) * halfband(y_i)[::2] per chunk and level, f32 accumulation.
+// Three octave levels per launch (base 0: levels 1-3 from the chunk, base 3: levels 4-6
+// from level 3): a workgroup owns D3_T outputs of level base + 3 and computes the level
+// base + 1 and base + 2 spans they depend on (plus the 2K halo, recomputed by both
+// neighbours) in LDS, so the two inner levels are written once and never read back from
+// HBM.  The arithmetic is halfband_tile<true, float>'s (nc_decim.h) bit for bit: ascending
+// taps, one f32 FMA each, x sqrt(2) through f64, zeros outside each level's length.  Every
+// level is staged as its even and odd phases with origin qa - 12 (qa = first output the
+// next level computes), so a thread's four consecutive outputs read their 27 odd-phase
+// values as 7 aligned float4 LDS loads and the centre values as one.  Measured: 1.19 ->
+// 0.77 ms per bench step (isolated); 512-output tiles (26 KB LDS) were as fast alone but
+// co-resided worse with stft_mel on the other stream (step 14.5 -> 15.5 ms); 256 (14 KB)
+// gave 14.1 ms.
+constexpr int D3_T = 256;
+constexpr int D3_N1 = 4 * D3_T + 144;  // level base+1 values computed (from 4 m0 - 72)
+constexpr int D3_N2 = 2 * D3_T + 48;   // level base+2 values computed (from 2 m0 - 24)
+constexpr int D3_P0 = 4 * D3_T + 168;  // level base pairs staged (values from 8 m0 - 168)
+
+// Outputs q = qa + 4i .. qa + 4i + 3 of one level from phases E/O with origin qa - 12.
+__device__ __forceinline__ void d3_quad(const float* __restrict__ E, const float* __restrict__ O, int i,
+                                        const float (&h)[2 * kHalfbandK + 1], float r[4]) {
+  constexpr int K = kHalfbandK;
+  float xo[28], xe[4];
+#pragma unroll
+  for (int v = 0; v < 7; ++v) {
+    const float4 t = *reinterpret_cast<const float4*>(O + 4 * i + 4 * v);
+    xo[4 * v] = t.x;
+    xo[4 * v + 1] = t.y;
+    xo[4 * v + 2] = t.z;
+    xo[4 * v + 3] = t.w;
+  }
+  {
+    const float4 t = *reinterpret_cast<const float4*>(E + 4 * i + 12);
+    xe[0] = t.x;
+    xe[1] = t.y;
+    xe[2] = t.z;
+    xe[3] = t.w;
+  }
+  float acc[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int j = 0; j <= 2 * K; ++j) {
+    const int n = j - K;
+    if (n != 0 && !(n & 1)) continue;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) acc[q] = fmaf(h[j], n == 0 ? xe[q] : xo[q + 12 - (n + 1) / 2], acc[q]);
+  }
+#pragma unroll
+  for (int q = 0; q < 4; ++q) r[q] = (float)((double)acc[q] * 1.4142135623730951);
+}
+
+// Computes level values q in [qa, qa + cnt) into the next level's phases (origin qa/2 - 12
+// in pair units relative to qa: value q lands at pair (q - qa) / 2, even -> E2, odd -> O2),
+// zeros outside [0, L); stores the owned span [qa + own0, qa + own0 + own_n) to dst.
+__device__ __forceinline__ void d3_level(const float* E, const float* O, int cnt, int64_t qa, int64_t L,
+                                         const float (&h)[2 * kHalfbandK + 1], float* E2, float* O2, float* dst,
+                                         int own0, int own_n) {
+  for (int i = threadIdx.x; i < cnt / 4; i += 256) {
+    float r[4];
+    d3_quad(E, O, i, h, r);
+    const int64_t q0 = qa + 4 * i;
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      if (q0 + q < 0 || q0 + q >= L) r[q] = 0.f;
+    if (E2) {
+      *reinterpret_cast<float2*>(E2 + 2 * i) = make_float2(r[0], r[2]);
+      *reinterpret_cast<float2*>(O2 + 2 * i) = make_float2(r[1], r[3]);
+    }
+    if (4 * i >= own0 && 4 * i < own0 + own_n && q0 < L) {
+      if (q0 + 3 < L) {
+        *reinterpret_cast<float4*>(dst + q0) = make_float4(r[0], r[1], r[2], r[3]);
+      } else {
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          if (q0 + q < L) dst[q0 + q] = r[q];
+      }
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void decimate3_kernel(const float* sig, const int64_t* chunk_off,
+                                                        const int64_t* oct_off, const int64_t* oct_len,
+                                                        float* ws_oct, int base, const double* __restrict__ taps) {
+  static_assert(kHalfbandK == 23, "phase windows assume 23");
+  __shared__ __attribute__((aligned(16))) float e0[D3_P0], o0[D3_P0];
+  __shared__ __attribute__((aligned(16))) float e1[D3_N1 / 2], o1[D3_N1 / 2];
   const int c = blockIdx.y;
-  const int64_t Lin = oct_len[c * 7 + level], Lout = oct_len[c * 7 + level + 1];
-  const int64_t m0 = (int64_t)blockIdx.x * DEC_OUT;
-  if (m0 >= Lout) return;
-  const float* in = level == 0 ? sig + chunk_off[c] : ws_oct + oct_off[c * 7 + level];
-  halfband_tile<true, float>(in, Lin, ws_oct + oct_off[c * 7 + level + 1], Lout, m0, taps);
+  const int64_t* len = oct_len + c * 7 + base;
+  const int64_t m0 = (int64_t)blockIdx.x * D3_T;
+  if (m0 >= len[3]) return;
+  float h[2 * kHalfbandK + 1];
+#pragma unroll
+  for (int j = 0; j <= 2 * kHalfbandK; ++j) h[j] = (float)taps[j];
+  const float* in = base == 0 ? sig + chunk_off[c] : ws_oct + oct_off[c * 7 + base];
+  const int64_t L0 = len[0];
+  // level base: values [8 m0 - 168, 8 m0 - 168 + 2 D3_P0) as (even, odd) pairs, 4 pairs per thread step
+  const int64_t v0 = 8 * m0 - 168;
+  const bool vec = ((reinterpret_cast<uintptr_t>(in) & 15) == 0);
+  for (int u = threadIdx.x; u < D3_P0 / 2; u += 256) {  // two pairs (4 values) per iteration
+    const int64_t i = v0 + 4 * u;
+    float4 v;
+    if (vec && i >= 0 && i + 3 < L0) {
+      v = *reinterpret_cast<const float4*>(in + i);
+    } else {
+      v.x = (i >= 0 && i < L0) ? in[i] : 0.f;
+      v.y = (i + 1 >= 0 && i + 1 < L0) ? in[i + 1] : 0.f;
+      v.z = (i + 2 >= 0 && i + 2 < L0) ? in[i + 2] : 0.f;
+      v.w = (i + 3 >= 0 && i + 3 < L0) ? in[i + 3] : 0.f;
+    }
+    *reinterpret_cast<float2*>(e0 + 2 * u) = make_float2(v.x, v.z);
+    *reinterpret_cast<float2*>(o0 + 2 * u) = make_float2(v.y, v.w);
+  }
+  __syncthreads();
+  float* out1 = ws_oct + oct_off[c * 7 + base + 1];
+  float* out2 = ws_oct + oct_off[c * 7 + base + 2];
+  float* out3 = ws_oct + oct_off[c * 7 + base + 3];
+  // level base+1: [4 m0 - 72, +D3_N1), owned [4 m0, 4 m0 + 4 T); phases -> e1/o1
+  d3_level(e0, o0, D3_N1, 4 * m0 - 72, len[1], h, e1, o1, out1, 72, 4 * D3_T);
+  __syncthreads();
+  // level base+2: [2 m0 - 24, +D3_N2), owned [2 m0, 2 m0 + 2 T); phases -> e0/o0 (reused)
+  d3_level(e1, o1, D3_N2, 2 * m0 - 24, len[2], h, e0, o0, out2, 24, 2 * D3_T);
+  __syncthreads();
+  // level base+3: [m0, m0 + T), all owned
+  d3_level(e0, o0, D3_T, m0, len[3], h, nullptr, nullptr, out3, 0, D3_T);
 }
 
 // ------------------------------------------------------------------------------ 2. tuning peaks
@@ -690,13 +803,13 @@ int launch_chroma_mean(Context& ctx, const float* sig, const int64_t* chunk_off,
   // grids are sized by the longest chunk; blocks past a chunk's own length exit.  (Forking
   // the decimation onto a second stream, concurrent with the tuning estimate, measured no
   // gain: the chip is already full with the window chain on the caller's other stream.)
-  for (int lvl = 0; lvl < 6; ++lvl) {
-    const int64_t mo = (max_chunk_len >> (lvl + 1)) + 1;
-    dim3 grid((unsigned)((mo + DEC_OUT - 1) / DEC_OUT), (unsigned)n);
+  for (int base = 0; base < 6; base += 3) {
+    const int64_t mo = (max_chunk_len >> (base + 3)) + 1;  // >= the longest chunk's level base + 3
+    dim3 grid((unsigned)((mo + D3_T - 1) / D3_T), (unsigned)n);
     {
       KTimer kt_(ctx, "decimate", st);
-      hipLaunchKernelGGL(decimate_kernel, grid, dim3(256), 0, st, sig, chunk_off, w.oct_off, w.oct_len, w.ws_oct,
-                         lvl, ctx.t.halfband);
+      hipLaunchKernelGGL(decimate3_kernel, grid, dim3(256), 0, st, sig, chunk_off, w.oct_off, w.oct_len, w.ws_oct,
+                         base, ctx.t.halfband);
     }
   }
   PeakArgs pa;
