@@ -13,10 +13,13 @@ from pathlib import Path
 
 REPO = Path(__file__).resolve().parents[1]
 TAGS = {"cqt_chroma_kernel": "cqt_chroma", "stft_mel_kernel": "stft_mel", "tuning_peaks_kernel": "tuning_peaks",
-        "trim_blocks_kernel": "trim_blocks", "window_tg_kernel": "window_tg", "decimate_kernel": "decimate"}
+        "trim_blocks_kernel": "trim_blocks", "window_tg_kernel": "window_tg", "decimate_kernel": "decimate", "decimate3_kernel": "decimate"}
 # algorithmic bytes per step of the config-3 bench: 3968 windows x 882 000 B,
-# 896 chunks x 1 764 000 B, 64 pairs of 3 969 000 + 3 175 200 samples x 4 B for the trim pass
-ALG_STEP = {"cqt_chroma": 896 * 1764000, "stft_mel": 3968 * 882000, "trim_blocks": 64 * (3969000 + 3175200) * 4}
+# 896 chunks x 1 764 000 B, 64 pairs of 3 969 000 + 3 175 200 samples x 4 B for the trim pass;
+# the octave chain reads levels 0 and 3 and writes levels 1-6 once per 441 000-sample chunk
+# (441 000 + 55 125 read, 220 500 + 110 250 + 55 125 + 27 563 + 13 782 + 6 891 written, f32)
+ALG_STEP = {"cqt_chroma": 896 * 1764000, "stft_mel": 3968 * 882000, "trim_blocks": 64 * (3969000 + 3175200) * 4,
+            "decimate": 896 * 4 * (441000 + 55125 + 220500 + 110250 + 55125 + 27563 + 13782 + 6891)}
 
 
 def per_dispatch(d: Path, counter: str):
@@ -41,9 +44,10 @@ def main(out):
     commit = subprocess.run(["git", "rev-parse", "--short", "HEAD"], cwd=REPO, capture_output=True,
                             text=True).stdout.strip() or "unknown"
     kern = {}
-    # one trim pass per analyze call: the profiled run's call count, hence launches per step of
-    # every kernel (the pair-group schedule sets how many launches one step makes)
-    calls = max(1, len(fetch.get("trim_blocks", [])))
+    # two trim launches per analyze call (engine.Engine.analyze: the first pair group's files,
+    # then the rest): the profiled run's call count, hence launches per step of every kernel
+    # (the pair-group schedule sets how many launches one step makes)
+    calls = max(1, len(fetch.get("trim_blocks", [])) // 2)
     for tag in sorted(set(fetch) | set(write)):
         f = sum(fetch.get(tag, [0])) / max(1, len(fetch.get(tag, [])))
         w = sum(write.get(tag, [0])) / max(1, len(write.get(tag, [])))
