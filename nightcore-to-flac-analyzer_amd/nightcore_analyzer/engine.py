@@ -240,13 +240,18 @@ class Engine:
         self.host_stats: Optional[Dict[str, float]] = None  # {phase: seconds} when enabled
         # the chroma chain runs on its own stream, concurrently with the window/tempo chain
         # (NC_SERIAL_STREAMS=1 queues it on the launch stream instead: isolated per-kernel timings)
+        # NC_STREAM_PRIO="chroma,tail" sets the two side streams' priorities (torch: lower = more
+        # urgent; the launch stream stays at 0).  Both side streams ahead of the window chain
+        # measured 14.20 ms per bench step against 14.26 at 0,0 (tools/prio_probe.sh, two
+        # alternated reps each: small, but the same sign in both)
+        prio = [int(v) for v in os.environ.get("NC_STREAM_PRIO", "-1,-1").split(",")]
         self.chroma_stream = torch.cuda.current_stream(self.dev) if os.environ.get("NC_SERIAL_STREAMS") == "1" \
-            else torch.cuda.Stream(self.dev)
+            else torch.cuda.Stream(self.dev, priority=prio[0])
         # consensus tail (bootstraps + D2H of a group) on a third stream: the window chain of the
         # next group starts as soon as this group's window chain is done, instead of queueing
         # behind a bootstrap that waits for this group's (longer) chroma chain
         self.tail_stream = torch.cuda.current_stream(self.dev) if os.environ.get("NC_SERIAL_STREAMS") == "1" \
-            else torch.cuda.Stream(self.dev)
+            else torch.cuda.Stream(self.dev, priority=prio[1])
         # leading tuning frames of a chunk computed inside the window STFT (nc_window_stage_tuning);
         # NC_SHARE_TUNING=0 runs every tuning frame in the chroma chain instead (same results)
         self.share_tuning = os.environ.get("NC_SHARE_TUNING", "1") != "0"

@@ -54,6 +54,20 @@ def test_chroma_mean_and_tuning_match_oracle(gpu_ctx, seed):
         np.testing.assert_allclose(got[i], ref_c, rtol=0, atol=2e-5)
 
 
+def test_chroma_ragged_chunks_across_decimator_tiles(gpu_ctx):
+    """The fused octave chain (cqt.hip decimate3_kernel) owns 2048 level-0 samples per tile:
+    chunk lengths one sample either side of a tile edge and at odd offsets (no aligned
+    float4 path) must give the oracle's chroma like the 20 s chunks do."""
+    nc, src = synth.make_pair(30.0, 1003)
+    sig = np.concatenate([src, nc]).astype(np.float32)
+    chunks = [(1, 2048 * 40 + 1), (3, 2048 * 41 - 1), (len(src) + 5, 2048 * 64), (len(src) + 2, 2048 * 48 + 2047)]
+    got, tun, _, _ = _chroma_gpu(gpu_ctx, sig, chunks)
+    for i, (o, L) in enumerate(chunks):
+        y = sig[o:o + L]
+        ref_c = ncref.chroma_cqt(y, 22050, 512, 36, tuning=float(tun[i])).mean(axis=1)
+        np.testing.assert_allclose(got[i], ref_c, rtol=0, atol=2e-5, err_msg=f"chunk {i} len {L}")
+
+
 def test_chunk_lags_match_reference_glue(gpu_ctx):
     nc, src = synth.make_pair(65.0, 1001)
     plan = refglue.chunk_plan(len(src), len(nc))
