@@ -186,6 +186,7 @@ class Params:
     auto_align: bool = False
     compute_pitch: bool = True
     compute_ibi: bool = True
+    ibi_beats: bool = False      # also copy the hop-64 beat frames back (detail["ibi_beats"]: (nc, src))
 
 
 def _group_bounds(B: int, group_pairs, ) -> List[Tuple[int, int]]:
@@ -915,7 +916,7 @@ class Engine:
         # ---------------------------------------------------------------- 5. IBI pass (window stream)
         ibi = None
         if p.compute_ibi:
-            ibi = self._ibi_pass(signals, d["f_off"], d["f_len"], f_len, prior, B)
+            ibi = self._ibi_pass(signals, d["f_off"], d["f_len"], f_len, prior, B, p.ibi_beats)
         ev_window = torch.cuda.Event()
         ev_window.record(s1)
 
@@ -956,6 +957,8 @@ class Engine:
                         h.copy_(v, non_blocking=True)
                         pinned.append(h)
                         host["ibi_" + k] = h.numpy()
+                    else:
+                        host["ibi_" + k] = v
             ev = torch.cuda.Event()
             ev.record(s3)
         return dict(p=p, host=host, pinned=pinned, event=ev, keep=(d, o, ar, ibi, peaks), has_ibi=ibi is not None,
@@ -1027,7 +1030,7 @@ class Engine:
         return dict(onset=onset, fbase=fbase, fbase_h=fb_h, frames=frames, tg=tg, bpm=bpm, lag=lag, nbeats=nb,
                     margin=mg, beats=beats, ibis=ibis, nibi=nibi)
 
-    def _ibi_pass(self, signals, d_off, d_len, f_len, prior, B):
+    def _ibi_pass(self, signals, d_off, d_len, f_len, prior, B, keep_beats=False):
         dev, st = self.dev, self.stream()
         nF = 2 * B
         starts = torch.cat([prior[:B], torch.full((1,), 120.0, dtype=torch.float64, device=dev)])
@@ -1059,7 +1062,10 @@ class Engine:
                   dd["b_off"].data_ptr(), b_n.data_ptr(), B, C.N_BOOTSTRAP, dd["seed"].data_ptr(), il, gl, ih, gh,
                   4, out[0:B].data_ptr(), out[B:2 * B].data_ptr(), out[2 * B:].data_ptr(), None,
                   dd["wsoff"].data_ptr(), dd["cap"].data_ptr(), ws.data_ptr(), ws.numel(), st)
-        return dict(out=out, nibi=nibi, nbeats=nb, bpm=bpm, lag=lag, margin=mg)
+        res = dict(out=out, nibi=nibi, nbeats=nb, bpm=bpm, lag=lag, margin=mg)
+        if keep_beats:
+            res.update(beats=core["beats"], fbase=fb_h)
+        return res
 
     # -------------------------------------------------------------- host assembly + logs
     def _assemble_pair(self, b, p: Params, h, ibi, starts, w0, w1, f_len, strip_len, lead, trail, intro,
@@ -1184,6 +1190,9 @@ class Engine:
             out.detail.update(ibi_nbeats=(int(ibi["nbeats"][2 * b]), int(ibi["nbeats"][2 * b + 1])),
                               ibi_n=(int(nb_[2 * b]), int(nb_[2 * b + 1])),
                               ibi_lag=(int(ibi["lag"][2 * b]), int(ibi["lag"][2 * b + 1])))
+            if "beats" in ibi:
+                fb, bt, nbt = ibi["fbase"], ibi["beats"], ibi["nbeats"]
+                out.detail["ibi_beats"] = tuple(bt[fb[f]:fb[f] + max(0, int(nbt[f]))].copy() for f in (fn, fs))
         L("Done.")
         out.result = res
         return out

@@ -178,14 +178,22 @@ def tempogram_mean(onset: np.ndarray, win: int, block: int = 4096) -> np.ndarray
     materialises the whole (win, n) matrix; the mean is identical up to f64
     summation order)."""
     onset = np.asarray(onset, dtype=np.float32)
+    return tempogram_sum(onset, win, 0, onset.shape[-1], block) / onset.shape[-1]
+
+
+def tempogram_sum(onset: np.ndarray, win: int, f0: int, f1: int, block: int = 4096) -> np.ndarray:
+    """Sum over tempogram frames [f0, f1) of the inf-normalised autocorrelation columns
+    (the body of tempogram_mean; a frame range lets a fixture script split one long
+    signal's tempogram over processes)."""
+    onset = np.asarray(onset, dtype=np.float32)
     n = onset.shape[-1]
     p = win // 2
     padded = np.pad(onset, (p, p), mode="linear_ramp", end_values=(0, 0))
     w = hann(win)
     n_pad = 2 * win - 1
     acc = np.zeros(win, dtype=np.float64)
-    for b0 in range(0, n, block):
-        b1 = min(n, b0 + block)
+    for b0 in range(f0, f1, block):
+        b1 = min(f1, b0 + block)
         idx = np.arange(b0, b1)[:, None] + np.arange(win)[None, :]
         fr = padded[idx] * w[None, :]                       # f64
         ps = np.abs(np.fft.rfft(fr, n=n_pad, axis=-1)) ** 2
@@ -193,7 +201,7 @@ def tempogram_mean(onset: np.ndarray, win: int, block: int = 4096) -> np.ndarray
         mx = np.max(np.abs(ac), axis=-1, keepdims=True)
         mx[mx < TINY64] = 1.0
         acc += np.sum(ac / mx, axis=0)
-    return acc / n
+    return acc
 
 
 def tempo_frequencies(n_bins, sr=22050, hop=512) -> np.ndarray:

@@ -10,6 +10,9 @@ PIPELINE_CASES = [
     ("chords75_silence", 75.0, 1002, "chords", {"src_trim_sec": 1.5}, "silence"),
     ("chords60_gate", 60.0, 1003, "chords", {"energy_gate_db": -20.0}, "quiet"),
     ("chords60_intro", 60.0, 1005, "chords", {"auto_align": True}, "intro"),
+    # the reference's two failure paths (pipeline.py:142-146, consensus.py:544-548): logs up to the raise
+    ("sweep30_gate_all", 30.0, 1000, "sweep", {"energy_gate_db": 1.0}, None),
+    ("sweep30_nc_tail_quiet", 30.0, 1000, "sweep", {}, "nc_tail_quiet"),
 ]
 
 # xcorr.find_content_offset cases: (seconds, seed, intro seconds, resample_poly up, down)
@@ -38,6 +41,11 @@ def edit(nc, src, how, seed, synth=None, seconds=None):
     if how == "silence":
         src = np.concatenate([np.zeros(50_000, np.float32), src, np.zeros(30_001, np.float32)])
         nc = np.concatenate([np.zeros(12_345, np.float32), nc])
+    elif how == "nc_tail_quiet":
+        # nc windows [10, 20) s at -50 dB: kept by the -60 dB silence trim, dropped by the
+        # -40 dB energy gate, leaving 2 nightcore tempo windows (< MIN_VALID = 3)
+        nc = nc.copy()
+        nc[10 * 22050:] *= np.float32(10 ** (-50 / 20))
     elif how == "quiet":
         a, b = 300_000, 300_000 + 12 * 22050
         src = src.copy()

@@ -431,7 +431,10 @@ def main(argv=None):
         _dump("spectral.json", gen_spectral(mods))
     if not argv or "pipeline" in argv:
         names = [a for a in argv if a not in ("units", "pipeline", "spectral")] or None
-        _dump("pipeline.json", gen_pipeline(mods, names))
+        cases = gen_pipeline(mods, names)
+        if names:        # regenerate only the named cases, keep the others
+            cases = {**json.loads((OUT / "pipeline.json").read_text()), **cases}
+        _dump("pipeline.json", cases)
 
 
 if __name__ == "__main__":

@@ -1,0 +1,161 @@
+"""GPU parity of the engine's batched, multi-group path: the one bench.py times
+(BASELINE config 3: 64 three-minute pairs per GPU).
+
+``Engine.analyze`` splits a batch of more than 16 pairs into pair groups (6/26/26/6
+for 64), runs the silence trim in two launches (the first group's files, then the
+rest on the tail stream), keeps up to GROUPS_IN_FLIGHT groups queued and recycles
+the piptrack peak lists through a ring of GROUPS_IN_FLIGHT + 1 workspaces
+(engine.py ``_analyze`` / ``_launch_group``).  None of that runs for B <= 16, so
+these tests check, on batches that take it:
+
+* every pair of the config-3 batch equals its own B = 1 run (results, report
+  text, logs, chunk lags, tempo margins), and the first and last pairs equal the
+  CPU oracle (oracle/refglue.run_arrays: the port of pipeline.py:23-216);
+* every PIPELINE_CASES golden (the reference's own pipeline.run outputs) inside a
+  17-pair batch, with the default schedule and with group_pairs=3 (6 groups, more
+  than the peak ring's 4 slots), equals the fixture field for field, including
+  str(result), the logs and the CLI JSON.
+"""
+import dataclasses
+import math
+import multiprocessing as mp
+
+import numpy as np
+import pytest
+import torch
+
+from nightcore_analyzer import engine as E
+from nightcore_analyzer import export, synth
+from nightcore_analyzer.cli import output_dict
+
+from golden.cases import PIPELINE_CASES, make_case
+
+pytestmark = pytest.mark.gpu
+
+N_PAIRS = 64          # BASELINE config 3
+N_LOAD_LINES = 4      # pipeline.run's "Loading ..." lines come from the caller (pipeline._load)
+
+
+def _gen(seed):
+    return synth.make_pair(180.0, seed)
+
+
+@pytest.fixture(scope="module")
+def eng():
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    return E.get_engine(0)
+
+
+@pytest.fixture(scope="module")
+def bench_pairs():
+    # spawn: the children never touch the GPU and start from a clean interpreter
+    with mp.get_context("spawn").Pool(8) as pool:
+        return pool.map(_gen, [1000 + i for i in range(N_PAIRS)])
+
+
+def _norm(x):
+    if isinstance(x, dict):
+        return {k: _norm(v) for k, v in x.items()}
+    if isinstance(x, (list, tuple)):
+        return [_norm(v) for v in x]
+    if isinstance(x, float) and not math.isfinite(x):
+        return repr(x)
+    if isinstance(x, np.ndarray):
+        return _norm(x.tolist())
+    return x
+
+
+def _key(o: E.PairOutcome):
+    """Everything a caller can observe of one pair's outcome."""
+    d = {k: _norm(v) for k, v in o.detail.items()}
+    if o.error is not None:
+        return ("error", type(o.error).__name__, str(o.error), o.logs, d)
+    return ("ok", _norm(dataclasses.asdict(o.result)), str(o.result), o.logs, d)
+
+
+def test_group_schedule_is_multi_group():
+    assert [b - a for a, b in E._group_bounds(N_PAIRS, None)] == [6, 26, 26, 6]
+    assert len(E._group_bounds(17, 3)) == 6 > E.Engine.GROUPS_IN_FLIGHT + 1
+
+
+def test_config3_batch_equals_single_pair_runs(eng, bench_pairs):
+    p = E.Params(compute_ibi=False)                       # the bench's step
+    outs = eng.analyze(bench_pairs, p)
+    assert len(outs) == N_PAIRS
+    for i, (pair, o) in enumerate(zip(bench_pairs, outs)):
+        assert o.error is None, (i, o.error)
+        single, = eng.analyze([pair], p)
+        assert _key(o) == _key(single), f"pair {i} differs from its B=1 run"
+    # the same batch again (workspaces, peak ring and pinned buffers reused): identical
+    again = eng.analyze(bench_pairs, p)
+    assert [_key(o) for o in again] == [_key(o) for o in outs]
+
+
+@pytest.mark.parametrize("i", [0, N_PAIRS - 1])
+def test_config3_batch_matches_oracle(eng, bench_pairs, i):
+    from oracle import refglue
+    outs = eng.analyze(bench_pairs, E.Params(compute_ibi=False))
+    r, d = outs[i].result, outs[i].detail
+    nc, src = bench_pairs[i]
+    ref = refglue.run_arrays(nc, src, compute_ibi=False)
+    assert r.src_tempos_raw == ref["src_tempos"] and r.nc_tempos_raw == ref["nc_tempos"]
+    assert d["chunk_lags"] == ref["chunk_lags"]
+    assert d["nc_start_bpm"] == ref["nc_start_bpm"]
+    for k in ("tempo_ratio", "pitch_ratio", "classification", "n_source_tempo_windows", "n_nc_tempo_windows",
+              "nc_median_bpm", "src_median_bpm"):
+        assert getattr(r, k) == ref[k], k
+    assert tuple(r.tempo_ci) == tuple(ref["tempo_ci"]) and tuple(r.pitch_ci) == tuple(ref["pitch_ci"])
+    assert r.src_duration / r.nc_duration == 1.25          # exact sample-count ratio
+
+
+def _kw_classes():
+    out = {}
+    for name, _, _, _, kw, _ in PIPELINE_CASES:
+        out.setdefault(tuple(sorted(kw.items())), []).append(name)
+    return sorted(out.items(), key=lambda kv: kv[1][0])
+
+
+@pytest.mark.parametrize("group_pairs", [None, 3])
+@pytest.mark.parametrize("kw_names", _kw_classes(), ids=lambda kv: "+".join(kv[1]))
+def test_goldens_inside_multi_group_batch(eng, bench_pairs, golden_pipeline, kw_names, group_pairs):
+    kwkey, names = kw_names
+    kw = dict(kwkey)
+    p = E.Params(**kw)                                     # run()'s defaults + this case's kwargs
+    cases = [make_case(synth, n)[:2] for n in names]
+    pad = bench_pairs[:17 - len(cases)]
+    # goldens first, in the middle and last: each lands in a different group
+    batch = list(pad)
+    slots = [0, len(batch) // 2, len(batch)][:len(cases)]
+    for s, c in sorted(zip(slots, cases), key=lambda t: -t[0]):
+        batch.insert(s, c)
+    pos = {}
+    for n, c in zip(names, cases):
+        pos[n] = next(j for j, b in enumerate(batch) if b is c)
+    assert len(batch) >= 17
+    outs = eng.analyze(batch, p, group_pairs=group_pairs)
+    for n in names:
+        g = golden_pipeline[n]
+        o = outs[pos[n]]
+        assert o.logs == g["log"][N_LOAD_LINES:], n
+        if "error" in g:
+            assert o.error is not None and type(o.error).__name__ == g["error"]["type"], n
+            assert str(o.error) == g["error"]["message"], n
+            continue
+        assert o.error is None, (n, o.error)
+        r, exp = o.result, g["result"]
+        got = _norm({k: getattr(r, k) for k in exp})
+        for k in exp:
+            assert got[k] == exp[k], (n, k)
+        assert str(r) == g["str"], n
+        assert _norm(export.to_dict(r)) == g["export_dict"], n
+        if "cli_json" in g:
+            assert _norm(output_dict(r)) == g["cli_json"], n
+    # the padding pairs equal their own B = 1 runs under the same parameters
+    for j, pair in enumerate(batch):
+        if any(pair is c for c in cases):
+            continue
+        if j % 4:                                          # a sample keeps the test short
+            continue
+        single, = eng.analyze([pair], p)
+        assert _key(outs[j]) == _key(single), j

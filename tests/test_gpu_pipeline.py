@@ -44,6 +44,7 @@ def test_run_matches_reference_golden(name, golden_pipeline):
             NA.run(nc, src, log=logs.append, **kw)
         assert type(ei.value).__name__ == g["error"]["type"]
         assert str(ei.value) == g["error"]["message"]
+        assert logs == g["log"]          # every line the reference logged before raising
         return
     r = NA.run(nc, src, log=logs.append, **kw)
     exp = g["result"]

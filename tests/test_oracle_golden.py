@@ -107,3 +107,15 @@ def test_run_arrays_matches_reference_pipeline(golden_pipeline, name, ibi):
     assert list(res["tempo_ci"]) == e["tempo_ci"] and list(res["pitch_ci"]) == e["pitch_ci"]
     if ibi:
         assert res["ibi_ratio"] == e["ibi_ratio"] and list(res["ibi_ci"]) == e["ibi_ci"]
+
+
+@pytest.mark.parametrize("name", ["sweep30_gate_all", "sweep30_nc_tail_quiet"])
+def test_run_arrays_failure_paths_match_reference(golden_pipeline, name):
+    """The reference's two failure exits (pipeline.py:142-146 RuntimeError, consensus.py:544-548
+    ValueError): the oracle raises the same type with the same message."""
+    g = golden_pipeline[name]
+    nc, src, kw = make_case(synth, name)
+    assert _sha(nc) == g["nc_sha256"] and _sha(src) == g["src_sha256"]
+    with pytest.raises(Exception) as ei:
+        refglue.run_arrays(nc, src, compute_ibi=False, **kw)
+    assert type(ei.value).__name__ == g["error"]["type"] and str(ei.value) == g["error"]["message"]
