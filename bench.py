@@ -90,6 +90,15 @@ def _cpu_worker(args):
     return nw, t0, t1, res["tempo_ratio"], res["pitch_ratio"], ncp
 
 
+def host_cores():
+    """Host cores this process may run on (one CPU worker per core).  On the
+    GPU box the affinity mask can show the whole machine; the per-GPU CPU share is what
+    OMP_NUM_THREADS is set to there, so the count is capped at it when it is set."""
+    n = len(os.sched_getaffinity(0))
+    cap = os.environ.get("OMP_NUM_THREADS")
+    return max(1, min(n, int(cap))) if cap and cap.isdigit() else n
+
+
 def cpu_baseline(seconds, base_seed, workers):
     """The oracle (oracle/refglue.py, the CPU port of the reference glue on the numpy
     restatement of librosa) on the first `workers` pairs of the batch, one pair per
@@ -122,7 +131,9 @@ def main():
     ap.add_argument("--no-config5", action="store_true", help="skip the 60-min pair (BASELINE configs[4]) timing")
     ap.add_argument("--no-spectral", action="store_true", help="skip the spectral.analyze (SURVEY.md §8f) timing")
     ap.add_argument("--no-resample", action="store_true", help="skip the load-time resampler (SURVEY.md §8f) timing")
-    ap.add_argument("--cpu-workers", type=int, default=8, help="CPU baseline processes (one pair each)")
+    ap.add_argument("--cpu-workers", type=int, default=0,
+                    help="CPU baseline processes, one pair each (0: the host cores this process may run on)")
+    ap.add_argument("--no-upload", action="store_true", help="skip the upload-included throughput")
     ap.add_argument("--workers", type=int, default=min(16, os.cpu_count() or 1))
     args = ap.parse_args()
 
@@ -131,12 +142,13 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # the synthetic pairs are made (forked workers) before this process touches the GPU
+    pairs = make_pairs(args.pairs, args.seconds, 1000 + rank * args.pairs, max(1, args.workers // max(1, world)))
     if world > 1:
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     from nightcore_analyzer import engine as E
 
-    pairs = make_pairs(args.pairs, args.seconds, 1000 + rank * args.pairs, max(1, args.workers // max(1, world)))
     eng = E.get_engine(local)
     flat = []
     for nc, src in pairs:
@@ -156,6 +168,10 @@ def main():
     for _ in range(max(0, args.warmup - 1)):
         eng.analyze(signals=signals, params=params)
 
+    # timed region: K steps with the kernels' own execution spans recorded (nc_profile mode 2:
+    # two fire-and-forget atomics per wave, no host work per launch), so the per-kernel
+    # durations below come from exactly the launches the headline number times
+    eng.kernel_profile(2)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -166,49 +182,100 @@ def main():
     if world > 1:
         dist.barrier()
     el = time.perf_counter() - t0
+    spans = eng.kernel_spans()
+    eng.kernel_profile(False)
     if world > 1:
         t = torch.tensor([el], dtype=torch.float64, device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
+    step_ms = el / args.steps * 1e3
+    # {kernel: (average launch ms, launches per step)} from the spans of the timed region
+    kper = {k: (ms / n, n / args.steps) for k, (ms, n) in spans.items()}
 
-    # per-kernel timing with HIP events on the launch stream (separate, non-timed steps): entry points
-    # (engine) and, inside them, the dominant kernels (libncgpu nc_profile_*, same stream)
+    # entry-point HIP-event timers (separate, untimed steps)
     eng.start_timers()
-    eng.kernel_profile(True)
     ksteps = max(1, min(args.steps, 3))
     for _ in range(ksteps):
         eng.analyze(signals=signals, params=params)
     timers = eng.stop_timers()
-    ktimes = eng.kernel_times()
-    eng.kernel_profile(False)
     per = {k: (ms / n, n // ksteps) for k, (ms, n) in timers.items()}
-    kper = {k: (ms / n, n / ksteps) for k, (ms, n) in ktimes.items()}
-    # algorithmic bytes per launch = SURVEY.md §8d per-unit bytes x units per launch
+
+    # algorithmic bytes / flops per launch = SURVEY.md §8d per-unit figure x units per launch
     units = {"stft_mel": (win_per_step, WIN_BYTES, WIN_FLOP), "cqt_chroma": (chunks_per_step, CHUNK_BYTES, CHUNK_FLOP)}
+
+    def roof(tag, times):
+        if tag not in times or tag not in units:
+            return None
+        avg_ms, launches = times[tag]
+        alg = units[tag][0] / launches * units[tag][1]
+        flop = units[tag][0] / launches * units[tag][2]
+        a = alg / (avg_ms * 1e-3) / 1e9
+        c = flop / (avg_ms * 1e-3) / 1e12
+        return {"bound": "hbm", "kernel": tag, "achieved": a, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": a / HBM_PEAK_GBS, "traffic": None, "alg_bytes_per_launch": alg, "avg_launch_ms": avg_ms,
+                "launches_per_step": launches,
+                # the roof that actually binds: f32 VALU, no MFMA on this path
+                "compute": {"bound": "valu_f32", "achieved": c, "peak": VALU_PEAK_TFS, "unit": "TFLOP/s",
+                            "frac": c / VALU_PEAK_TFS, "alg_flop_per_launch": flop}}
+
+    # the dominant kernel = the largest total execution time per step among the kernels with a
+    # §8d unit (what rocprofv3 --stats ranks first); cqt_chroma (north_star's named target) is
+    # always reported beside it
     dom = max(units, key=lambda k: kper.get(k, (0, 0))[0] * kper.get(k, (0, 0))[1])
-    avg_ms, launches = kper[dom]
-    alg_per_launch = units[dom][0] / launches * units[dom][1]
-    achieved = alg_per_launch / (avg_ms * 1e-3) / 1e9
-    flop_per_launch = units[dom][0] / launches * units[dom][2]
-    tflops = flop_per_launch / (avg_ms * 1e-3) / 1e12
+    roofline = roof(dom, kper)
     traffic = _pmc_traffic(dom)
-    step_ms = el / args.steps * 1e3
-    # the same kernel launched alone (streams serialized for one more untimed step): its own
-    # speed, where the launches above share the chip with the other stream's chain
+    if traffic:
+        roofline.update(traffic=traffic["bytes_per_launch"], traffic_source=traffic["source"])
+    if dom != "cqt_chroma" and "cqt_chroma" in kper:
+        roofline["cqt_chroma"] = roof("cqt_chroma", kper)
+    # the same kernels launched alone (streams serialized for one more untimed step): their own
+    # speed, where the timed launches share the chip with the other streams' chains
     eng.set_serial(True)
-    eng.kernel_profile(True)
+    eng.kernel_profile(2)
     eng.analyze(signals=signals, params=params)
-    iso = eng.kernel_times()
+    iso = eng.kernel_spans()
     eng.kernel_profile(False)
     eng.set_serial(False)
-    iso_ms = iso[dom][0] / iso[dom][1] if dom in iso else None
-    isolated = None
-    if iso_ms:
-        a_iso = units[dom][0] / iso[dom][1] * units[dom][1] / (iso_ms * 1e-3) / 1e9
-        f_iso = units[dom][0] / iso[dom][1] * units[dom][2] / (iso_ms * 1e-3) / 1e12
-        isolated = {"avg_launch_ms": iso_ms, "achieved": a_iso, "frac": a_iso / HBM_PEAK_GBS,
-                    "compute_achieved": f_iso, "compute_frac": f_iso / VALU_PEAK_TFS,
-                    "kernels_ms_per_step": {k: round(v[0], 4) for k, v in iso.items()}}
+    iso_t = {k: (ms / n, n) for k, (ms, n) in iso.items()}
+    roofline["isolated"] = {"kernels_ms_per_step": {k: round(v[0], 4) for k, v in iso.items()},
+                            **{k: roof(k, iso_t) for k in units if k in iso_t}}
+
+    # upload included: the same K steps with every step's 64 pairs copied host -> HBM from
+    # pinned memory on a copy stream, double-buffered (step j + 1 uploads while step j runs)
+    upl = None
+    if not args.no_upload:
+        host = signals.buf.cpu().pin_memory()
+        bufs = [signals.buf, torch.empty_like(signals.buf)]
+        cs = torch.cuda.Stream(eng.dev)
+        evs = [torch.cuda.Event(), torch.cuda.Event()]
+
+        def upload(j):
+            with torch.cuda.stream(cs):
+                bufs[j % 2].copy_(host, non_blocking=True)
+                evs[j % 2].record(cs)
+        n_up = max(2, min(args.steps, 10))
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        upload(0)
+        for j in range(n_up):
+            if j + 1 < n_up:
+                upload(j + 1)
+            torch.cuda.current_stream(eng.dev).wait_event(evs[j % 2])
+            eng.analyze(signals=E.DeviceSignals(bufs[j % 2], signals.off, signals.length), params=params)
+        torch.cuda.synchronize()
+        t_up = time.perf_counter() - t1
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        with torch.cuda.stream(cs):
+            e0.record(cs)
+            bufs[1].copy_(host, non_blocking=True)
+            e1.record(cs)
+        torch.cuda.synchronize()
+        h2d_ms = e0.elapsed_time(e1)
+        upl = {"value": world * win_per_step * n_up / t_up, "unit": "windows/s", "steps": n_up,
+               "ms_per_step": t_up / n_up * 1e3, "bytes_per_step": int(host.numel() * 4),
+               "h2d_ms_per_step_alone": h2d_ms, "h2d_gb_per_s": host.numel() * 4 / (h2d_ms * 1e-3) / 1e9,
+               "how": "pinned host staging, H2D on its own stream, double-buffered against the analysis"}
+        del host, bufs
 
     ibi = None
     if not args.no_ibi and rank == 0:
@@ -232,7 +299,8 @@ def main():
     cfg5 = None
     if not args.no_config5 and rank == 0 and world == 1:
         from nightcore_analyzer import xcorr as X
-        nc5, src5 = make_pairs(1, 3600.0, 5000, 1)[0]
+        from nightcore_analyzer import synth
+        nc5, src5 = synth.make_pair(3600.0, 5000)          # in-process: no fork after GPU init
         sig5 = eng.upload_signals([nc5, src5])
         eng.analyze(signals=sig5, params=E.Params(compute_ibi=True))
         torch.cuda.synchronize()
@@ -265,10 +333,10 @@ def main():
             ev.synchronize()
             res = eng.spectral_finish(h)
         t_spec = (time.perf_counter() - t1) / reps
-        eng.kernel_profile(True)
+        eng.kernel_profile(2)
         for _ in range(reps):
             eng.spectral_frames(signals.buf, signals.off, signals.length, srs)[0].synchronize()
-        sk = {k: (ms / n, n / reps) for k, (ms, n) in eng.kernel_times().items()}
+        sk = {k: (ms / n, n / reps) for k, (ms, n) in eng.kernel_spans().items()}
         eng.kernel_profile(False)
         frames = int(h["T"].sum())
         fr_ms = sk["spectral_frames"][0]
@@ -359,24 +427,16 @@ def main():
                                    "pipeline.run analysis without the hop-64 IBI pass",
                        "pairs_per_gpu": args.pairs, "windows_per_gpu_step": win_per_step,
                        "cqt_chunks_per_gpu_step": chunks_per_step, "parallelism": f"dp{world} (pairs sharded)"},
-            "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS,
-                         "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
-                         "traffic": traffic["bytes_per_launch"] if traffic else None,
-                         "traffic_source": traffic["source"] if traffic else None,
-                         "alg_bytes_per_launch": alg_per_launch, "avg_launch_ms": avg_ms,
-                         "launches_per_step": launches,
-                         # the roof that actually binds: f32 VALU, no MFMA on this path
-                         "compute": {"bound": "valu_f32", "achieved": tflops, "peak": VALU_PEAK_TFS,
-                                     "unit": "TFLOP/s", "frac": tflops / VALU_PEAK_TFS,
-                                     "alg_flop_per_launch": flop_per_launch},
-                         # achieved/avg_launch_ms above: launches as they run in the step, sharing
-                         # the chip with the concurrent chain (what rocprofv3 --stats averages);
-                         # isolated: the same kernel with the other streams idle
-                         "isolated": isolated},
+            # avg_launch_ms: the kernel's execution spans over the timed steps (rocprofv3's
+            # kernel duration, sharing the chip with the concurrent chain); isolated: the same
+            # kernels with the other streams idle
+            "roofline": roofline,
             "kernels_ms_per_step": {k: round(v[0] * v[1], 4) for k, v in kper.items()},
             "entry_points_ms_per_step": {k: round(v[0] * v[1], 4) for k, v in per.items()},
             "check": {"tempo_ratio_pair0": tr, "pitch_ratio_pair0": pr},
         }
+        if upl is not None:
+            line["upload_included"] = upl
         if ibi is not None:
             line["ibi_pass"] = ibi
         if cfg5 is not None:
@@ -386,7 +446,7 @@ def main():
         if rsmp is not None:
             line["resample"] = rsmp
         if world == 1 and not args.no_cpu_baseline:
-            line["cpu_baseline"] = cpu_baseline(args.seconds, 1000, args.cpu_workers)
+            line["cpu_baseline"] = cpu_baseline(args.seconds, 1000, args.cpu_workers or host_cores())
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.barrier()

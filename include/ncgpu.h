@@ -48,14 +48,21 @@ int nc_destroy(nc_ctx* ctx);
 /* number of compute units seen by the context (256 on MI355X) */
 int nc_num_cu(const nc_ctx* ctx);
 
-/* Opt-in per-kernel timing (no reference equivalent; measurement only).  While
- * enabled, the dominant kernels are bracketed by HIP events on their stream;
- * nc_profile_read(tag) waits for the recorded launches, returns their summed
- * duration and count, and resets the tag.  Tags: "stft_mel", "window_tg",
- * "tuning_peaks", "decimate", "cqt_chroma", "trim_blocks", "tempo_beat",
- * "tg_slide", "spectral_frames", "spectral_bins".  Enabling (or disabling) discards pending records. */
+/* Opt-in per-kernel timing (no reference equivalent; measurement only).
+ * on = 1: the dominant kernels are bracketed by HIP events on their stream AND record
+ *         their own execution span; on = 2: spans only (no host work per launch, cheap
+ *         enough for a timed region); on = 0: off.
+ * nc_profile_read(tag) waits for the recorded launches, returns their summed event
+ * duration and count, and resets the tag's events.  nc_profile_read_span(tag) returns
+ * the summed execution spans (first wave start .. last wave end on the device wall
+ * clock: the duration rocprofv3 --kernel-trace reports, without the time a kernel
+ * queues behind other streams' work) and resets the tag's spans.  Tags: "stft_mel",
+ * "window_tg", "tuning_peaks", "decimate", "cqt_chroma", "trim_blocks", "tempo_beat",
+ * "tg_slide", "spectral_frames", "spectral_bins".  Enabling (or disabling) discards
+ * pending records. */
 int nc_profile_enable(nc_ctx* ctx, int on);
 int nc_profile_read(nc_ctx* ctx, const char* tag, double* total_ms, int* launches);
+int nc_profile_read_span(nc_ctx* ctx, const char* tag, double* total_ms, int* launches);
 
 /* ---------------------------------------------------------------------------
  * K1a  silence trim — replaces io.strip_silence (io.py:58-79) ->

@@ -48,6 +48,7 @@ struct BeatArgs {
   int tab_cap;          // doubles for the window / penalty table
   int ring_cap;         // !SMALL: LDS ring of the last ring_cap cumulative scores (power of 2)
   int phase;            // !SMALL: 0 one launch, 1 up to the normalised onset, 2 from the local score
+  unsigned long long* span = nullptr;  // nc_profile execution span (nc_device.h)
 };
 
 __host__ __device__ __forceinline__ size_t al16(size_t n) { return (n + 15) & ~(size_t)15; }
@@ -110,6 +111,7 @@ constexpr int kBeatWin = 1024;  // long-sequence DP window (frames staged per gl
 template <int NT, bool SMALL>
 __global__ __launch_bounds__(NT) void tempo_beat_kernel(BeatArgs a) {
 #pragma clang fp contract(off)
+  const Span span_(a.span);
   extern __shared__ __attribute__((aligned(16))) char smem[];
   __shared__ BlockScratch<NT> bs;
   __shared__ int hist[256];
@@ -575,6 +577,7 @@ int launch_tempo_beats(Context& ctx, BeatArgs a, int n_seq, int max_len, hipStre
   if (small_lds <= 64 * 1024) {
     {
       KTimer kt_(ctx, "tempo_beat", st);
+      a.span = kt_.span();
       hipLaunchKernelGGL((tempo_beat_kernel<256, true>), dim3(n_seq), dim3(256), small_lds, st, a);
     }
   } else {
@@ -593,6 +596,7 @@ int launch_tempo_beats(Context& ctx, BeatArgs a, int n_seq, int max_len, hipStre
     }
     {
       KTimer kt_(ctx, "tempo_beat", st);
+      a.span = kt_.span();
       a.phase = 1;
       hipLaunchKernelGGL((tempo_beat_kernel<1024, false>), dim3(n_seq), dim3(1024), lds, st, a);
       hipLaunchKernelGGL((beat_localscore_kernel<256>), dim3((unsigned)((max_len + 255) / 256), n_seq), dim3(256),

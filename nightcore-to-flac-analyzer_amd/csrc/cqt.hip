@@ -165,7 +165,9 @@ __device__ __forceinline__ void d3_level(const float* E, const float* O, int cnt
 
 __global__ __launch_bounds__(256) void decimate3_kernel(const float* sig, const int64_t* chunk_off,
                                                         const int64_t* oct_off, const int64_t* oct_len,
-                                                        float* ws_oct, int base, const double* __restrict__ taps) {
+                                                        float* ws_oct, int base, const double* __restrict__ taps,
+                                                        unsigned long long* span) {
+  const Span span_(span);
   static_assert(kHalfbandK == 23, "phase windows assume 23");
   __shared__ __attribute__((aligned(16))) float e0[D3_P0], o0[D3_P0];
   __shared__ __attribute__((aligned(16))) float e1[D3_N1 / 2], o1[D3_N1 / 2];
@@ -234,9 +236,11 @@ struct PeakArgs {
   float* peak_mag;
   int* chunk_npk;         // [n] zeroed by the launcher (or by the caller, with tf_skip)
   const int* tf_skip;     // nullable [n]: leading tuning frames whose peaks the window stage appended
+  unsigned long long* span = nullptr;  // nc_profile execution span (nc_device.h)
 };
 
 __global__ __launch_bounds__(TP_WAVES * 64) void tuning_peaks_kernel(PeakArgs a) {
+  const Span span_(a.span);
   extern __shared__ __attribute__((aligned(16))) char smem[];
   float2* sh_tw = reinterpret_cast<float2*>(smem);
   const int lane0 = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform (SGPR)
@@ -496,6 +500,7 @@ struct CqtArgs {
   int pmax;
   int klo, khi;            // FFT bins the rows touch
   double* partial;  // [n][nblk][12]
+  unsigned long long* span = nullptr;  // nc_profile execution span (nc_device.h)
 };
 
 // butterfly b of lane l in the last stage: {l, 128-l, 128+l, 256-l}, lane 0 {0, 64, 192, 128}
@@ -513,6 +518,7 @@ size_t cqt_lds_bytes() {
 }
 
 __global__ __launch_bounds__(CQ_WAVES * 64) void cqt_chroma_kernel(CqtArgs a) {
+  const Span span_(a.span);
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int NT = CQ_WAVES * 64;
   const int c = blockIdx.y;
@@ -809,7 +815,7 @@ int launch_chroma_mean(Context& ctx, const float* sig, const int64_t* chunk_off,
     {
       KTimer kt_(ctx, "decimate", st);
       hipLaunchKernelGGL(decimate3_kernel, grid, dim3(256), 0, st, sig, chunk_off, w.oct_off, w.oct_len, w.ws_oct,
-                         base, ctx.t.halfband);
+                         base, ctx.t.halfband, kt_.span());
     }
   }
   PeakArgs pa;
@@ -833,6 +839,7 @@ int launch_chroma_mean(Context& ctx, const float* sig, const int64_t* chunk_off,
     const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(groups, ctx.num_cu));
     {
       KTimer kt_(ctx, "tuning_peaks", st);
+      pa.span = kt_.span();
       hipLaunchKernelGGL(tuning_peaks_kernel, dim3(grid), dim3(TP_WAVES * 64), lds, st, pa);
     }
   }
@@ -869,6 +876,7 @@ int launch_chroma_mean(Context& ctx, const float* sig, const int64_t* chunk_off,
   const int nblk = (int)((1 + max_chunk_len / 512 + CQ_FR - 1) / CQ_FR);
   {
     KTimer kt_(ctx, "cqt_chroma", st);
+    ca.span = kt_.span();
     hipLaunchKernelGGL(cqt_chroma_kernel, dim3((nblk + CQ_BPW - 1) / CQ_BPW, n), dim3(CQ_WAVES * 64), cqt_lds_bytes(), st, ca);
   }
   hipLaunchKernelGGL(chroma_finalize_kernel, dim3(n), dim3(64), 0, st, w.partial, w.tf_base, w.n_frames, n,

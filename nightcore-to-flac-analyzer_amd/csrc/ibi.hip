@@ -121,9 +121,11 @@ struct TgSlideArgs {
   int N;
   int n_tblk;     // tiles per file along frames (max over files)
   double* slab;   // [n_files][n_tblk][N]
+  unsigned long long* span = nullptr;  // nc_profile execution span (nc_device.h)
 };
 
 __global__ __launch_bounds__(TG_KB) void tg_slide_kernel(TgSlideArgs a) {
+  const Span span_(a.span);
   extern __shared__ __attribute__((aligned(16))) char smem[];
   double* sh_r = reinterpret_cast<double*>(smem);         // [TG_TB]
   float* sh_x = reinterpret_cast<float*>(sh_r + TG_TB);   // [TG_TB + N]
@@ -256,6 +258,7 @@ int launch_ibi_tempogram(Context& ctx, const float* onset, const int64_t* frame_
   const size_t lds = TG_TB * sizeof(double) + (size_t)(TG_TB + N) * sizeof(float);
   {
     KTimer kt_(ctx, "tg_slide", st);
+    a.span = kt_.span();
     hipLaunchKernelGGL(tg_slide_kernel, dim3(((N + 1) / 2 + TG_KB - 1) / TG_KB, n_tblk, n_files), dim3(TG_KB), lds, st,
                      a);
   }

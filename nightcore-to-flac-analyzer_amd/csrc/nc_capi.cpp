@@ -156,7 +156,11 @@ int nc_num_cu(const nc_ctx* ctx) { return ctx ? ctx->c.num_cu : -1; }
 int nc_profile_enable(nc_ctx* ctx, int on) {
   CHECK_CTX(ctx);
   SET_DEVICE(ctx);
-  nc::profile_enable(ctx->c, on != 0);
+  if (on < 0 || on > 2) {
+    nc::set_error("nc_profile_enable: mode must be 0 (off), 1 (events + spans) or 2 (spans only)");
+    return -1;
+  }
+  nc::profile_enable(ctx->c, on);
   return 0;
 }
 
@@ -168,6 +172,16 @@ int nc_profile_read(nc_ctx* ctx, const char* tag, double* total_ms, int* launche
   }
   SET_DEVICE(ctx);
   return nc::profile_read(ctx->c, tag, total_ms, launches);
+}
+
+int nc_profile_read_span(nc_ctx* ctx, const char* tag, double* total_ms, int* launches) {
+  CHECK_CTX(ctx);
+  if (!tag || !total_ms || !launches) {
+    nc::set_error("nc_profile_read_span: null argument");
+    return -1;
+  }
+  SET_DEVICE(ctx);
+  return nc::profile_read_span(ctx->c, tag, total_ms, launches);
 }
 
 size_t nc_trim_workspace_bytes(const int64_t* host_file_len, int n_files) {

@@ -14,6 +14,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "nc_span.h"
+
 #define NC_WAVE 64
 
 namespace nc {
@@ -49,6 +51,37 @@ __device__ __forceinline__ double wave_max(double v) {
   for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o, 64));
   return v;
 }
+
+// ------------------------------------------------------------------ kernel spans (nc_profile)
+// A profiled launch gets kSpanLines (start, end) slots, one 128-byte line each (start init
+// ~0, end init 0).  The first kSpanEdge workgroups of the grid lower a start (thread 0),
+// the last kSpanEdge raise an end (lane 0 of every wave) on the 100 MHz wall clock, each
+// in line (linear workgroup id mod kSpanLines): min start .. max end is the kernel's
+// execution span, the duration rocprofv3 --kernel-trace reports, unaffected by queueing
+// behind other streams' kernels.  Device-scope atomics on one address serialise (tens of
+// ns each), hence the lines and the edge-only recording: a launch issues at most
+// 2 kSpanEdge x waves atomics, <= kSpanEdge / kSpanLines x waves per line.  Fire-and-forget;
+// null = not profiled.
+__device__ __forceinline__ unsigned span_lin() {
+  return blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
+}
+__device__ __forceinline__ void span_begin(unsigned long long* sp) {
+  if (sp && threadIdx.x == 0 && span_lin() < (unsigned)kSpanEdge)
+    atomicMin(sp + (span_lin() % kSpanLines) * kSpanStride, (unsigned long long)wall_clock64());
+}
+__device__ __forceinline__ void span_end(unsigned long long* sp) {
+  if (sp && (threadIdx.x & 63) == 0) {
+    const unsigned n = gridDim.x * gridDim.y * gridDim.z, l = span_lin();
+    if (l + (unsigned)kSpanEdge >= n) atomicMax(sp + (l % kSpanLines) * kSpanStride + 1, (unsigned long long)wall_clock64());
+  }
+}
+
+// RAII form for a kernel body: begins at construction, ends at every exit of the scope
+struct Span {
+  unsigned long long* sp;
+  __device__ __forceinline__ explicit Span(unsigned long long* p) : sp(p) { span_begin(p); }
+  __device__ __forceinline__ ~Span() { span_end(sp); }
+};
 
 // float <-> order-preserving int (for atomicMax on floats of either sign)
 __device__ __forceinline__ int f2ord(float f) {

@@ -77,16 +77,20 @@ class KTimer {
   ~KTimer();
   KTimer(const KTimer&) = delete;
   KTimer& operator=(const KTimer&) = delete;
+  // device span slot of this launch (nc_device.h span_begin/span_end), or null
+  unsigned long long* span() const { return span_; }
 
  private:
+  unsigned long long* span_ = nullptr;
   Context& ctx_;
   const char* tag_;
   hipStream_t st_;
   void* stop_ = nullptr;
 };
 void free_timers(Context& ctx);
-void profile_enable(Context& ctx, bool on);
+void profile_enable(Context& ctx, int mode);
 int profile_read(Context& ctx, const char* tag, double* total_ms, int* launches);
+int profile_read_span(Context& ctx, const char* tag, double* total_ms, int* launches);
 
 // bootstrap.hip job description (see nc_bootstrap_ratio in include/ncgpu.h)
 struct BootArgs {

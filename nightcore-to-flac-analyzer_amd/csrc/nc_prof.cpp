@@ -1,14 +1,25 @@
-// nc_prof.cpp — opt-in per-kernel HIP-event timers (nc_profile_enable / nc_profile_read).
-// bench.py uses them to time the dominant kernel of the step on the stream it runs on,
-// so its roofline numbers come from the same launches rocprofv3 sees.
+// nc_prof.cpp — opt-in per-kernel timers (nc_profile_enable / nc_profile_read /
+// nc_profile_read_span).  bench.py uses them to time the step's kernels on the streams
+// they run on, so its roofline numbers come from the same launches rocprofv3 sees.
+//
+// Two measurements per profiled launch:
+//  * HIP events recorded around the launch on its stream (mode 1 only).  They include
+//    any time the kernel waits behind other streams' work after the start event;
+//  * the kernel's execution span, recorded by the kernel itself (nc_device.h
+//    span_begin / span_end: min wave start .. max wave end on the 100 MHz wall clock) —
+//    what rocprofv3 --kernel-trace reports as the kernel's duration.  No host work per
+//    launch beyond handing the kernel its slot, so mode 2 (spans only) is cheap enough to
+//    stay on during a timed region.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <map>
 #include <string>
 #include <utility>
 #include <vector>
 
 #include "nc_engine.h"
+#include "nc_span.h"
 
 namespace nc {
 
@@ -16,20 +27,41 @@ struct KernelTimers {
   struct Slot {
     std::vector<std::pair<hipEvent_t, hipEvent_t>> ev;
     size_t used = 0;
+    std::vector<int> spans;     // span slots of this tag's launches since the last read
   };
   std::map<std::string, Slot> slots;
+  bool events = true;
+  unsigned long long* span_buf = nullptr;   // [kSpanCap][kSpanLines][kSpanStride]: (start, end, pad)
+  int span_used = 0;
+  double clock_khz = 100000.0;
   ~KernelTimers() {
     for (auto& kv : slots)
       for (auto& p : kv.second.ev) {
         (void)hipEventDestroy(p.first);
         (void)hipEventDestroy(p.second);
       }
+    if (span_buf) (void)hipFree(span_buf);
   }
 };
 
+constexpr size_t kSpanLaunchU64 = (size_t)kSpanLines * kSpanStride;
+
+static void span_reset(KernelTimers& t) {
+  std::vector<unsigned long long> h((size_t)kSpanCap * kSpanLaunchU64, 0ull);
+  for (size_t i = 0; i < h.size(); i += kSpanStride) h[i] = ~0ull;
+  (void)hipMemcpy(t.span_buf, h.data(), h.size() * sizeof(unsigned long long), hipMemcpyHostToDevice);
+  t.span_used = 0;
+}
+
 KTimer::KTimer(Context& ctx, const char* tag, hipStream_t st) : ctx_(ctx), tag_(tag), st_(st) {
   if (!ctx_.timers) return;
-  auto& slot = ctx_.timers->slots[tag_];
+  KernelTimers& t = *ctx_.timers;
+  auto& slot = t.slots[tag_];
+  if (t.span_buf && t.span_used < kSpanCap) {
+    slot.spans.push_back(t.span_used);
+    span_ = t.span_buf + (size_t)t.span_used++ * kSpanLaunchU64;
+  }
+  if (!t.events) return;
   if (slot.used == slot.ev.size()) {
     hipEvent_t a = nullptr, b = nullptr;
     if (hipEventCreate(&a) != hipSuccess || hipEventCreate(&b) != hipSuccess) return;
@@ -53,9 +85,19 @@ void free_timers(Context& ctx) {
 
 namespace nc {
 
-void profile_enable(Context& ctx, bool on) {
+// mode 0: off; 1: events + spans; 2: spans only
+void profile_enable(Context& ctx, int mode) {
   free_timers(ctx);
-  if (on) ctx.timers = new KernelTimers();
+  if (!mode) return;
+  auto* t = new KernelTimers();
+  t->events = mode == 1;
+  if (hipMalloc(&t->span_buf, sizeof(unsigned long long) * kSpanCap * kSpanLaunchU64) != hipSuccess)
+    t->span_buf = nullptr;
+  int khz = 0;
+  if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, ctx.device) == hipSuccess && khz > 0)
+    t->clock_khz = khz;
+  if (t->span_buf) span_reset(*t);
+  ctx.timers = t;
 }
 
 int profile_read(Context& ctx, const char* tag, double* total_ms, int* launches) {
@@ -81,6 +123,48 @@ int profile_read(Context& ctx, const char* tag, double* total_ms, int* launches)
   *total_ms = tot;
   *launches = (int)slot.used;
   slot.used = 0;
+  return 0;
+}
+
+// Summed execution spans of `tag`'s launches since the last span read.  Waits for the
+// device; the span buffer is recycled once no tag has unread spans.
+int profile_read_span(Context& ctx, const char* tag, double* total_ms, int* launches) {
+  *total_ms = 0.0;
+  *launches = 0;
+  KernelTimers* t = ctx.timers;
+  if (!t || !t->span_buf) return 0;
+  auto it = t->slots.find(tag);
+  if (it == t->slots.end() || it->second.spans.empty()) return 0;
+  if (hipDeviceSynchronize() != hipSuccess) {
+    set_error("nc_profile_read_span: device synchronize failed");
+    return -1;
+  }
+  std::vector<unsigned long long> h((size_t)t->span_used * kSpanLaunchU64);
+  if (t->span_used && hipMemcpy(h.data(), t->span_buf, h.size() * sizeof(unsigned long long),
+                                hipMemcpyDeviceToHost) != hipSuccess) {
+    set_error("nc_profile_read_span: copy failed");
+    return -1;
+  }
+  double tot = 0.0;
+  int n = 0;
+  for (int s : it->second.spans) {
+    unsigned long long a = ~0ull, b = 0ull;
+    for (int l = 0; l < kSpanLines; ++l) {
+      const unsigned long long* p = h.data() + (size_t)s * kSpanLaunchU64 + (size_t)l * kSpanStride;
+      a = std::min(a, p[0]);
+      b = std::max(b, p[1]);
+    }
+    if (b >= a && a != ~0ull) {          // launches with no work (empty grids) record nothing
+      tot += (double)(b - a) / t->clock_khz;
+      ++n;
+    }
+  }
+  it->second.spans.clear();
+  *total_ms = tot;
+  *launches = n;
+  bool any = false;
+  for (auto& kv : t->slots) any |= !kv.second.spans.empty();
+  if (!any) span_reset(*t);
   return 0;
 }
 

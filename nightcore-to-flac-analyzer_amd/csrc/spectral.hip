@@ -51,6 +51,7 @@ struct SpecArgs {
   double* rec;                // [total_frames][SF_REC]
   const float2* tw;
   const float* hann2048;
+  unsigned long long* span = nullptr;  // nc_profile execution span (nc_device.h)
 };
 
 __device__ __forceinline__ int sf_file_of(const int64_t* base, int n, int64_t g) {
@@ -70,6 +71,7 @@ static size_t spectral_frames_lds_bytes() {
 }
 
 __global__ __launch_bounds__(SF_THREADS) void spectral_frames_kernel(SpecArgs a) {
+  const Span span_(a.span);
   extern __shared__ __attribute__((aligned(16))) char smem[];
   float2* sh_tw = reinterpret_cast<float2*>(smem);
   const int lane0 = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -328,7 +330,8 @@ __global__ __launch_bounds__(NT) void spectral_file_kernel(const int64_t* frame_
 template <int NT>
 __global__ __launch_bounds__(NT) void spectral_bins_kernel(const int64_t* frame_base, const float* db_rows,
                                                            const double* stats, int fb, int nblk,
-                                                           double* partial) {
+                                                           double* partial, unsigned long long* span) {
+  const Span span_(span);
   const int f = blockIdx.y, blk = blockIdx.x;
   const int64_t t0 = frame_base[f] + (int64_t)blk * fb, t1 = min(frame_base[f + 1], t0 + fb);
   if (t0 >= t1) return;
@@ -409,6 +412,7 @@ int launch_spectral(Context& ctx, const float* sig, const int64_t* file_off, con
   const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(n_groups, (int64_t)ctx.num_cu));
   {
     KTimer kt_(ctx, "spectral_frames", st);
+    a.span = kt_.span();
     hipLaunchKernelGGL(spectral_frames_kernel, dim3(grid), dim3(SF_THREADS), lds, st, a);
   }
   NC_HIP(hipGetLastError());
@@ -420,7 +424,7 @@ int launch_spectral(Context& ctx, const float* sig, const int64_t* file_off, con
   {
     KTimer kt_(ctx, "spectral_bins", st);
     hipLaunchKernelGGL(spectral_bins_kernel<256>, dim3(nblk, n_files), dim3(256), 0, st, frame_base, rows,
-                       stats_out, fb, nblk, partial);
+                       stats_out, fb, nblk, partial, kt_.span());
   }
   NC_HIP(hipGetLastError());
   hipLaunchKernelGGL(spectral_bins_finish, dim3((SF_BINS + 255) / 256, n_files), dim3(256), 0, st, frame_base,

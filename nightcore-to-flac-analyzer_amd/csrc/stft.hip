@@ -51,6 +51,7 @@ size_t stft_mel_lds_bytes(int mel_j) {
 }
 
 __global__ __launch_bounds__(SM_THREADS) void stft_mel_kernel(StftMelArgs a) {
+  const Span span_(a.span);
   extern __shared__ __attribute__((aligned(16))) char smem[];
   float2* sh_tw = reinterpret_cast<float2*>(smem);
   float4* sh_w4 = reinterpret_cast<float4*>(sh_tw + al4(SmTw::size));  // [mel_j0 + mel_j1][64]
@@ -214,6 +215,7 @@ int launch_stft_mel(Context& ctx, const StftMelArgs& args, hipStream_t st) {
   const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(n_groups, (int64_t)ctx.num_cu * (lds <= 80 * 1024 ? 2 : 1)));
   {
     KTimer kt_(ctx, "stft_mel", st);
+    a.span = kt_.span();
     hipLaunchKernelGGL(stft_mel_kernel, dim3(grid), dim3(SM_THREADS), lds, st, a);
   }
   NC_HIP(hipGetLastError());

@@ -41,6 +41,7 @@ struct StftMelArgs {
   float* peak_pitch;
   float* peak_mag;
   int* chunk_npk;
+  unsigned long long* span = nullptr;  // nc_profile execution span (nc_device.h)
 };
 
 int launch_stft_mel(Context& ctx, const StftMelArgs& args, hipStream_t st);

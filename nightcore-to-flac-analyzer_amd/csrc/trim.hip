@@ -22,7 +22,9 @@ constexpr int TR_BPG = 4 * TR_BPW;         // blocks per workgroup (4 waves)
 
 __global__ __launch_bounds__(256) void trim_blocks_kernel(const float* sig, const int64_t* file_off,
                                                           const int64_t* file_len, const int64_t* frame_base,
-                                                          const int64_t* tile_base, int n_files, double* blk) {
+                                                          const int64_t* tile_base, int n_files, double* blk,
+                                                          unsigned long long* span) {
+  const Span span_(span);
   const int lane = threadIdx.x & 63;
   const int64_t tile = blockIdx.x;
   if (tile >= tile_base[n_files]) return;
@@ -160,7 +162,7 @@ int launch_trim(Context& ctx, const float* sig, const int64_t* file_off, const i
   {
     KTimer kt_(ctx, "trim_blocks", st);
     hipLaunchKernelGGL(trim_blocks_kernel, dim3((unsigned)tiles), dim3(256), 0, st, sig, file_off, file_len,
-                       frame_base, tile_base, n_files, blk);
+                       frame_base, tile_base, n_files, blk, kt_.span());
   }
   hipLaunchKernelGGL(trim_bounds_kernel, dim3(n_files), dim3(256), 0, st, blk, frame_base, file_len, top_db,
                      out_start, out_end);

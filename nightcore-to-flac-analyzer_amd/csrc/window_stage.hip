@@ -54,9 +54,11 @@ struct WinTgArgs {
   float* onset_out;   // [n_win][T]
   double* tg_out;     // [n_win][acw]
   double* energy_out; // [n_win]
+  unsigned long long* span = nullptr;  // nc_profile execution span (nc_device.h)
 };
 
 __global__ __launch_bounds__(WT_THREADS) void window_tg_kernel(WinTgArgs a) {
+  const Span span_(a.span);
   extern __shared__ __attribute__((aligned(16))) char smem[];
   __shared__ BlockScratch<WT_THREADS> red;
   const int w = blockIdx.x;
@@ -276,6 +278,7 @@ int launch_window_stage(Context& ctx, const float* sig, const int64_t* win_off, 
   }
   {
     KTimer kt_(ctx, "window_tg", st);
+    a.span = kt_.span();
     hipLaunchKernelGGL(window_tg_kernel, dim3(n_win), dim3(WT_THREADS), lds, st, a);
   }
   NC_HIP(hipGetLastError());

@@ -306,20 +306,32 @@ class Engine:
     KERNEL_TAGS = ("stft_mel", "window_tg", "tuning_peaks", "decimate", "cqt_chroma", "trim_blocks", "tempo_beat",
                    "tg_slide", "spectral_frames", "spectral_bins")
 
-    def kernel_profile(self, on: bool) -> None:
-        """Enable/disable the library's per-kernel HIP-event timers (nc_profile_enable)."""
-        self.ctx.call("nc_profile_enable", 1 if on else 0)
+    def kernel_profile(self, on) -> None:
+        """The library's per-kernel timers (nc_profile_enable): False/0 off, True/1 HIP events
+        around each launch plus the kernels' own execution spans, 2 spans only (cheap enough
+        to leave on in a timed region)."""
+        self.ctx.call("nc_profile_enable", int(on))
 
-    def kernel_times(self) -> Dict[str, Tuple[float, int]]:
-        """{kernel tag: (total ms, launches)} since the last read (nc_profile_read); waits for them."""
+    def _profile_read(self, fn: str) -> Dict[str, Tuple[float, int]]:
         import ctypes as C
         out = {}
         for tag in self.KERNEL_TAGS:
             ms, n = C.c_double(0.0), C.c_int(0)
-            self.ctx.call("nc_profile_read", tag.encode(), C.byref(ms), C.byref(n))
+            self.ctx.call(fn, tag.encode(), C.byref(ms), C.byref(n))
             if n.value:
                 out[tag] = (ms.value, n.value)
         return out
+
+    def kernel_times(self) -> Dict[str, Tuple[float, int]]:
+        """{kernel tag: (total ms, launches)} of the HIP-event brackets since the last read
+        (nc_profile_read); waits for them."""
+        return self._profile_read("nc_profile_read")
+
+    def kernel_spans(self) -> Dict[str, Tuple[float, int]]:
+        """{kernel tag: (total ms, launches)} of the kernels' execution spans since the last
+        read (nc_profile_read_span: first wave start .. last wave end, rocprofv3's kernel
+        duration); waits for them."""
+        return self._profile_read("nc_profile_read_span")
 
     def upload_signals(self, arrays: Sequence[np.ndarray]) -> DeviceSignals:
         lens = np.array([len(a) for a in arrays], dtype=np.int64)
