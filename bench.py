@@ -134,6 +134,9 @@ def main():
     ap.add_argument("--cpu-workers", type=int, default=0,
                     help="CPU baseline processes, one pair each (0: the host cores this process may run on)")
     ap.add_argument("--no-upload", action="store_true", help="skip the upload-included throughput")
+    ap.add_argument("--shard", choices=("pairs", "windows"), default="pairs",
+                    help="N > 1: whole pairs per rank (default), or every pair's windows split over the ranks "
+                         "(nightcore_analyzer.sharded; not yet measured on multi-GPU hardware)")
     ap.add_argument("--workers", type=int, default=min(16, os.cpu_count() or 1))
     args = ap.parse_args()
 
@@ -143,7 +146,11 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     # the synthetic pairs are made (forked workers) before this process touches the GPU
-    pairs = make_pairs(args.pairs, args.seconds, 1000 + rank * args.pairs, max(1, args.workers // max(1, world)))
+    win_mode = args.shard == "windows"
+    # pair mode: each rank its own pairs (weak scaling); window mode: every rank the same
+    # pairs, their windows split over the ranks (strong scaling)
+    pairs = make_pairs(args.pairs, args.seconds, 1000 + (0 if win_mode else rank * args.pairs),
+                       max(1, args.workers // max(1, world)))
     if world > 1:
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
@@ -157,7 +164,16 @@ def main():
     torch.cuda.synchronize()
     params = E.Params(compute_ibi=False)
 
-    outs = eng.analyze(signals=signals, params=params)
+    if win_mode:
+        from nightcore_analyzer.sharded import DeviceStages, analyze_sharded
+        stages = DeviceStages(eng, signals)
+
+        def step():
+            return analyze_sharded(stages, params)
+    else:
+        def step():
+            return eng.analyze(signals=signals, params=params)
+    outs = step()
     bad = [i for i, o in enumerate(outs) if o.error is not None]
     if bad:
         raise RuntimeError(f"pairs {bad} failed: {outs[bad[0]].error}")
@@ -166,7 +182,7 @@ def main():
     tr = outs[0].result.tempo_ratio
     pr = outs[0].result.pitch_ratio
     for _ in range(max(0, args.warmup - 1)):
-        eng.analyze(signals=signals, params=params)
+        step()
 
     # timed region: K steps with the kernels' own execution spans recorded (nc_profile mode 2:
     # two fire-and-forget atomics per wave, no host work per launch), so the per-kernel
@@ -177,7 +193,7 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        eng.analyze(signals=signals, params=params)
+        step()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -196,7 +212,7 @@ def main():
     eng.start_timers()
     ksteps = max(1, min(args.steps, 3))
     for _ in range(ksteps):
-        eng.analyze(signals=signals, params=params)
+        step()
     timers = eng.stop_timers()
     per = {k: (ms / n, n // ksteps) for k, (ms, n) in timers.items()}
 
@@ -232,7 +248,7 @@ def main():
     # speed, where the timed launches share the chip with the other streams' chains
     eng.set_serial(True)
     eng.kernel_profile(2)
-    eng.analyze(signals=signals, params=params)
+    step()
     iso = eng.kernel_spans()
     eng.kernel_profile(False)
     eng.set_serial(False)
@@ -243,7 +259,7 @@ def main():
     # upload included: the same K steps with every step's 64 pairs copied host -> HBM from
     # pinned memory on a copy stream, double-buffered (step j + 1 uploads while step j runs)
     upl = None
-    if not args.no_upload:
+    if not args.no_upload and not win_mode:
         host = signals.buf.cpu().pin_memory()
         bufs = [signals.buf, torch.empty_like(signals.buf)]
         cs = torch.cuda.Stream(eng.dev)
@@ -412,21 +428,21 @@ def main():
     if rank == 0:
         line = {
             "metric": "10 s windows/sec (CQT+onset, 22.05 kHz mono) at 1/2/4/8 GPUs; % HBM roofline",
-            "value": world * win_per_step * args.steps / el,
+            "value": (1 if win_mode else world) * win_per_step * args.steps / el,
             "unit": "windows/s",
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": step_ms,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if win_mode else "weak",
             "vs_baseline": None,
             "dtype": "f32",
             "data": "synthetic (SURVEY.md §8d chords+clicks+noise, nc = resample_poly(src, 4, 5)), resident in HBM",
             "config": {"workload": "config 3: per GPU a batch of 64 x 3-min 22.05 kHz mono pairs; step = "
                                    "pipeline.run analysis without the hop-64 IBI pass",
                        "pairs_per_gpu": args.pairs, "windows_per_gpu_step": win_per_step,
-                       "cqt_chunks_per_gpu_step": chunks_per_step, "parallelism": f"dp{world} (pairs sharded)"},
+                       "cqt_chunks_per_gpu_step": chunks_per_step, "parallelism": f"dp{world} (" + ("windows sharded, record all-gathers)" if win_mode else "pairs sharded)")},
             # avg_launch_ms: the kernel's execution spans over the timed steps (rocprofv3's
             # kernel duration, sharing the chip with the concurrent chain); isolated: the same
             # kernels with the other streams idle

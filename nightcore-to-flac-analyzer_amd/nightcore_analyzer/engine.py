@@ -227,6 +227,107 @@ def _group_bounds(B: int, group_pairs, ) -> List[Tuple[int, int]]:
     return out
 
 
+@dataclass
+class BatchPlan:
+    """Host plan of one batch of pairs (files nc_0, src_0, nc_1, src_1, ...): the trimmed
+    file spans, the 10 s windows and the 20 s chunk pairs, as the reference derives them
+    (io.py:58-112, pipeline.py:91-136, pitch.py:121-138).  Window order: every source
+    window (pair-major), then every nightcore window; w0[f]..w1[f] are file f's windows."""
+    nF: int
+    B: int
+    f_off: np.ndarray
+    f_len: np.ndarray
+    strip_len: np.ndarray
+    lead: np.ndarray
+    trail: np.ndarray
+    intro: list
+    win_n: int
+    hop_n: int
+    starts: list
+    w0: np.ndarray
+    w1: np.ndarray
+    win_abs: np.ndarray
+    n_win: int
+    n_src_w: int
+    chunk_off: list
+    chunk_len: list
+    pair_chunks: list
+    n_chunks: int
+    n_cp: int
+
+
+def plan_batch(off: np.ndarray, length: np.ndarray, start: np.ndarray, end: np.ndarray, p: "Params",
+               align: Optional[List[Tuple[float, float]]] = None) -> BatchPlan:
+    """Silence-trim bounds [start, end) of every file -> BatchPlan (host only, deterministic:
+    every rank of a sharded run derives the same plan)."""
+    nF = len(off)
+    B = nF // 2
+    f_off = np.asarray(off, np.int64) + start
+    f_len = end - start
+    strip_len = f_len.copy()
+    lead = start / SR
+    trail = (np.asarray(length, np.int64) - end) / SR
+    intro = [None] * B
+    if p.src_trim_sec > 0.0:
+        k = int(p.src_trim_sec * SR)
+        for b in range(B):
+            f = 2 * b + 1
+            cut = min(k, int(f_len[f]))
+            f_off[f] += cut
+            f_len[f] -= cut
+            intro[b] = p.src_trim_sec
+    elif align is not None:
+        for b, (raw, _) in enumerate(align):
+            if raw >= ALIGN_MIN_OFFSET:                  # pipeline.py:114-116
+                f = 2 * b + 1
+                cut = min(int(raw * SR), int(f_len[f]))
+                f_off[f] += cut
+                f_len[f] -= cut
+                intro[b] = raw
+
+    win_n, hop_n = int(p.window_sec * SR), int(p.hop_sec * SR)
+    starts = []
+    for f in range(nF):
+        L = int(f_len[f])
+        s = np.arange(0, max(0, L - win_n) + 1, hop_n, dtype=np.int64) if L >= win_n and hop_n > 0 \
+            else np.zeros(0, np.int64)
+        starts.append(s)
+    # window order: all source windows (pair-major), then all nightcore windows
+    order = [2 * b + 1 for b in range(B)] + [2 * b for b in range(B)]
+    w0 = np.zeros(nF, np.int64)
+    w1 = np.zeros(nF, np.int64)
+    win_abs, pos = [], 0
+    for f in order:
+        w0[f] = pos
+        win_abs.append(f_off[f] + starts[f])
+        pos += len(starts[f])
+        w1[f] = pos
+    n_win = pos
+    n_src_w = int(sum(len(starts[2 * b + 1]) for b in range(B)))
+    win_abs = np.concatenate(win_abs) if win_abs else np.zeros(0, np.int64)
+
+    chunk_off, chunk_len, pair_chunks = [], [], []
+    if p.compute_pitch:
+        cn = int(CHUNK_SEC * SR)
+        for b in range(B):
+            ns, nn = int(f_len[2 * b + 1]), int(f_len[2 * b])
+            n = min(ns // cn, nn // cn)
+            first = len(chunk_off) // 2
+            if n < 1:
+                chunk_off += [f_off[2 * b + 1], f_off[2 * b]]
+                chunk_len += [ns, nn]
+                n = 1
+            else:
+                for i in range(n):
+                    chunk_off += [f_off[2 * b + 1] + i * cn, f_off[2 * b] + i * cn]
+                    chunk_len += [cn, cn]
+            pair_chunks.append((first, first + n))
+    n_chunks = len(chunk_off)
+    n_cp = n_chunks // 2
+    return BatchPlan(nF, B, f_off, f_len, strip_len, lead, trail, intro, win_n, hop_n, starts, w0, w1, win_abs, n_win,
+                     n_src_w, chunk_off, chunk_len, pair_chunks, n_chunks, n_cp)
+
+
 # ------------------------------------------------------------------------------ engine
 class Engine:
     def __init__(self, device: int = 0):
@@ -666,73 +767,15 @@ class Engine:
                       align: Optional[List[Tuple[float, float]]] = None) -> dict:
         """Queue the whole device pipeline of one group of pairs; returns the pending group."""
         dev, st = self.dev, self.stream()
-        nF = signals.n_files
-        B = nF // 2
-        f_off = signals.off + start
-        f_len = end - start
-        strip_len = f_len.copy()
-        lead = start / SR
-        trail = (signals.length - end) / SR
-        intro = [None] * B
-        if p.src_trim_sec > 0.0:
-            k = int(p.src_trim_sec * SR)
-            for b in range(B):
-                f = 2 * b + 1
-                cut = min(k, int(f_len[f]))
-                f_off[f] += cut
-                f_len[f] -= cut
-                intro[b] = p.src_trim_sec
-        elif align is not None:
-            for b, (raw, _) in enumerate(align):
-                if raw >= ALIGN_MIN_OFFSET:                  # pipeline.py:114-116
-                    f = 2 * b + 1
-                    cut = min(int(raw * SR), int(f_len[f]))
-                    f_off[f] += cut
-                    f_len[f] -= cut
-                    intro[b] = raw
-
-        # ---------------------------------------------------------------- 2. plan
-        win_n, hop_n = int(p.window_sec * SR), int(p.hop_sec * SR)
-        starts = []
-        for f in range(nF):
-            L = int(f_len[f])
-            s = np.arange(0, max(0, L - win_n) + 1, hop_n, dtype=np.int64) if L >= win_n and hop_n > 0 \
-                else np.zeros(0, np.int64)
-            starts.append(s)
-        # window order: all source windows (pair-major), then all nightcore windows
-        order = [2 * b + 1 for b in range(B)] + [2 * b for b in range(B)]
-        w0 = np.zeros(nF, np.int64)
-        w1 = np.zeros(nF, np.int64)
-        win_abs, pos = [], 0
-        for f in order:
-            w0[f] = pos
-            win_abs.append(f_off[f] + starts[f])
-            pos += len(starts[f])
-            w1[f] = pos
-        n_win = pos
-        n_src_w = int(sum(len(starts[2 * b + 1]) for b in range(B)))
-        win_abs = np.concatenate(win_abs) if win_abs else np.zeros(0, np.int64)
+        pl = plan_batch(signals.off, signals.length, start, end, p, align)
+        nF, B = pl.nF, pl.B
+        f_off, f_len, strip_len, lead, trail, intro = pl.f_off, pl.f_len, pl.strip_len, pl.lead, pl.trail, pl.intro
+        win_n, hop_n, starts, w0, w1 = pl.win_n, pl.hop_n, pl.starts, pl.w0, pl.w1
+        win_abs, n_win, n_src_w = pl.win_abs, pl.n_win, pl.n_src_w
+        chunk_off, chunk_len, pair_chunks, n_chunks, n_cp = pl.chunk_off, pl.chunk_len, pl.pair_chunks, \
+            pl.n_chunks, pl.n_cp
         T = 1 + win_n // HOP_LENGTH
         acw = int(int(8.0 * SR) // HOP_LENGTH)
-
-        chunk_off, chunk_len, pair_chunks = [], [], []
-        if p.compute_pitch:
-            cn = int(CHUNK_SEC * SR)
-            for b in range(B):
-                ns, nn = int(f_len[2 * b + 1]), int(f_len[2 * b])
-                n = min(ns // cn, nn // cn)
-                first = len(chunk_off) // 2
-                if n < 1:
-                    chunk_off += [f_off[2 * b + 1], f_off[2 * b]]
-                    chunk_len += [ns, nn]
-                    n = 1
-                else:
-                    for i in range(n):
-                        chunk_off += [f_off[2 * b + 1] + i * cn, f_off[2 * b] + i * cn]
-                        chunk_len += [cn, cn]
-                pair_chunks.append((first, first + n))
-        n_chunks = len(chunk_off)
-        n_cp = n_chunks // 2
 
         # shared tuning frames: a standard 20 s chunk that starts where a window of the same file
         # starts has its first tp tuning frames in that window's STFT (nc_window_stage_tuning)
@@ -992,7 +1035,7 @@ class Engine:
         g["starts_l"] = [x.tolist() for x in g["starts"]]
         g["w0"], g["w1"] = g["w0"].tolist(), g["w1"].tolist()
         ibi = {k[4:]: v for k, v in h.items() if k.startswith("ibi_")} if g["has_ibi"] else None
-        out = [self._assemble_pair(b, g["p"], h, ibi, g["starts_l"], g["w0"], g["w1"], g["f_len"], g["strip_len"],
+        out = [assemble_pair(b, g["p"], h, ibi, g["starts_l"], g["w0"], g["w1"], g["f_len"], g["strip_len"],
                                    g["lead"], g["trail"], g["intro"][b], g["win_n"], g["pair_chunks"], g["n_cp"],
                                    g["nj"], g["n_pitch_jobs"], g["align"][b] if g["align"] else None)
                for b in range(g["B"])]
@@ -1079,135 +1122,135 @@ class Engine:
             res.update(beats=core["beats"], fbase=fb_h)
         return res
 
-    # -------------------------------------------------------------- host assembly + logs
-    def _assemble_pair(self, b, p: Params, h, ibi, starts, w0, w1, f_len, strip_len, lead, trail, intro,
-                       win_n, pair_chunks, n_cp, nj, n_pitch_jobs, align=None) -> PairOutcome:
-        out = PairOutcome()
-        L = out._log_ops.append   # str, or a callable rendering the line(s) when logs are read
-        fn, fs = 2 * b, 2 * b + 1
-        nc_len, src_len = int(f_len[fn]), int(f_len[fs])
-        if p.silence_strip_db is not None:
-            L(lambda: [f"Stripping silence (top_db={p.silence_strip_db} dB)…",
-                       f"  nightcore: −{lead[fn]:.2f}s leading, −{trail[fn]:.2f}s trailing"
-                       f"  →  {strip_len[fn] / SR:.1f} s",
-                       f"  source:    −{lead[fs]:.2f}s leading, −{trail[fs]:.2f}s trailing"
-                       f"  →  {strip_len[fs] / SR:.1f} s"])
-        if p.src_trim_sec > 0.0:
-            L(f"Manual source trim: skipping {p.src_trim_sec:.2f}s from source start")
-        elif align is not None:                              # pipeline.py:111-125
-            raw, spd = align
-            L("Detecting intro offset (RMS envelope alignment)…")
-            if raw >= ALIGN_MIN_OFFSET:
-                L(f"  Intro detected — trimming {raw:.2f}s from source start  (speed hint: {spd:.4f}×)")
-            else:
-                L(f"  No significant intro offset detected  (raw: {raw:.2f}s < {ALIGN_MIN_OFFSET:.1f}s threshold)")
-        L(lambda: [f"Slicing into {p.window_sec:.0f} s windows (hop {p.hop_sec:.0f} s)…",
-                   f"  nightcore: {len(starts[fn])} windows  |  source: {len(starts[fs])} windows",
-                   f"Energy gating (threshold {p.energy_gate_db} dB below peak)…"])
-        act = h["active_l"]
-        src_w = [w for w in range(w0[fs], w1[fs]) if act[w]]
-        nc_w = [w for w in range(w0[fn], w1[fn]) if act[w]]
-        L(lambda: f"  after gating — nightcore: {len(nc_w)} windows  |  source: {len(src_w)} windows")
-        out.detail.update(energy_src=h["energy"][w0[fs]:w1[fs]].copy(), energy_nc=h["energy"][w0[fn]:w1[fn]].copy(),
-                          n_src_windows=len(src_w), n_nc_windows=len(nc_w),
-                          nc_duration=nc_len / SR, src_duration=src_len / SR)
-        if not nc_w or not src_w:
-            out.error = RuntimeError("All windows were discarded by the energy gate.  "
-                                     "Try raising --energy-gate (e.g. --energy-gate -60).")
-            return out
-
-        # pitch
-        pitch_boot = None
-        if p.compute_pitch:
-            L("Estimating pitch (chromagram cross-correlation)…")
-            c0, c1 = pair_chunks[b]
-            n = c1 - c0
-            lags = h["clag_l"][c0:c1]
-            shifts = h["pvals"][c0:c1]
-            pv = h["pvals_l"]
-            src_p = pv[2 * n_cp + c0:2 * n_cp + c1]
-            nc_p = pv[n_cp + c0:n_cp + c1]
-            point_st = C._median(shifts.tolist())
-            if n >= MIN_CHUNKS:
-                j = b
-                lo_st, hi_st = h["sout_l"][n_pitch_jobs + j], h["sout_l"][2 * n_pitch_jobs + j]
-            else:
-                lo_st = hi_st = point_st
-                L(f"    Only {n} chunk(s) available (need ≥ {MIN_CHUNKS}) — "
-                  "pitch CI is degenerate; estimate may be less reliable.")
-            L(lambda: f"    Chroma xcorr: {point_st:+.3f} st  95% CI [{lo_st:+.3f}, {hi_st:+.3f}] st"
-                      f"  ({n} chunk{'s' if n != 1 else ''})")
-            L("    essentia not available — skipping MELODIA refinement")
-            L("  Pitch method: chroma_xcorr")
-            method = "chroma_xcorr"
-            pj = len(w0) // 2 + b     # pitch job index: after the B tempo jobs
-            bo = h["bout_l"]
-            pitch_boot = (bo[pj], (bo[nj + pj], bo[2 * nj + pj]))
-            out.detail.update(chunk_lags=lags, tuning=h["tuning"][2 * c0:2 * c1].copy(),
-                              chroma=h["chroma"][24 * c0:24 * c1].reshape(-1, 12).copy())
+# ------------------------------------------------------------------------------ host assembly + logs
+def assemble_pair(b, p: Params, h, ibi, starts, w0, w1, f_len, strip_len, lead, trail, intro,
+                   win_n, pair_chunks, n_cp, nj, n_pitch_jobs, align=None) -> PairOutcome:
+    out = PairOutcome()
+    L = out._log_ops.append   # str, or a callable rendering the line(s) when logs are read
+    fn, fs = 2 * b, 2 * b + 1
+    nc_len, src_len = int(f_len[fn]), int(f_len[fs])
+    if p.silence_strip_db is not None:
+        L(lambda: [f"Stripping silence (top_db={p.silence_strip_db} dB)…",
+                   f"  nightcore: −{lead[fn]:.2f}s leading, −{trail[fn]:.2f}s trailing"
+                   f"  →  {strip_len[fn] / SR:.1f} s",
+                   f"  source:    −{lead[fs]:.2f}s leading, −{trail[fs]:.2f}s trailing"
+                   f"  →  {strip_len[fs] / SR:.1f} s"])
+    if p.src_trim_sec > 0.0:
+        L(f"Manual source trim: skipping {p.src_trim_sec:.2f}s from source start")
+    elif align is not None:                              # pipeline.py:111-125
+        raw, spd = align
+        L("Detecting intro offset (RMS envelope alignment)…")
+        if raw >= ALIGN_MIN_OFFSET:
+            L(f"  Intro detected — trimming {raw:.2f}s from source start  (speed hint: {spd:.4f}×)")
         else:
-            L("Skipping pitch estimation.")
-            src_p, nc_p, method = [], [], None
-
-        # tempo
-        L("Estimating tempo (librosa)…")
-        tempos = {}
-        for side, ws_ in (("src", src_w), ("nc", nc_w)):
-            if side == "src":
-                L("  ← source →")
-            vals = []
-            f = fs if side == "src" else fn
-            st_f, base = starts[f], w0[f]
-            bpm_l, nb_l, nws = h["bpm_l"], h["nbeats_l"], len(ws_)
-            L(lambda st_f=st_f, base=base, ws_=ws_, nws=nws: [
-                f"    tempo window {i + 1}/{nws}  [{st_f[w - base] / SR:.1f}–{(st_f[w - base] + win_n) / SR:.1f} s]"
-                for i, w in enumerate(ws_)])
-            vals = [bpm_l[w] if nb_l[w] >= MIN_BEATS else None for w in ws_]
-            L(lambda vals=vals, n=nws:
-              f"    {sum(1 for v in vals if v is not None)}/{n} windows yielded a confident tempo estimate")
-            tempos[side] = vals
-            if side == "src":
-                valid_src = [t for t in vals if t is not None]
-                nc_dur, src_dur = nc_len / SR, src_len / SR
-                if valid_src and nc_dur > 0 and src_dur > 0:
-                    med = C._median(valid_src)
-                    pr_ = h['prior_l'][b]
-                    L(lambda: f"  NC tempo prior: {pr_:.1f} BPM  "
-                              f"(src median {med:.1f} BPM × dur ratio {src_dur / nc_dur:.4f})")
-                L("  ← nightcore →")
-        out.detail.update(src_tempos=tempos["src"], nc_tempos=tempos["nc"], nc_start_bpm=h["prior_l"][b],
-                          tempo_margin_src=h["margin"][src_w].copy(), tempo_margin_nc=h["margin"][nc_w].copy())
-        L("Computing consensus…")
-        try:
-            bo = h["bout_l"]
-            tempo_boot = (bo[b], (bo[nj + b], bo[2 * nj + b]))
-            res = C.assemble(src_p, nc_p, tempos["src"], tempos["nc"], nc_duration=nc_len / SR,
-                             src_duration=src_len / SR, pitch_boot=pitch_boot, tempo_boot=tempo_boot)
-        except ValueError as exc:
-            out.error = exc
-            return out
-        res.intro_offset_sec = intro
-        res.pitch_method = method
-        if ibi is not None:
-            L("Computing IBI ratio (high-precision beat timestamps, hop=64)…")
-            nb_ = ibi["nibi"]
-            Bn = len(nb_) // 2
-            if nb_[2 * b] >= 4 and nb_[2 * b + 1] >= 4:
-                o = ibi["out"]
-                res.ibi_ratio = float(o[b])
-                res.ibi_ci = (float(o[Bn + b]), float(o[2 * Bn + b]))
-                L(lambda: f"  IBI ratio: {res.ibi_ratio:.6f}×  95% CI [{res.ibi_ci[0]:.6f}, {res.ibi_ci[1]:.6f}]")
-            else:
-                L("  IBI ratio: insufficient beats — skipped")
-            out.detail.update(ibi_nbeats=(int(ibi["nbeats"][2 * b]), int(ibi["nbeats"][2 * b + 1])),
-                              ibi_n=(int(nb_[2 * b]), int(nb_[2 * b + 1])),
-                              ibi_lag=(int(ibi["lag"][2 * b]), int(ibi["lag"][2 * b + 1])))
-            if "beats" in ibi:
-                fb, bt, nbt = ibi["fbase"], ibi["beats"], ibi["nbeats"]
-                out.detail["ibi_beats"] = tuple(bt[fb[f]:fb[f] + max(0, int(nbt[f]))].copy() for f in (fn, fs))
-        L("Done.")
-        out.result = res
+            L(f"  No significant intro offset detected  (raw: {raw:.2f}s < {ALIGN_MIN_OFFSET:.1f}s threshold)")
+    L(lambda: [f"Slicing into {p.window_sec:.0f} s windows (hop {p.hop_sec:.0f} s)…",
+               f"  nightcore: {len(starts[fn])} windows  |  source: {len(starts[fs])} windows",
+               f"Energy gating (threshold {p.energy_gate_db} dB below peak)…"])
+    act = h["active_l"]
+    src_w = [w for w in range(w0[fs], w1[fs]) if act[w]]
+    nc_w = [w for w in range(w0[fn], w1[fn]) if act[w]]
+    L(lambda: f"  after gating — nightcore: {len(nc_w)} windows  |  source: {len(src_w)} windows")
+    out.detail.update(energy_src=h["energy"][w0[fs]:w1[fs]].copy(), energy_nc=h["energy"][w0[fn]:w1[fn]].copy(),
+                      n_src_windows=len(src_w), n_nc_windows=len(nc_w),
+                      nc_duration=nc_len / SR, src_duration=src_len / SR)
+    if not nc_w or not src_w:
+        out.error = RuntimeError("All windows were discarded by the energy gate.  "
+                                 "Try raising --energy-gate (e.g. --energy-gate -60).")
         return out
+
+    # pitch
+    pitch_boot = None
+    if p.compute_pitch:
+        L("Estimating pitch (chromagram cross-correlation)…")
+        c0, c1 = pair_chunks[b]
+        n = c1 - c0
+        lags = h["clag_l"][c0:c1]
+        shifts = h["pvals"][c0:c1]
+        pv = h["pvals_l"]
+        src_p = pv[2 * n_cp + c0:2 * n_cp + c1]
+        nc_p = pv[n_cp + c0:n_cp + c1]
+        point_st = C._median(shifts.tolist())
+        if n >= MIN_CHUNKS:
+            j = b
+            lo_st, hi_st = h["sout_l"][n_pitch_jobs + j], h["sout_l"][2 * n_pitch_jobs + j]
+        else:
+            lo_st = hi_st = point_st
+            L(f"    Only {n} chunk(s) available (need ≥ {MIN_CHUNKS}) — "
+              "pitch CI is degenerate; estimate may be less reliable.")
+        L(lambda: f"    Chroma xcorr: {point_st:+.3f} st  95% CI [{lo_st:+.3f}, {hi_st:+.3f}] st"
+                  f"  ({n} chunk{'s' if n != 1 else ''})")
+        L("    essentia not available — skipping MELODIA refinement")
+        L("  Pitch method: chroma_xcorr")
+        method = "chroma_xcorr"
+        pj = len(w0) // 2 + b     # pitch job index: after the B tempo jobs
+        bo = h["bout_l"]
+        pitch_boot = (bo[pj], (bo[nj + pj], bo[2 * nj + pj]))
+        out.detail.update(chunk_lags=lags, tuning=h["tuning"][2 * c0:2 * c1].copy(),
+                          chroma=h["chroma"][24 * c0:24 * c1].reshape(-1, 12).copy())
+    else:
+        L("Skipping pitch estimation.")
+        src_p, nc_p, method = [], [], None
+
+    # tempo
+    L("Estimating tempo (librosa)…")
+    tempos = {}
+    for side, ws_ in (("src", src_w), ("nc", nc_w)):
+        if side == "src":
+            L("  ← source →")
+        vals = []
+        f = fs if side == "src" else fn
+        st_f, base = starts[f], w0[f]
+        bpm_l, nb_l, nws = h["bpm_l"], h["nbeats_l"], len(ws_)
+        L(lambda st_f=st_f, base=base, ws_=ws_, nws=nws: [
+            f"    tempo window {i + 1}/{nws}  [{st_f[w - base] / SR:.1f}–{(st_f[w - base] + win_n) / SR:.1f} s]"
+            for i, w in enumerate(ws_)])
+        vals = [bpm_l[w] if nb_l[w] >= MIN_BEATS else None for w in ws_]
+        L(lambda vals=vals, n=nws:
+          f"    {sum(1 for v in vals if v is not None)}/{n} windows yielded a confident tempo estimate")
+        tempos[side] = vals
+        if side == "src":
+            valid_src = [t for t in vals if t is not None]
+            nc_dur, src_dur = nc_len / SR, src_len / SR
+            if valid_src and nc_dur > 0 and src_dur > 0:
+                med = C._median(valid_src)
+                pr_ = h['prior_l'][b]
+                L(lambda: f"  NC tempo prior: {pr_:.1f} BPM  "
+                          f"(src median {med:.1f} BPM × dur ratio {src_dur / nc_dur:.4f})")
+            L("  ← nightcore →")
+    out.detail.update(src_tempos=tempos["src"], nc_tempos=tempos["nc"], nc_start_bpm=h["prior_l"][b],
+                      tempo_margin_src=h["margin"][src_w].copy(), tempo_margin_nc=h["margin"][nc_w].copy())
+    L("Computing consensus…")
+    try:
+        bo = h["bout_l"]
+        tempo_boot = (bo[b], (bo[nj + b], bo[2 * nj + b]))
+        res = C.assemble(src_p, nc_p, tempos["src"], tempos["nc"], nc_duration=nc_len / SR,
+                         src_duration=src_len / SR, pitch_boot=pitch_boot, tempo_boot=tempo_boot)
+    except ValueError as exc:
+        out.error = exc
+        return out
+    res.intro_offset_sec = intro
+    res.pitch_method = method
+    if ibi is not None:
+        L("Computing IBI ratio (high-precision beat timestamps, hop=64)…")
+        nb_ = ibi["nibi"]
+        Bn = len(nb_) // 2
+        if nb_[2 * b] >= 4 and nb_[2 * b + 1] >= 4:
+            o = ibi["out"]
+            res.ibi_ratio = float(o[b])
+            res.ibi_ci = (float(o[Bn + b]), float(o[2 * Bn + b]))
+            L(lambda: f"  IBI ratio: {res.ibi_ratio:.6f}×  95% CI [{res.ibi_ci[0]:.6f}, {res.ibi_ci[1]:.6f}]")
+        else:
+            L("  IBI ratio: insufficient beats — skipped")
+        out.detail.update(ibi_nbeats=(int(ibi["nbeats"][2 * b]), int(ibi["nbeats"][2 * b + 1])),
+                          ibi_n=(int(nb_[2 * b]), int(nb_[2 * b + 1])),
+                          ibi_lag=(int(ibi["lag"][2 * b]), int(ibi["lag"][2 * b + 1])))
+        if "beats" in ibi:
+            fb, bt, nbt = ibi["fbase"], ibi["beats"], ibi["nbeats"]
+            out.detail["ibi_beats"] = tuple(bt[fb[f]:fb[f] + max(0, int(nbt[f]))].copy() for f in (fn, fs))
+    L("Done.")
+    out.result = res
+    return out
 
 
 _engines: Dict[Tuple[int, int], Engine] = {}

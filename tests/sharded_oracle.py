@@ -1,0 +1,92 @@
+"""The stage interface of nightcore_analyzer.sharded (DeviceStages on a GPU) restated
+over the CPU oracle, so the window-sharded orchestration — record exchange, energy
+gate, nc prior, consensus placement, result gather — runs in multi-process gloo tests
+without a GPU.  Test infrastructure only (imports oracle/)."""
+from __future__ import annotations
+
+import numpy as np
+
+from oracle import ncref, refglue
+
+
+class OracleStages:
+    def __init__(self, pairs, fail_in=None):
+        flat = []
+        for nc, src in pairs:
+            flat += [np.asarray(nc, np.float32), np.asarray(src, np.float32)]
+        self.length = np.array([len(a) for a in flat], np.int64)
+        self.off = np.concatenate([[0], np.cumsum(self.length)[:-1]]).astype(np.int64)
+        self.buf = np.concatenate(flat) if flat else np.zeros(0, np.float32)
+        self._wins = []
+        self.fail_in = fail_in            # stage name that raises (error-propagation test)
+
+    def _check(self, name):
+        if self.fail_in == name:
+            raise RuntimeError(f"injected failure in {name}")
+
+    def trim(self, p):
+        se = [ncref.trim(self.buf[o:o + n], p.silence_strip_db)[1] for o, n in zip(self.off, self.length)]
+        return np.array([s for s, _ in se], np.int64), np.array([e for _, e in se], np.int64)
+
+    def align(self, start, end):
+        out = []
+        for b in range(len(self.off) // 2):
+            fn, fs = 2 * b, 2 * b + 1
+            src = self.buf[self.off[fs] + start[fs]:self.off[fs] + end[fs]]
+            nc = self.buf[self.off[fn] + start[fn]:self.off[fn] + end[fn]]
+            out.append(refglue.find_content_offset(src, nc))
+        return out
+
+    def windows(self, win_abs, win_n):
+        self._check("windows")
+        self._wins = [self.buf[a:a + win_n] for a in win_abs]
+        return np.array([refglue.rms_db(w) for w in self._wins], np.float64)
+
+    def tempo(self, sel, start_bpm):
+        self._check("tempo")
+        out = np.zeros((len(sel), 4))
+        for k, (i, sb) in enumerate(zip(sel, start_bpm)):
+            t = refglue.estimate_tempo(self._wins[i], 22050, float(sb))
+            out[k] = (t, 4, 0, np.nan) if t is not None else (0.0, 0, 0, np.nan)
+        return out
+
+    def chunks(self, chunk_off, chunk_len):
+        out = np.zeros((len(chunk_off) // 2, 27))
+        for k in range(len(chunk_off) // 2):
+            a = self.buf[chunk_off[2 * k]:chunk_off[2 * k] + chunk_len[2 * k]]
+            b = self.buf[chunk_off[2 * k + 1]:chunk_off[2 * k + 1] + chunk_len[2 * k + 1]]
+            ca, cb = refglue.mean_chroma(a), refglue.mean_chroma(b)
+            out[k, 0] = refglue.cyclic_xcorr_peak(ca, cb)
+            out[k, 3:15], out[k, 15:27] = ca, cb
+        return out
+
+    def bootstrap(self, jobs, seed):
+        """numpy default_rng(seed) per job: ratio of medians (draw order A then B), or the
+        median of A alone; 'linear' 2.5 / 97.5 percentiles (consensus.py:243-312, pitch.py:143-150)."""
+        res = []
+        for A, B in jobs:
+            rng = np.random.default_rng(seed)
+            A = np.asarray(A, np.float64)
+            boot = np.empty(2000)
+            if B is None:
+                point = float(np.median(A))
+                for i in range(2000):
+                    boot[i] = np.median(rng.choice(A, size=len(A), replace=True))
+            else:
+                B = np.asarray(B, np.float64)
+                point = float(np.median(A) / np.median(B))
+                for i in range(2000):
+                    a = rng.choice(A, size=len(A), replace=True)
+                    b = rng.choice(B, size=len(B), replace=True)
+                    boot[i] = np.median(a) / np.median(b)
+            res.append((point, (float(np.percentile(boot, 2.5)), float(np.percentile(boot, 97.5)))))
+        return res
+
+    def ibi(self, f_off, f_len, start_bpm):
+        ibis, nibi = [], []
+        for o, n, sb in zip(f_off, f_len, start_bpm):
+            v = refglue.estimate_ibis_global(self.buf[o:o + n], 22050, start_bpm=float(sb))
+            ibis.append(v if v is not None and len(v) >= 4 else None)
+            nibi.append(0 if v is None else len(v))
+        z = np.zeros(len(f_off), np.int64)
+        return ibis, np.array(nibi, np.int64), z, z

@@ -27,13 +27,15 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, q):
+def _worker(rank, world, port, q, fail_rank=-1):
     import torch.distributed as dist
     from nightcore_analyzer.distributed import run_batch_distributed
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
 
     def fake_analyze(pairs, scale):   # stands in for the GPU engine
+        if rank == fail_rank:
+            raise ValueError(f"rank {rank} failed")
         return [("rank", rank, p * scale) for p in pairs]
 
     out = run_batch_distributed(list(range(7)), analyze_fn=fake_analyze, scale=10)
@@ -42,16 +44,31 @@ def _worker(rank, world, port, q):
     dist.destroy_process_group()
 
 
-def test_run_batch_distributed_gloo_world2():
+def _spawn(fail_rank=-1):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q, fail_rank)) for r in range(2)]
     for p in procs:
         p.start()
     res = dict(q.get(timeout=120) for _ in range(2))
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
+    return res
+
+
+def test_run_batch_distributed_gloo_world2():
+    res = _spawn()
     expect = [("rank", 0 if i < 4 else 1, i * 10) for i in range(7)]
     assert res[0] == expect and res[1] == expect
+
+
+def test_run_batch_distributed_failing_rank_delivers_its_exception():
+    """A rank whose analysis raises still joins the result gather (no rank blocks): its
+    pairs come back as the exception, the other rank's as results."""
+    res = _spawn(fail_rank=1)
+    for r in (0, 1):
+        assert res[r][:4] == [("rank", 0, i * 10) for i in range(4)]
+        assert all(isinstance(e, ValueError) and str(e) == "rank 1 failed" for e in res[r][4:])
+        assert len(res[r]) == 7

@@ -1,0 +1,114 @@
+"""GPU runs of the window-sharded path (nightcore_analyzer.sharded with DeviceStages):
+
+* one rank: every outcome equals Engine.analyze of the same batch (results, report,
+  logs, per-window detail) — the stage-by-stage path is the same computation;
+* two ranks on the one GPU of the box (gloo for the record exchange, libncgpu for the
+  stages): a single pair split over both ranks reproduces the reference's own
+  pipeline.run goldens, on both ranks.
+
+The 8-GPU RCCL run is the driver's; here the exchange is the same all_gather_into_tensor
+call on CPU tensors.
+"""
+import dataclasses
+import math
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+from nightcore_analyzer import engine as E
+from nightcore_analyzer import synth
+from golden.cases import make_case
+
+pytestmark = pytest.mark.gpu
+N_LOAD_LINES = 4
+
+
+def _norm(x):
+    if isinstance(x, dict):
+        return {k: _norm(v) for k, v in x.items()}
+    if isinstance(x, (list, tuple)):
+        return [_norm(v) for v in x]
+    if isinstance(x, float) and not math.isfinite(x):
+        return repr(x)
+    if isinstance(x, np.ndarray):
+        return _norm(x.tolist())
+    return x
+
+
+def _key(o):
+    d = {k: _norm(v) for k, v in o.detail.items()}
+    if o.error is not None:
+        return ("error", type(o.error).__name__, str(o.error), o.logs, d)
+    return ("ok", _norm(dataclasses.asdict(o.result)), str(o.result), o.logs, d)
+
+
+@pytest.fixture(scope="module")
+def eng():
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    return E.get_engine(0)
+
+
+@pytest.mark.parametrize("names", [["chords80", "sweep30", "sweep30_nc_tail_quiet"], ["chords60_intro"],
+                                   ["sweep30_gate_all"]])
+def test_sharded_single_rank_equals_engine(eng, names):
+    from nightcore_analyzer.sharded import run_window_sharded
+    cases = [make_case(synth, n) for n in names]
+    kw = cases[0][2]
+    pairs = [c[:2] for c in cases] + ([synth.make_pair(180.0, 1000)] if not kw else [])
+    p = E.Params(**kw)
+    ref = eng.analyze(pairs, p)
+    got = run_window_sharded(pairs, p)
+    assert [_key(o) for o in got] == [_key(o) for o in ref]
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _worker(rank, world, port, names, q):
+    import torch.distributed as dist
+    from nightcore_analyzer.sharded import run_window_sharded
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        pairs = [make_case(synth, n)[:2] for n in names]
+        outs = run_window_sharded(pairs, E.Params(), device=0)
+        q.put((rank, [(None if o.error is None else str(o.error),
+                       None if o.result is None else _norm(dataclasses.asdict(o.result)),
+                       None if o.result is None else str(o.result), o.logs) for o in outs]))
+    except Exception as exc:     # noqa: BLE001
+        q.put((rank, repr(exc)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_sharded_two_ranks_one_pair_matches_reference(eng, golden_pipeline):
+    names = ["chords80"]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, names, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=240) for _ in range(2))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    g = golden_pipeline["chords80"]
+    for r in (0, 1):
+        assert isinstance(res[r], list), res[r]
+        (err, result, text, logs), = res[r]
+        assert err is None
+        assert logs == g["log"][N_LOAD_LINES:]
+        for k, v in g["result"].items():
+            assert result[k] == v, k
+        assert text == g["str"]
