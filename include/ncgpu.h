@@ -172,6 +172,10 @@ int nc_chroma_mean_shared(nc_ctx* ctx, const float* sig, const int64_t* chunk_of
  * dot(chroma[src_idx[p]], roll(chroma[nc_idx[p]], -k)), in [-5, 6]. */
 int nc_chroma_lag(nc_ctx* ctx, const float* chroma, const int* src_idx, const int* nc_idx, int n_pairs,
                   int* lag_out, void* stream);
+/* nc_chroma_lag plus margin_out[p] = (best - second best xcorr) / |best|: how far the
+ * lag decision is from a tie (no reference equivalent; diagnostics). */
+int nc_chroma_lag_margin(nc_ctx* ctx, const float* chroma, const int* src_idx, const int* nc_idx, int n_pairs,
+                         int* lag_out, double* margin_out, void* stream);
 
 /* ---------------------------------------------------------------------------
  * device glue between the kernels (so a batch needs no host round trip)

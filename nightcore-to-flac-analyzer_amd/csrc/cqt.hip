@@ -706,24 +706,34 @@ __global__ void chroma_finalize_kernel(const double* partial, const int64_t* tf_
 }
 
 // ------------------------------------------------------------------------------ 6. lag
+// lag_out[p]: the reference's first argmax over the 12 cyclic lags (f32 dots, compared in
+// f64); margin_out[p] (nullable): (best - second best) / |best|, the decision's distance
+// from a tie (the soxr_hq -> Kaiser decimator stand-in can move a near-tie)
 __global__ void chroma_lag_kernel(const float* chroma, const int* src_idx, const int* nc_idx, int n_pairs,
-                                  int* lag_out) {
+                                  int* lag_out, double* margin_out) {
   const int p = blockIdx.x * blockDim.x + threadIdx.x;
   if (p >= n_pairs) return;
   const float* s = chroma + (size_t)src_idx[p] * 12;
   const float* q = chroma + (size_t)nc_idx[p] * 12;
   int best = 0;
-  double bv = 0.0;
+  double bv = 0.0, xc[12];
   for (int k = 0; k < 12; ++k) {
     float d = 0.0f;
     for (int j = 0; j < 12; ++j) d = fmaf(s[j], q[(j + k) % 12], d);
     const double v = (double)d;
+    xc[k] = v;
     if (k == 0 || v > bv || (v != v && bv == bv)) {
       bv = v;
       best = k;
     }
   }
   lag_out[p] = best > 6 ? best - 12 : best;
+  if (margin_out) {
+    double second = -INFINITY;
+    for (int k = 0; k < 12; ++k)
+      if (k != best) second = fmax(second, xc[k]);
+    margin_out[p] = bv != 0.0 ? (bv - second) / fabs(bv) : 0.0;
+  }
 }
 
 // ------------------------------------------------------------------------------ host
@@ -886,10 +896,10 @@ int launch_chroma_mean(Context& ctx, const float* sig, const int64_t* chunk_off,
 }
 
 int launch_chroma_lag(const float* chroma, const int* src_idx, const int* nc_idx, int n_pairs, int* lag_out,
-                      hipStream_t st) {
+                      double* margin_out, hipStream_t st) {
   if (n_pairs <= 0) return 0;
   hipLaunchKernelGGL(chroma_lag_kernel, dim3((n_pairs + 63) / 64), dim3(64), 0, st, chroma, src_idx, nc_idx,
-                     n_pairs, lag_out);
+                     n_pairs, lag_out, margin_out);
   NC_HIP(hipGetLastError());
   return 0;
 }

@@ -41,7 +41,7 @@ int launch_chroma_mean(Context& ctx, const float* sig, const int64_t* chunk_off,
                        int* out_tuning_idx, const int* tf_skip, int64_t tf_skip_total, float* ext_pitch,
                        float* ext_mag, int* ext_npk, void* wait_event, void* ws, size_t ws_bytes, hipStream_t st);
 int launch_chroma_lag(const float* chroma, const int* src_idx, const int* nc_idx, int n_pairs, int* lag_out,
-                      hipStream_t st);
+                      double* margin_out, hipStream_t st);
 
 size_t bootstrap_job_bytes(int cap, int n_boot);
 int launch_bootstrap(const BootArgs& a, int n_jobs, hipStream_t st);
@@ -288,7 +288,14 @@ int nc_chroma_lag(nc_ctx* ctx, const float* chroma, const int* src_idx, const in
                   void* stream) {
   CHECK_CTX(ctx);
   SET_DEVICE(ctx);
-  return nc::launch_chroma_lag(chroma, src_idx, nc_idx, n_pairs, lag_out, (hipStream_t)stream);
+  return nc::launch_chroma_lag(chroma, src_idx, nc_idx, n_pairs, lag_out, nullptr, (hipStream_t)stream);
+}
+
+int nc_chroma_lag_margin(nc_ctx* ctx, const float* chroma, const int* src_idx, const int* nc_idx, int n_pairs,
+                         int* lag_out, double* margin_out, void* stream) {
+  CHECK_CTX(ctx);
+  SET_DEVICE(ctx);
+  return nc::launch_chroma_lag(chroma, src_idx, nc_idx, n_pairs, lag_out, margin_out, (hipStream_t)stream);
 }
 
 int nc_window_energy(nc_ctx* ctx, const float* sig, const int64_t* win_off, int n_win, int win_len,

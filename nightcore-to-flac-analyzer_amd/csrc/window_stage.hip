@@ -272,8 +272,8 @@ int launch_window_stage(Context& ctx, const float* sig, const int64_t* win_off, 
   a.tg_out = tg_out;
   a.energy_out = energy_out;
   const size_t lds = (size_t)T * sizeof(double) + (size_t)(T + acw + WT_SEG * acw + acw) * sizeof(double);
-  if (lds > 64 * 1024) {
-    set_error("window stage: window too long for LDS");
+  if (lds > 160 * 1024) {
+    set_error("window stage: window too long for LDS (window_sec above ~225 s at hop 512)");
     return -2;
   }
   {

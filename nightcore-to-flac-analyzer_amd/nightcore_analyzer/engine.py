@@ -22,6 +22,7 @@ The host never touches audio samples after the upload; there is no CPU path.
 from __future__ import annotations
 
 import gc
+import logging
 import math
 import os
 import threading
@@ -76,6 +77,8 @@ def percentile_params(n_boot: int, ci: float) -> Tuple[float, float, float, floa
 
 
 PEAK_SLOTS = 192   # piptrack peak slots per tuning frame (csrc/nc_piptrack.h kPeakSlots)
+NEAR_TIE = 1e-3    # chroma-lag decisions closer than this (relative xcorr gap) are reported
+_logger = logging.getLogger("nightcore_analyzer")
 
 
 class _Upload:
@@ -117,6 +120,7 @@ class _Arena:
 
     def __init__(self):
         self.parts: List[Tuple[str, np.dtype, int]] = []
+        self.host: Optional[torch.Tensor] = None
 
     def add(self, name: str, n: int, dtype) -> None:
         self.parts.append((name, np.dtype(dtype), max(1, int(n))))
@@ -132,9 +136,29 @@ class _Arena:
         return {name: self.buf[o:o + n * dt.itemsize].view(_TORCH_DTYPE[dt.str])
                 for (name, dt, n), o in zip(self.parts, self.offs)}
 
+    def alloc_host(self) -> None:
+        """Allocate the pinned host mirror now (before partial copies)."""
+        if getattr(self, "host", None) is None:
+            self.host = torch.empty(self.nbytes, dtype=torch.uint8, pin_memory=True)
+
+    def copy_parts(self, parts) -> None:
+        """Queue D2H copies of some parts on the current stream, into the same places of the
+        host mirror that to_host() fills: [name] or (name, first element, end element)."""
+        self.alloc_host()
+        idx = {name: i for i, (name, _, _) in enumerate(self.parts)}
+        for part in parts:
+            name, a, b = (part, 0, None) if isinstance(part, str) else part
+            _, dt, n = self.parts[idx[name]]
+            b = n if b is None else b
+            o = self.offs[idx[name]]
+            lo, hi = o + a * dt.itemsize, o + b * dt.itemsize
+            if hi > lo:
+                self.host[lo:hi].copy_(self.buf[lo:hi], non_blocking=True)
+
     def to_host(self) -> Tuple[torch.Tensor, Dict[str, np.ndarray]]:
         """Queue the D2H copy; the numpy views are valid once the stream reaches it."""
-        host = torch.empty(self.nbytes, dtype=torch.uint8, pin_memory=True)
+        self.alloc_host()
+        host = self.host
         host.copy_(self.buf, non_blocking=True)
         hb = host.numpy()
         return host, {name: hb[o:o + n * dt.itemsize].view(dt) for (name, dt, n), o in zip(self.parts, self.offs)}
@@ -256,10 +280,23 @@ class BatchPlan:
     n_cp: int
 
 
+def beat_needs_workspace(T: int, acw: int) -> bool:
+    """nc_tempo_beats runs a T-frame sequence in LDS up to 64 KB (csrc/beat.hip
+    launch_tempo_beats), longer ones through a global workspace."""
+    tab = ((2 * (acw - 1) + 2) * 8 + 15) // 16 * 16
+    return tab + T * 21 + 16 > 64 * 1024
+
+
+MAX_WINDOW_FRAMES = (160 * 1024 - 8 * (3 * 344)) // 16   # window_tg LDS (csrc/window_stage.hip): ~225 s
+
+
 def plan_batch(off: np.ndarray, length: np.ndarray, start: np.ndarray, end: np.ndarray, p: "Params",
                align: Optional[List[Tuple[float, float]]] = None) -> BatchPlan:
     """Silence-trim bounds [start, end) of every file -> BatchPlan (host only, deterministic:
     every rank of a sharded run derives the same plan)."""
+    if 1 + int(p.window_sec * SR) // HOP_LENGTH > MAX_WINDOW_FRAMES:
+        raise ValueError(f"window_sec={p.window_sec} is longer than the engine's per-window stage supports "
+                         f"({(MAX_WINDOW_FRAMES - 1) * HOP_LENGTH / SR:.0f} s)")
     nF = len(off)
     B = nF // 2
     f_off = np.asarray(off, np.int64) + start
@@ -326,6 +363,44 @@ def plan_batch(off: np.ndarray, length: np.ndarray, start: np.ndarray, end: np.n
     n_cp = n_chunks // 2
     return BatchPlan(nF, B, f_off, f_len, strip_len, lead, trail, intro, win_n, hop_n, starts, w0, w1, win_abs, n_win,
                      n_src_w, chunk_off, chunk_len, pair_chunks, n_chunks, n_cp)
+
+
+class _HostViews(dict):
+    """A group's host result views, plus python-list forms ("bpm_l", ...) made on first
+    access for the scalar lookups of the assembly loops (dropped by ``refresh`` when a
+    later stage's copy has landed)."""
+
+    def __missing__(self, key):
+        if key.endswith("_l") and key[:-2] in self:
+            v = self[key[:-2]].tolist()
+            self[key] = v
+            return v
+        raise KeyError(key)
+
+    def refresh(self) -> None:
+        for k in [k for k in self if k.endswith("_l")]:
+            del self[k]
+
+
+class _StageWaiter:
+    """wait(stage) for assemble_pair when lines are streamed: emit the pair's lines so far,
+    then wait for that stage's results (engine._launch_group stage_copy)."""
+
+    def __init__(self, out: PairOutcome, g: dict, h: _HostViews, emit):
+        self.out, self.g, self.h, self.emit = out, g, h, emit
+        self.done = 0
+
+    def flush(self) -> None:
+        lines = self.out.logs                       # renders the deferred lines
+        for line in lines[self.done:]:
+            self.emit(line)
+        self.done = len(lines)
+
+    def __call__(self, stage: str) -> None:
+        self.flush()
+        ev = self.g["stage_ev"].get(stage) if stage != "final" else None
+        (ev or self.g["event"]).synchronize()
+        self.h.refresh()
 
 
 # ------------------------------------------------------------------------------ engine
@@ -626,7 +701,8 @@ class Engine:
         return self.spectral_finish(h)
 
     def analyze(self, pairs: Optional[Sequence[Tuple[np.ndarray, np.ndarray]]] = None, params: Params = None,
-                signals: Optional[DeviceSignals] = None, group_pairs=None) -> List[PairOutcome]:
+                signals: Optional[DeviceSignals] = None, group_pairs=None,
+                log: Optional[Callable[[int, str], None]] = None) -> List[PairOutcome]:
         """Run pipeline.run's analysis for every (nc, src) pair.  ``signals``
         (files ordered nc_0, src_0, nc_1, src_1, ...) may be passed already
         resident in HBM; otherwise ``pairs`` are uploaded.
@@ -641,16 +717,22 @@ class Engine:
         over the host's live objects costs ~10 ms, as long as several groups of device
         work, and lands at a random point of the pipeline.  The call creates no reference
         cycles (everything it allocates is freed by reference counting), and the
-        collector's previous state is restored on return."""
+        collector's previous state is restored on return.
+
+        ``log(pair index, line)``, when given, receives each pair's log lines while the
+        pipeline runs, in the reference's order (pipeline.py:77-215): the device copies
+        each stage's results back as the stage completes (energy gate, pitch, source
+        tempo, nightcore tempo, consensus), and a pair's lines up to a stage are emitted
+        as soon as that stage's results are on the host."""
         gc_was_enabled = gc.isenabled()
         gc.disable()
         try:
-            return self._analyze(pairs, params, signals, group_pairs)
+            return self._analyze(pairs, params, signals, group_pairs, log)
         finally:
             if gc_was_enabled:
                 gc.enable()
 
-    def _analyze(self, pairs, params, signals, group_pairs) -> List[PairOutcome]:
+    def _analyze(self, pairs, params, signals, group_pairs, log=None) -> List[PairOutcome]:
         p = params or Params()
         if signals is None:
             flat = []
@@ -694,13 +776,14 @@ class Engine:
             sub = DeviceSignals(signals.buf, signals.off[sl], signals.length[sl])
             t0 = time.perf_counter()
             pending.append(self._launch_group(sub, p, start[sl].copy(), end[sl].copy(),
-                                              align[g0:g1] if align is not None else None))
+                                              align[g0:g1] if align is not None else None, log is not None))
+            pending[-1]["g0"] = g0
             if hs is not None:
                 hs["launch"] = hs.get("launch", 0.0) + time.perf_counter() - t0
             if len(pending) > self.GROUPS_IN_FLIGHT:
-                outs += self._finish_group(pending.pop(0))
+                outs += self._finish_group(pending.pop(0), log)
         for g in pending:
-            outs += self._finish_group(g)
+            outs += self._finish_group(g, log)
         return outs
 
     def _trim_launch(self, signals: DeviceSignals, f0: int, f1: int, p: Params, stream, ws_name: str):
@@ -764,7 +847,7 @@ class Engine:
         return se_h[:nF].copy(), se_h[nF:].copy()
 
     def _launch_group(self, signals: DeviceSignals, p: Params, start: np.ndarray, end: np.ndarray,
-                      align: Optional[List[Tuple[float, float]]] = None) -> dict:
+                      align: Optional[List[Tuple[float, float]]] = None, stream_logs: bool = False) -> dict:
         """Queue the whole device pipeline of one group of pairs; returns the pending group."""
         dev, st = self.dev, self.stream()
         pl = plan_batch(signals.off, signals.length, start, end, p, align)
@@ -865,7 +948,7 @@ class Engine:
         # one zero-filled output arena, copied back in one D2H
         ar = _Arena()
         for name, n, dt in (("chroma", n_chunks * 12, np.float32), ("tuning", n_chunks, np.float32),
-                            ("clag", n_cp, np.int32), ("vals", TV + PV, np.float64), ("energy", n_win, np.float64),
+                            ("clag", n_cp, np.int32), ("cmargin", n_cp, np.float64), ("vals", TV + PV, np.float64), ("energy", n_win, np.float64),
                             ("active", n_win, np.uint8), ("bpm", n_win, np.float64), ("lag", n_win, np.int32),
                             ("nbeats", n_win, np.int32), ("margin", n_win, np.float64), ("prior", B, np.float64),
                             ("bout", 3 * nj, np.float64), ("sout", 3 * max(1, n_pitch_jobs), np.float64),
@@ -880,6 +963,18 @@ class Engine:
         # leading frames' piptrack peaks to this group's peak lists (its own, zeroed in the
         # arena) and the chroma chain waits for them before the tuning select.
         s1, s2 = torch.cuda.current_stream(dev), self.chroma_stream
+        stage_ev: Dict[str, torch.cuda.Event] = {}
+
+        def stage_copy(stage: str, stream, parts) -> None:
+            """With streamed logs: copy a stage's results back as soon as it completes (into
+            the places of the pinned mirror the final copy also fills, before the final
+            copy's stream waits on this one)."""
+            if stream_logs:
+                with torch.cuda.stream(stream):
+                    ar.copy_parts(parts)
+                    e = torch.cuda.Event()
+                    e.record(stream)
+                    stage_ev[stage] = e
         peaks = None
         ev_stft = None
         if share:
@@ -933,25 +1028,45 @@ class Engine:
                 self.call("nc_chroma_mean", signals.buf.data_ptr(), d["chunk_off"].data_ptr(),
                           d["chunk_len"].data_ptr(), n_chunks, tot_len, int(max(chunk_len)), o["chroma"].data_ptr(),
                           o["tuning"].data_ptr(), None, ws_c.data_ptr(), ws_c.numel(), st2)
-            self.call("nc_chroma_lag", o["chroma"].data_ptr(), d["lag_src"].data_ptr(), d["lag_nc"].data_ptr(), n_cp,
-                      o["clag"].data_ptr(), st2)
+            self.call("nc_chroma_lag_margin", o["chroma"].data_ptr(), d["lag_src"].data_ptr(),
+                      d["lag_nc"].data_ptr(), n_cp, o["clag"].data_ptr(), o["cmargin"].data_ptr(), st2)
             self.call("nc_pitch_hz", o["clag"].data_ptr(), n_cp, pvals[0:n_cp].data_ptr(),
                       pvals[n_cp:2 * n_cp].data_ptr(), pvals[2 * n_cp:3 * n_cp].data_ptr(), st2)
+        n_boot = C.N_BOOTSTRAP
+        il, gl, ih, gh = percentile_params(n_boot, C.CI_LEVEL)
+        bout, sout = o["bout"], o["sout"]
+        if n_pitch_jobs:
+            # chunk-shift bootstrap (pitch.py:143-150, seed 0): needs only the chroma chain
+            ws2 = self.workspace("boot_s", s_tot)
+            ws2.record_stream(s2)
+            self.call("nc_bootstrap_ratio", o["vals"].data_ptr(), d["s_off"].data_ptr(), d["s_n"].data_ptr(), None,
+                      None, n_pitch_jobs, n_boot, d["s_seed"].data_ptr(), il, gl, ih, gh, MIN_CHUNKS,
+                      sout[0:n_pitch_jobs].data_ptr(), sout[n_pitch_jobs:2 * n_pitch_jobs].data_ptr(),
+                      sout[2 * n_pitch_jobs:3 * n_pitch_jobs].data_ptr(), None, d["s_wsoff"].data_ptr(),
+                      d["s_cap"].data_ptr(), ws2.data_ptr(), ws2.numel(), st2)
+        stage_copy("pitch", s2, ["clag", "cmargin", ("vals", TV, TV + PV), "sout", "chroma", "tuning"])
         ev_chroma = torch.cuda.Event()
         ev_chroma.record(s2)
 
         # ---------------------------------------------------------------- 4b. tempo (window stream)
+        # windows longer than ~66 s do not fit the beat tracker's LDS path: global workspace
+        bws, bws_n, btot = None, 0, 0
+        if n_win and beat_needs_workspace(T, acw):
+            wsb = self.workspace("beats", self.ctx.lib.nc_tempo_beats_workspace_bytes(n_win * T))
+            bws, bws_n, btot = wsb.data_ptr(), wsb.numel(), n_win * T
         if n_win:
             self.call("nc_energy_gate", energy.data_ptr(), d["w0"].data_ptr(), d["w1"].data_ptr(), nF,
                       float(p.energy_gate_db), active.data_ptr(), st)
+            stage_copy("gate", s1, ["energy", "active"])
             if n_src_w:
                 self.call("nc_tempo_beats", onset.data_ptr(), d["on_off"].data_ptr(), d["on_len"].data_ptr(),
                           n_src_w, T, tg.data_ptr(), acw, d["start120"].data_ptr(), d["src_pair"].data_ptr(),
                           active.data_ptr(), HOP_LENGTH, 1, bpm.data_ptr(), lag.data_ptr(), nbeats.data_ptr(),
-                          margin.data_ptr(), None, 0, None, 0, st)
+                          margin.data_ptr(), None, btot, bws, bws_n, st)
             self.call("nc_tempo_prior", bpm.data_ptr(), nbeats.data_ptr(), active.data_ptr(),
                       d["src_w0"].data_ptr(), d["src_w1"].data_ptr(), d["src_len"].data_ptr(),
                       d["nc_len"].data_ptr(), B, prior.data_ptr(), st)
+            stage_copy("src", s1, [("bpm", 0, n_src_w), ("nbeats", 0, n_src_w), ("margin", 0, n_src_w), "prior"])
             n_nc_w = n_win - n_src_w
             if n_nc_w:
                 self.call("nc_tempo_beats", onset.data_ptr(),
@@ -959,7 +1074,8 @@ class Engine:
                           tg[n_src_w * acw:].data_ptr(), acw, prior.data_ptr(), d["nc_pair"].data_ptr(),
                           active[n_src_w:].data_ptr(), HOP_LENGTH, 1, bpm[n_src_w:].data_ptr(),
                           lag[n_src_w:].data_ptr(), nbeats[n_src_w:].data_ptr(), margin[n_src_w:].data_ptr(),
-                          None, 0, None, 0, st)
+                          None, btot, bws, bws_n, st)
+            stage_copy("nc", s1, [("bpm", n_src_w, n_win), ("nbeats", n_src_w, n_win), ("margin", n_src_w, n_win)])
             # valid-tempo compaction per side: the counts land in the bootstrap jobs' a_n / b_n
             for side, cnt in (("nc", d["a_n"]), ("src", d["b_n"])):
                 self.call("nc_collect_valid", bpm.data_ptr(), nbeats.data_ptr(), active.data_ptr(),
@@ -967,6 +1083,7 @@ class Engine:
                           cnt.data_ptr(), st)
         else:
             prior.fill_(120.0)
+            stage_copy("gate", s1, ["prior"])
 
         # ---------------------------------------------------------------- 5. IBI pass (window stream)
         ibi = None
@@ -982,23 +1099,12 @@ class Engine:
         s3.wait_event(ev_window)
         s3.wait_event(ev_chroma)
         st3 = s3.cuda_stream
-        n_boot = C.N_BOOTSTRAP
-        il, gl, ih, gh = percentile_params(n_boot, C.CI_LEVEL)
-        bout, sout = o["bout"], o["sout"]
         ws = self.workspace("boot", tot)
         ws.record_stream(s3)
         self.call("nc_bootstrap_ratio", o["vals"].data_ptr(), d["a_off"].data_ptr(), d["a_n"].data_ptr(),
                   d["b_off"].data_ptr(), d["b_n"].data_ptr(), nj, n_boot, d["seed"].data_ptr(), il, gl, ih, gh,
                   C.MIN_VALID, bout[0:nj].data_ptr(), bout[nj:2 * nj].data_ptr(), bout[2 * nj:].data_ptr(), None,
                   d["wsoff"].data_ptr(), d["cap"].data_ptr(), ws.data_ptr(), ws.numel(), st3)
-        if n_pitch_jobs:
-            ws2 = self.workspace("boot_s", s_tot)
-            ws2.record_stream(s3)
-            self.call("nc_bootstrap_ratio", o["vals"].data_ptr(), d["s_off"].data_ptr(), d["s_n"].data_ptr(), None,
-                      None, n_pitch_jobs, n_boot, d["s_seed"].data_ptr(), il, gl, ih, gh, MIN_CHUNKS,
-                      sout[0:n_pitch_jobs].data_ptr(), sout[n_pitch_jobs:2 * n_pitch_jobs].data_ptr(),
-                      sout[2 * n_pitch_jobs:3 * n_pitch_jobs].data_ptr(), None, d["s_wsoff"].data_ptr(),
-                      d["s_cap"].data_ptr(), ws2.data_ptr(), ws2.numel(), st3)
 
         # ---------------------------------------------------------------- 7. async D2H into pinned buffers
         with torch.cuda.stream(s3):
@@ -1016,29 +1122,37 @@ class Engine:
                         host["ibi_" + k] = v
             ev = torch.cuda.Event()
             ev.record(s3)
-        return dict(p=p, host=host, pinned=pinned, event=ev, keep=(d, o, ar, ibi, peaks), has_ibi=ibi is not None,
+        return dict(p=p, host=host, pinned=pinned, event=ev, stage_ev=stage_ev, keep=(d, o, ar, ibi, peaks),
+                    has_ibi=ibi is not None,
                     align=align,
                     starts=starts, w0=w0, w1=w1, f_len=f_len,
                     strip_len=strip_len, lead=lead, trail=trail, intro=intro, win_n=win_n,
                     pair_chunks=pair_chunks, n_cp=n_cp, nj=nj, n_pitch_jobs=n_pitch_jobs, B=B)
 
-    def _finish_group(self, g: dict) -> List[PairOutcome]:
-        """Wait for one group's results (sync 2 of that group) and assemble them on the host."""
+    def _finish_group(self, g: dict, log=None) -> List[PairOutcome]:
+        """Wait for one group's results (sync 2 of that group) and assemble them on the host.
+        With ``log``, each pair's lines go out stage by stage as the stages' results land."""
         hs = self.host_stats
         t0 = time.perf_counter()
-        g["event"].synchronize()
+        if log is None:
+            g["event"].synchronize()
         t1 = time.perf_counter()
-        h = dict(g["host"])
-        # python-list views for the scalar accesses of the per-pair assembly loops
-        for k in ("active", "bpm", "nbeats", "prior", "clag", "pvals", "bout", "sout"):
-            h[k + "_l"] = h[k].tolist()
+        h = _HostViews(g["host"])
         g["starts_l"] = [x.tolist() for x in g["starts"]]
         g["w0"], g["w1"] = g["w0"].tolist(), g["w1"].tolist()
-        ibi = {k[4:]: v for k, v in h.items() if k.startswith("ibi_")} if g["has_ibi"] else None
-        out = [assemble_pair(b, g["p"], h, ibi, g["starts_l"], g["w0"], g["w1"], g["f_len"], g["strip_len"],
-                                   g["lead"], g["trail"], g["intro"][b], g["win_n"], g["pair_chunks"], g["n_cp"],
-                                   g["nj"], g["n_pitch_jobs"], g["align"][b] if g["align"] else None)
-               for b in range(g["B"])]
+        ibi = {k[4:]: v for k, v in g["host"].items() if k.startswith("ibi_")} if g["has_ibi"] else None
+        out = []
+        for b in range(g["B"]):
+            o = PairOutcome()
+            wait = None
+            if log is not None:
+                wait = _StageWaiter(o, g, h, lambda line, i=g["g0"] + b: log(i, line))
+            assemble_pair(b, g["p"], h, ibi, g["starts_l"], g["w0"], g["w1"], g["f_len"], g["strip_len"], g["lead"],
+                          g["trail"], g["intro"][b], g["win_n"], g["pair_chunks"], g["n_cp"], g["nj"],
+                          g["n_pitch_jobs"], g["align"][b] if g["align"] else None, out=o, wait=wait)
+            if wait is not None:
+                wait.flush()
+            out.append(o)
         if hs is not None:
             hs["wait"] = hs.get("wait", 0.0) + t1 - t0
             hs["assemble"] = hs.get("assemble", 0.0) + time.perf_counter() - t1
@@ -1124,8 +1238,14 @@ class Engine:
 
 # ------------------------------------------------------------------------------ host assembly + logs
 def assemble_pair(b, p: Params, h, ibi, starts, w0, w1, f_len, strip_len, lead, trail, intro,
-                   win_n, pair_chunks, n_cp, nj, n_pitch_jobs, align=None) -> PairOutcome:
-    out = PairOutcome()
+                  win_n, pair_chunks, n_cp, nj, n_pitch_jobs, align=None, out: Optional[PairOutcome] = None,
+                  wait=None) -> PairOutcome:
+    """One pair's AnalysisResult (or run()'s exception) and its log lines, in the order of
+    pipeline.py:77-215, from the host views of its group.  ``wait(stage)`` ("gate",
+    "pitch", "src", "nc", "final") is called before the lines that need a stage's
+    results (streamed logs); without it every result is already on the host."""
+    out = out if out is not None else PairOutcome()
+    wait = wait or (lambda stage: None)
     L = out._log_ops.append   # str, or a callable rendering the line(s) when logs are read
     fn, fs = 2 * b, 2 * b + 1
     nc_len, src_len = int(f_len[fn]), int(f_len[fs])
@@ -1147,6 +1267,7 @@ def assemble_pair(b, p: Params, h, ibi, starts, w0, w1, f_len, strip_len, lead, 
     L(lambda: [f"Slicing into {p.window_sec:.0f} s windows (hop {p.hop_sec:.0f} s)…",
                f"  nightcore: {len(starts[fn])} windows  |  source: {len(starts[fs])} windows",
                f"Energy gating (threshold {p.energy_gate_db} dB below peak)…"])
+    wait("gate")
     act = h["active_l"]
     src_w = [w for w in range(w0[fs], w1[fs]) if act[w]]
     nc_w = [w for w in range(w0[fn], w1[fn]) if act[w]]
@@ -1165,6 +1286,7 @@ def assemble_pair(b, p: Params, h, ibi, starts, w0, w1, f_len, strip_len, lead, 
         L("Estimating pitch (chromagram cross-correlation)…")
         c0, c1 = pair_chunks[b]
         n = c1 - c0
+        wait("pitch")
         lags = h["clag_l"][c0:c1]
         shifts = h["pvals"][c0:c1]
         pv = h["pvals_l"]
@@ -1183,11 +1305,13 @@ def assemble_pair(b, p: Params, h, ibi, starts, w0, w1, f_len, strip_len, lead, 
         L("    essentia not available — skipping MELODIA refinement")
         L("  Pitch method: chroma_xcorr")
         method = "chroma_xcorr"
-        pj = len(w0) // 2 + b     # pitch job index: after the B tempo jobs
-        bo = h["bout_l"]
-        pitch_boot = (bo[pj], (bo[nj + pj], bo[2 * nj + pj]))
-        out.detail.update(chunk_lags=lags, tuning=h["tuning"][2 * c0:2 * c1].copy(),
+        margins = h["cmargin"][c0:c1].copy()
+        out.detail.update(chunk_lags=lags, chunk_lag_margin=margins, tuning=h["tuning"][2 * c0:2 * c1].copy(),
                           chroma=h["chroma"][24 * c0:24 * c1].reshape(-1, 12).copy())
+        if len(margins) and margins.min() < NEAR_TIE:
+            # not in the reference's log stream (kept identical); Python logging only
+            _logger.info("chroma lag near-tie in pair %d: chunk(s) %s, relative margin %s", b,
+                         np.flatnonzero(margins < NEAR_TIE).tolist(), np.round(margins[margins < NEAR_TIE], 6).tolist())
     else:
         L("Skipping pitch estimation.")
         src_p, nc_p, method = [], [], None
@@ -1201,10 +1325,16 @@ def assemble_pair(b, p: Params, h, ibi, starts, w0, w1, f_len, strip_len, lead, 
         vals = []
         f = fs if side == "src" else fn
         st_f, base = starts[f], w0[f]
-        bpm_l, nb_l, nws = h["bpm_l"], h["nbeats_l"], len(ws_)
+        nws = len(ws_)
         L(lambda st_f=st_f, base=base, ws_=ws_, nws=nws: [
             f"    tempo window {i + 1}/{nws}  [{st_f[w - base] / SR:.1f}–{(st_f[w - base] + win_n) / SR:.1f} s]"
             for i, w in enumerate(ws_)])
+        wait(side)
+        bpm_l, nb_l = h["bpm_l"], h["nbeats_l"]
+        if any(nb_l[w] < 0 for w in ws_):
+            # the device beat list overflowed its capacity: an engine limit, not "no tempo"
+            out.error = _native.NativeError(f"beat tracker capacity exceeded in a {side} window of pair {b}")
+            return out
         vals = [bpm_l[w] if nb_l[w] >= MIN_BEATS else None for w in ws_]
         L(lambda vals=vals, n=nws:
           f"    {sum(1 for v in vals if v is not None)}/{n} windows yielded a confident tempo estimate")
@@ -1221,6 +1351,11 @@ def assemble_pair(b, p: Params, h, ibi, starts, w0, w1, f_len, strip_len, lead, 
     out.detail.update(src_tempos=tempos["src"], nc_tempos=tempos["nc"], nc_start_bpm=h["prior_l"][b],
                       tempo_margin_src=h["margin"][src_w].copy(), tempo_margin_nc=h["margin"][nc_w].copy())
     L("Computing consensus…")
+    wait("final")
+    if p.compute_pitch:
+        pj = len(w0) // 2 + b     # pitch job index: after the B tempo jobs
+        bo = h["bout_l"]
+        pitch_boot = (bo[pj], (bo[nj + pj], bo[2 * nj + pj]))
     try:
         bo = h["bout_l"]
         tempo_boot = (bo[b], (bo[nj + b], bo[2 * nj + b]))

@@ -2,8 +2,8 @@
 (drop-in for the reference's nightcore_analyzer/io.py).
 
 * ``load_audio`` (io.py:44-55) decodes on the CPU — file decode is out of the
-  engine's scope (north_star); WAV (PCM 8/16/24/32-bit, float) and ``.npy`` are
-  read with the standard library / numpy, down-mixed to mono float32 and, if
+  engine's scope (north_star); WAV (PCM 8/16/24/32-bit, IEEE float, plain or
+  WAVE_FORMAT_EXTENSIBLE) and ``.npy`` are parsed with numpy, down-mixed to mono float32 and, if
   the file is not at 22 050 Hz, resampled on the GPU by ``nc_resample_poly``
   (bit-identical to scipy.signal.resample_poly; the reference uses librosa.load's
   soxr_hq, which is absent here — see DESIGN.md).
@@ -14,7 +14,6 @@
 """
 from __future__ import annotations
 
-import wave
 from dataclasses import dataclass
 from pathlib import Path
 from typing import List, Optional
@@ -45,23 +44,51 @@ def _rms_db(audio: np.ndarray) -> float:
     return float(window_energies(get_engine(), audio, np.array([0]), len(audio))[0])
 
 
+_WAVE_PCM, _WAVE_FLOAT, _WAVE_EXTENSIBLE = 1, 3, 0xFFFE
+
+
 def _read_wav(path: Path):
-    with wave.open(str(path), "rb") as w:
-        ch, width, sr, n = w.getnchannels(), w.getsampwidth(), w.getframerate(), w.getnframes()
-        raw = w.readframes(n)
-    if width == 1:
+    """RIFF/WAVE -> (mono float32, rate): PCM 8 (unsigned) / 16 / 24 / 32-bit and IEEE float
+    32 / 64-bit, plain or WAVE_FORMAT_EXTENSIBLE (the sub-format GUID's first two bytes
+    carry the format tag), scaled to [-1, 1) as soundfile does and averaged over channels
+    (librosa.load(mono=True))."""
+    data = Path(path).read_bytes()
+    if len(data) < 12 or data[:4] not in (b"RIFF", b"RF64") or data[8:12] != b"WAVE":
+        raise ValueError(f"{path}: not a RIFF/WAVE file")
+    fmt = raw = None
+    pos = 12
+    while pos + 8 <= len(data):
+        cid, size = data[pos:pos + 4], int.from_bytes(data[pos + 4:pos + 8], "little")
+        body = data[pos + 8:pos + 8 + size]
+        if cid == b"fmt ":
+            fmt = body
+        elif cid == b"data":
+            raw = body
+        pos += 8 + size + (size & 1)
+    if fmt is None or raw is None or len(fmt) < 16:
+        raise ValueError(f"{path}: WAVE file without fmt/data chunks")
+    tag, ch = int.from_bytes(fmt[0:2], "little"), int.from_bytes(fmt[2:4], "little")
+    sr, bits = int.from_bytes(fmt[4:8], "little"), int.from_bytes(fmt[14:16], "little")
+    if tag == _WAVE_EXTENSIBLE and len(fmt) >= 26:
+        tag = int.from_bytes(fmt[24:26], "little")          # SubFormat GUID data1 (low 16 bits)
+    width = bits // 8
+    n = len(raw) // (width * ch) * width * ch
+    raw = raw[:n]
+    if tag == _WAVE_FLOAT and width in (4, 8):
+        x = np.frombuffer(raw, "<f4" if width == 4 else "<f8").astype(np.float32)
+    elif tag == _WAVE_PCM and width == 1:
         x = (np.frombuffer(raw, np.uint8).astype(np.float32) - 128.0) / 128.0
-    elif width == 2:
+    elif tag == _WAVE_PCM and width == 2:
         x = np.frombuffer(raw, "<i2").astype(np.float32) / 32768.0
-    elif width == 3:
+    elif tag == _WAVE_PCM and width == 3:
         b = np.frombuffer(raw, np.uint8).reshape(-1, 3).astype(np.int32)
         v = b[:, 0] | (b[:, 1] << 8) | (b[:, 2] << 16)
         v = np.where(v >= 1 << 23, v - (1 << 24), v)
         x = v.astype(np.float32) / float(1 << 23)
-    elif width == 4:
-        x = np.frombuffer(raw, "<i4").astype(np.float32) / 2147483648.0
+    elif tag == _WAVE_PCM and width == 4:
+        x = (np.frombuffer(raw, "<i4").astype(np.float64) / 2147483648.0).astype(np.float32)
     else:
-        raise ValueError(f"unsupported WAV sample width {width}")
+        raise ValueError(f"{path}: unsupported WAVE format tag {tag} with {bits}-bit samples")
     return x.reshape(-1, ch).mean(axis=1).astype(np.float32), sr
 
 
@@ -75,15 +102,7 @@ def load_audio(path: str, sr: Optional[int] = SAMPLE_RATE) -> tuple[np.ndarray, 
         if y.ndim > 1:
             y = y.mean(axis=0).astype(np.float32)
     elif p.suffix.lower() == ".wav":
-        try:
-            y, file_sr = _read_wav(p)
-        except wave.Error:
-            import scipy.io.wavfile
-            file_sr, y = scipy.io.wavfile.read(p)
-            y = np.asarray(y, np.float32)
-            if y.ndim > 1:
-                y = y.mean(axis=1)
-            y = y.astype(np.float32)
+        y, file_sr = _read_wav(p)
     else:
         raise NotImplementedError(
             f"{p.suffix} decoding is outside the engine (the reference uses librosa.load/soundfile, "

@@ -52,10 +52,11 @@ def run(nightcore_path: str, source_path: str, *, window_sec: float = WINDOW_SEC
     nc = _load(nightcore_path, _log, "nightcore")
     src = _load(source_path, _log, "source")
     from .engine import get_engine
+    # log lines stream out as the device stages complete (pipeline.py:77-215 logs as it goes;
+    # the GUI worker forwards each line live, gui/worker.py:46-53)
     outcome, = get_engine().analyze([(nc, src)], _params(window_sec, hop_sec, energy_gate_db, silence_strip_db,
-                                                         src_trim_sec, auto_align, compute_pitch))
-    for line in outcome.logs:
-        _log(line)
+                                                         src_trim_sec, auto_align, compute_pitch),
+                                    log=(lambda i, line: _log(line)) if log is not None else None)
     if outcome.error is not None:
         raise outcome.error
     return outcome.result
@@ -75,11 +76,6 @@ def run_batch(pairs: Sequence[Tuple[PathOrArray, PathOrArray]], *, window_sec: f
     arrays = [(_load(n, quiet, "nightcore"), _load(s, quiet, "source")) for n, s in pairs]
     from .engine import get_engine
     outs = get_engine().analyze(arrays, _params(window_sec, hop_sec, energy_gate_db, silence_strip_db,
-                                                src_trim_sec, auto_align, compute_pitch, compute_ibi))
-    res = []
-    for i, o in enumerate(outs):
-        if log is not None:
-            for line in o.logs:
-                log(f"[pair {i}] {line}")
-        res.append(o.error if o.error is not None else o.result)
-    return res
+                                                src_trim_sec, auto_align, compute_pitch, compute_ibi),
+                                log=(lambda i, line: log(f"[pair {i}] {line}")) if log is not None else None)
+    return [o.error if o.error is not None else o.result for o in outs]

@@ -49,8 +49,8 @@ from .engine import (ALIGN_MIN_OFFSET, CHUNK_SEC, HOP_LENGTH, IBI_HOP, MIN_BEATS
 # per-window record: energy_db, bpm, nbeats, tempo lag, decision margin
 W_ENERGY, W_BPM, W_NBEATS, W_LAG, W_MARGIN = range(5)
 W_FIELDS = 5
-# per-chunk-pair record: lag, tuning (src, nc), mean chroma (src 12, nc 12)
-CP_FIELDS = 3 + 24
+# per-chunk-pair record: lag, tuning (src, nc), mean chroma (src 12, nc 12), lag margin
+CP_FIELDS = 3 + 24 + 1
 
 
 class ShardError(RuntimeError):
@@ -172,7 +172,7 @@ class DeviceStages:
         lag = torch.zeros(n, dtype=torch.int32, device=eng.dev)
         nb = torch.zeros(n, dtype=torch.int32, device=eng.dev)
         mg = torch.zeros(n, dtype=torch.float64, device=eng.dev)
-        ws = eng.workspace("beats", eng.ctx.lib.nc_tempo_beats_workspace_bytes(n * T))
+        ws = eng.workspace("beats", eng.ctx.lib.nc_tempo_beats_workspace_bytes(n * T))   # any window length
         eng.call("nc_tempo_beats", w["onset"].data_ptr(), d["on_off"].data_ptr(), d["on_len"].data_ptr(), n, T,
                  tg.data_ptr(), acw, d["start"].data_ptr(), None, None, HOP_LENGTH, 1, bpm.data_ptr(),
                  lag.data_ptr(), nb.data_ptr(), mg.data_ptr(), None, n * T, ws.data_ptr(), ws.numel(), eng.stream())
@@ -203,12 +203,14 @@ class DeviceStages:
         eng.call("nc_chroma_mean", self.sig.buf.data_ptr(), d["off"].data_ptr(), d["len"].data_ptr(), n, tot,
                  int(max(chunk_len)), chroma.data_ptr(), tun.data_ptr(), None, ws.data_ptr(), ws.numel(),
                  eng.stream())
-        eng.call("nc_chroma_lag", chroma.data_ptr(), d["si"].data_ptr(), d["ni"].data_ptr(), n // 2, lag.data_ptr(),
-                 eng.stream())
+        mg = torch.empty(n // 2, dtype=torch.float64, device=eng.dev)
+        eng.call("nc_chroma_lag_margin", chroma.data_ptr(), d["si"].data_ptr(), d["ni"].data_ptr(), n // 2,
+                 lag.data_ptr(), mg.data_ptr(), eng.stream())
         out[:, 0] = lag.cpu().numpy()
         t = tun.cpu().numpy().reshape(-1, 2)
         out[:, 1:3] = t
-        out[:, 3:] = chroma.cpu().numpy().reshape(-1, 24)
+        out[:, 3:27] = chroma.cpu().numpy().reshape(-1, 24)
+        out[:, 27] = mg.cpu().numpy()
         return out
 
     def bootstrap(self, jobs, seed: int):
@@ -358,9 +360,10 @@ def _consensus(stages, p: Params, pl, align, active, energy, table, prior, cps, 
 
     pvals = np.concatenate([shifts, nc_hz, src_hz]) if n_cp else np.zeros(3)
     tun = cps[:, 1:3].reshape(-1).astype(np.float32) if n_cp else np.zeros(0, np.float32)
-    chroma = cps[:, 3:].reshape(-1).astype(np.float32) if n_cp else np.zeros(0, np.float32)
+    chroma = cps[:, 3:27].reshape(-1).astype(np.float32) if n_cp else np.zeros(0, np.float32)
     h = {"active_l": active.tolist(), "energy": energy, "clag_l": lags, "pvals": pvals, "pvals_l": pvals.tolist(),
          "sout_l": sout.tolist(), "bout_l": bout.tolist(), "tuning": tun, "chroma": chroma,
+         "cmargin": cps[:, 27].copy() if n_cp else np.zeros(0),
          "bpm_l": bpm.tolist(), "nbeats_l": [int(v) for v in nbeats], "prior_l": prior.tolist(),
          "margin": table[:, W_MARGIN]}
     starts_l = [s.tolist() for s in pl.starts]

@@ -159,3 +159,21 @@ def test_goldens_inside_multi_group_batch(eng, bench_pairs, golden_pipeline, kw_
             continue
         single, = eng.analyze([pair], p)
         assert _key(outs[j]) == _key(single), j
+
+
+def test_streamed_logs_equal_outcome_logs(eng, bench_pairs, golden_pipeline):
+    """Engine.analyze(log=...) emits every pair's lines stage by stage while the groups run
+    (run() / run_batch forward them live, as the reference logs while it works): per pair,
+    the streamed lines are exactly the outcome's logs, the goldens' lines included, and
+    the results equal the unstreamed run."""
+    names = ["chords80", "sweep30", "sweep30_nc_tail_quiet"]
+    batch = [make_case(synth, n)[:2] for n in names] + list(bench_pairs[:15])
+    got = {}
+    outs = eng.analyze(batch, E.Params(), group_pairs=4, log=lambda i, line: got.setdefault(i, []).append(line))
+    ref = eng.analyze(batch, E.Params(), group_pairs=4)
+    assert sorted(got) == list(range(len(batch)))
+    for i, (o, r) in enumerate(zip(outs, ref)):
+        assert got[i] == o.logs == r.logs, i
+        assert _key(o) == _key(r), i
+    for i, n in enumerate(names):
+        assert got[i] == golden_pipeline[n]["log"][N_LOAD_LINES:], n

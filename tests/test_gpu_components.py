@@ -127,3 +127,17 @@ def test_full_size_pair_properties(eng):
     assert abs(r.pitch_ratio - 2 ** (float(np.median(ref_lags)) / 36)) < 1e-12
     assert r.classification == "time_stretch_only"
     assert abs(r.ibi_ratio - 1.25) < 0.01
+
+
+def test_long_windows_match_oracle(eng):
+    """--window 90 (cli.py:37): 3 876-frame windows take the beat tracker's global-workspace
+    path and a window_tg launch above 64 KB of LDS; tempos equal the oracle's."""
+    nc, src = synth.make_pair(300.0, 1014)
+    p = E.Params(window_sec=90.0, hop_sec=45.0, compute_ibi=False)
+    out, = eng.analyze([(nc, src)], p)
+    ref = refglue.run_arrays(nc, src, window_sec=90.0, hop_sec=45.0, compute_ibi=False)
+    assert out.error is None, out.error
+    assert out.result.src_tempos_raw == ref["src_tempos"] and out.result.nc_tempos_raw == ref["nc_tempos"]
+    assert out.result.tempo_ratio == ref["tempo_ratio"]
+    with pytest.raises(ValueError):
+        eng.analyze([(nc, src)], E.Params(window_sec=240.0, hop_sec=60.0))
