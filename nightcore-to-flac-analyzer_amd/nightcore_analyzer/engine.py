@@ -196,7 +196,7 @@ class PairOutcome:
                 else:
                     r = x()
                     lines.extend(r) if isinstance(r, list) else lines.append(r)
-            self._log_ops = lines
+            self._log_ops[:] = lines        # in place: assemble_pair keeps appending to this list
         return self._log_ops
 
 
