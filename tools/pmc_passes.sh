@@ -5,6 +5,7 @@ set -o pipefail
 OUT=$1; shift
 export TMPDIR=/tmp
 R=$GRAFT_REPO_ROOT
+mkdir -p $R/$OUT
 P1="SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE"
 P2="SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_INSTS_SALU SQ_INSTS_SMEM SQ_BUSY_CYCLES GRBM_GUI_ACTIVE GRBM_COUNT"
 for t in "$@"; do
