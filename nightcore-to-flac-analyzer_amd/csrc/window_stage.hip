@@ -10,35 +10,36 @@
 //                  t' = t - (1 + n_fft / (2 hop))                      tempo.py:44
 //     tg_mean[k] = mean_t ac_t[k] / ac_t[0],  ac_t = autocorr(hann(win) * ramp_pad(onset)[t:t+win])
 //                                                                      tempo.py:45/63
-//   the autocorrelation evaluated by five sliding f64 sums per lag (nc_slide.h).
+//   the lag sums evaluated as six correlations of prefix-sum sequences (nc_tgcorr.h).
 // librosa restated in oracle/ncref.py (mel_db, onset_strength, tempogram_mean).
 #include <algorithm>
 
 #include "nc_block.h"
 #include "nc_engine.h"
 #include "nc_slide.h"
+#include "nc_tgcorr.h"
 
 #include "stft_args.h"
 
 namespace nc {
 
-// Tuning knobs (compile-time; tools/wtg_variants.sh sweeps them):
-//   NC_WT_SEG   frame segments per window, each an independent set of recurrences
-//   NC_WT_PAIR  lags per thread (1, or 2 = k and acw-1-k interleaved)
-//   NC_WT_SKIP  diagnosis only: 1 skips the sliding sums, 2 also skips onset + normaliser
-#ifndef NC_WT_SEG
-#define NC_WT_SEG 1
+// The tempogram sum is evaluated as six lag correlations (nc_tgcorr.h): per window,
+//   T tg_mean[k] = sum_{i<3} phi_i(k) (Hank_i(k) - Toep_i(k)),  phi = (1, cos theta k, sin theta k),
+//   Hank_i(k) = sum_u a_i[u] x[u + k],  Toep_i(k) = sum_u b_i[u] x[u - k],
+// with a_i / b_i built from prefix sums of the frame normalisers (derivation in nc_tgcorr.h).
+// Diagnosis knobs (tools/wtg_variants.sh): NC_WT_THREADS workgroup size, NC_WT_STAGE
+// stops after 1 onset, 2 normalisers, 3 prefix sums + sequences (4 = the whole kernel).
+#ifndef NC_WT_THREADS
+#define NC_WT_THREADS 512
 #endif
-#ifndef NC_WT_PAIR
-#define NC_WT_PAIR 2
+#ifndef NC_WT_RINV_BLOCKED
+#define NC_WT_RINV_BLOCKED 1
 #endif
-#ifndef NC_WT_SKIP
-#define NC_WT_SKIP 0
+#ifndef NC_WT_STAGE
+#define NC_WT_STAGE 4
 #endif
-constexpr int WT_SEG = NC_WT_SEG;
-constexpr int WT_PAIR = NC_WT_PAIR;
-constexpr int WT_WAVES = (WT_PAIR == 2 ? 3 : 6) * WT_SEG;  // ceil(344 / WT_PAIR / 64) waves per segment
-constexpr int WT_THREADS = WT_WAVES * 64;
+constexpr int WT_THREADS = NC_WT_THREADS;  // 8 waves; ~78 KB LDS -> two windows per CU
+constexpr size_t kWinTgLdsCap = 160 * 1024 - 1024;  // dynamic LDS; the rest holds BlockScratch
 
 struct WinTgArgs {
   const float* sdb;            // [n_win * T][128]
@@ -57,22 +58,34 @@ struct WinTgArgs {
   unsigned long long* span = nullptr;  // nc_profile execution span (nc_device.h)
 };
 
-__global__ __launch_bounds__(WT_THREADS) void window_tg_kernel(WinTgArgs a) {
-  const Span span_(a.span);
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  __shared__ BlockScratch<WT_THREADS> red;
-  const int w = blockIdx.x;
-  if (a.active && !a.active[w]) return;
-  const int T = a.T, acw = a.acw, p = acw / 2;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  double* sh_rinv = reinterpret_cast<double*>(smem);          // [T]
-  double* sh_x = sh_rinv + T;                                 // [T + acw] ramp-padded onset (f32 values)
-  const int64_t g0 = (int64_t)w * T;
+// LDS carve-up of one window (doubles), shared by the kernel and its launcher.
+struct WinTgLds {
+  int T, acw, U, xoff, xlen, seq, scr, scr_len, total;
+  __host__ __device__ WinTgLds(int T_, int acw_) : T(T_), acw(acw_) {
+    U = tgc_extent(T, acw);
+    xoff = tgc_pad(acw);                          // x[i] at xoff + i; zeros outside [0, T + 2 (acw / 2))
+    xlen = U + 2 * xoff;
+    seq = xlen;                                   // [6][U] correlation sequences
+    const int pre = T + acw + 2 * acw + 5 * (T + 1);  // rinv, Hann^2, (cos, sin) table, prefix sums
+    const int post = tgc_segments(acw, WT_THREADS) * tgc_blocks(acw) * TGC_LB;  // per-segment partials
+    scr = seq + 6 * U;
+    scr_len = pre > post ? pre : post;
+    total = scr + scr_len;
+  }
+};
 
-  // window max (top_db clamp) and energy, fixed-order reductions
+// Window max (top_db clamp) and energy, then the ramp-padded onset envelope into
+// x[0, T + 2 (acw / 2)).  Each wave owns a contiguous run of frames and walks it 8 frames
+// at a time, loading the 9 S_db rows those frames difference (rows shared between
+// neighbours) before using any of them, so 18 row loads per lane are in flight instead of 2.
+template <int NT>
+__device__ __forceinline__ void wtg_onset(const WinTgArgs& a, int w, double* sh_x, BlockScratch<NT>& red) {
+  const int T = a.T, p = a.acw / 2;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int64_t g0 = (int64_t)w * T;
   float m = -INFINITY;
   double e = 0.0;
-  for (int i = tid; i < T; i += WT_THREADS) {
+  for (int i = tid; i < T; i += NT) {
     m = fmaxf(m, a.frame_max[g0 + i]);
     e += a.frame_energy[g0 + i];
   }
@@ -81,116 +94,201 @@ __global__ __launch_bounds__(WT_THREADS) void window_tg_kernel(WinTgArgs a) {
   if (tid == 0) a.energy_out[w] = 20.0 * log10(fmax(sqrt(esum / (double)a.win_len), 1e-10));
   const float c = gmax - 80.0f;
 
-  // onset envelope: each wave owns a contiguous run of frames and walks it 8 frames at a
-  // time, loading the 9 S_db rows those frames difference (rows shared between neighbours)
-  // before using any of them, so 18 row loads per lane are in flight instead of 2
-  if (NC_WT_SKIP >= 2) {
-    for (int t = tid; t < T; t += WT_THREADS) sh_x[p + t] = 0.0;
-  } else {
-    constexpr int FB = 8;
-    const int per = (T + WT_WAVES - 1) / WT_WAVES;
-    const int ta = wave * per, tb = min(T, ta + per);
-    // rows of batch t0 + FB are requested before batch t0 is differenced (software pipeline)
-    auto load_rows = [&](int t0, float (&ra)[FB + 1], float (&rb)[FB + 1]) {
+  constexpr int FB = 8, NW = NT / 64;
+  const int per = (T + NW - 1) / NW;
+  const int ta = wave * per, tb = min(T, ta + per);
+  // rows of batch t0 + FB are requested before batch t0 is differenced (software pipeline)
+  auto load_rows = [&](int t0, float (&ra)[FB + 1], float (&rb)[FB + 1]) {
 #pragma unroll
-      for (int q = 0; q <= FB; ++q) {
-        const int j = t0 + q - a.pad_onset;  // row j feeds frames j + pad (as j) and j + pad - 1 (as j + 1)
-        const bool ok = j >= 0 && j < T;
-        const float* r = a.sdb + (g0 + (ok ? j : 0)) * 128;
-        ra[q] = ok ? r[lane] : 0.0f;
-        rb[q] = ok ? r[lane + 64] : 0.0f;
-      }
-    };
-    float ra[FB + 1], rb[FB + 1], na[FB + 1], nb[FB + 1];
-    if (ta < tb) load_rows(ta, ra, rb);
-    for (int t0 = ta; t0 < tb; t0 += FB) {
-      if (t0 + FB < tb) load_rows(t0 + FB, na, nb);
+    for (int q = 0; q <= FB; ++q) {
+      const int j = t0 + q - a.pad_onset;  // row j feeds frames j + pad (as j) and j + pad - 1 (as j + 1)
+      const bool ok = j >= 0 && j < T;
+      const float* r = a.sdb + (g0 + (ok ? j : 0)) * 128;
+      ra[q] = ok ? r[lane] : 0.0f;
+      rb[q] = ok ? r[lane + 64] : 0.0f;
+    }
+  };
+  float ra[FB + 1], rb[FB + 1], na[FB + 1], nb[FB + 1];
+  if (ta < tb) load_rows(ta, ra, rb);
+  for (int t0 = ta; t0 < tb; t0 += FB) {
+    if (t0 + FB < tb) load_rows(t0 + FB, na, nb);
 #pragma unroll
-      for (int q = 0; q < FB; ++q) {
-        const int t = t0 + q;
-        if (t >= tb) break;
-        float val = 0.0f;
-        if (t >= a.pad_onset) {
-          const float a0 = fmaxf(ra[q], c), a1 = fmaxf(ra[q + 1], c);
-          const float b0 = fmaxf(rb[q], c), b1 = fmaxf(rb[q + 1], c);
-          const float part = fmaxf(0.0f, a1 - a0) + fmaxf(0.0f, b1 - b0);
-          val = wave_sum(part) * (1.0f / 128.0f);
-        }
-        if (lane == 0) {
-          sh_x[p + t] = val;
-          a.onset_out[g0 + t] = val;
-        }
+    for (int q = 0; q < FB; ++q) {
+      const int t = t0 + q;
+      if (t >= tb) break;
+      float val = 0.0f;
+      if (t >= a.pad_onset) {
+        const float a0 = fmaxf(ra[q], c), a1 = fmaxf(ra[q + 1], c);
+        const float b0 = fmaxf(rb[q], c), b1 = fmaxf(rb[q + 1], c);
+        const float part = fmaxf(0.0f, a1 - a0) + fmaxf(0.0f, b1 - b0);
+        val = wave_sum(part) * (1.0f / 128.0f);
       }
+      if (lane == 0) {
+        sh_x[p + t] = val;
+        a.onset_out[g0 + t] = val;
+      }
+    }
 #pragma unroll
-      for (int q = 0; q <= FB; ++q) {
-        ra[q] = na[q];
-        rb[q] = nb[q];
-      }
+    for (int q = 0; q <= FB; ++q) {
+      ra[q] = na[q];
+      rb[q] = nb[q];
     }
   }
   __syncthreads();
   {  // linear_ramp padding to 0 at both ends (numpy.pad, f64 ramp rounded to f32)
     const double st0 = sh_x[p] / (double)p, stl = sh_x[p + T - 1] / (double)p;
-    for (int i = tid; i < p; i += WT_THREADS) {
+    for (int i = tid; i < p; i += NT) {
       sh_x[i] = (double)(float)((double)i * st0);
       sh_x[p + T + i] = (double)(float)((double)(p - 1 - i) * stl);
     }
   }
   __syncthreads();
-  // per-frame normaliser 1 / ac_t[0] = 1 / sum_j hann[j]^2 x[t+j]^2: Hann^2 staged in LDS,
-  // four interleaved partial sums per frame (independent FMA chains), joined in a fixed order
-  double* sh_wsq = sh_x + (T + acw) + WT_SEG * acw;
-  for (int j = tid; j < acw; j += WT_THREADS) sh_wsq[j] = a.wsq[j];
-  __syncthreads();
-  for (int t = tid; t < T; t += WT_THREADS) {
+}
+
+// Per-frame normaliser 1 / ac_t[0] = 1 / sum_j hann[j]^2 x[t+j]^2 (Hann^2 in LDS), four
+// interleaved partial sums per frame (independent FMA chains) joined in a fixed order.
+template <int NT>
+__device__ __forceinline__ void wtg_rinv(const double* sh_x, const double* sh_wsq, int T, int acw, double* sh_rinv) {
+  for (int t = threadIdx.x; t < T; t += NT) {
     double s4[4] = {0.0, 0.0, 0.0, 0.0};
-    const int n = NC_WT_SKIP >= 2 ? 0 : acw;
     int j = 0;
-    for (; j + 4 <= n; j += 4) {
+    for (; j + 4 <= acw; j += 4) {
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const double v = sh_x[t + j + q];
         s4[q] = fma(sh_wsq[j + q], v * v, s4[q]);
       }
     }
-    for (; j < n; ++j) {
+    for (; j < acw; ++j) {
       const double v = sh_x[t + j];
       s4[0] = fma(sh_wsq[j], v * v, s4[0]);
     }
     sh_rinv[t] = tg_rinv((s4[0] + s4[1]) + (s4[2] + s4[3]));
   }
+}
+
+// The same normalisers register-blocked: 5 consecutive frames x 1/5 of the taps per
+// thread over y = x^2, the five tap-segment partials added in segment order.
+// y [T + acw] and part [5][T] are LDS scratch.
+template <int NT>
+__device__ __forceinline__ void wtg_rinv_blocked(const double* sh_x, const double* sh_wsq, int T, int acw, double* y,
+                                                 double* part, double* sh_rinv) {
+  constexpr int RB = 5, JS = 5;
+  const int tid = threadIdx.x;
+  for (int i = tid; i < T + acw; i += NT) y[i] = sh_x[i] * sh_x[i];
+  __syncthreads();
+  const int nb = (T + RB - 1) / RB;
+  for (int task = tid; task < nb * JS; task += NT) {
+    const int b = task % nb, js = task / nb, t0 = b * RB;
+    const int ja = acw * js / JS, jb = acw * (js + 1) / JS;
+    double acc[RB], yw[RB];
+#pragma unroll
+    for (int q = 0; q < RB; ++q) {
+      acc[q] = 0.0;
+      yw[q] = q < RB - 1 ? y[min(t0 + ja + q, T + acw - 1)] : 0.0;
+    }
+#pragma unroll 1
+    for (int j = ja; j < jb; ++j) {
+      yw[RB - 1] = y[min(t0 + j + RB - 1, T + acw - 1)];
+      const double wj = sh_wsq[j];
+#pragma unroll
+      for (int q = 0; q < RB; ++q) acc[q] = fma(wj, yw[q], acc[q]);
+#pragma unroll
+      for (int q = 0; q < RB - 1; ++q) yw[q] = yw[q + 1];
+    }
+#pragma unroll
+    for (int q = 0; q < RB; ++q)
+      if (t0 + q < T) part[js * T + t0 + q] = acc[q];
+  }
+  __syncthreads();
+  for (int t = tid; t < T; t += NT) {
+    double s = part[t];
+#pragma unroll
+    for (int q = 1; q < JS; ++q) s += part[q * T + t];
+    sh_rinv[t] = tg_rinv(s);
+  }
+}
+
+__global__ __launch_bounds__(WT_THREADS) __attribute__((amdgpu_waves_per_eu(4))) void window_tg_kernel(WinTgArgs a) {
+  const Span span_(a.span);
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  __shared__ BlockScratch<WT_THREADS> red;
+  const int w = blockIdx.x;
+  if (a.active && !a.active[w]) return;
+  const int T = a.T, acw = a.acw, p = acw / 2, tid = threadIdx.x;
+  const WinTgLds L(T, acw);
+  double* lds = reinterpret_cast<double*>(smem);
+  double* sh_x = lds + L.xoff;    // ramp-padded onset (f32 values), zeros either side
+  double* seq = lds + L.seq;      // [6][U]
+  double* sh_rinv = lds + L.scr;  // [T]
+  double* sh_wsq = sh_rinv + T;   // [acw]
+  double* sh_cs = sh_wsq + acw;   // [acw][2] (cos, sin)(theta j)
+  double* sh_q = sh_cs + 2 * acw; // [5][T + 1] prefix sums
+
+  for (int i = tid; i < L.xoff; i += WT_THREADS) lds[i] = 0.0;
+  for (int i = T + 2 * p + tid; i < L.xlen - L.xoff; i += WT_THREADS) sh_x[i] = 0.0;
+  for (int j = tid; j < acw; j += WT_THREADS) {
+    sh_wsq[j] = a.wsq[j];
+    double s, cc;
+    sincospi(2.0 * (double)j / (double)acw, &s, &cc);
+    sh_cs[2 * j] = cc;
+    sh_cs[2 * j + 1] = s;
+  }
+  wtg_onset<WT_THREADS>(a, w, sh_x, red);
+#if NC_WT_RINV_BLOCKED
+  if (NC_WT_STAGE >= 2) wtg_rinv_blocked<WT_THREADS>(sh_x, sh_wsq, T, acw, seq, sh_q, sh_rinv);
+#else
+  if (NC_WT_STAGE >= 2) wtg_rinv<WT_THREADS>(sh_x, sh_wsq, T, acw, sh_rinv);
+#endif
+  __syncthreads();
+  if (NC_WT_STAGE >= 3) {
+    tgc_prefix(sh_rinv, sh_cs, T, acw, sh_q, tid, WT_THREADS);
+    __syncthreads();
+    tgc_sequences(sh_x, sh_q, sh_cs, T, acw, L.U, seq, tid, WT_THREADS);
+  }
+  __syncthreads();
+  double* part = lds + L.scr;  // [segments][blocks * LB], over the normaliser scratch
+  if (NC_WT_STAGE >= 4) tgc_correlate(sh_x, seq, acw, L.U, part, tid, WT_THREADS);
+  __syncthreads();
+  const int nseg = tgc_segments(acw, WT_THREADS), stride = tgc_blocks(acw) * TGC_LB;
+  for (int k = tid; k < acw; k += WT_THREADS) {
+    double acc = part[k];
+    for (int q = 1; q < nseg; ++q) acc += part[q * stride + k];
+    a.tg_out[(size_t)w * acw + k] = acc / (double)T;
+  }
+}
+
+// Windows whose correlation sequences do not fit in LDS (window_sec above ~29 s): the
+// sliding sums of nc_slide.h, lags k and acw-1-k per thread (equal start-up work).
+constexpr int WS_THREADS = 192;
+__host__ __device__ inline size_t wtg_slide_lds_doubles(int T, int acw) { return (size_t)T + (T + acw) + 2 * (size_t)acw; }
+
+__global__ __launch_bounds__(WS_THREADS) void window_tg_slide_kernel(WinTgArgs a) {
+  const Span span_(a.span);
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  __shared__ BlockScratch<WS_THREADS> red;
+  const int w = blockIdx.x;
+  if (a.active && !a.active[w]) return;
+  const int T = a.T, acw = a.acw, tid = threadIdx.x;
+  double* sh_rinv = reinterpret_cast<double*>(smem);  // [T]
+  double* sh_x = sh_rinv + T;                         // [T + acw]
+  double* part = sh_x + (T + acw);                    // [acw]
+  double* sh_wsq = part + acw;                        // [acw]
+  for (int j = tid; j < acw; j += WS_THREADS) sh_wsq[j] = a.wsq[j];
+  wtg_onset<WS_THREADS>(a, w, sh_x, red);
+  wtg_rinv<WS_THREADS>(sh_x, sh_wsq, T, acw, sh_rinv);
   __syncthreads();
   auto xf = [&](int i) { return sh_x[i]; };
   auto rf = [&](int t) { return sh_rinv[t]; };
-  // lags k and acw-1-k per thread: two independent f64 recurrences (latency hiding), and
-  // their start-up sums (acw - k and k + 1 terms) add up to the same work on every thread;
-  // the frames are split into WT_SEG segments, each started by its own direct sums, and
-  // the segment partials are added in segment order
-  double* part = sh_x + (T + acw);  // [WT_SEG][acw]
-  const int seg = tid / (WT_THREADS / WT_SEG), st = tid % (WT_THREADS / WT_SEG);
-  const int ta = T * seg / WT_SEG, tb = T * (seg + 1) / WT_SEG;
-  if (NC_WT_SKIP == 0) {
-    if (WT_PAIR == 2) {
-      for (int i = st; i < (acw + 1) / 2; i += WT_THREADS / WT_SEG) {
-        const int ka = i, kb = acw - 1 - i;
-        double sa, sb;
-        slide_lag_sum2(xf, rf, acw, ka, kb, ta, tb, sa, sb);
-        part[seg * acw + ka] = sa;
-        if (kb != ka) part[seg * acw + kb] = sb;
-      }
-    } else {
-      for (int k = st; k < acw; k += WT_THREADS / WT_SEG) part[seg * acw + k] = slide_lag_sum(xf, rf, acw, k, ta, tb);
-    }
-  } else {
-    for (int k = st; k < acw; k += WT_THREADS / WT_SEG) part[seg * acw + k] = 0.0;
+  for (int i = tid; i < (acw + 1) / 2; i += WS_THREADS) {
+    const int ka = i, kb = acw - 1 - i;
+    double sa, sb;
+    slide_lag_sum2(xf, rf, acw, ka, kb, 0, T, sa, sb);
+    part[ka] = sa;
+    if (kb != ka) part[kb] = sb;
   }
   __syncthreads();
-  for (int k = tid; k < acw; k += WT_THREADS) {
-    double acc = part[k];
-#pragma unroll
-    for (int q = 1; q < WT_SEG; ++q) acc += part[q * acw + k];
-    a.tg_out[(size_t)w * acw + k] = acc / (double)T;
-  }
+  for (int k = tid; k < acw; k += WS_THREADS) a.tg_out[(size_t)w * acw + k] = part[k] / (double)T;
 }
 
 static inline size_t a256(size_t n) { return (n + 255) & ~(size_t)255; }
@@ -271,15 +369,23 @@ int launch_window_stage(Context& ctx, const float* sig, const int64_t* win_off, 
   a.onset_out = onset_out;
   a.tg_out = tg_out;
   a.energy_out = energy_out;
-  const size_t lds = (size_t)T * sizeof(double) + (size_t)(T + acw + WT_SEG * acw + acw) * sizeof(double);
-  if (lds > 160 * 1024) {
+  // the correlation kernel while its sequences fit in LDS (~104 B / frame: two windows
+  // per CU at the default 10 s, one up to ~29 s), else the sliding sums (~16 B / frame:
+  // up to ~225 s)
+  const size_t lds_corr = (size_t)WinTgLds(T, acw).total * sizeof(double);
+  const size_t lds_slide = wtg_slide_lds_doubles(T, acw) * sizeof(double);
+  const bool corr = lds_corr <= kWinTgLdsCap;
+  if (!corr && lds_slide > kWinTgLdsCap) {
     set_error("window stage: window too long for LDS (window_sec above ~225 s at hop 512)");
     return -2;
   }
   {
     KTimer kt_(ctx, "window_tg", st);
     a.span = kt_.span();
-    hipLaunchKernelGGL(window_tg_kernel, dim3(n_win), dim3(WT_THREADS), lds, st, a);
+    if (corr)
+      hipLaunchKernelGGL(window_tg_kernel, dim3(n_win), dim3(WT_THREADS), lds_corr, st, a);
+    else
+      hipLaunchKernelGGL(window_tg_slide_kernel, dim3(n_win), dim3(WS_THREADS), lds_slide, st, a);
   }
   NC_HIP(hipGetLastError());
   return 0;

@@ -129,13 +129,16 @@ def test_full_size_pair_properties(eng):
     assert abs(r.ibi_ratio - 1.25) < 0.01
 
 
-def test_long_windows_match_oracle(eng):
-    """--window 90 (cli.py:37): 3 876-frame windows take the beat tracker's global-workspace
-    path and a window_tg launch above 64 KB of LDS; tempos equal the oracle's."""
+@pytest.mark.parametrize("window_sec,hop_sec", [(25.0, 12.5), (90.0, 45.0)])
+def test_long_windows_match_oracle(eng, window_sec, hop_sec):
+    """--window 25 / 90 (cli.py:37): 1 077-frame windows run the correlation window_tg at one
+    workgroup per CU (~110 KB LDS); 3 876-frame windows take the sliding-sum window_tg
+    (above the correlation kernel's LDS) and the beat tracker's global-workspace path.
+    Tempos equal the oracle's."""
     nc, src = synth.make_pair(300.0, 1014)
-    p = E.Params(window_sec=90.0, hop_sec=45.0, compute_ibi=False)
+    p = E.Params(window_sec=window_sec, hop_sec=hop_sec, compute_ibi=False)
     out, = eng.analyze([(nc, src)], p)
-    ref = refglue.run_arrays(nc, src, window_sec=90.0, hop_sec=45.0, compute_ibi=False)
+    ref = refglue.run_arrays(nc, src, window_sec=window_sec, hop_sec=hop_sec, compute_ibi=False)
     assert out.error is None, out.error
     assert out.result.src_tempos_raw == ref["src_tempos"] and out.result.nc_tempos_raw == ref["nc_tempos"]
     assert out.result.tempo_ratio == ref["tempo_ratio"]

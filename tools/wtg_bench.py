@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
-"""Times nc_window_stage (stft_mel + window_tg) of one libncgpu.so variant on 560
-synthetic 10 s windows with the library's own per-kernel HIP-event timers.
-    python3 tools/wtg_bench.py tools/var/<name>/libncgpu.so"""
+"""Times nc_window_stage (stft_mel + window_tg) of libncgpu.so variants on N synthetic
+10 s windows (default 3968, the bench step's count) with the library's own per-kernel
+HIP-event timers.
+    python3 tools/wtg_bench.py N tools/var/<name>/libncgpu.so ..."""
 import ctypes as C
 import sys
 from pathlib import Path
@@ -14,7 +15,7 @@ sys.path.insert(0, str(REPO / "nightcore-to-flac-analyzer_amd"))
 from nightcore_analyzer import synth  # noqa: E402
 
 
-def main(path):
+def main(path, n):
     lib = C.CDLL(path)
     P, I32, SZ = C.c_void_p, C.c_int, C.c_size_t
     lib.nc_create.argtypes = [I32, C.POINTER(P)]
@@ -26,7 +27,7 @@ def main(path):
     ctx = P()
     assert lib.nc_create(0, C.byref(ctx)) == 0
     src = synth.make_source(180.0, 1000)
-    n, L, T, acw = 560, 220500, 431, 344
+    L, T, acw = 220500, 431, 344
     wins = np.stack([src[(i % 35) * 110250:(i % 35) * 110250 + L] for i in range(n)]).astype(np.float32)
     dev = torch.device("cuda")
     sig = torch.from_numpy(wins.reshape(-1)).to(dev)
@@ -52,8 +53,9 @@ def main(path):
         ms, k = C.c_double(), I32()
         lib.nc_profile_read(ctx, tag, C.byref(ms), C.byref(k))
         out[tag.decode()] = round(ms.value / max(1, k.value) * 1e3, 1)
-    print(Path(path).parent.name, "us per launch:", out, "tg[0][:3]", tg[:3].cpu().numpy())
+    print(Path(path).parent.name, n, "us per launch:", out, "tg[0][:3]", tg[:3].cpu().numpy(), flush=True)
 
 
 if __name__ == "__main__":
-    main(sys.argv[1])
+    for p in sys.argv[2:]:
+        main(p, int(sys.argv[1]))
