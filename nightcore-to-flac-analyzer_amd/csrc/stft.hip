@@ -26,6 +26,9 @@ namespace nc {
 #ifndef NC_SM_WAVES
 #define NC_SM_WAVES 14
 #endif
+#ifndef NC_SM_DIAG  // diagnosis variants only: 1 no mel, 2 no sample loads, 4 no S_db stores
+#define NC_SM_DIAG 0
+#endif
 #ifndef NC_SM_MEL_GLOBAL  // 1: mel lane weights read through L1 instead of staged in LDS
 #define NC_SM_MEL_GLOBAL 0
 #endif
@@ -96,7 +99,10 @@ __global__ __launch_bounds__(SM_THREADS) void stft_mel_kernel(StftMelArgs a) {
     FftIn<1024> in;
     double e = 0.0;
     const bool interior = s0 >= 0 && s0 + 2048 <= L && ((off & 1) == 0);
-    if (interior) {
+    if (NC_SM_DIAG & 2) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) in[0][r] = make_float2((float)(lane + r), (float)(g - r));
+    } else if (interior) {
       const float2* x2 = reinterpret_cast<const float2*>(x + s0);
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
@@ -162,7 +168,10 @@ __global__ __launch_bounds__(SM_THREADS) void stft_mel_kernel(StftMelArgs a) {
     // Slaney mel: lane l owns bands l and 127 - l, read as float4 steps from a 16-byte aligned
     // first bin with zero-padded weights (fmaf chain in bin order, as the CSR form)
     float acc0 = 0.0f, acc1 = 0.0f;
-    {
+    if (NC_SM_DIAG & 1) {
+      acc0 = pw[lane];
+      acc1 = pw[1023 - lane];
+    } else {
       const int lo = a.mel_lo4[lane], nj = a.mel_nj4[lane];
       for (int j = 0; j < a.mel_j0; ++j)
         if (j < nj) {
@@ -171,7 +180,7 @@ __global__ __launch_bounds__(SM_THREADS) void stft_mel_kernel(StftMelArgs a) {
           acc0 = fmaf(w.w, p.w, fmaf(w.z, p.z, fmaf(w.y, p.y, fmaf(w.x, p.x, acc0))));
         }
     }
-    {
+    if (!(NC_SM_DIAG & 1)) {
       const int lo = a.mel_lo4[64 + lane], nj = a.mel_nj4[64 + lane];
       const float4* w1 = mw4 + a.mel_j0 * 64;
       for (int j = 0; j < a.mel_j1; ++j)
@@ -184,8 +193,10 @@ __global__ __launch_bounds__(SM_THREADS) void stft_mel_kernel(StftMelArgs a) {
     const float db0 = 10.0f * log10f(fmaxf(1e-10f, acc0));
     const float db1 = 10.0f * log10f(fmaxf(1e-10f, acc1));
     float* row = a.sdb + g * 128;
-    row[lane] = db0;
-    row[127 - lane] = db1;
+    if (!(NC_SM_DIAG & 4) || db0 == 12345.0f) {
+      row[lane] = db0;
+      row[127 - lane] = db1;
+    }
     const float mx = wave_max(fmaxf(db0, db1));
     if (lane == 0) a.frame_max[g] = mx;
   }

@@ -77,7 +77,7 @@ struct WinTgLds {
 // Window max (top_db clamp) and energy, then the ramp-padded onset envelope into
 // x[0, T + 2 (acw / 2)).  Each wave owns a contiguous run of frames and walks it 8 frames
 // at a time, loading the 9 S_db rows those frames difference (rows shared between
-// neighbours) before using any of them, so 18 row loads per lane are in flight instead of 2.
+// neighbours) before using any of them, so 9 row loads per lane are in flight instead of 1.
 template <int NT>
 __device__ __forceinline__ void wtg_onset(const WinTgArgs& a, int w, double* sh_x, BlockScratch<NT>& red) {
   const int T = a.T, p = a.acw / 2;
@@ -97,42 +97,60 @@ __device__ __forceinline__ void wtg_onset(const WinTgArgs& a, int w, double* sh_
   constexpr int FB = 8, NW = NT / 64;
   const int per = (T + NW - 1) / NW;
   const int ta = wave * per, tb = min(T, ta + per);
-  // rows of batch t0 + FB are requested before batch t0 is differenced (software pipeline)
-  auto load_rows = [&](int t0, float (&ra)[FB + 1], float (&rb)[FB + 1]) {
+  // lane l holds bands 2l, 2l+1 of a row (one 8-byte load per row); rows of batch t0 + FB
+  // are requested before batch t0 is differenced (software pipeline)
+  auto load_rows = [&](int t0, float2 (&ra)[FB + 1]) {
 #pragma unroll
     for (int q = 0; q <= FB; ++q) {
       const int j = t0 + q - a.pad_onset;  // row j feeds frames j + pad (as j) and j + pad - 1 (as j + 1)
       const bool ok = j >= 0 && j < T;
-      const float* r = a.sdb + (g0 + (ok ? j : 0)) * 128;
-      ra[q] = ok ? r[lane] : 0.0f;
-      rb[q] = ok ? r[lane + 64] : 0.0f;
+      const float2* r = reinterpret_cast<const float2*>(a.sdb + (g0 + (ok ? j : 0)) * 128);
+      ra[q] = ok ? r[lane] : make_float2(0.0f, 0.0f);
     }
   };
-  float ra[FB + 1], rb[FB + 1], na[FB + 1], nb[FB + 1];
-  if (ta < tb) load_rows(ta, ra, rb);
+  float2 ra[FB + 1], na[FB + 1];
+  if (ta < tb) load_rows(ta, ra);
   for (int t0 = ta; t0 < tb; t0 += FB) {
-    if (t0 + FB < tb) load_rows(t0 + FB, na, nb);
+    if (t0 + FB < tb) load_rows(t0 + FB, na);
+    float part[FB];
 #pragma unroll
     for (int q = 0; q < FB; ++q) {
-      const int t = t0 + q;
-      if (t >= tb) break;
-      float val = 0.0f;
-      if (t >= a.pad_onset) {
-        const float a0 = fmaxf(ra[q], c), a1 = fmaxf(ra[q + 1], c);
-        const float b0 = fmaxf(rb[q], c), b1 = fmaxf(rb[q + 1], c);
-        const float part = fmaxf(0.0f, a1 - a0) + fmaxf(0.0f, b1 - b0);
-        val = wave_sum(part) * (1.0f / 128.0f);
+      const float a0 = fmaxf(ra[q].x, c), a1 = fmaxf(ra[q + 1].x, c);
+      const float b0 = fmaxf(ra[q].y, c), b1 = fmaxf(ra[q + 1].y, c);
+      part[q] = fmaxf(0.0f, a1 - a0) + fmaxf(0.0f, b1 - b0);
+    }
+    // transposed reduction of the FB = 8 frame partials: lane bits 5, 4, 3 halve the
+    // frame set (4 + 2 + 1 exchanges), bits 2..0 finish one frame per lane (3): frame f's
+    // band sum ends in lane 8 f
+    {
+      const bool h5 = lane & 32, h4 = lane & 16, h3 = lane & 8;
+      float p4[4], p2[2], p1;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const float keep = h5 ? part[q + 4] : part[q], give = h5 ? part[q] : part[q + 4];
+        p4[q] = keep + __shfl_xor(give, 32, 64);
       }
-      if (lane == 0) {
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        const float keep = h4 ? p4[q + 2] : p4[q], give = h4 ? p4[q] : p4[q + 2];
+        p2[q] = keep + __shfl_xor(give, 16, 64);
+      }
+      {
+        const float keep = h3 ? p2[1] : p2[0], give = h3 ? p2[0] : p2[1];
+        p1 = keep + __shfl_xor(give, 8, 64);
+      }
+      p1 += __shfl_xor(p1, 4, 64);
+      p1 += __shfl_xor(p1, 2, 64);
+      p1 += __shfl_xor(p1, 1, 64);
+      const int f = lane >> 3, t = t0 + f;
+      if ((lane & 7) == 0 && t < tb) {
+        const float val = t >= a.pad_onset ? p1 * (1.0f / 128.0f) : 0.0f;
         sh_x[p + t] = val;
         a.onset_out[g0 + t] = val;
       }
     }
 #pragma unroll
-    for (int q = 0; q <= FB; ++q) {
-      ra[q] = na[q];
-      rb[q] = nb[q];
-    }
+    for (int q = 0; q <= FB; ++q) ra[q] = na[q];
   }
   __syncthreads();
   {  // linear_ramp padding to 0 at both ends (numpy.pad, f64 ramp rounded to f32)

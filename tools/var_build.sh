@@ -11,7 +11,7 @@ for spec in "$@"; do
   objs=$(ls $PKG/build/*.o)
   for file in ${files//,/ }; do
     base=$(basename $file .hip)
-    /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 $flags -x hip -c $PKG/csrc/$file -o tools/var/$name/$base.o
+    /opt/rocm/bin/hipcc -O3 -fno-slp-vectorize -std=c++17 -fPIC --offload-arch=gfx950 $flags -x hip -c $PKG/csrc/$file -o tools/var/$name/$base.o
     objs=$(echo "$objs" | grep -v "/$base.o")
     objs="$objs tools/var/$name/$base.o"
   done
