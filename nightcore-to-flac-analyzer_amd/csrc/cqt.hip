@@ -306,7 +306,7 @@ __global__ __launch_bounds__(TP_WAVES * 64) void tuning_peaks_kernel(PeakArgs a)
       if (1024 - k <= kPipHi + 1) S[1024 - k] = p2;
       pmax = fmaxf(pmax, fmaxf(p1, p2));
     });
-    const float mx = __fsqrt_rn(wave_max(pmax));
+    const float mx = __fsqrt_rn(wave_max_u(pmax));
     // |X| over the stencil's bins, in place (6 per lane)
 #pragma unroll
     for (int q = 0; q < (kPipHi - kPipLo + 3 + 63) / 64; ++q) {

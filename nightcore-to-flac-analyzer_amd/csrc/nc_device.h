@@ -14,6 +14,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 #include "nc_span.h"
 
 #define NC_WAVE 64
@@ -50,6 +52,51 @@ __device__ __forceinline__ double wave_max(double v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o, 64));
   return v;
+}
+
+// DPP reductions whose result is wave-uniform (read from lane 63 into an SGPR): quad
+// swaps, half-row and row mirrors, then row_bcast15 / row_bcast31 into the odd / upper
+// rows -- VALU ops with a DPP source instead of the LDS-crossbar ds_bpermute of __shfl_xor.
+// Lanes outside a row mask take `old` (the operation's identity).  Fixed order, so
+// deterministic; the order differs from wave_sum's butterfly.
+template <int CTRL, int ROWMASK = 0xf>
+__device__ __forceinline__ int dpp_i(int v, int old) {
+  return __builtin_amdgcn_update_dpp(old, v, CTRL, ROWMASK, 0xf, false);
+}
+template <class Op>
+__device__ __forceinline__ float wave_reduce_u(float v, float id, Op op) {
+  auto step = [&](auto ctrl, auto rmask) {
+    constexpr int C = decltype(ctrl)::value, M = decltype(rmask)::value;
+    v = op(v, __int_as_float(dpp_i<C, M>(__float_as_int(v), __float_as_int(id))));
+  };
+  step(std::integral_constant<int, 0xB1>{}, std::integral_constant<int, 0xf>{});   // quad_perm [1,0,3,2]
+  step(std::integral_constant<int, 0x4E>{}, std::integral_constant<int, 0xf>{});   // quad_perm [2,3,0,1]
+  step(std::integral_constant<int, 0x141>{}, std::integral_constant<int, 0xf>{});  // row_half_mirror
+  step(std::integral_constant<int, 0x140>{}, std::integral_constant<int, 0xf>{});  // row_mirror
+  step(std::integral_constant<int, 0x142>{}, std::integral_constant<int, 0xa>{});  // row_bcast15
+  step(std::integral_constant<int, 0x143>{}, std::integral_constant<int, 0xc>{});  // row_bcast31
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63));
+}
+__device__ __forceinline__ float wave_max_u(float v) {
+  return wave_reduce_u(v, -INFINITY, [](float x, float y) { return fmaxf(x, y); });
+}
+__device__ __forceinline__ double wave_sum_u(double v) {
+  auto step = [&](auto ctrl, auto rmask) {
+    constexpr int C = decltype(ctrl)::value, M = decltype(rmask)::value;
+    const long long b = __double_as_longlong(v);
+    const int lo = dpp_i<C, M>((int)(unsigned)b, 0), hi = dpp_i<C, M>((int)(unsigned)(b >> 32), 0);
+    v += __longlong_as_double((long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo));
+  };
+  step(std::integral_constant<int, 0xB1>{}, std::integral_constant<int, 0xf>{});
+  step(std::integral_constant<int, 0x4E>{}, std::integral_constant<int, 0xf>{});
+  step(std::integral_constant<int, 0x141>{}, std::integral_constant<int, 0xf>{});
+  step(std::integral_constant<int, 0x140>{}, std::integral_constant<int, 0xf>{});
+  step(std::integral_constant<int, 0x142>{}, std::integral_constant<int, 0xa>{});
+  step(std::integral_constant<int, 0x143>{}, std::integral_constant<int, 0xc>{});
+  const long long b = __double_as_longlong(v);
+  const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)b, 63);
+  const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(b >> 32), 63);
+  return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
 }
 
 // ------------------------------------------------------------------ kernel spans (nc_profile)

@@ -120,7 +120,7 @@ __global__ __launch_bounds__(SF_THREADS) void spectral_frames_kernel(SpecArgs a)
         in[0][r] = make_float2(x0 * hann[2 * n], x1 * hann[2 * n + 1]);
       }
     }
-    ss64 = wave_sum(ss64);
+    ss64 = wave_sum_u(ss64);
     if (lane == 0) a.rms_out[g] = sqrtf((float)(ss64 / 2048.0));
 
     stockham_stage_regs<1024, 16, 1, 64, false, 0, 0>(in, fftbuf, sh_tw, lane);
@@ -157,12 +157,12 @@ __global__ __launch_bounds__(SF_THREADS) void spectral_frames_kernel(SpecArgs a)
 #pragma unroll
     for (int j = 0; j < 16; ++j) bin(lane + 64 * j);
     if (lane == 0) bin(1024);
-    l1 = wave_sum(l1);
-    m1 = wave_sum(m1);
-    mx = wave_max(mx);
+    l1 = wave_sum_u(l1);
+    m1 = wave_sum_u(m1);
+    mx = wave_max_u(mx);
     double bsum[SF_NBANDS];
 #pragma unroll
-    for (int b = 0; b < SF_NBANDS; ++b) bsum[b] = wave_sum((double)band[b]);
+    for (int b = 0; b < SF_NBANDS; ++b) bsum[b] = wave_sum_u((double)band[b]);
 
     // rolloff: lane l holds bins [16 l, 16 l + 16) (lane 63 also bin 1024) as an f32 running sum
     float run[17];

@@ -136,7 +136,7 @@ __global__ __launch_bounds__(SM_THREADS) void stft_mel_kernel(StftMelArgs a) {
       }
     }
     if (a.frame_energy) {
-      e = wave_sum(e);
+      e = wave_sum_u(e);
       if (lane == 0) a.frame_energy[g] = e;
     }
     // 1024-point complex FFT of the packed frame: stages 1-2 through LDS, the last stage on
@@ -159,7 +159,7 @@ __global__ __launch_bounds__(SM_THREADS) void stft_mel_kernel(StftMelArgs a) {
         float pm = pw[1024];
 #pragma unroll
         for (int j = 0; j < 16; ++j) pm = fmaxf(pm, pw[lane + 64 * j]);
-        const float mx = __fsqrt_rn(wave_max(pm));
+        const float mx = __fsqrt_rn(wave_max_u(pm));
         const int64_t base = uniform64(a.chunk_tf_base[c]) * kPeakSlots;
         piptrack_append([&](int k) { return __fsqrt_rn(pw[k]); }, mx, lane, &a.chunk_npk[c], a.peak_pitch + base,
                         a.peak_mag + base);
@@ -197,7 +197,7 @@ __global__ __launch_bounds__(SM_THREADS) void stft_mel_kernel(StftMelArgs a) {
       row[lane] = db0;
       row[127 - lane] = db1;
     }
-    const float mx = wave_max(fmaxf(db0, db1));
+    const float mx = wave_max_u(fmaxf(db0, db1));
     if (lane == 0) a.frame_max[g] = mx;
   }
 }
