@@ -12,7 +12,8 @@ import os
 import threading
 from pathlib import Path
 
-_LIB_PATH = Path(__file__).resolve().parent / "_lib" / "libncgpu.so"
+# NCGPU_LIB: another build of the library (A/B timing of kernel variants, tools/ab_bench.sh)
+_LIB_PATH = Path(os.environ.get("NCGPU_LIB") or Path(__file__).resolve().parent / "_lib" / "libncgpu.so")
 _lock = threading.Lock()
 _lib = None
 

@@ -48,7 +48,7 @@ def analyze(path, steps=5):
     import csv
     rows = list(csv.DictReader(open(path)))
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
-    marks = [i for i, r in enumerate(rows) if "cumsum" in r["Kernel_Name"].lower() or "scan" in r["Kernel_Name"].lower()]
+    marks = [i for i, r in enumerate(rows) if "single_scan_kernel" in r["Kernel_Name"] or "cumsum" in r["Kernel_Name"].lower()]
     i0, i1 = marks[-2], marks[-1]
     sel = rows[i0 + 1:i1]
     t_begin, t_end = int(rows[i0]["End_Timestamp"]), int(rows[i1]["Start_Timestamp"])
