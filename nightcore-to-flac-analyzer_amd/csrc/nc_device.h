@@ -102,7 +102,8 @@ __device__ __forceinline__ double wave_sum_u(double v) {
 // ------------------------------------------------------------------ kernel spans (nc_profile)
 // A profiled launch gets kSpanLines (start, end) slots, one 128-byte line each (start init
 // ~0, end init 0).  The first kSpanEdge workgroups of the grid lower a start (thread 0),
-// the last kSpanEdge raise an end (lane 0 of every wave) on the 100 MHz wall clock, each
+// the last kSpanEdge raise an end (lane 0 of every wave) on the 100 MHz wall clock (both
+// recorded at exit, the start as read at entry), each
 // in line (linear workgroup id mod kSpanLines): min start .. max end is the kernel's
 // execution span, the duration rocprofv3 --kernel-trace reports, unaffected by queueing
 // behind other streams' kernels.  Device-scope atomics on one address serialise (tens of
@@ -112,22 +113,24 @@ __device__ __forceinline__ double wave_sum_u(double v) {
 __device__ __forceinline__ unsigned span_lin() {
   return blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
 }
-__device__ __forceinline__ void span_begin(unsigned long long* sp) {
-  if (sp && threadIdx.x == 0 && span_lin() < (unsigned)kSpanEdge)
-    atomicMin(sp + (span_lin() % kSpanLines) * kSpanStride, (unsigned long long)wall_clock64());
-}
-__device__ __forceinline__ void span_end(unsigned long long* sp) {
+__device__ __forceinline__ void span_record(unsigned long long* sp, unsigned long long t0) {
   if (sp && (threadIdx.x & 63) == 0) {
     const unsigned n = gridDim.x * gridDim.y * gridDim.z, l = span_lin();
-    if (l + (unsigned)kSpanEdge >= n) atomicMax(sp + (l % kSpanLines) * kSpanStride + 1, (unsigned long long)wall_clock64());
+    unsigned long long* line = sp + (l % kSpanLines) * kSpanStride;
+    if (threadIdx.x == 0 && l < (unsigned)kSpanEdge) atomicMin(line, t0);
+    if (l + (unsigned)kSpanEdge >= n) atomicMax(line + 1, (unsigned long long)wall_clock64());
   }
 }
 
-// RAII form for a kernel body: begins at construction, ends at every exit of the scope
+// RAII form for a kernel body: the start time is read at construction (a wave-uniform
+// value in SGPRs) and both records are made at every exit of the scope, so the kernel
+// prologue has no divergent branch (a lane-0 atomic at entry cost cqt_chroma 13 VGPRs
+// and its spill-free allocation, decimate3 one wave per SIMD)
 struct Span {
   unsigned long long* sp;
-  __device__ __forceinline__ explicit Span(unsigned long long* p) : sp(p) { span_begin(p); }
-  __device__ __forceinline__ ~Span() { span_end(sp); }
+  unsigned long long t0;
+  __device__ __forceinline__ explicit Span(unsigned long long* p) : sp(p), t0(p ? wall_clock64() : 0ull) {}
+  __device__ __forceinline__ ~Span() { span_record(sp, t0); }
 };
 
 // float <-> order-preserving int (for atomicMax on floats of either sign)

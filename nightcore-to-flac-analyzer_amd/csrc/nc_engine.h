@@ -77,7 +77,7 @@ class KTimer {
   ~KTimer();
   KTimer(const KTimer&) = delete;
   KTimer& operator=(const KTimer&) = delete;
-  // device span slot of this launch (nc_device.h span_begin/span_end), or null
+  // device span slot of this launch (nc_device.h Span / span_record), or null
   unsigned long long* span() const { return span_; }
 
  private:

@@ -6,7 +6,7 @@
 //  * HIP events recorded around the launch on its stream (mode 1 only).  They include
 //    any time the kernel waits behind other streams' work after the start event;
 //  * the kernel's execution span, recorded by the kernel itself (nc_device.h
-//    span_begin / span_end: min wave start .. max wave end on the 100 MHz wall clock) —
+//    Span / span_record: min wave start .. max wave end on the 100 MHz wall clock) —
 //    what rocprofv3 --kernel-trace reports as the kernel's duration.  No host work per
 //    launch beyond handing the kernel its slot, so mode 2 (spans only) is cheap enough to
 //    stay on during a timed region.
