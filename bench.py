@@ -43,6 +43,12 @@ VALU_PEAK_TFS = 157.3          # MI355X f32 vector (= f32 MFMA) peak, MI355X_MIC
 #   -> 63 495; a 10 s window has 431 frames.
 CHUNK_FLOP = 7 * 862 * 30400
 WIN_FLOP = 431 * 63495
+# window_tg (csrc/nc_tgcorr.h) per 10 s window: the six lag correlations, 345 lags x 6 x
+# (T + acw = 775) f64 FMAs, plus the normalisers, 431 frames x 344 taps; its own I/O is the
+# S_db rows + frame max / energy in, onset + tempogram mean + energy out.
+F64_PEAK_TFS = 78.6            # MI355X f64 vector peak, MI355X_MICROARCH.md
+WTG_FLOP = 2 * (345 * 6 * 775 + 431 * 344)
+WTG_BYTES = 431 * (128 * 4 + 4 + 8) + 431 * 4 + 344 * 8 + 8
 
 
 def _gen(args):
@@ -218,21 +224,25 @@ def main():
 
     # algorithmic bytes / flops per launch = SURVEY.md §8d per-unit figure x units per launch
     units = {"stft_mel": (win_per_step, WIN_BYTES, WIN_FLOP), "cqt_chroma": (chunks_per_step, CHUNK_BYTES, CHUNK_FLOP)}
+    # compute roof per kernel: f32 VALU for the FFT kernels, f64 VALU for the tempogram
+    compute_roof = {"window_tg": ("valu_f64", F64_PEAK_TFS)}
 
-    def roof(tag, times):
-        if tag not in times or tag not in units:
+    def roof(tag, times, table=None):
+        table = table or units
+        if tag not in times or tag not in table:
             return None
         avg_ms, launches = times[tag]
-        alg = units[tag][0] / launches * units[tag][1]
-        flop = units[tag][0] / launches * units[tag][2]
+        alg = table[tag][0] / launches * table[tag][1]
+        flop = table[tag][0] / launches * table[tag][2]
         a = alg / (avg_ms * 1e-3) / 1e9
         c = flop / (avg_ms * 1e-3) / 1e12
+        cb, cp = compute_roof.get(tag, ("valu_f32", VALU_PEAK_TFS))
         return {"bound": "hbm", "kernel": tag, "achieved": a, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": a / HBM_PEAK_GBS, "traffic": None, "alg_bytes_per_launch": alg, "avg_launch_ms": avg_ms,
                 "launches_per_step": launches,
-                # the roof that actually binds: f32 VALU, no MFMA on this path
-                "compute": {"bound": "valu_f32", "achieved": c, "peak": VALU_PEAK_TFS, "unit": "TFLOP/s",
-                            "frac": c / VALU_PEAK_TFS, "alg_flop_per_launch": flop}}
+                # the roof that actually binds: VALU, no MFMA on this path
+                "compute": {"bound": cb, "achieved": c, "peak": cp, "unit": "TFLOP/s",
+                            "frac": c / cp, "alg_flop_per_launch": flop}}
 
     # the dominant kernel = the largest total execution time per step among the kernels with a
     # §8d unit (what rocprofv3 --stats ranks first); cqt_chroma (north_star's named target) is
@@ -244,6 +254,10 @@ def main():
         roofline.update(traffic=traffic["bytes_per_launch"], traffic_source=traffic["source"])
     if dom != "cqt_chroma" and "cqt_chroma" in kper:
         roofline["cqt_chroma"] = roof("cqt_chroma", kper)
+    # the per-window tempogram kernel against its f64 roof (its bytes are the S_db scratch)
+    wtg_units = {"window_tg": (win_per_step, WTG_BYTES, WTG_FLOP)}
+    if "window_tg" in kper:
+        roofline["window_tg"] = roof("window_tg", kper, wtg_units)
     # the same kernels launched alone (streams serialized for one more untimed step): their own
     # speed, where the timed launches share the chip with the other streams' chains
     eng.set_serial(True)
@@ -254,7 +268,8 @@ def main():
     eng.set_serial(False)
     iso_t = {k: (ms / n, n) for k, (ms, n) in iso.items()}
     roofline["isolated"] = {"kernels_ms_per_step": {k: round(v[0], 4) for k, v in iso.items()},
-                            **{k: roof(k, iso_t) for k in units if k in iso_t}}
+                            **{k: roof(k, iso_t) for k in units if k in iso_t},
+                            **({"window_tg": roof("window_tg", iso_t, wtg_units)} if "window_tg" in iso_t else {})}
 
     # upload included: the same K steps with every step's 64 pairs copied host -> HBM from
     # pinned memory on a copy stream, double-buffered (step j + 1 uploads while step j runs)
