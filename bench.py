@@ -140,6 +140,8 @@ def main():
     ap.add_argument("--cpu-workers", type=int, default=0,
                     help="CPU baseline processes, one pair each (0: the host cores this process may run on)")
     ap.add_argument("--no-upload", action="store_true", help="skip the upload-included throughput")
+    ap.add_argument("--no-pipeline", action="store_true",
+                    help="time K separate analyze calls instead of one pipelined analyze_batches call")
     ap.add_argument("--shard", choices=("pairs", "windows"), default="pairs",
                     help="N > 1: whole pairs per rank (default), or every pair's windows split over the ranks "
                          "(nightcore_analyzer.sharded; not yet measured on multi-GPU hardware)")
@@ -197,13 +199,26 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    # pair mode: the K steps are K complete analyses of the batch, issued as one pipelined
+    # Engine.analyze_batches call (batch k + 1's trims and first groups are queued while batch
+    # k's last groups run: no device idle at a batch's start-up); --no-pipeline times K
+    # separate analyze calls (reported beside it as single_call_ms_per_step)
+    pipelined = not win_mode and not args.no_pipeline
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
+    if pipelined:
+        res = eng.analyze_batches([signals] * args.steps, params)
+    else:
+        for _ in range(args.steps):
+            step()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     el = time.perf_counter() - t0
+    if pipelined:
+        if len(res) != args.steps or any(len(r) != len(outs) for r in res):
+            raise RuntimeError("analyze_batches returned an incomplete result")
+        if any(r[0].result.tempo_ratio != tr or r[0].result.pitch_ratio != pr for r in res):
+            raise RuntimeError("a pipelined batch differs from the single-call result")
     spans = eng.kernel_spans()
     eng.kernel_profile(False)
     if world > 1:
@@ -213,6 +228,17 @@ def main():
     step_ms = el / args.steps * 1e3
     # {kernel: (average launch ms, launches per step)} from the spans of the timed region
     kper = {k: (ms / n, n / args.steps) for k, (ms, n) in spans.items()}
+
+    # the same steps as separate analyze calls (each with its own start-up), for comparison
+    single_ms = None
+    if pipelined:
+        torch.cuda.synchronize()
+        ts = time.perf_counter()
+        nsc = max(1, min(args.steps, 5))
+        for _ in range(nsc):
+            step()
+        torch.cuda.synchronize()
+        single_ms = (time.perf_counter() - ts) / nsc * 1e3
 
     # entry-point HIP-event timers (separate, untimed steps)
     eng.start_timers()
@@ -455,7 +481,10 @@ def main():
             "dtype": "f32",
             "data": "synthetic (SURVEY.md §8d chords+clicks+noise, nc = resample_poly(src, 4, 5)), resident in HBM",
             "config": {"workload": "config 3: per GPU a batch of 64 x 3-min 22.05 kHz mono pairs; step = "
-                                   "pipeline.run analysis without the hop-64 IBI pass",
+                                   "pipeline.run analysis of the batch without the hop-64 IBI pass"
+                                   + ("; the K steps issued as one pipelined analyze_batches call (batch k+1's "
+                                      "trim and first groups queued while batch k's last groups run)" if pipelined else ""),
+                       "single_call_ms_per_step": single_ms,
                        "pairs_per_gpu": args.pairs, "windows_per_gpu_step": win_per_step,
                        "cqt_chunks_per_gpu_step": chunks_per_step, "parallelism": f"dp{world} (" + ("windows sharded, record all-gathers)" if win_mode else "pairs sharded)")},
             # avg_launch_ms: the kernel's execution spans over the timed steps (rocprofv3's

@@ -429,6 +429,10 @@ class Engine:
         # behind a bootstrap that waits for this group's (longer) chroma chain
         self.tail_stream = torch.cuda.current_stream(self.dev) if os.environ.get("NC_SERIAL_STREAMS") == "1" \
             else torch.cuda.Stream(self.dev, priority=prio[1])
+        # the silence trims of the next batch of analyze_batches, queued while the current
+        # batch's last groups run (not behind their bootstraps on the tail stream)
+        self.trim_stream = torch.cuda.current_stream(self.dev) if os.environ.get("NC_SERIAL_STREAMS") == "1" \
+            else torch.cuda.Stream(self.dev)
         # leading tuning frames of a chunk computed inside the window STFT (nc_window_stage_tuning);
         # NC_SHARE_TUNING=0 runs every tuning frame in the chroma chain instead (same results)
         self.share_tuning = os.environ.get("NC_SHARE_TUNING", "1") != "0"
@@ -438,10 +442,10 @@ class Engine:
         every kernel then runs alone, so per-kernel timers measure its isolated speed rather
         than its share of a concurrently loaded chip.  Measurement only (bench.py)."""
         if on:
-            self._streams = (self.chroma_stream, self.tail_stream)
-            self.chroma_stream = self.tail_stream = torch.cuda.current_stream(self.dev)
+            self._streams = (self.chroma_stream, self.tail_stream, self.trim_stream)
+            self.chroma_stream = self.tail_stream = self.trim_stream = torch.cuda.current_stream(self.dev)
         elif getattr(self, "_streams", None):
-            self.chroma_stream, self.tail_stream = self._streams
+            self.chroma_stream, self.tail_stream, self.trim_stream = self._streams
             self._streams = None
 
     # -------------------------------------------------------------- plumbing
@@ -732,6 +736,22 @@ class Engine:
             if gc_was_enabled:
                 gc.enable()
 
+    def analyze_batches(self, batches: Sequence[DeviceSignals], params: Params = None,
+                        group_pairs=None) -> List[List[PairOutcome]]:
+        """``analyze`` of several resident batches back to back, pipelined: the silence trims
+        of batch k + 1 are queued (on their own stream) as soon as batch k's last group is
+        launched, and batch k + 1's first groups are launched while batch k's last groups
+        still run, so the device does not idle through a batch's start-up (trim read-back,
+        host plan of the first group).  Every batch is analysed completely and independently;
+        the results equal one ``analyze`` call per batch."""
+        gc_was_enabled = gc.isenabled()
+        gc.disable()
+        try:
+            return self._analyze_many(list(batches), params or Params(), group_pairs, None)
+        finally:
+            if gc_was_enabled:
+                gc.enable()
+
     def _analyze(self, pairs, params, signals, group_pairs, log=None) -> List[PairOutcome]:
         p = params or Params()
         if signals is None:
@@ -739,65 +759,95 @@ class Engine:
             for nc, src in pairs:
                 flat += [nc, src]
             signals = self.upload_signals(flat)
-        B = signals.n_files // 2
-        hs = self.host_stats
-        groups = _group_bounds(B, group_pairs)
-        t0 = time.perf_counter()
-        align = None
-        rest = None
-        if p.silence_strip_db is not None and len(groups) > 1 and not (p.auto_align and p.src_trim_sec == 0.0):
-            # io.strip_silence bounds in two launches: the first group's files alone (the only
-            # blocking read-back before the device has work), the others on the tail stream,
-            # read back while the first group runs
-            nF, f1 = signals.n_files, 2 * groups[0][1]
-            first = self._trim_launch(signals, 0, f1, p, torch.cuda.current_stream(self.dev), "trim0")
-            rest = self._trim_launch(signals, f1, nF, p, self.tail_stream, "trim1")
-            start = np.zeros(nF, np.int64)
-            end = np.zeros(nF, np.int64)
-            start[:f1], end[:f1] = self._trim_wait(first)
-        else:
-            start, end = self._trim_all(signals, p)
-            if p.auto_align and p.src_trim_sec == 0.0:      # pipeline.py:111-125 (manual trim has priority)
-                align = self.align_offsets(signals.buf, signals.off[1::2] + start[1::2], end[1::2] - start[1::2],
-                                           signals.off[0::2] + start[0::2], end[0::2] - start[0::2])
-        if hs is not None:
-            hs["trim"] = hs.get("trim", 0.0) + time.perf_counter() - t0
-        # up to GROUPS_IN_FLIGHT groups are queued before the host waits for the oldest: the
-        # window stream never idles behind the host assembly of an earlier group, the assembly
-        # of group g overlaps the device work of the groups after it, and the depth of the
-        # device queues (and the memory held by queued groups) stays bounded for long batches
-        outs: List[PairOutcome] = []
-        pending: List[dict] = []
-        for gi, (g0, g1) in enumerate(groups):
-            if gi == 1 and rest is not None:
-                f1 = 2 * groups[0][1]
-                start[f1:], end[f1:] = self._trim_wait(rest)
-            sl = slice(2 * g0, 2 * g1)
-            sub = DeviceSignals(signals.buf, signals.off[sl], signals.length[sl])
-            t0 = time.perf_counter()
-            pending.append(self._launch_group(sub, p, start[sl].copy(), end[sl].copy(),
-                                              align[g0:g1] if align is not None else None, log is not None))
-            pending[-1]["g0"] = g0
-            if hs is not None:
-                hs["launch"] = hs.get("launch", 0.0) + time.perf_counter() - t0
-            if len(pending) > self.GROUPS_IN_FLIGHT:
-                outs += self._finish_group(pending.pop(0), log)
-        for g in pending:
-            outs += self._finish_group(g, log)
-        return outs
+        return self._analyze_many([signals], p, group_pairs, log)[0]
 
-    def _trim_launch(self, signals: DeviceSignals, f0: int, f1: int, p: Params, stream, ws_name: str):
+    def _split_trim(self, signals: DeviceSignals, p: Params, groups) -> bool:
+        return p.silence_strip_db is not None and len(groups) > 1 and not (p.auto_align and p.src_trim_sec == 0.0)
+
+    def _analyze_many(self, batches: List[DeviceSignals], p: Params, group_pairs, log=None) -> List[List[PairOutcome]]:
+        hs = self.host_stats
+        launch = torch.cuda.current_stream(self.dev)
+        # the signals are complete on the launch stream here; trims of later batches wait for
+        # this point only, not for the groups queued on the launch stream after it
+        ev_sig = torch.cuda.Event()
+        ev_sig.record(launch)
+        results: List[List[PairOutcome]] = [[] for _ in batches]
+        # up to GROUPS_IN_FLIGHT groups (of any batch) are queued before the host waits for the
+        # oldest: the window stream never idles behind the host assembly of an earlier group,
+        # the assembly of group g overlaps the device work of the groups after it, and the depth
+        # of the device queues (and the memory held by queued groups) stays bounded
+        pending: List[dict] = []
+
+        def trim_begin(bi: int, ahead: bool) -> dict:
+            """io.strip_silence bounds of batch bi: two launches when the batch has several
+            groups (the first group's files, then the rest), read back when needed."""
+            signals = batches[bi]
+            groups = _group_bounds(signals.n_files // 2, group_pairs)
+            if not self._split_trim(signals, p, groups):
+                return dict(groups=groups, split=False)
+            nF, f1 = signals.n_files, 2 * groups[0][1]
+            st0 = self.trim_stream if ahead else launch
+            first = self._trim_launch(signals, 0, f1, p, st0, "trim0", ev_sig)
+            rest = self._trim_launch(signals, f1, nF, p, self.trim_stream if ahead else self.tail_stream, "trim1",
+                                     ev_sig)
+            return dict(groups=groups, split=True, first=first, rest=rest, f1=f1)
+
+        nxt = None
+        for bi, signals in enumerate(batches):
+            t0 = time.perf_counter()
+            tr = nxt if nxt is not None else trim_begin(bi, False)
+            nxt = None
+            groups = tr["groups"]
+            align = None
+            if tr["split"]:
+                nF, f1 = signals.n_files, tr["f1"]
+                start = np.zeros(nF, np.int64)
+                end = np.zeros(nF, np.int64)
+                start[:f1], end[:f1] = self._trim_wait(tr["first"])
+            else:
+                start, end = self._trim_all(signals, p)
+                if p.auto_align and p.src_trim_sec == 0.0:  # pipeline.py:111-125 (manual trim has priority)
+                    align = self.align_offsets(signals.buf, signals.off[1::2] + start[1::2], end[1::2] - start[1::2],
+                                               signals.off[0::2] + start[0::2], end[0::2] - start[0::2])
+            if hs is not None:
+                hs["trim"] = hs.get("trim", 0.0) + time.perf_counter() - t0
+            for gi, (g0, g1) in enumerate(groups):
+                if gi == 1 and tr["split"]:
+                    f1 = tr["f1"]
+                    start[f1:], end[f1:] = self._trim_wait(tr["rest"])
+                sl = slice(2 * g0, 2 * g1)
+                sub = DeviceSignals(signals.buf, signals.off[sl], signals.length[sl])
+                t0 = time.perf_counter()
+                g = self._launch_group(sub, p, start[sl].copy(), end[sl].copy(),
+                                       align[g0:g1] if align is not None else None, log is not None)
+                g["g0"], g["bi"] = g0, bi
+                pending.append(g)
+                if gi == len(groups) - 1 and bi + 1 < len(batches):
+                    nxt = trim_begin(bi + 1, True)
+                if hs is not None:
+                    hs["launch"] = hs.get("launch", 0.0) + time.perf_counter() - t0
+                if len(pending) > self.GROUPS_IN_FLIGHT:
+                    g = pending.pop(0)
+                    results[g["bi"]] += self._finish_group(g, log)
+        for g in pending:
+            results[g["bi"]] += self._finish_group(g, log)
+        return results
+
+    def _trim_launch(self, signals: DeviceSignals, f0: int, f1: int, p: Params, stream, ws_name: str,
+                     ev_sig: Optional[torch.cuda.Event] = None):
         """Queue nc_trim_bounds for files [f0, f1) on `stream` and the async copy of the bounds
-        into pinned memory; returns (event, pinned bounds, keep-alive)."""
+        into pinned memory; returns (event, pinned bounds, keep-alive).  On a side stream the
+        trim first waits for ev_sig (the signals complete on the launch stream)."""
         dev = self.dev
         off, length = signals.off[f0:f1], signals.length[f0:f1]
         n = f1 - f0
         lens = np.ascontiguousarray(length, np.int64)
         launch = torch.cuda.current_stream(dev)
         if stream != launch:          # the signals may still be in flight on the launch stream
-            ev_in = torch.cuda.Event()
-            ev_in.record(launch)
-            stream.wait_event(ev_in)
+            if ev_sig is None:
+                ev_sig = torch.cuda.Event()
+                ev_sig.record(launch)
+            stream.wait_event(ev_sig)
         with torch.cuda.stream(stream):
             up = _Upload()
             up.add("off", off, np.int64)

@@ -177,3 +177,25 @@ def test_streamed_logs_equal_outcome_logs(eng, bench_pairs, golden_pipeline):
         assert _key(o) == _key(r), i
     for i, n in enumerate(names):
         assert got[i] == golden_pipeline[n]["log"][N_LOAD_LINES:], n
+
+
+def test_pipelined_batches_equal_separate_calls(eng, bench_pairs):
+    """Engine.analyze_batches (bench.py's timed loop): batch k + 1's trims and first groups
+    are queued while batch k's last groups run (trims on their own stream).  Every batch's
+    outcomes equal its own analyze call, for multi-group batches (split trim), a single-group
+    batch and a repeated batch."""
+    p = E.Params(compute_ibi=False)
+    flat = lambda prs: [a for nc, src in prs for a in (nc, src)]
+    a = eng.upload_signals(flat(bench_pairs[:20]))
+    b = eng.upload_signals(flat(bench_pairs[20:25]))
+    c = eng.upload_signals(flat(bench_pairs[25:45]))
+    batches = [a, b, c, a]
+    got = eng.analyze_batches(batches, p)
+    assert len(got) == len(batches)
+    for sig, outs in zip(batches, got):
+        ref = eng.analyze(signals=sig, params=p)
+        assert [_key(o) for o in outs] == [_key(o) for o in ref]
+    # with a small group size: many groups per batch, more than the peak ring's slots
+    got3 = eng.analyze_batches([a, c], p, group_pairs=3)
+    assert [_key(o) for o in got3[0]] == [_key(o) for o in eng.analyze(signals=a, params=p)]
+    assert [_key(o) for o in got3[1]] == [_key(o) for o in eng.analyze(signals=c, params=p)]
