@@ -15,7 +15,7 @@ REPO = Path(__file__).resolve().parents[1]
 sys.path.insert(0, str(REPO / "nightcore-to-flac-analyzer_amd"))
 from nightcore_analyzer import synth  # noqa: E402
 
-TAGS = (b"stft_mel", b"window_tg", b"decimate", b"tuning_peaks", b"cqt_chroma")
+TAGS = (b"stft_mel", b"window_tg", b"decimate", b"tuning_peaks", b"tuning_select", b"cqt_chroma")
 
 
 def bench(path, src):
