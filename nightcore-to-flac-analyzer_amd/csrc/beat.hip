@@ -317,7 +317,69 @@ __global__ __launch_bounds__(NT) void tempo_beat_kernel(BeatArgs a) {
   const int FW = SMALL ? N : max(B, (kBeatWin / B) * B);
   double* lsw = SMALL ? ls : ring + a.ring_cap;
   int* bkw = SMALL ? back : reinterpret_cast<int*>(lsw + kBeatWin);
-  for (int w0 = 0; w0 < N; w0 += FW) {
+  // Short sequences run the block DP on wave 0 alone, 8 lanes per frame: blocks of
+  // Bq = min(dmin, 8) frames, lane (frame lane >> 3, chunk lane & 7) scans its eighth of the
+  // candidate range [dmin, dmax] in ascending d (loads in batches of 8), the 8 chunk winners
+  // of a frame meet by DPP (quad swaps, half-row mirror: no LDS round trip), and the chunk-0
+  // lane writes cum / back.  The next block reads those scores through the wave's own
+  // in-order LDS traffic, so no barrier or wait separates blocks.  Same candidates and the
+  // same tie rule (largest score, then smallest d): bit-identical scores and back-pointers.
+  const bool wave_dp = SMALL;
+  if (wave_dp && threadIdx.x < 64) {
+    const int lane = threadIdx.x;
+    const int Bq = max(1, min(dmin, 8));
+    const int Cw = (D + 7) / 8;
+    const int fr = lane >> 3, gw = lane & 7;
+    const int dlo_w = dmin + gw * Cw, dend_w = min(dmax + 1, dlo_w + Cw);
+    auto take = [](double& best, int& bd, double v, int d) {
+      if (v > best || (v == best && d < bd)) {
+        best = v;
+        bd = d;
+      }
+    };
+    auto dpp_pair = [&](auto ctrl, double& best, int& bd) {
+      constexpr int Cc = decltype(ctrl)::value;
+      const long long bits = __double_as_longlong(best);
+      const int lo = dpp_i<Cc>((int)(unsigned)bits, 0), hi = dpp_i<Cc>((int)(unsigned)(bits >> 32), 0);
+      const double v = __longlong_as_double((long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo));
+      take(best, bd, v, dpp_i<Cc>(bd, 0));
+    };
+    for (int b0 = 0; b0 < N; b0 += Bq) {
+      const int i = b0 + fr;
+      const bool valid = fr < Bq && i < N;
+      double best = -INFINITY;
+      int bd = 0x7fffffff;
+      if (valid) {
+        const int dh = min(dend_w, i + 1);
+        for (int d0 = dlo_w; d0 < dh; d0 += 8) {
+          double sc[8];
+#pragma unroll
+          for (int u = 0; u < 8; ++u) {
+            const int d = min(d0 + u, dh - 1);  // past the range: a valid slot, masked below
+            const double v = cum[i - d] - tab[d];
+            sc[u] = d0 + u < dh ? v : -INFINITY;
+          }
+#pragma unroll
+          for (int u = 0; u < 8; ++u)
+            if (sc[u] > best) {
+              best = sc[u];
+              bd = d0 + u;
+            }
+        }
+      }
+      // all 64 lanes take part in the exchanges; the patterns stay inside a frame's 8 lanes
+      dpp_pair(std::integral_constant<int, 0xB1>{}, best, bd);   // quad_perm [1,0,3,2]
+      dpp_pair(std::integral_constant<int, 0x4E>{}, best, bd);   // quad_perm [2,3,0,1]
+      dpp_pair(std::integral_constant<int, 0x141>{}, best, bd);  // row_half_mirror: the other quad
+      if (valid && gw == 0) {
+        const bool found = (i >= dmin) && (best > -INFINITY);
+        cum[i] = found ? ls[i] + best : ls[i];
+        back[i] = (i < i0 || !found) ? -1 : i - bd;
+      }
+      asm volatile("" ::: "memory");  // LDS traffic of one wave is in order; keep the compiler's too
+    }
+  }
+  for (int w0 = 0; w0 < (wave_dp ? 0 : N); w0 += FW) {
     const int w1 = min(N, w0 + FW);
     if (!SMALL) {
       for (int q = threadIdx.x; q < w1 - w0; q += NT) lsw[q] = ls[w0 + q];
