@@ -116,6 +116,7 @@ __global__ __launch_bounds__(NT) void tempo_beat_kernel(BeatArgs a) {
   __shared__ BlockScratch<NT> bs;
   __shared__ int hist[256];
   __shared__ int sh_int[4];
+  __shared__ double sel_med[2];
   __shared__ double dp_best[NT];
   __shared__ int dp_d[NT];
 #ifdef NC_BEAT_PROF
@@ -461,7 +462,32 @@ __global__ __launch_bounds__(NT) void tempo_beat_kernel(BeatArgs a) {
   int tail = N - 1;
   if (cnt > 0) {
     double med;
-    if (cnt & 1) {
+    if (cnt <= NT) {
+      // few peaks (short sequences): compact their scores, then every peak counts the scores
+      // below / not above its own; the order statistics cnt/2 (and cnt/2 - 1) are the scores
+      // whose [lt, le) rank interval holds them.  One pass, two barriers, in place of the
+      // 8-pass radix select (same values: the k-th smallest in f64 order)
+      double* cv = dp_best;  // free after the DP
+      if (threadIdx.x == 0) sh_int[0] = 0;
+      __syncthreads();
+      for (int i = threadIdx.x; i < N; i += NT)
+        if (marks[i]) cv[atomicAdd(&sh_int[0], 1)] = cum[i];
+      __syncthreads();
+      const int k1 = (cnt - 1) / 2, k2 = cnt / 2;
+      if ((int)threadIdx.x < cnt) {
+        const double v = cv[threadIdx.x];
+        int lt = 0, le = 0;
+        for (int j = 0; j < cnt; ++j) {
+          const double u = cv[j];
+          lt += u < v;
+          le += u <= v;
+        }
+        if (lt <= k1 && k1 < le) sel_med[0] = v;
+        if (lt <= k2 && k2 < le) sel_med[1] = v;
+      }
+      __syncthreads();
+      med = (cnt & 1) ? sel_med[1] : (sel_med[0] + sel_med[1]) / 2.0;
+    } else if (cnt & 1) {
       med = block_kth_flagged<NT>(cum, marks, N, cnt / 2, hist, bs);
     } else {
       const double lo = block_kth_flagged<NT>(cum, marks, N, cnt / 2 - 1, hist, bs);
