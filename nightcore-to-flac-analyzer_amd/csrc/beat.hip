@@ -174,8 +174,11 @@ __global__ __launch_bounds__(NT) void tempo_beat_kernel(BeatArgs a) {
   const double fs = (double)a.sr;
   const double start = a.prior_idx ? a.start_bpm[a.prior_idx[s]] : a.start_bpm[s];
   const double lstart = log2(start);
-  double bv = -INFINITY;
-  int bi = 0x7fffffff;
+  // one pass keeps each thread's best and second best (numpy argmax order); the global
+  // best L comes from the first, the runner-up (decision margin) from the second wherever
+  // the thread's best is L itself
+  double bv = -INFINITY, b2v = -INFINITY;
+  int bi = 0x7fffffff, b2i = 0x7fffffff;
   for (int k = threadIdx.x; k < a.acw; k += NT) {
     double lp = -INFINITY;
     if (k > 0) {
@@ -187,29 +190,22 @@ __global__ __launch_bounds__(NT) void tempo_beat_kernel(BeatArgs a) {
     }
     const double sc = log1p(1e6 * tg[k]) + lp;
     if (np_better(sc, k, bv, bi)) {
+      b2v = bv;
+      b2i = bi;
       bv = sc;
       bi = k;
+    } else if (np_better(sc, k, b2v, b2i)) {
+      b2v = sc;
+      b2i = k;
     }
   }
+  double sv = bv;
+  int si = bi;
   block_argmax<NT>(bv, bi, bs);
   const int L = bi;
-  double sv = -INFINITY;
-  int si = 0x7fffffff;
-  for (int k = threadIdx.x; k < a.acw; k += NT) {
-    if (k == L) continue;
-    double lp = -INFINITY;
-    if (k > 0) {
-      const double bpm = (60.0 * fs) / ((double)a.hop * (double)k);
-      if (bpm < a.max_tempo) {
-        const double d = (log2(bpm) - lstart) / 1.0;
-        lp = -0.5 * (d * d);
-      }
-    }
-    const double sc = log1p(1e6 * tg[k]) + lp;
-    if (np_better(sc, k, sv, si)) {
-      sv = sc;
-      si = k;
-    }
+  if (si == L) {
+    sv = b2v;
+    si = b2i;
   }
   block_argmax<NT>(sv, si, bs);
   const double bpm = L > 0 ? (60.0 * fs) / ((double)a.hop * (double)L) : INFINITY;
