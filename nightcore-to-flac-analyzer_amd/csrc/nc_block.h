@@ -166,16 +166,35 @@ __device__ __forceinline__ bool np_better(double a, int ia, double b, int ib) {
   if (a < b) return false;
   return ia < ib;
 }
+// numpy-order argmax over the wave, the result in every lane: DPP quad swaps, half-row and
+// row mirrors, row broadcasts into the odd / upper rows (lanes outside a row mask see the
+// identity (-inf, INT_MAX)), then lane 63's pair.  np_better is a total order, so the
+// reduction order does not change the result.
 __device__ __forceinline__ void wave_argmax(double& v, int& i) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    const double ov = __shfl_xor(v, o, 64);
-    const int oi = __shfl_xor(i, o, 64);
+  const long long idb = __double_as_longlong(-INFINITY);
+  auto step = [&](auto ctrl, auto rmask) {
+    constexpr int C = decltype(ctrl)::value, M = decltype(rmask)::value;
+    const long long b = __double_as_longlong(v);
+    const int lo = dpp_i<C, M>((int)(unsigned)b, (int)(unsigned)idb);
+    const int hi = dpp_i<C, M>((int)(unsigned)(b >> 32), (int)(unsigned)(idb >> 32));
+    const int oi = dpp_i<C, M>(i, 0x7fffffff);
+    const double ov = __longlong_as_double((long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo));
     if (np_better(ov, oi, v, i)) {
       v = ov;
       i = oi;
     }
-  }
+  };
+  step(std::integral_constant<int, 0xB1>{}, std::integral_constant<int, 0xf>{});
+  step(std::integral_constant<int, 0x4E>{}, std::integral_constant<int, 0xf>{});
+  step(std::integral_constant<int, 0x141>{}, std::integral_constant<int, 0xf>{});
+  step(std::integral_constant<int, 0x140>{}, std::integral_constant<int, 0xf>{});
+  step(std::integral_constant<int, 0x142>{}, std::integral_constant<int, 0xa>{});
+  step(std::integral_constant<int, 0x143>{}, std::integral_constant<int, 0xc>{});
+  const long long b = __double_as_longlong(v);
+  const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)b, 63);
+  const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(b >> 32), 63);
+  v = __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+  i = __builtin_amdgcn_readlane(i, 63);
 }
 template <int NT>
 __device__ __forceinline__ void block_argmax(double& v, int& i, BlockScratch<NT>& s) {
