@@ -501,6 +501,9 @@ __global__ __launch_bounds__(NT) void tuning_select_kernel(const float* peak_pit
 #ifndef NC_CQ_FR
 #define NC_CQ_FR 32
 #endif
+#ifndef NC_CQ_TB  // basis taps per batch of LDS loads (0: one tap at a time, per-lane guarded)
+#define NC_CQ_TB 2  // measured per 224 chunks: 0 -> 1158-1171 us, 2 -> 1144, 4/8 -> 1152
+#endif
 #ifndef NC_CQ_BPW
 #define NC_CQ_BPW 3
 #endif
@@ -658,6 +661,29 @@ __global__ __launch_bounds__(CQ_WAVES * 64) void cqt_chroma_kernel(CqtArgs a) {
     // lane piece of a sparse row (complex64 accumulation in row order) for both frames; the
     // row's second half (partner lane) is then added to its first half
     float ar = 0.0f, ai = 0.0f, br = 0.0f, bi = 0.0f;
+#if NC_CQ_TB
+    // taps in batches of NC_CQ_TB loads issued together (one LDS wait per batch); taps past
+    // the piece have zero weights and read its last bin, so they add exactly 0; a scheduling
+    // barrier per batch keeps the compiler from hoisting every load at once (VGPR spills)
+    if (!(NC_CQ_DIAG & 1)) {
+      const int plast = plo + max(plen, 1) - 1;
+#pragma unroll
+      for (int j0 = 0; j0 < CQ_PMAX; j0 += NC_CQ_TB) {
+        float4 d[NC_CQ_TB];
+#pragma unroll
+        for (int q = 0; q < NC_CQ_TB; ++q) d[q] = D[min(plo + j0 + q, plast)];
+#pragma unroll
+        for (int q = 0; q < NC_CQ_TB; ++q) {
+          const float2 wj = w[j0 + q];
+          ar = fmaf(wj.x, d[q].x, fmaf(-wj.y, d[q].y, ar));
+          ai = fmaf(wj.x, d[q].y, fmaf(wj.y, d[q].x, ai));
+          br = fmaf(wj.x, d[q].z, fmaf(-wj.y, d[q].w, br));
+          bi = fmaf(wj.x, d[q].w, fmaf(wj.y, d[q].z, bi));
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+#else
 #pragma unroll
     for (int j = 0; j < CQ_PMAX; ++j) {
       if (!(NC_CQ_DIAG & 1) && j < plen) {
@@ -668,6 +694,7 @@ __global__ __launch_bounds__(CQ_WAVES * 64) void cqt_chroma_kernel(CqtArgs a) {
         bi = fmaf(w[j].x, d.w, fmaf(w[j].y, d.z, bi));
       }
     }
+#endif
     const int src = partner < 0 ? ln : partner;
     const float ar2 = __shfl(ar, src, 64), ai2 = __shfl(ai, src, 64);
     const float br2 = __shfl(br, src, 64), bi2 = __shfl(bi, src, 64);
