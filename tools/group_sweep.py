@@ -2,7 +2,8 @@
 """Step time of the config-3 workload (64 x 3-min pairs) against the engine's pair-group
 schedule (the unit of host/device pipelining and of kernel batch size).
     python3 tools/group_sweep.py [--pipelined] [--rounds R] SCHEDULE ...
-SCHEDULE: an int (groups of that size) or a comma list of sizes; "default" = the engine's.
+SCHEDULE: an int (groups of that size) or a comma list of sizes; "default" = the engine's;
+a suffix "@G" runs it with G groups in flight (Engine.GROUPS_IN_FLIGHT).
 --pipelined times 10 steps as one Engine.analyze_batches call (bench.py's timed loop);
 schedules are alternated over R rounds so that clock drift hits them alike."""
 import sys
@@ -30,7 +31,11 @@ def main():
     sig = eng.upload_signals([a for nc, src in pairs for a in (nc, src)])
     params = E.Params(compute_ibi=False)
 
+    gif0 = eng.GROUPS_IN_FLIGHT
+
     def sched(arg):
+        arg, _, gif = arg.partition("@")
+        eng.GROUPS_IN_FLIGHT = int(gif) if gif else gif0
         if arg == "default":
             return None
         return [int(v) for v in arg.split(",")] if "," in arg else int(arg)

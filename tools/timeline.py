@@ -29,8 +29,11 @@ def run(steps=5):
     torch.cuda.synchronize()
     torch.cumsum(marker, 0)
     t0 = time.perf_counter()
-    for _ in range(steps):
-        eng.analyze(signals=sig, params=params)
+    if "--pipelined" in sys.argv:
+        eng.analyze_batches([sig] * steps, params)
+    else:
+        for _ in range(steps):
+            eng.analyze(signals=sig, params=params)
     torch.cumsum(marker, 0)
     torch.cuda.synchronize()
     print("wall ms per step", (time.perf_counter() - t0) / steps * 1e3)
