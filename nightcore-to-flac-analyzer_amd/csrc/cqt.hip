@@ -633,6 +633,25 @@ __global__ __launch_bounds__(CQ_WAVES * 64) void cqt_chroma_kernel(CqtArgs a) {
     if (NC_CQ_PREFETCH && it + CQ_WAVES < n_items) load_item(it + CQ_WAVES, ln, in);
     stockham_stage<1024, 16, 16, 64, false, 0, 0>(fftbuf, sh_tw, ln);
     float2 v[4][4];
+    if constexpr (NC_LDS_SPLIT && !(NC_CQ_DIAG & 48)) {
+      // lpad(J + 256 r) = lpad(J) + 272 r: four bases, immediate offsets, one wait
+      float2 o[16];
+      lds_read16<0, 2176, 4352, 6528, 0, 2176, 4352, 6528, 0, 2176, 4352, 6528, 0, 2176, 4352, 6528>(
+          o, lds_addr(fftbuf + lpad(Jb(ln, 0))), lds_addr(fftbuf + lpad(Jb(ln, 1))),
+          lds_addr(fftbuf + lpad(Jb(ln, 2))), lds_addr(fftbuf + lpad(Jb(ln, 3))));
+#pragma unroll
+      for (int b = 0; b < 4; ++b)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[b][r] = o[4 * b + r];
+      // (the twiddles stay compiler-scheduled here: batching them needs registers this kernel
+      // does not have)
+#pragma unroll
+      for (int b = 0; b < 4; ++b) {
+#pragma unroll
+        for (int r = 1; r < 4; ++r) v[b][r] = cmul(v[b][r], sh_tw3[(3 * b + r - 1) * 64 + ln]);
+        DFT<4>::run(v[b]);
+      }
+    } else {
 #pragma unroll
     for (int b = 0; b < 4; ++b)
 #pragma unroll
@@ -645,6 +664,7 @@ __global__ __launch_bounds__(CQ_WAVES * 64) void cqt_chroma_kernel(CqtArgs a) {
       for (int r = 1; r < 4; ++r)
         v[b][r] = cmul(v[b][r], (NC_CQ_DIAG & 16) ? make_float2(0.7f, 0.3f * r) : sh_tw3[(3 * b + r - 1) * 64 + ln]);
       DFT<4>::run(v[b]);
+    }
     }
     // v[b][r] = Z[J[b] + 256 r]; the mirror of k = J[b] is Z[(256 - J[b]) + 768]
     float4* D = reinterpret_cast<float4*>(fftbuf);  // D[k - klo] = (X_t[k], X_{t+1}[k]); all reads above precede

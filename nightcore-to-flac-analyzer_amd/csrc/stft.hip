@@ -19,6 +19,10 @@
 #include "nc_block.h"
 #include "nc_engine.h"
 #include "nc_piptrack.h"
+
+#ifndef NC_SM_TWB  // stage-3 twiddles as asm batches too
+#define NC_SM_TWB 1
+#endif
 #include "stft_args.h"
 
 namespace nc {
@@ -144,7 +148,7 @@ __global__ __launch_bounds__(SM_THREADS) void stft_mel_kernel(StftMelArgs a) {
     stockham_stage_regs<1024, 16, 1, 64, false, 0, 0>(in, fftbuf, twl, lane);
     stockham_stage<1024, 16, 16, 64, false, 0, 0>(fftbuf, twl, lane);
     float2 v[4][4];
-    fft1024_last_mirror<SmTw::s3>(fftbuf, twl, lane, v);
+    fft1024_last_mirror<SmTw::s3, NC_SM_TWB>(fftbuf, twl, lane, v);
     float* pw = reinterpret_cast<float*>(fftbuf);  // power P[k], k in [0, 1024] (all Z reads precede)
     rsplit_mirror<SmTw::split>(v, twl, lane, [&](int k, float2 X, float2 XN) {
       pw[k] = fmaf(X.x, X.x, X.y * X.y);
