@@ -36,6 +36,10 @@ namespace nc {
 #ifndef NC_SM_MEL_GLOBAL  // 1: mel lane weights read through L1 instead of staged in LDS
 #define NC_SM_MEL_GLOBAL 0
 #endif
+#ifndef NC_SM_HANN_LDS  // 1: the 2048-tap Hann window staged in LDS (else read through L1 per frame)
+#define NC_SM_HANN_LDS 1
+#endif
+constexpr int SM_HANN2 = NC_SM_HANN_LDS ? 1024 : 0;  // float2 elements of the staged window
 constexpr int SM_WAVES = NC_SM_WAVES;
 constexpr int SM_THREADS = SM_WAVES * 64;
 using SmTw = StagedTw<1024>;  // per-stage twiddle table in LDS (conflict-free reads)
@@ -54,7 +58,7 @@ __host__ __device__ __forceinline__ int al4(int n) { return (n + 3) & ~3; }
 
 size_t stft_mel_lds_bytes(int mel_j) {
   return (size_t)al4(SmTw::size) * sizeof(float2) + (NC_SM_MEL_GLOBAL ? 0 : (size_t)mel_j * 64 * sizeof(float4)) +
-         (size_t)SM_WAVES * LdsSize<1024>::value * sizeof(float2);
+         (size_t)SM_HANN2 * sizeof(float2) + (size_t)SM_WAVES * LdsSize<1024>::value * sizeof(float2);
 }
 
 __global__ __launch_bounds__(SM_THREADS) void stft_mel_kernel(StftMelArgs a) {
@@ -63,10 +67,11 @@ __global__ __launch_bounds__(SM_THREADS) void stft_mel_kernel(StftMelArgs a) {
   float2* sh_tw = reinterpret_cast<float2*>(smem);
   float4* sh_w4 = reinterpret_cast<float4*>(sh_tw + al4(SmTw::size));  // [mel_j0 + mel_j1][64]
   const int lane0 = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform (SGPR)
-  float2* fftbuf = reinterpret_cast<float2*>(sh_w4 + (NC_SM_MEL_GLOBAL ? 0 : (a.mel_j0 + a.mel_j1) * 64)) +
-                   wave * LdsSize<1024>::value;
+  float2* sh_hann = reinterpret_cast<float2*>(sh_w4 + (NC_SM_MEL_GLOBAL ? 0 : (a.mel_j0 + a.mel_j1) * 64));
+  float2* fftbuf = sh_hann + SM_HANN2 + wave * LdsSize<1024>::value;
 
   fill_staged_tw<1024>(sh_tw, a.tw, threadIdx.x, SM_THREADS);
+  for (int i = threadIdx.x; i < SM_HANN2; i += SM_THREADS) sh_hann[i] = reinterpret_cast<const float2*>(a.hann2048)[i];
   if (!NC_SM_MEL_GLOBAL)
     for (int i = threadIdx.x; i < (a.mel_j0 + a.mel_j1) * 64; i += SM_THREADS) sh_w4[i] = a.mel_w4[i];
   const float4* mw4 = NC_SM_MEL_GLOBAL ? a.mel_w4 : sh_w4;
@@ -108,11 +113,20 @@ __global__ __launch_bounds__(SM_THREADS) void stft_mel_kernel(StftMelArgs a) {
       for (int r = 0; r < 16; ++r) in[0][r] = make_float2((float)(lane + r), (float)(g - r));
     } else if (interior) {
       const float2* x2 = reinterpret_cast<const float2*>(x + s0);
+      float2 xv[16], hw[16];  // samples and window pairs (h[2n], h[2n + 1]), n = lane + 64 r
+#pragma unroll
+      for (int r = 0; r < 16; ++r) xv[r] = x2[lane + 64 * r];  // issued first: the LDS batch hides under them
+      if constexpr (NC_SM_HANN_LDS) {
+        lds_read16_strided<0, 64 * 8>(hw, lds_addr(sh_hann + lane));
+      } else {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) hw[r] = reinterpret_cast<const float2*>(hann)[lane + 64 * r];
+      }
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int n = lane + 64 * r;
-        const float2 v = x2[n];
-        const float2 h = reinterpret_cast<const float2*>(hann)[n];
+        const float2 v = xv[r];
+        const float2 h = hw[r];
         if (r >= 8 && r < 12) {
           const int q = 2 * n - 1024;
           if (q < a.hop) {
@@ -226,6 +240,10 @@ int launch_stft_mel(Context& ctx, const StftMelArgs& args, hipStream_t st) {
     return -2;
   }
   const size_t lds = stft_mel_lds_bytes(a.mel_j0 + a.mel_j1);
+  if (lds > 160 * 1024) {
+    set_error("stft_mel: LDS layout exceeds 160 KiB");
+    return -2;
+  }
   const int64_t n_groups = (a.total_frames + SM_WAVES - 1) / SM_WAVES;
   const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(n_groups, (int64_t)ctx.num_cu * (lds <= 80 * 1024 ? 2 : 1)));
   {
