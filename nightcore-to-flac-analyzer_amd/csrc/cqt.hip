@@ -488,7 +488,7 @@ __global__ __launch_bounds__(NT) void tuning_select_kernel(const float* peak_pit
 // k < 256 together with its mirror 1024 - k, so the two spectra separate in registers:
 //   X_t[k] = (Z[k] + conj Z[N-k]) / 2,   X_{t+1}[k] = (Z[k] - conj Z[N-k]) / 2i.
 // Only the bins the basis rows touch, [klo, khi], are written back (one float4 per bin
-// holding both frames); each lane's piece of a sparse row (weights in registers, loaded
+// holding both frames, doubled: the row weights carry the 1/2); each lane's piece of a sparse row (weights in registers, loaded
 // once per workgroup for the chunk's tuning) reads them with 16-byte loads.  Per row
 // |C| sqrt(sr/my_sr) / sqrt(len) goes to an LDS row tile; then per frame the 12-bin
 // chroma (bins 3c-1, 3c, 3c+1 of each octave, ascending), its inf-norm and the f64 sum
@@ -632,6 +632,8 @@ __global__ __launch_bounds__(CQ_WAVES * 64) void cqt_chroma_kernel(CqtArgs a) {
     const int pr = it / 7, oct = it - 7 * pr;
     const int fl = 2 * pr;
     if (!NC_CQ_PREFETCH) load_item(it, ln, in);
+    // the row's 1/sqrt(len), requested with the samples so its latency hides under the FFT
+    const float il = isl[kCqtBins - kCqtFilt * (oct + 1) + max(pfilt, 0)];
     stockham_stage_regs<1024, 16, 1, 64, false, 0, 0>(in, fftbuf, sh_tw, ln);
     // with NC_CQ_PREFETCH the next item's samples stream in while this one finishes
     if (NC_CQ_PREFETCH && it + CQ_WAVES < n_items) load_item(it + CQ_WAVES, ln, in);
@@ -679,7 +681,8 @@ __global__ __launch_bounds__(CQ_WAVES * 64) void cqt_chroma_kernel(CqtArgs a) {
         const float2 m = b == 0 ? v[3][3] : b == 1 ? v[2][3] : b == 2 ? v[1][3] : (ln ? v[0][3] : v[3][3]);
         const float2 za = v[b][0], zb = cconj(m);
         const float2 s = csub(za, zb);
-        D[k - a.klo] = make_float4(0.5f * (za.x + zb.x), 0.5f * (za.y + zb.y), 0.5f * s.y, -0.5f * s.x);
+        // 2 X_t[k] and 2 X_t+1[k]: the weights carry the 1/2 (exact, so the row sums are unchanged)
+        D[k - a.klo] = make_float4(za.x + zb.x, za.y + zb.y, s.y, -s.x);
       }
     }
     // lane piece of a sparse row (complex64 accumulation in row order) for both frames; the
@@ -729,10 +732,12 @@ __global__ __launch_bounds__(CQ_WAVES * 64) void cqt_chroma_kernel(CqtArgs a) {
       bi += bi2;
     }
     if (pfilt >= 0) {
-      const float oscale = sqrtf((float)(1 << oct));  // fft_basis *= sqrt(sr / my_sr)
-      const float il = isl[kCqtBins - kCqtFilt * (oct + 1) + pfilt];
-      sh_mag[pfilt] = hypotf(ar * oscale, ai * oscale) * il;
-      sh_mag[36 + pfilt] = hypotf(br * oscale, bi * oscale) * il;
+      // fft_basis *= sqrt(sr / my_sr) = sqrtf(2^oct), correctly rounded: 2^(oct/2), times
+      // sqrtf(2) for odd octaves (exact power-of-two products)
+      const float oscale = (float)(1 << (oct >> 1)) * ((oct & 1) ? 0x1.6a09e6p+0f : 1.0f);
+      const float xr = ar * oscale, xi = ai * oscale, yr = br * oscale, yi = bi * oscale;
+      sh_mag[pfilt] = hypotf(xr, xi) * il;  // numpy's abs of complex64
+      sh_mag[36 + pfilt] = hypotf(yr, yi) * il;
     }
     // this octave's share of the 12 chroma bins of both frames: bins 3c-1, 3c, 3c+1 (mod 36),
     // in ascending order (c = 0: 0, 1, 35); tile row = bin octave 6 - oct (ascending bins)

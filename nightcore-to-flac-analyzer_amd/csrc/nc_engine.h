@@ -53,7 +53,7 @@ struct Tables {
   int* cqt_plen = nullptr;
   int* cqt_partner = nullptr;   // [kNTunings][64] lane holding this row's second half, or -1
   int* cqt_pfilt = nullptr;     // [kNTunings][64] row completed by this lane, or -1
-  float2* cqt_wcol = nullptr;   // [kNTunings][cqt_pmax][64] piece weights, column-major per tap
+  float2* cqt_wcol = nullptr;   // [kNTunings][cqt_pmax][64] piece weights / 2, column-major per tap
   int cqt_pmax = 0;
   int cqt_klo = 0, cqt_khi = 0; // FFT bins any row touches (over all tunings)
   double* halfband = nullptr;   // 2K+1 taps

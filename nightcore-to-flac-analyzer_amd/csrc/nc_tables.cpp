@@ -349,7 +349,8 @@ void build_tables(Context& ctx) {
     for (int ti = 0; ti < kNTunings; ++ti)
       for (int l = 0; l < (int)sched[ti].size(); ++l)
         for (int j = 0; j < sched[ti][l].len; ++j)
-          wcol[((size_t)ti * t.cqt_pmax + j) * 64 + l] = cw[sched[ti][l].off + j];
+          wcol[((size_t)ti * t.cqt_pmax + j) * 64 + l] =  // x 1/2: the frame-pair separation's halving
+              make_float2(0.5f * cw[sched[ti][l].off + j].x, 0.5f * cw[sched[ti][l].off + j].y);
     t.cqt_plo = upload(plo);
     t.cqt_plen = upload(plen);
     t.cqt_partner = upload(ppart);
