@@ -170,9 +170,15 @@ __device__ __forceinline__ void d3_level(const float* E, const float* O, int cnt
 // kernel from 73 to 129 VGPRs, three waves per SIMD instead of six.
 constexpr int D3_LD = (D3_P0 / 2 + 255) / 256;  // float4 input loads per thread per tile
 
+// the f32 taps by value: kernel arguments are scalar loads, so the taps stay in SGPRs
+// (v_fmac takes one SGPR operand) instead of holding ~37 VGPRs for the whole kernel
+struct D3Taps {
+  float h[2 * kHalfbandK + 1];
+};
+
 __global__ __launch_bounds__(256) void decimate3_kernel(const float* sig, const int64_t* chunk_off,
                                                         const int64_t* oct_off, const int64_t* oct_len,
-                                                        float* ws_oct, int base, const double* __restrict__ taps,
+                                                        float* ws_oct, int base, D3Taps taps,
                                                         unsigned long long* span) {
   const Span span_(span);
   static_assert(kHalfbandK == 23, "phase windows assume 23");
@@ -182,9 +188,7 @@ __global__ __launch_bounds__(256) void decimate3_kernel(const float* sig, const 
   const int64_t* len = oct_len + c * 7 + base;
   const int64_t m0 = (int64_t)blockIdx.x * D3_T;
   if (m0 >= len[3]) return;
-  float h[2 * kHalfbandK + 1];
-#pragma unroll
-  for (int j = 0; j <= 2 * kHalfbandK; ++j) h[j] = (float)taps[j];
+  const float (&h)[2 * kHalfbandK + 1] = taps.h;
   const float* in = base == 0 ? sig + chunk_off[c] : ws_oct + oct_off[c * 7 + base];
   const int64_t L0 = len[0];
   const bool vec = ((reinterpret_cast<uintptr_t>(in) & 15) == 0);
@@ -909,8 +913,10 @@ int launch_chroma_mean(Context& ctx, const float* sig, const int64_t* chunk_off,
     dim3 grid((unsigned)((mo + D3_T - 1) / D3_T), (unsigned)n);
     {
       KTimer kt_(ctx, "decimate", st);
+      D3Taps taps;
+      std::copy(ctx.t.halfband_f32, ctx.t.halfband_f32 + 2 * kHalfbandK + 1, taps.h);
       hipLaunchKernelGGL(decimate3_kernel, grid, dim3(256), 0, st, sig, chunk_off, w.oct_off, w.oct_len, w.ws_oct,
-                         base, ctx.t.halfband, kt_.span());
+                         base, taps, kt_.span());
     }
   }
   PeakArgs pa;

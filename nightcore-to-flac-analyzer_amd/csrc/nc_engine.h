@@ -57,6 +57,7 @@ struct Tables {
   int cqt_pmax = 0;
   int cqt_klo = 0, cqt_khi = 0; // FFT bins any row touches (over all tunings)
   double* halfband = nullptr;   // 2K+1 taps
+  float halfband_f32[2 * kHalfbandK + 1] = {};  // host copy, rounded to f32 (decimate3 kernel argument)
 };
 
 struct KernelTimers;  // nc_prof.cpp

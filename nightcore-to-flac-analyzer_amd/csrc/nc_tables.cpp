@@ -202,6 +202,7 @@ void build_tables(Context& ctx) {
     }
     for (auto& v : h) v /= sum;
     t.halfband = upload(h);
+    for (int j = 0; j < M; ++j) t.halfband_f32[j] = (float)h[j];
   }
 
   // CQT bases for every tuning on the 0.01-bin grid (oracle/ncref.py cqt_mag / vqt_filter_fft)
