@@ -166,9 +166,14 @@ __device__ __forceinline__ void d3_level(const float* E, const float* O, int cnt
 // The level-base input of a tile is requested as D3_LD float4 loads per thread, all issued
 // before any is staged (one global latency per tile instead of one per load; 276 -> 242 us
 // per 224 chunks).  Walking several tiles per workgroup with the next tile's loads in
-// flight during the levels measured slower (382 us): the live prefetch registers take the
-// kernel from 73 to 129 VGPRs, three waves per SIMD instead of six.
+// flight during the levels (NC_D3_TPW > 1) measures slower, 355 against 228 us: the tile
+// loop moves the taps out of SGPRs and the kernel to 105 VGPRs, four waves per SIMD
+// instead of eight.
 constexpr int D3_LD = (D3_P0 / 2 + 255) / 256;  // float4 input loads per thread per tile
+#ifndef NC_D3_TPW  // consecutive tiles per workgroup, the next one's input loaded during the levels
+#define NC_D3_TPW 1
+#endif
+constexpr int D3_TPW = NC_D3_TPW;
 
 // the f32 taps by value: kernel arguments are scalar loads, so the taps stay in SGPRs
 // (v_fmac takes one SGPR operand) instead of holding ~37 VGPRs for the whole kernel
@@ -186,16 +191,18 @@ __global__ __launch_bounds__(256) void decimate3_kernel(const float* sig, const 
   __shared__ __attribute__((aligned(16))) float e1[D3_N1 / 2], o1[D3_N1 / 2];
   const int c = blockIdx.y;
   const int64_t* len = oct_len + c * 7 + base;
-  const int64_t m0 = (int64_t)blockIdx.x * D3_T;
-  if (m0 >= len[3]) return;
+  const int64_t mb = (int64_t)blockIdx.x * (D3_TPW * D3_T);
+  if (mb >= len[3]) return;
   const float (&h)[2 * kHalfbandK + 1] = taps.h;
   const float* in = base == 0 ? sig + chunk_off[c] : ws_oct + oct_off[c * 7 + base];
   const int64_t L0 = len[0];
   const bool vec = ((reinterpret_cast<uintptr_t>(in) & 15) == 0);
-  // level base: values [8 m0 - 168, 8 m0 - 168 + 2 D3_P0), 4 values (2 pairs) per float4
-  {
+  float* out1 = ws_oct + oct_off[c * 7 + base + 1];
+  float* out2 = ws_oct + oct_off[c * 7 + base + 2];
+  float* out3 = ws_oct + oct_off[c * 7 + base + 3];
+  // level base of tile m0: values [8 m0 - 168, 8 m0 - 168 + 2 D3_P0), 4 values (2 pairs) per float4
+  auto load_tile = [&](int64_t m0, float4 (&pf)[D3_LD]) {
     const int64_t v0 = 8 * m0 - 168;
-    float4 pf[D3_LD];
 #pragma unroll
     for (int k = 0; k < D3_LD; ++k) {
       const int u = threadIdx.x + 256 * k;
@@ -213,6 +220,14 @@ __global__ __launch_bounds__(256) void decimate3_kernel(const float* sig, const 
       }
       pf[k] = v;
     }
+  };
+  float4 pf[D3_LD];
+  load_tile(mb, pf);
+#pragma unroll 1
+  for (int tt = 0; tt < D3_TPW; ++tt) {
+    const int64_t m0 = mb + (int64_t)tt * D3_T;
+    if (m0 >= len[3]) break;
+    if (tt) __syncthreads();  // the previous tile's last level has read e0/o0
 #pragma unroll
     for (int k = 0; k < D3_LD; ++k) {
       const int u = threadIdx.x + 256 * k;
@@ -221,19 +236,18 @@ __global__ __launch_bounds__(256) void decimate3_kernel(const float* sig, const 
         *reinterpret_cast<float2*>(o0 + 2 * u) = make_float2(pf[k].y, pf[k].w);
       }
     }
+    __syncthreads();
+    // the next tile's input is in flight while this one's levels run
+    if (tt + 1 < D3_TPW && m0 + D3_T < len[3]) load_tile(m0 + D3_T, pf);
+    // level base+1: [4 m0 - 72, +D3_N1), owned [4 m0, 4 m0 + 4 T); phases -> e1/o1
+    d3_level(e0, o0, D3_N1, 4 * m0 - 72, len[1], h, e1, o1, out1, 72, 4 * D3_T);
+    __syncthreads();
+    // level base+2: [2 m0 - 24, +D3_N2), owned [2 m0, 2 m0 + 2 T); phases -> e0/o0 (reused)
+    d3_level(e1, o1, D3_N2, 2 * m0 - 24, len[2], h, e0, o0, out2, 24, 2 * D3_T);
+    __syncthreads();
+    // level base+3: [m0, m0 + T), all owned
+    d3_level(e0, o0, D3_T, m0, len[3], h, nullptr, nullptr, out3, 0, D3_T);
   }
-  __syncthreads();
-  float* out1 = ws_oct + oct_off[c * 7 + base + 1];
-  float* out2 = ws_oct + oct_off[c * 7 + base + 2];
-  float* out3 = ws_oct + oct_off[c * 7 + base + 3];
-  // level base+1: [4 m0 - 72, +D3_N1), owned [4 m0, 4 m0 + 4 T); phases -> e1/o1
-  d3_level(e0, o0, D3_N1, 4 * m0 - 72, len[1], h, e1, o1, out1, 72, 4 * D3_T);
-  __syncthreads();
-  // level base+2: [2 m0 - 24, +D3_N2), owned [2 m0, 2 m0 + 2 T); phases -> e0/o0 (reused)
-  d3_level(e1, o1, D3_N2, 2 * m0 - 24, len[2], h, e0, o0, out2, 24, 2 * D3_T);
-  __syncthreads();
-  // level base+3: [m0, m0 + T), all owned
-  d3_level(e0, o0, D3_T, m0, len[3], h, nullptr, nullptr, out3, 0, D3_T);
 }
 
 // ------------------------------------------------------------------------------ 2. tuning peaks
@@ -910,7 +924,7 @@ int launch_chroma_mean(Context& ctx, const float* sig, const int64_t* chunk_off,
   // gain: the chip is already full with the window chain on the caller's other stream.)
   for (int base = 0; base < 6; base += 3) {
     const int64_t mo = (max_chunk_len >> (base + 3)) + 1;  // >= the longest chunk's level base + 3
-    dim3 grid((unsigned)((mo + D3_T - 1) / D3_T), (unsigned)n);
+    dim3 grid((unsigned)((mo + D3_TPW * D3_T - 1) / (D3_TPW * D3_T)), (unsigned)n);
     {
       KTimer kt_(ctx, "decimate", st);
       D3Taps taps;
