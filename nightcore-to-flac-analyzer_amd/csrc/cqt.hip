@@ -183,12 +183,13 @@ struct D3Taps {
 
 __global__ __launch_bounds__(256) void decimate3_kernel(const float* sig, const int64_t* chunk_off,
                                                         const int64_t* oct_off, const int64_t* oct_len,
-                                                        float* ws_oct, int base, D3Taps taps,
+                                                        float* ws_oct, int base, D3Taps taps, float* xmax,
                                                         unsigned long long* span) {
   const Span span_(span);
   static_assert(kHalfbandK == 23, "phase windows assume 23");
   __shared__ __attribute__((aligned(16))) float e0[D3_P0], o0[D3_P0];
   __shared__ __attribute__((aligned(16))) float e1[D3_N1 / 2], o1[D3_N1 / 2];
+  __shared__ float wmax[4];
   const int c = blockIdx.y;
   const int64_t* len = oct_len + c * 7 + base;
   const int64_t mb = (int64_t)blockIdx.x * (D3_TPW * D3_T);
@@ -222,12 +223,14 @@ __global__ __launch_bounds__(256) void decimate3_kernel(const float* sig, const 
     }
   };
   float4 pf[D3_LD];
+  float bmax = 0.0f;
   load_tile(mb, pf);
 #pragma unroll 1
   for (int tt = 0; tt < D3_TPW; ++tt) {
     const int64_t m0 = mb + (int64_t)tt * D3_T;
     if (m0 >= len[3]) break;
     if (tt) __syncthreads();  // the previous tile's last level has read e0/o0
+    float m = 0.0f;  // max |level 0| over the tile's input (the MFMA CQT's f16 scale)
 #pragma unroll
     for (int k = 0; k < D3_LD; ++k) {
       const int u = threadIdx.x + 256 * k;
@@ -235,8 +238,19 @@ __global__ __launch_bounds__(256) void decimate3_kernel(const float* sig, const 
         *reinterpret_cast<float2*>(e0 + 2 * u) = make_float2(pf[k].x, pf[k].z);
         *reinterpret_cast<float2*>(o0 + 2 * u) = make_float2(pf[k].y, pf[k].w);
       }
+      if (base == 0) m = fmaxf(m, fmaxf(fmaxf(fabsf(pf[k].x), fabsf(pf[k].y)), fmaxf(fabsf(pf[k].z), fabsf(pf[k].w))));
+    }
+    if (base == 0 && xmax) {
+      m = wave_max(m);
+      if ((threadIdx.x & 63) == 0) wmax[threadIdx.x >> 6] = m;
     }
     __syncthreads();
+    // one maximum per workgroup, no atomics: slot c + oct_off[c][3] / 256 + blockIdx.x (distinct
+    // per chunk; read back by cqt_mfma_kernel)
+    if (base == 0 && xmax && threadIdx.x == 0) {
+      bmax = fmaxf(bmax, fmaxf(fmaxf(wmax[0], wmax[1]), fmaxf(wmax[2], wmax[3])));
+      xmax[c + oct_off[c * 7 + 3] / 256 + blockIdx.x] = bmax;
+    }
     // the next tile's input is in flight while this one's levels run
     if (tt + 1 < D3_TPW && m0 + D3_T < len[3]) load_tile(m0 + D3_T, pf);
     // level base+1: [4 m0 - 72, +D3_N1), owned [4 m0, 4 m0 + 4 T); phases -> e1/o1
@@ -795,14 +809,366 @@ __global__ __launch_bounds__(CQ_WAVES * 64) void cqt_chroma_kernel(CqtArgs a) {
   }
 }
 
+// ------------------------------------------------------------------------------ 4'. CQT on MFMA
+// The CQT response is linear in the frame: C_j[t] = sum_b fb[j][b] rfft(x_t)[b] =
+// sum_n x_t[n] h_j[n] with h_j[n] = sum_b fb[j][b] e^{-2 pi i b n / 1024} (nc_tables.cpp).
+// Per octave that is a real GEMM [frames x 1024] . [1024 x 72] (Re and Im of the 36 rows),
+// run on the f16 matrix cores with both operands split into hi + lo halves (x = xh + xl,
+// products xh.hh + xh.hl + xl.hh, f32 accumulation): 22 significant bits per operand, so
+// |C| matches the f32 FFT path to ~1e-6 of the frame's largest bin.  The frame operand is
+// scaled by 2^ex with max|y_o| * 2^ex < 2^13 (max|y_0| from decimate3, bounded per octave by
+// (sqrt(2) sum|h|)^o) and the filters by 2^e_j; C = acc * 2^-(ex + e_j) exactly.
+//
+// One workgroup per (chunk, 64-frame tile), one wave per octave (7 waves): 4 row tiles x 5
+// column tiles x 3 products = 60 MFMA 16x16x32 per k-step of 32 taps, 32 k-steps.  Operands:
+//  * filter slices (one k-step: 10 fragments x 1 KB) stream through a 3-deep LDS ring by
+//    LDS-DMA (global_load_lds), two k-steps ahead;
+//  * octaves >= CM_LO (hop <= 64): the tile's whole span is split once into an LDS image
+//    (f16 hi, lo) that every k-step's fragments read;
+//  * octaves < CM_LO (hop >= 128: little overlap between rows): each k-step's 64 row pieces
+//    (32 samples each) stream through a per-wave 3-deep LDS ring by LDS-DMA, two k-steps
+//    ahead, and are split at use.
+// One raw s_barrier per k-step (no vmcnt drain: the DMA two steps ahead stays in flight).
+// Epilogue as cqt_chroma_kernel: |C| sqrt(sr/my_sr) / sqrt(len) -> octave chroma partials ->
+// the 7 octaves summed per frame -> inf-norm -> f64 sum over the tile's frames.
+#ifndef NC_CQ_MFMA
+#define NC_CQ_MFMA 1
+#endif
+#ifndef NC_CM_DIAG  // diagnosis builds only: 1 global rows fetched once, 2 filter slices fetched once
+#define NC_CM_DIAG 0
+#endif
+#ifndef NC_CM_LO
+#define NC_CM_LO 3
+#endif
+#ifndef NC_CM_FR
+#define NC_CM_FR 64
+#endif
+constexpr int CM_FR = NC_CM_FR;                    // frames per workgroup tile
+constexpr int CM_RT = CM_FR / 16;                  // row tiles per wave
+static_assert(CM_FR == 32 || CM_FR == 64, "tile");
+constexpr int CM_KS = kCqtNfft / 32;               // k-steps of 32 taps
+constexpr int CM_NT = 5;                           // column tiles (72 of 80 columns used)
+constexpr int CM_R = 3;                            // ring depth (filter slices, row pieces)
+constexpr int CM_SLICE = CM_NT * 2 * 64;           // uint4 fragments per k-step slice
+constexpr int CM_NTH = 7 * 64;
+constexpr int CM_LO = NC_CM_LO;
+static_assert(CM_LO >= 1 && CM_LO <= 6, "both wave kinds present");
+constexpr int CM_GQ = (CM_NT * 2 + (7 - CM_LO) - 1) / (7 - CM_LO);  // filter DMA pieces per image wave
+typedef _Float16 cm_half8 __attribute__((ext_vector_type(8)));
+typedef float cm_f4 __attribute__((ext_vector_type(4)));
+typedef unsigned cm_u4 __attribute__((ext_vector_type(4)));
+
+// s_waitcnt immediate for vmcnt(n) alone (vmcnt [3:0] + [15:14]; expcnt, lgkmcnt at maximum)
+__host__ __device__ constexpr int cm_vmcnt(int n) { return (n & 15) | ((n >> 4) << 14) | 0x70 | 0xf00; }
+
+// LDS images: span 63 hop + 1024 samples as f16 hi then lo, 8 halves of padding after every
+// hop samples when hop >= 16 (row r starts at r (hop + 8): a fragment's 16 rows on distinct
+// 16-byte bank groups); a row's 8-sample piece never straddles a pad
+__host__ __device__ constexpr int cm_hop(int o) { return 512 >> o; }
+__host__ __device__ constexpr int cm_pad(int o) { return cm_hop(o) >= 16 ? 8 : 0; }
+__host__ __device__ constexpr int cm_span(int o) { return (CM_FR - 1) * cm_hop(o) + kCqtNfft; }
+__host__ __device__ constexpr int cm_img(int o) {  // halves per hi (or lo) image, 16-byte multiple
+  return (cm_span(o) + (cm_span(o) / cm_hop(o)) * cm_pad(o) + 7) & ~7;
+}
+__host__ __device__ constexpr int cm_aoff(int o) {  // byte offset of octave o's image pair
+  return o <= CM_LO ? 0 : cm_aoff(o - 1) + 4 * cm_img(o - 1);
+}
+// K-loop LDS: filter ring [CM_R][CM_SLICE] uint4 | row rings [CM_LO][CM_R][CM_FR rows][32] f32 |
+// images.  Epilogue (overlay): octave rows [7][CM_FR][36] f32 | partials [CM_FR][7][12] f32
+constexpr int CM_BBYTES = CM_R * CM_SLICE * 16;
+constexpr int CM_RBYTES = CM_LO * CM_R * CM_FR * 32 * 4;
+constexpr int CM_KBYTES = CM_BBYTES + CM_RBYTES + cm_aoff(7);
+constexpr int CM_MBYTES = 7 * CM_FR * kCqtFilt * 4;
+constexpr int CM_EBYTES = CM_MBYTES + CM_FR * CQ_TILE * 4;
+size_t cqm_lds_bytes() { return CM_KBYTES > CM_EBYTES ? CM_KBYTES : CM_EBYTES; }
+
+struct CqmArgs {
+  const float* sig;
+  const int64_t* chunk_off;
+  const int64_t* oct_off;
+  const int64_t* oct_len;
+  const int* n_frames;
+  const int* tuning_idx;
+  const float* ws_oct;
+  const int64_t* tf_base;
+  const uint4* bfrag;    // Tables::cqm_b
+  const int* bexp;       // Tables::cqm_bexp
+  const float* cqt_isl;
+  const float* xmax;     // decimate3 workgroup maxima of |level 0| (slot c + oct_off[c][3] / 256 + tile)
+  int d3_span;           // level-3 outputs per decimate3 workgroup
+  float gpow[7];
+  double* partial;       // [tf_base[c] / CM_FR + c + tile][12]
+  unsigned long long* span = nullptr;
+};
+
+// One LDS-DMA instruction: 16 bytes per lane from gsrc to lds_dst + 16 lane (lds_dst
+// wave-uniform).  Inline asm rather than __builtin_amdgcn_global_load_lds: the compiler
+// drains vmcnt(0) before any later LDS read when it sees the builtin, which would retire the
+// DMA issued two k-steps ahead every step; the kernel counts its own vmcnt instead.
+__device__ __forceinline__ void cm_dma16(const void* gsrc, const void* lds_dst) {
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(gsrc), "s"(lds_addr(lds_dst))
+               : "memory");
+}
+
+// 8 samples -> f16 hi (f32 truncated to 11 significant bits: exact in f16) and lo (the
+// exact f32 remainder, rounded toward zero)
+__device__ __forceinline__ void cm_split(const float (&v)[8], float s, cm_half8& hi, cm_half8& lo) {
+  cm_u4 h, l;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const float x0 = v[2 * j] * s, x1 = v[2 * j + 1] * s;
+    const float h0 = __uint_as_float(__float_as_uint(x0) & 0xffffe000u);
+    const float h1 = __uint_as_float(__float_as_uint(x1) & 0xffffe000u);
+    h[j] = __builtin_bit_cast(unsigned, __builtin_amdgcn_cvt_pkrtz(h0, h1));
+    l[j] = __builtin_bit_cast(unsigned, __builtin_amdgcn_cvt_pkrtz(x0 - h0, x1 - h1));
+  }
+  hi = __builtin_bit_cast(cm_half8, h);
+  lo = __builtin_bit_cast(cm_half8, l);
+}
+
+__global__ __launch_bounds__(CM_NTH) void cqt_mfma_kernel(CqmArgs a) {
+  const Span span_(a.span);
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  uint4* sB = reinterpret_cast<uint4*>(smem);  // [CM_R][CM_SLICE]
+  const int c = blockIdx.y;
+  const int T = a.n_frames[c];
+  const int t0 = blockIdx.x * CM_FR;
+  if (t0 >= T) return;
+  const int nfr = min(CM_FR, T - t0);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int oct = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int ti = a.tuning_idx[c];
+  const uint4* bsrc = a.bfrag + (size_t)ti * (CM_KS * CM_SLICE);
+  const bool img_w = oct >= CM_LO;  // wave-uniform: image wave or row-ring wave
+
+  // this wave's octave: rows t0 .. t0 + 63, row t at sample t hop - 512
+  const float* y = oct == 0 ? a.sig + a.chunk_off[c] : a.ws_oct + a.oct_off[c * 7 + oct];
+  const int64_t Ly = a.oct_len[c * 7 + oct];
+  const int hop = 512 >> oct;
+  int ex = 0;
+  {
+    const int64_t l3 = a.oct_len[c * 7 + 3];
+    const int ntl = (int)((l3 + a.d3_span - 1) / a.d3_span);
+    const float* xm = a.xmax + c + a.oct_off[c * 7 + 3] / 256;
+    float m0 = 0.0f;
+    for (int i = lane; i < ntl; i += 64) m0 = fmaxf(m0, xm[i]);
+    const float mx = wave_max_u(m0) * a.gpow[oct];
+    if (mx > 0.0f) {
+      int e;
+      frexpf(mx, &e);  // mx < 2^e
+      ex = min(13 - e, 100);
+    }
+  }
+  const float sx = ldexpf(1.0f, ex);
+  const int64_t s0 = (int64_t)t0 * hop - 512;  // first sample of the tile's span
+  const int S = (CM_FR - 1) * hop + kCqtNfft;
+  const bool vec = s0 >= 0 && s0 + S <= Ly && (reinterpret_cast<uintptr_t>(y) & 15) == 0;
+  const int kq = 8 * (lane >> 4);
+
+  // --- image waves: split the span once
+  constexpr int aoffs[8] = {cm_aoff(0), cm_aoff(1), cm_aoff(2), cm_aoff(3), cm_aoff(4), cm_aoff(5), cm_aoff(6), cm_aoff(7)};
+  const int pad = img_w ? cm_pad(oct) : 0;
+  const int img = img_w ? cm_img(oct) : 0;
+  _Float16* aimg = reinterpret_cast<_Float16*>(smem + CM_BBYTES + CM_RBYTES + (img_w ? aoffs[oct] : 0));
+  if (img_w) {
+    for (int i = lane; i < S / 8; i += 64) {
+      float v[8];
+      if (vec) {
+        const float4 u0 = *reinterpret_cast<const float4*>(y + s0 + 8 * i);
+        const float4 u1 = *reinterpret_cast<const float4*>(y + s0 + 8 * i + 4);
+        v[0] = u0.x; v[1] = u0.y; v[2] = u0.z; v[3] = u0.w;
+        v[4] = u1.x; v[5] = u1.y; v[6] = u1.z; v[7] = u1.w;
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int64_t q = s0 + 8 * i + j;
+          v[j] = (q >= 0 && q < Ly) ? y[q] : 0.0f;
+        }
+      }
+      cm_half8 h, l;
+      cm_split(v, sx, h, l);
+      const int pos = 8 * i + (8 * i / hop) * pad;
+      *reinterpret_cast<cm_half8*>(aimg + pos) = h;
+      *reinterpret_cast<cm_half8*>(aimg + img + pos) = l;
+    }
+  }
+  // image fragment base per row tile (rows past T - 1 read real or zero samples of the span
+  // and are discarded)
+  int abase[CM_RT];
+#pragma unroll
+  for (int rt = 0; rt < CM_RT; ++rt) abase[rt] = (16 * rt + (lane & 15)) * (hop + pad) + kq + (kq / hop) * pad;
+
+  // --- row-ring waves: slot [CM_FR rows][8 x 16 B], 16-byte piece p of row r stored at
+  // (p ^ ((r >> 1) & 7)): a fragment read's 16 rows hit 16 distinct bank groups.  One DMA
+  // instruction moves rows 8i .. 8i + 7 (lane l: row 8i + l / 8, slot l % 8).
+  float* ring = reinterpret_cast<float*>(smem + CM_BBYTES) + (img_w ? 0 : oct) * (CM_R * CM_FR * 32);
+  const int dr = lane >> 3;  // DMA row within an 8-row group
+  auto fetch_rows = [&](int ks) {
+    float* slot = ring + (ks % CM_R) * (CM_FR * 32);
+    if (vec) {
+#pragma unroll
+      for (int i = 0; i < CM_FR / 8; ++i) {
+        const int r = 8 * i + dr;
+        const int piece = (lane & 7) ^ ((r >> 1) & 7);
+        cm_dma16(y + s0 + (int64_t)r * hop + 32 * ks + 4 * piece, slot + i * 256);
+      }
+    } else {  // edge tiles: guarded loads, written to the same layout
+#pragma unroll
+      for (int i = 0; i < CM_FR / 8; ++i) {
+        const int r = 8 * i + dr;
+        const int piece = (lane & 7) ^ ((r >> 1) & 7);
+        float4 v;
+        const int64_t q = s0 + (int64_t)r * hop + 32 * ks + 4 * piece;
+        v.x = (q >= 0 && q < Ly) ? y[q] : 0.0f;
+        v.y = (q + 1 >= 0 && q + 1 < Ly) ? y[q + 1] : 0.0f;
+        v.z = (q + 2 >= 0 && q + 2 < Ly) ? y[q + 2] : 0.0f;
+        v.w = (q + 3 >= 0 && q + 3 < Ly) ? y[q + 3] : 0.0f;
+        reinterpret_cast<float4*>(slot)[i * 64 + lane] = v;
+      }
+    }
+  };
+  // filter slices: the image waves share the 10 DMA pieces of a slice
+  const int g = oct - CM_LO, ng = 7 - CM_LO;
+  auto fetch_slice = [&](int ks) {
+#pragma unroll
+    for (int q = 0; q < CM_GQ; ++q) {
+      int i = g + ng * q;
+      if (i >= CM_NT * 2) i = g;  // duplicate of this wave's first piece (same bytes, same place)
+      cm_dma16(bsrc + ks * CM_SLICE + i * 64 + lane, sB + (ks % CM_R) * CM_SLICE + i * 64);
+    }
+  };
+  auto fetch = [&](int ks) {
+    if (img_w) fetch_slice(ks);
+    else fetch_rows(ks);
+  };
+
+  cm_f4 acc[CM_RT][CM_NT];
+#pragma unroll
+  for (int rt = 0; rt < CM_RT; ++rt)
+#pragma unroll
+    for (int nt = 0; nt < CM_NT; ++nt) acc[rt][nt] = cm_f4{0.f, 0.f, 0.f, 0.f};
+  fetch(0);
+  fetch(1);
+#pragma unroll 1
+  for (int ks = 0; ks < CM_KS; ++ks) {
+    // retire this wave's DMA of step ks (the step ks + 1 DMA, issued after it, may stay in
+    // flight); then every wave's: the barrier also ends every read of step ks - 1's slot
+    if (ks + 1 < CM_KS) {
+      if (img_w) __builtin_amdgcn_s_waitcnt(cm_vmcnt(CM_GQ));
+      else __builtin_amdgcn_s_waitcnt(cm_vmcnt(CM_FR / 8));
+    } else {
+      __builtin_amdgcn_s_waitcnt(cm_vmcnt(0));
+    }
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): image and edge-row LDS writes
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (ks + 2 < CM_KS && !((NC_CM_DIAG & 2) && img_w) && !((NC_CM_DIAG & 1) && !img_w)) fetch(ks + 2);
+    cm_half8 ah[CM_RT], al[CM_RT];
+    if (img_w) {
+      const int kt = 32 * ks + (32 * ks / hop) * pad;
+#pragma unroll
+      for (int rt = 0; rt < CM_RT; ++rt) {
+        ah[rt] = *reinterpret_cast<const cm_half8*>(aimg + abase[rt] + kt);
+        al[rt] = *reinterpret_cast<const cm_half8*>(aimg + img + abase[rt] + kt);
+      }
+    } else {
+      const float4* slot = reinterpret_cast<const float4*>(ring + (ks % CM_R) * (CM_FR * 32));
+#pragma unroll
+      for (int rt = 0; rt < CM_RT; ++rt) {
+        const int r = 16 * rt + (lane & 15);
+        const int p0 = 2 * (lane >> 4), sw = (r >> 1) & 7;
+        const float4 u0 = slot[r * 8 + (p0 ^ sw)], u1 = slot[r * 8 + ((p0 + 1) ^ sw)];
+        const float v[8] = {u0.x, u0.y, u0.z, u0.w, u1.x, u1.y, u1.z, u1.w};
+        cm_split(v, sx, ah[rt], al[rt]);
+      }
+    }
+    const uint4* sb = sB + (ks % CM_R) * CM_SLICE + lane;
+#pragma unroll
+    for (int nt = 0; nt < CM_NT; ++nt) {
+      const cm_half8 bh = __builtin_bit_cast(cm_half8, sb[(nt * 2) * 64]);
+      const cm_half8 bl = __builtin_bit_cast(cm_half8, sb[(nt * 2 + 1) * 64]);
+#pragma unroll
+      for (int rt = 0; rt < CM_RT; ++rt) {
+        acc[rt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[rt], bh, acc[rt][nt], 0, 0, 0);
+        acc[rt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[rt], bl, acc[rt][nt], 0, 0, 0);
+        acc[rt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al[rt], bh, acc[rt][nt], 0, 0, 0);
+      }
+    }
+  }
+  __syncthreads();  // every wave's last ring / image reads done before the epilogue overlay
+  float* sh_part = reinterpret_cast<float*>(smem + CM_MBYTES);  // [CM_FR][7][12]
+
+  // |C| per (frame, row) into this wave's [CM_FR][36] region (over the filter stages)
+  {
+    float* mg = reinterpret_cast<float*>(smem) + oct * (CM_FR * kCqtFilt);
+    const float oscale = (float)(1 << (oct >> 1)) * ((oct & 1) ? 0x1.6a09e6p+0f : 1.0f);
+    const float* isl = a.cqt_isl + ti * kCqtBins + (kCqtBins - kCqtFilt * (oct + 1));
+    const int* bx = a.bexp + ti * kCqtFilt;
+    const int col = lane & 15;
+    const float inv0 = ldexpf(1.0f, -(ex + bx[col])), inv1 = ldexpf(1.0f, -(ex + bx[16 + col]));
+    const float inv2 = ldexpf(1.0f, -(ex + bx[32 + (col & 3)]));
+    const float il0 = isl[col], il1 = isl[16 + col], il2 = isl[32 + (col & 3)];
+#pragma unroll
+    for (int rt = 0; rt < CM_RT; ++rt)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int fr = 16 * rt + 4 * (lane >> 4) + i;
+        float* m = mg + fr * kCqtFilt;
+        m[col] = hypotf(acc[rt][0][i] * inv0 * oscale, acc[rt][1][i] * inv0 * oscale) * il0;
+        m[16 + col] = hypotf(acc[rt][2][i] * inv1 * oscale, acc[rt][3][i] * inv1 * oscale) * il1;
+        const float im = __shfl_down(acc[rt][4][i], 4, 16);
+        if (col < 4) m[32 + col] = hypotf(acc[rt][4][i] * inv2 * oscale, im * inv2 * oscale) * il2;
+      }
+  }
+  __syncthreads();
+  // this octave's share of the 12 chroma bins: bins 3c-1, 3c, 3c+1 (mod 36), ascending
+  {
+    const float* mg = reinterpret_cast<const float*>(smem) + oct * (CM_FR * kCqtFilt);
+    for (int q = lane; q < nfr * 12; q += 64) {
+      const int fl = q / 12, cc = q - 12 * fl;
+      const float* m = mg + fl * kCqtFilt;
+      const float p = cc == 0 ? (m[0] + m[1]) + m[35] : (m[3 * cc - 1] + m[3 * cc]) + m[3 * cc + 1];
+      sh_part[fl * CQ_TILE + (6 - oct) * 12 + cc] = p;
+    }
+  }
+  __syncthreads();
+  float* sh_ch = reinterpret_cast<float*>(smem);  // [CM_FR][12] (the octave rows are consumed)
+  float* sh_nv = sh_ch + CM_FR * 12;
+  for (int q = tid; q < nfr * 12; q += CM_NTH) {
+    const int fl = q / 12, cc = q - 12 * fl;
+    const float* pt = sh_part + fl * CQ_TILE + cc;
+    float ch = 0.0f;
+#pragma unroll
+    for (int o = 0; o < 7; ++o) ch += pt[12 * o];
+    sh_ch[q] = ch;
+  }
+  __syncthreads();
+  for (int q = tid; q < nfr * 12; q += CM_NTH) {
+    const int fl = q / 12;
+    float mx = 0.0f;
+    for (int j = 0; j < 12; ++j) mx = fmaxf(mx, fabsf(sh_ch[fl * 12 + j]));
+    const double len = (mx < 1.17549435e-38f) ? 1.0 : (double)mx;
+    sh_nv[q] = (float)((double)sh_ch[q] / len);
+  }
+  __syncthreads();
+  if (tid < 12) {
+    double s = 0.0;
+    for (int fl = 0; fl < nfr; ++fl) s += (double)sh_nv[fl * 12 + tid];
+    a.partial[(a.tf_base[c] / CM_FR + c + blockIdx.x) * 12 + tid] = s;
+  }
+}
+
 __global__ void chroma_finalize_kernel(const double* partial, const int64_t* tf_base, const int* n_frames, int n,
-                                       float* out_chroma) {
+                                       int fr, float* out_chroma) {
   const int c = blockIdx.x;
   const int k = threadIdx.x;
   if (k >= 12 || c >= n) return;
   const int T = n_frames[c];
-  const int nb = (T + CQ_FR - 1) / CQ_FR;
-  const int64_t r0 = tf_base[c] / CQ_FR + c;
+  const int nb = (T + fr - 1) / fr;
+  const int64_t r0 = tf_base[c] / fr + c;
   double s = 0.0;
   for (int b = 0; b < nb; ++b) s += partial[(r0 + b) * 12 + k];
   out_chroma[c * 12 + k] = (float)(s / (double)T);
@@ -853,6 +1219,7 @@ struct ChromaWs {
   int* chunk_npk;
   double* partial;
   int* tuning_idx;
+  float* xmax;  // decimate3 workgroup maxima of |level 0|
 };
 
 static inline size_t al256(size_t n) { return (n + 255) & ~(size_t)255; }
@@ -868,6 +1235,7 @@ size_t chroma_ws_bytes(int n, int64_t total_len) {
   b += al256(sizeof(float) * (size_t)tfr * kPeakSlots) * 2;
   b += al256(sizeof(double) * (size_t)(tfr / CQ_FR + n + 1) * 12);
   b += al256(sizeof(int64_t) * (n + 1));
+  b += al256(sizeof(float) * (size_t)(n + (total_len + 64 * 7 * (int64_t)n) / 256 + 2));
   return b + 4096;
 }
 
@@ -910,6 +1278,7 @@ int launch_chroma_mean(Context& ctx, const float* sig, const int64_t* chunk_off,
   w.peak_mag = reinterpret_cast<float*>(take(sizeof(float) * (size_t)tfr * kPeakSlots));
   w.partial = reinterpret_cast<double*>(take(sizeof(double) * (size_t)(tfr / CQ_FR + n + 1) * 12));
   int64_t* tp_base = reinterpret_cast<int64_t*>(take(sizeof(int64_t) * (n + 1)));
+  w.xmax = reinterpret_cast<float*>(take(sizeof(float) * (size_t)(n + (total_len + 64 * 7 * (int64_t)n) / 256 + 2)));
   if (ext) {  // the caller's lists (zeroed counts): the window stage appends to them too
     w.peak_pitch = ext_pitch;
     w.peak_mag = ext_mag;
@@ -930,7 +1299,7 @@ int launch_chroma_mean(Context& ctx, const float* sig, const int64_t* chunk_off,
       D3Taps taps;
       std::copy(ctx.t.halfband_f32, ctx.t.halfband_f32 + 2 * kHalfbandK + 1, taps.h);
       hipLaunchKernelGGL(decimate3_kernel, grid, dim3(256), 0, st, sig, chunk_off, w.oct_off, w.oct_len, w.ws_oct,
-                         base, taps, kt_.span());
+                         base, taps, NC_CQ_MFMA ? w.xmax : nullptr, kt_.span());
     }
   }
   PeakArgs pa;
@@ -965,6 +1334,34 @@ int launch_chroma_mean(Context& ctx, const float* sig, const int64_t* chunk_off,
     hipLaunchKernelGGL((tuning_select_kernel<NC_TS_NT>), dim3(n), dim3(NC_TS_NT), 0, st, w.peak_pitch, w.peak_mag,
                        w.chunk_npk, w.tf_base, w.tuning_idx, out_tuning, kt_.span());
   }
+#if NC_CQ_MFMA
+  {
+    CqmArgs ma;
+    ma.sig = sig;
+    ma.chunk_off = chunk_off;
+    ma.oct_off = w.oct_off;
+    ma.oct_len = w.oct_len;
+    ma.n_frames = w.n_frames;
+    ma.tuning_idx = w.tuning_idx;
+    ma.ws_oct = w.ws_oct;
+    ma.tf_base = w.tf_base;
+    ma.bfrag = ctx.t.cqm_b;
+    ma.bexp = ctx.t.cqm_bexp;
+    ma.cqt_isl = ctx.t.cqt_inv_sqrt_len;
+    ma.xmax = w.xmax;
+    ma.d3_span = D3_TPW * D3_T;
+    std::copy(ctx.t.cqm_gpow, ctx.t.cqm_gpow + 7, ma.gpow);
+    ma.partial = w.partial;
+    const int ntile = (int)((1 + max_chunk_len / 512 + CM_FR - 1) / CM_FR);
+    {
+      KTimer kt_(ctx, "cqt_chroma", st);
+      ma.span = kt_.span();
+      hipLaunchKernelGGL(cqt_mfma_kernel, dim3(ntile, n), dim3(CM_NTH), cqm_lds_bytes(), st, ma);
+    }
+    hipLaunchKernelGGL(chroma_finalize_kernel, dim3(n), dim3(64), 0, st, w.partial, w.tf_base, w.n_frames, n, CM_FR,
+                       out_chroma);
+  }
+#else
   CqtArgs ca;
   ca.sig = sig;
   ca.chunk_off = chunk_off;
@@ -998,7 +1395,8 @@ int launch_chroma_mean(Context& ctx, const float* sig, const int64_t* chunk_off,
     hipLaunchKernelGGL(cqt_chroma_kernel, dim3((nblk + CQ_BPW - 1) / CQ_BPW, n), dim3(CQ_WAVES * 64), cqt_lds_bytes(), st, ca);
   }
   hipLaunchKernelGGL(chroma_finalize_kernel, dim3(n), dim3(64), 0, st, w.partial, w.tf_base, w.n_frames, n,
-                     out_chroma);
+                     CQ_FR, out_chroma);
+#endif
   NC_HIP(hipGetLastError());
   return 0;
 }

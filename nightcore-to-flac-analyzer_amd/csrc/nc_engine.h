@@ -58,6 +58,12 @@ struct Tables {
   int cqt_klo = 0, cqt_khi = 0; // FFT bins any row touches (over all tunings)
   double* halfband = nullptr;   // 2K+1 taps
   float halfband_f32[2 * kHalfbandK + 1] = {};  // host copy, rounded to f32 (decimate3 kernel argument)
+  // MFMA CQT (cqt_mfma_kernel): the 36 rows as 1024-tap time-domain filters, split into f16
+  // hi + lo at a per-filter power-of-two scale, in 16x16x32 B-fragment order
+  // [tuning][k-step 32][n-tile 5][hi, lo][lane 64] x 8 halves (nc_tables.cpp)
+  uint4* cqm_b = nullptr;
+  int* cqm_bexp = nullptr;      // [kNTunings][36] filter scale exponents
+  float cqm_gpow[7] = {};       // bound of max|octave o| / max|octave 0|: (sqrt(2) sum|h|)^o, rounded up
 };
 
 struct KernelTimers;  // nc_prof.cpp

@@ -362,6 +362,76 @@ void build_tables(Context& ctx) {
     t.cqt_off = upload(coff);
     t.cqt_w = upload(cw);
     t.cqt_inv_sqrt_len = upload(isl);
+
+    // MFMA CQT filters.  librosa's response C_j[t] = sum_b fb[j][b] rfft(frame_t)[b] is linear
+    // in the frame, so it equals sum_n frame_t[n] h_j[n] with the complex 1024-tap filter
+    // h_j[n] = sum_b fb[j][b] exp(-2 pi i b n / 1024) (the sparsified rows make h_j dense over
+    // all 1024 taps, so no tap is dropped).  Columns of the real GEMM: n-tile 0/1 = Re/Im of
+    // rows 0-15, 2/3 = Re/Im of rows 16-31, 4 = Re of rows 32-35 (cols 0-3) and their Im
+    // (cols 4-7), cols 8-15 zero.  Each row is scaled by 2^e_j (max |Re|, |Im| < 2^13) and
+    // split v = hi + lo, hi = f16(v), lo = f16(v - hi): 22 significant bits.
+    constexpr int KS = kCqtNfft / 32, NT = 5;
+    std::vector<std::complex<double>> ex(nfft);
+    for (int m = 0; m < nfft; ++m) ex[m] = std::polar(1.0, -2.0 * M_PI * (double)m / (double)nfft);
+    std::vector<uint4> frag((size_t)kNTunings * KS * NT * 2 * 64);
+    std::vector<int> bexp(kNTunings * nf);
+    std::vector<std::complex<double>> h((size_t)nf * nfft);
+    for (int ti = 0; ti < kNTunings; ++ti) {
+      for (int f = 0; f < nf; ++f) {
+        const int lo = clo[ti * nf + f], len = clen[ti * nf + f], off = coff[ti * nf + f];
+        double mx = 0.0;
+        for (int n = 0; n < nfft; ++n) {
+          std::complex<double> s = 0.0;
+          for (int b = 0; b < len; ++b) {
+            const float2 w = cw[off + b];
+            s += std::complex<double>(w.x, w.y) * ex[((lo + b) * n) & (nfft - 1)];
+          }
+          h[(size_t)f * nfft + n] = s;
+          mx = std::max(mx, std::max(std::fabs(s.real()), std::fabs(s.imag())));
+        }
+        int e = 0;
+        if (mx > 0.0) std::frexp(mx, &e);
+        bexp[ti * nf + f] = 13 - e;
+      }
+      for (int ks = 0; ks < KS; ++ks)
+        for (int nt = 0; nt < NT; ++nt)
+          for (int l = 0; l < 64; ++l) {
+            const int col = l & 15;
+            int f = -1;
+            bool im = false;
+            if (nt < 4) {
+              f = 16 * (nt >> 1) + col;
+              im = nt & 1;
+            } else if (col < 8) {
+              f = 32 + (col & 3);
+              im = col >= 4;
+            }
+            _Float16 hv[8], lv[8];
+            for (int j = 0; j < 8; ++j) {
+              const int n = 32 * ks + 8 * (l >> 4) + j;
+              double v = 0.0;
+              if (f >= 0) {
+                const std::complex<double> z = h[(size_t)f * nfft + n];
+                v = std::ldexp(im ? z.imag() : z.real(), bexp[ti * nf + f]);
+              }
+              hv[j] = (_Float16)v;
+              lv[j] = (_Float16)(v - (double)hv[j]);
+            }
+            const size_t idx = ((((size_t)ti * KS + ks) * NT + nt) * 2) * 64 + l;
+            std::memcpy(&frag[idx], hv, 16);
+            std::memcpy(&frag[idx + 64], lv, 16);
+          }
+    }
+    t.cqm_b = upload(frag);
+    t.cqm_bexp = upload(bexp);
+  }
+  // octave bound: |y_{o+1}| <= sqrt(2) sum|h| max|y_o| (f32 accumulation adds < 1e-6
+  // relative; the factor is rounded up by 1e-4 and the kernel keeps 3 bits of headroom)
+  {
+    double s = 0.0;
+    for (int j = 0; j < 2 * kHalfbandK + 1; ++j) s += std::fabs((double)t.halfband_f32[j]);
+    const double g = std::sqrt(2.0) * s * (1.0 + 1e-4);
+    for (int o = 0; o < 7; ++o) t.cqm_gpow[o] = (float)(std::pow(g, o) * (1.0 + 1e-4));
   }
 }
 
@@ -369,7 +439,8 @@ void free_tables(Context& ctx) {
   Tables& t = ctx.t;
   void* ptrs[] = {t.tw, t.hann2048, t.hann_ac512, t.hann_ac64, t.wsq512, t.wsq64, t.mel_lo,  t.mel_len, t.mel_off,
                   t.mel_w,  t.cqt_lo,   t.cqt_len,    t.cqt_off,  t.cqt_w,   t.cqt_inv_sqrt_len, t.halfband,
-                  t.cqt_plo, t.cqt_plen, t.cqt_partner, t.cqt_pfilt, t.cqt_wcol, t.mel_w4, t.mel_lo4, t.mel_nj4};
+                  t.cqt_plo, t.cqt_plen, t.cqt_partner, t.cqt_pfilt, t.cqt_wcol, t.mel_w4, t.mel_lo4, t.mel_nj4,
+                  t.cqm_b,   t.cqm_bexp};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   t = Tables();
