@@ -568,6 +568,10 @@ struct CqtArgs {
   int pmax;
   int klo, khi;            // FFT bins the rows touch
   double* partial;  // [n][nblk][12]
+  // hybrid mode (gpart non-null): only octaves 0 .. n_oct - 1, whose chroma partial rows go to
+  // gpart[(tf_base[c] + t)][7][12] for cqt_tail_kernel (the MFMA kernel writes the others)
+  float* gpart = nullptr;
+  int n_oct = 7;
   unsigned long long* span = nullptr;  // nc_profile execution span (nc_device.h)
 };
 
@@ -629,11 +633,12 @@ __global__ __launch_bounds__(CQ_WAVES * 64) void cqt_chroma_kernel(CqtArgs a) {
   const int t0 = fb * CQ_FR;
   const int nfr = min(CQ_FR, T - t0);
   const int npair = (nfr + 1) >> 1;
-  const int n_items = npair * 7;
+  const int no = a.n_oct;  // octaves per frame pair (7, or the FFT share in hybrid mode)
+  const int n_items = npair * no;
   // the two frames of item `item` in the stage-1 register layout z[l + 64 r]
   auto load_item = [&](int item, int ln, FftIn<1024>& in) {
-    const int oct = item % 7;
-    const int t = t0 + 2 * (item / 7);
+    const int oct = item % no;
+    const int t = t0 + 2 * (item / no);
     const float* y = oct == 0 ? a.sig + a.chunk_off[c] : a.ws_oct + a.oct_off[c * 7 + oct];
     const int64_t Ly = a.oct_len[c * 7 + oct];
     const int hop = 512 >> oct;
@@ -661,7 +666,7 @@ __global__ __launch_bounds__(CQ_WAVES * 64) void cqt_chroma_kernel(CqtArgs a) {
     // out of the loop into registers (which would spill)
     int ln = lane;
     asm volatile("" : "+v"(ln));
-    const int pr = it / 7, oct = it - 7 * pr;
+    const int pr = it / no, oct = it - no * pr;
     const int fl = 2 * pr;
     if (!NC_CQ_PREFETCH) load_item(it, ln, in);
     // the row's 1/sqrt(len), requested with the samples so its latency hides under the FFT
@@ -782,6 +787,14 @@ __global__ __launch_bounds__(CQ_WAVES * 64) void cqt_chroma_kernel(CqtArgs a) {
   }
   __syncthreads();
   if (NC_CQ_DIAG & 4) continue;
+  if (a.gpart) {  // hybrid: this kernel's octave rows out, the tail runs in cqt_tail_kernel
+    for (int q = tid; q < nfr * no * 12; q += NT) {
+      const int fl = q / (no * 12), r = q - fl * (no * 12), o = r / 12, cc = r - 12 * o;
+      a.gpart[((a.tf_base[c] + t0 + fl) * 7 + (6 - o)) * 12 + cc] = sh_part[fl * CQ_TILE + (6 - o) * 12 + cc];
+    }
+    __syncthreads();  // the slots are reused by the next block's items
+    continue;
+  }
   // chroma c = sum over the 7 octaves (ascending bins) of the octave partials
   for (int q = tid; q < nfr * 12; q += NT) {
     const int fl = q / 12, cc = q - 12 * fl;
@@ -810,6 +823,11 @@ __global__ __launch_bounds__(CQ_WAVES * 64) void cqt_chroma_kernel(CqtArgs a) {
 }
 
 // ------------------------------------------------------------------------------ 4'. CQT on MFMA
+// Hybrid CQT: octaves 0 .. CM_LO - 1 run the FFT kernel above (hop >= 128: frames barely
+// overlap, so a GEMM would re-read every sample 2-8 times from HBM), octaves CM_LO .. 6
+// (hop <= 64) run here on the matrix cores; both write per-(frame, octave) chroma partial
+// rows and cqt_tail_kernel finishes the frames.
+//
 // The CQT response is linear in the frame: C_j[t] = sum_b fb[j][b] rfft(x_t)[b] =
 // sum_n x_t[n] h_j[n] with h_j[n] = sum_b fb[j][b] e^{-2 pi i b n / 1024} (nc_tables.cpp).
 // Per octave that is a real GEMM [frames x 1024] . [1024 x 72] (Re and Im of the 36 rows),
@@ -819,41 +837,32 @@ __global__ __launch_bounds__(CQ_WAVES * 64) void cqt_chroma_kernel(CqtArgs a) {
 // scaled by 2^ex with max|y_o| * 2^ex < 2^13 (max|y_0| from decimate3, bounded per octave by
 // (sqrt(2) sum|h|)^o) and the filters by 2^e_j; C = acc * 2^-(ex + e_j) exactly.
 //
-// One workgroup per (chunk, 64-frame tile), one wave per octave (7 waves): 4 row tiles x 5
-// column tiles x 3 products = 60 MFMA 16x16x32 per k-step of 32 taps, 32 k-steps.  Operands:
-//  * filter slices (one k-step: 10 fragments x 1 KB) stream through a 3-deep LDS ring by
-//    LDS-DMA (global_load_lds), two k-steps ahead;
-//  * octaves >= CM_LO (hop <= 64): the tile's whole span is split once into an LDS image
-//    (f16 hi, lo) that every k-step's fragments read;
-//  * octaves < CM_LO (hop >= 128: little overlap between rows): each k-step's 64 row pieces
-//    (32 samples each) stream through a per-wave 3-deep LDS ring by LDS-DMA, two k-steps
-//    ahead, and are split at use.
-// One raw s_barrier per k-step (no vmcnt drain: the DMA two steps ahead stays in flight).
-// Epilogue as cqt_chroma_kernel: |C| sqrt(sr/my_sr) / sqrt(len) -> octave chroma partials ->
-// the 7 octaves summed per frame -> inf-norm -> f64 sum over the tile's frames.
+// One workgroup per (chunk, 64-frame tile), one wave per octave: 4 row tiles x 5 column
+// tiles x 3 products = 60 MFMA 16x16x32 per k-step of 32 taps, 32 k-steps.  The tile's span
+// (63 hop + 1024 samples) is split once into an LDS image that every k-step's fragments
+// read; the filter slices (one k-step: 10 fragments x 1 KB) stream through a CM_R-deep LDS
+// ring by LDS-DMA, with one raw s_barrier per k-step.  76 KB of LDS: two workgroups per CU,
+// whose k-steps interleave freely.
 #ifndef NC_CQ_MFMA
 #define NC_CQ_MFMA 1
 #endif
-#ifndef NC_CM_DIAG  // diagnosis builds only: 1 global rows fetched once, 2 filter slices fetched once
-#define NC_CM_DIAG 0
-#endif
-#ifndef NC_CM_LO
+#ifndef NC_CM_LO  // first octave on the matrix cores
 #define NC_CM_LO 3
 #endif
-#ifndef NC_CM_FR
-#define NC_CM_FR 64
+#ifndef NC_CM_R  // filter-slice ring depth
+#define NC_CM_R 2
 #endif
-constexpr int CM_FR = NC_CM_FR;                    // frames per workgroup tile
+constexpr int CM_FR = 64;                          // frames per workgroup tile
 constexpr int CM_RT = CM_FR / 16;                  // row tiles per wave
-static_assert(CM_FR == 32 || CM_FR == 64, "tile");
 constexpr int CM_KS = kCqtNfft / 32;               // k-steps of 32 taps
 constexpr int CM_NT = 5;                           // column tiles (72 of 80 columns used)
-constexpr int CM_R = 3;                            // ring depth (filter slices, row pieces)
+constexpr int CM_R = NC_CM_R;
 constexpr int CM_SLICE = CM_NT * 2 * 64;           // uint4 fragments per k-step slice
-constexpr int CM_NTH = 7 * 64;
 constexpr int CM_LO = NC_CM_LO;
-static_assert(CM_LO >= 1 && CM_LO <= 6, "both wave kinds present");
-constexpr int CM_GQ = (CM_NT * 2 + (7 - CM_LO) - 1) / (7 - CM_LO);  // filter DMA pieces per image wave
+constexpr int CM_NW = 7 - CM_LO;                   // waves (octaves) per workgroup
+constexpr int CM_NTH = CM_NW * 64;
+static_assert(CM_LO >= 1 && CM_LO <= 6 && CM_R >= 2, "hybrid split");
+constexpr int CM_GQ = (CM_NT * 2 + CM_NW - 1) / CM_NW;  // filter DMA pieces per wave per slice
 typedef _Float16 cm_half8 __attribute__((ext_vector_type(8)));
 typedef float cm_f4 __attribute__((ext_vector_type(4)));
 typedef unsigned cm_u4 __attribute__((ext_vector_type(4)));
@@ -873,14 +882,12 @@ __host__ __device__ constexpr int cm_img(int o) {  // halves per hi (or lo) imag
 __host__ __device__ constexpr int cm_aoff(int o) {  // byte offset of octave o's image pair
   return o <= CM_LO ? 0 : cm_aoff(o - 1) + 4 * cm_img(o - 1);
 }
-// K-loop LDS: filter ring [CM_R][CM_SLICE] uint4 | row rings [CM_LO][CM_R][CM_FR rows][32] f32 |
-// images.  Epilogue (overlay): octave rows [7][CM_FR][36] f32 | partials [CM_FR][7][12] f32
+// K-loop LDS: filter ring [CM_R][CM_SLICE] uint4 | images.  Epilogue overlay: octave rows
+// [CM_NW][CM_FR][36] f32
 constexpr int CM_BBYTES = CM_R * CM_SLICE * 16;
-constexpr int CM_RBYTES = CM_LO * CM_R * CM_FR * 32 * 4;
-constexpr int CM_KBYTES = CM_BBYTES + CM_RBYTES + cm_aoff(7);
-constexpr int CM_MBYTES = 7 * CM_FR * kCqtFilt * 4;
-constexpr int CM_EBYTES = CM_MBYTES + CM_FR * CQ_TILE * 4;
-size_t cqm_lds_bytes() { return CM_KBYTES > CM_EBYTES ? CM_KBYTES : CM_EBYTES; }
+constexpr int CM_KBYTES = CM_BBYTES + cm_aoff(7);
+constexpr int CM_MBYTES = CM_NW * CM_FR * kCqtFilt * 4;
+size_t cqm_lds_bytes() { return CM_KBYTES > CM_MBYTES ? CM_KBYTES : CM_MBYTES; }
 
 struct CqmArgs {
   const float* sig;
@@ -897,14 +904,14 @@ struct CqmArgs {
   const float* xmax;     // decimate3 workgroup maxima of |level 0| (slot c + oct_off[c][3] / 256 + tile)
   int d3_span;           // level-3 outputs per decimate3 workgroup
   float gpow[7];
-  double* partial;       // [tf_base[c] / CM_FR + c + tile][12]
+  float* gpart;          // [tf_base[c] + t][7][12] octave chroma partial rows
   unsigned long long* span = nullptr;
 };
 
 // One LDS-DMA instruction: 16 bytes per lane from gsrc to lds_dst + 16 lane (lds_dst
 // wave-uniform).  Inline asm rather than __builtin_amdgcn_global_load_lds: the compiler
-// drains vmcnt(0) before any later LDS read when it sees the builtin, which would retire the
-// DMA issued two k-steps ahead every step; the kernel counts its own vmcnt instead.
+// drains vmcnt(0) before any later LDS read when it sees the builtin; the kernel counts its
+// own vmcnt instead.
 __device__ __forceinline__ void cm_dma16(const void* gsrc, const void* lds_dst) {
   unsigned keep;
   asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
@@ -939,13 +946,23 @@ __global__ __launch_bounds__(CM_NTH) void cqt_mfma_kernel(CqmArgs a) {
   if (t0 >= T) return;
   const int nfr = min(CM_FR, T - t0);
   const int tid = threadIdx.x, lane = tid & 63;
-  const int oct = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int oct = CM_LO + wave;
   const int ti = a.tuning_idx[c];
   const uint4* bsrc = a.bfrag + (size_t)ti * (CM_KS * CM_SLICE);
-  const bool img_w = oct >= CM_LO;  // wave-uniform: image wave or row-ring wave
+  // the first two filter slices are in flight while the image is built
+  auto fetch_slice = [&](int ks) {
+#pragma unroll
+    for (int q = 0; q < CM_GQ; ++q) {
+      int i = wave + CM_NW * q;
+      if (i >= CM_NT * 2) i = wave;  // duplicate of this wave's first piece (same bytes, same place)
+      cm_dma16(bsrc + ks * CM_SLICE + i * 64 + lane, sB + (ks % CM_R) * CM_SLICE + i * 64);
+    }
+  };
+  fetch_slice(0);
 
   // this wave's octave: rows t0 .. t0 + 63, row t at sample t hop - 512
-  const float* y = oct == 0 ? a.sig + a.chunk_off[c] : a.ws_oct + a.oct_off[c * 7 + oct];
+  const float* y = a.ws_oct + a.oct_off[c * 7 + oct];
   const int64_t Ly = a.oct_len[c * 7 + oct];
   const int hop = 512 >> oct;
   int ex = 0;
@@ -968,122 +985,57 @@ __global__ __launch_bounds__(CM_NTH) void cqt_mfma_kernel(CqmArgs a) {
   const bool vec = s0 >= 0 && s0 + S <= Ly && (reinterpret_cast<uintptr_t>(y) & 15) == 0;
   const int kq = 8 * (lane >> 4);
 
-  // --- image waves: split the span once
+  // the span, split once (rows past T - 1 read real or zero samples and are discarded)
   constexpr int aoffs[8] = {cm_aoff(0), cm_aoff(1), cm_aoff(2), cm_aoff(3), cm_aoff(4), cm_aoff(5), cm_aoff(6), cm_aoff(7)};
-  const int pad = img_w ? cm_pad(oct) : 0;
-  const int img = img_w ? cm_img(oct) : 0;
-  _Float16* aimg = reinterpret_cast<_Float16*>(smem + CM_BBYTES + CM_RBYTES + (img_w ? aoffs[oct] : 0));
-  if (img_w) {
-    for (int i = lane; i < S / 8; i += 64) {
-      float v[8];
-      if (vec) {
-        const float4 u0 = *reinterpret_cast<const float4*>(y + s0 + 8 * i);
-        const float4 u1 = *reinterpret_cast<const float4*>(y + s0 + 8 * i + 4);
-        v[0] = u0.x; v[1] = u0.y; v[2] = u0.z; v[3] = u0.w;
-        v[4] = u1.x; v[5] = u1.y; v[6] = u1.z; v[7] = u1.w;
-      } else {
+  const int pad = cm_pad(oct);
+  const int img = cm_img(oct);
+  _Float16* aimg = reinterpret_cast<_Float16*>(smem + CM_BBYTES + aoffs[oct]);
+  for (int i = lane; i < S / 8; i += 64) {
+    float v[8];
+    if (vec) {
+      const float4 u0 = *reinterpret_cast<const float4*>(y + s0 + 8 * i);
+      const float4 u1 = *reinterpret_cast<const float4*>(y + s0 + 8 * i + 4);
+      v[0] = u0.x; v[1] = u0.y; v[2] = u0.z; v[3] = u0.w;
+      v[4] = u1.x; v[5] = u1.y; v[6] = u1.z; v[7] = u1.w;
+    } else {
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const int64_t q = s0 + 8 * i + j;
-          v[j] = (q >= 0 && q < Ly) ? y[q] : 0.0f;
-        }
+      for (int j = 0; j < 8; ++j) {
+        const int64_t q = s0 + 8 * i + j;
+        v[j] = (q >= 0 && q < Ly) ? y[q] : 0.0f;
       }
-      cm_half8 h, l;
-      cm_split(v, sx, h, l);
-      const int pos = 8 * i + (8 * i / hop) * pad;
-      *reinterpret_cast<cm_half8*>(aimg + pos) = h;
-      *reinterpret_cast<cm_half8*>(aimg + img + pos) = l;
     }
+    cm_half8 h, l;
+    cm_split(v, sx, h, l);
+    const int pos = 8 * i + (8 * i / hop) * pad;
+    *reinterpret_cast<cm_half8*>(aimg + pos) = h;
+    *reinterpret_cast<cm_half8*>(aimg + img + pos) = l;
   }
-  // image fragment base per row tile (rows past T - 1 read real or zero samples of the span
-  // and are discarded)
   int abase[CM_RT];
 #pragma unroll
   for (int rt = 0; rt < CM_RT; ++rt) abase[rt] = (16 * rt + (lane & 15)) * (hop + pad) + kq + (kq / hop) * pad;
-
-  // --- row-ring waves: slot [CM_FR rows][8 x 16 B], 16-byte piece p of row r stored at
-  // (p ^ ((r >> 1) & 7)): a fragment read's 16 rows hit 16 distinct bank groups.  One DMA
-  // instruction moves rows 8i .. 8i + 7 (lane l: row 8i + l / 8, slot l % 8).
-  float* ring = reinterpret_cast<float*>(smem + CM_BBYTES) + (img_w ? 0 : oct) * (CM_R * CM_FR * 32);
-  const int dr = lane >> 3;  // DMA row within an 8-row group
-  auto fetch_rows = [&](int ks) {
-    float* slot = ring + (ks % CM_R) * (CM_FR * 32);
-    if (vec) {
-#pragma unroll
-      for (int i = 0; i < CM_FR / 8; ++i) {
-        const int r = 8 * i + dr;
-        const int piece = (lane & 7) ^ ((r >> 1) & 7);
-        cm_dma16(y + s0 + (int64_t)r * hop + 32 * ks + 4 * piece, slot + i * 256);
-      }
-    } else {  // edge tiles: guarded loads, written to the same layout
-#pragma unroll
-      for (int i = 0; i < CM_FR / 8; ++i) {
-        const int r = 8 * i + dr;
-        const int piece = (lane & 7) ^ ((r >> 1) & 7);
-        float4 v;
-        const int64_t q = s0 + (int64_t)r * hop + 32 * ks + 4 * piece;
-        v.x = (q >= 0 && q < Ly) ? y[q] : 0.0f;
-        v.y = (q + 1 >= 0 && q + 1 < Ly) ? y[q + 1] : 0.0f;
-        v.z = (q + 2 >= 0 && q + 2 < Ly) ? y[q + 2] : 0.0f;
-        v.w = (q + 3 >= 0 && q + 3 < Ly) ? y[q + 3] : 0.0f;
-        reinterpret_cast<float4*>(slot)[i * 64 + lane] = v;
-      }
-    }
-  };
-  // filter slices: the image waves share the 10 DMA pieces of a slice
-  const int g = oct - CM_LO, ng = 7 - CM_LO;
-  auto fetch_slice = [&](int ks) {
-#pragma unroll
-    for (int q = 0; q < CM_GQ; ++q) {
-      int i = g + ng * q;
-      if (i >= CM_NT * 2) i = g;  // duplicate of this wave's first piece (same bytes, same place)
-      cm_dma16(bsrc + ks * CM_SLICE + i * 64 + lane, sB + (ks % CM_R) * CM_SLICE + i * 64);
-    }
-  };
-  auto fetch = [&](int ks) {
-    if (img_w) fetch_slice(ks);
-    else fetch_rows(ks);
-  };
+  for (int ks = 1; ks < CM_R - 1; ++ks) fetch_slice(ks);
 
   cm_f4 acc[CM_RT][CM_NT];
 #pragma unroll
   for (int rt = 0; rt < CM_RT; ++rt)
 #pragma unroll
     for (int nt = 0; nt < CM_NT; ++nt) acc[rt][nt] = cm_f4{0.f, 0.f, 0.f, 0.f};
-  fetch(0);
-  fetch(1);
 #pragma unroll 1
   for (int ks = 0; ks < CM_KS; ++ks) {
-    // retire this wave's DMA of step ks (the step ks + 1 DMA, issued after it, may stay in
-    // flight); then every wave's: the barrier also ends every read of step ks - 1's slot
-    if (ks + 1 < CM_KS) {
-      if (img_w) __builtin_amdgcn_s_waitcnt(cm_vmcnt(CM_GQ));
-      else __builtin_amdgcn_s_waitcnt(cm_vmcnt(CM_FR / 8));
-    } else {
-      __builtin_amdgcn_s_waitcnt(cm_vmcnt(0));
-    }
-    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): image and edge-row LDS writes
+    // retire this wave's DMA of slice ks (the younger ones may stay in flight); the barrier
+    // makes every wave's pieces visible and ends every read of the slot slice ks + R - 1 reuses
+    if (ks + CM_R - 2 < CM_KS) __builtin_amdgcn_s_waitcnt(cm_vmcnt(CM_GQ * (CM_R - 2)));
+    else __builtin_amdgcn_s_waitcnt(cm_vmcnt(0));
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the image writes (first step)
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
-    if (ks + 2 < CM_KS && !((NC_CM_DIAG & 2) && img_w) && !((NC_CM_DIAG & 1) && !img_w)) fetch(ks + 2);
+    if (ks + CM_R - 1 < CM_KS) fetch_slice(ks + CM_R - 1);
     cm_half8 ah[CM_RT], al[CM_RT];
-    if (img_w) {
-      const int kt = 32 * ks + (32 * ks / hop) * pad;
+    const int kt = 32 * ks + (32 * ks / hop) * pad;
 #pragma unroll
-      for (int rt = 0; rt < CM_RT; ++rt) {
-        ah[rt] = *reinterpret_cast<const cm_half8*>(aimg + abase[rt] + kt);
-        al[rt] = *reinterpret_cast<const cm_half8*>(aimg + img + abase[rt] + kt);
-      }
-    } else {
-      const float4* slot = reinterpret_cast<const float4*>(ring + (ks % CM_R) * (CM_FR * 32));
-#pragma unroll
-      for (int rt = 0; rt < CM_RT; ++rt) {
-        const int r = 16 * rt + (lane & 15);
-        const int p0 = 2 * (lane >> 4), sw = (r >> 1) & 7;
-        const float4 u0 = slot[r * 8 + (p0 ^ sw)], u1 = slot[r * 8 + ((p0 + 1) ^ sw)];
-        const float v[8] = {u0.x, u0.y, u0.z, u0.w, u1.x, u1.y, u1.z, u1.w};
-        cm_split(v, sx, ah[rt], al[rt]);
-      }
+    for (int rt = 0; rt < CM_RT; ++rt) {
+      ah[rt] = *reinterpret_cast<const cm_half8*>(aimg + abase[rt] + kt);
+      al[rt] = *reinterpret_cast<const cm_half8*>(aimg + img + abase[rt] + kt);
     }
     const uint4* sb = sB + (ks % CM_R) * CM_SLICE + lane;
 #pragma unroll
@@ -1098,12 +1050,11 @@ __global__ __launch_bounds__(CM_NTH) void cqt_mfma_kernel(CqmArgs a) {
       }
     }
   }
-  __syncthreads();  // every wave's last ring / image reads done before the epilogue overlay
-  float* sh_part = reinterpret_cast<float*>(smem + CM_MBYTES);  // [CM_FR][7][12]
+  __syncthreads();  // every wave's last ring / image reads done before the rows overlay them
 
-  // |C| per (frame, row) into this wave's [CM_FR][36] region (over the filter stages)
+  // |C| per (frame, row) into this wave's [CM_FR][36] region
+  float* mg = reinterpret_cast<float*>(smem) + wave * (CM_FR * kCqtFilt);
   {
-    float* mg = reinterpret_cast<float*>(smem) + oct * (CM_FR * kCqtFilt);
     const float oscale = (float)(1 << (oct >> 1)) * ((oct & 1) ? 0x1.6a09e6p+0f : 1.0f);
     const float* isl = a.cqt_isl + ti * kCqtBins + (kCqtBins - kCqtFilt * (oct + 1));
     const int* bx = a.bexp + ti * kCqtFilt;
@@ -1123,30 +1074,39 @@ __global__ __launch_bounds__(CM_NTH) void cqt_mfma_kernel(CqmArgs a) {
         if (col < 4) m[32 + col] = hypotf(acc[rt][4][i] * inv2 * oscale, im * inv2 * oscale) * il2;
       }
   }
-  __syncthreads();
+  __builtin_amdgcn_s_waitcnt(0xc07f);  // the wave reads back only its own rows
+  __builtin_amdgcn_wave_barrier();
   // this octave's share of the 12 chroma bins: bins 3c-1, 3c, 3c+1 (mod 36), ascending
-  {
-    const float* mg = reinterpret_cast<const float*>(smem) + oct * (CM_FR * kCqtFilt);
-    for (int q = lane; q < nfr * 12; q += 64) {
-      const int fl = q / 12, cc = q - 12 * fl;
-      const float* m = mg + fl * kCqtFilt;
-      const float p = cc == 0 ? (m[0] + m[1]) + m[35] : (m[3 * cc - 1] + m[3 * cc]) + m[3 * cc + 1];
-      sh_part[fl * CQ_TILE + (6 - oct) * 12 + cc] = p;
-    }
-  }
-  __syncthreads();
-  float* sh_ch = reinterpret_cast<float*>(smem);  // [CM_FR][12] (the octave rows are consumed)
-  float* sh_nv = sh_ch + CM_FR * 12;
-  for (int q = tid; q < nfr * 12; q += CM_NTH) {
+  float* gp = a.gpart + (a.tf_base[c] + t0) * (7 * 12) + (6 - oct) * 12;
+  for (int q = lane; q < nfr * 12; q += 64) {
     const int fl = q / 12, cc = q - 12 * fl;
-    const float* pt = sh_part + fl * CQ_TILE + cc;
+    const float* m = mg + fl * kCqtFilt;
+    gp[fl * (7 * 12) + cc] = cc == 0 ? (m[0] + m[1]) + m[35] : (m[3 * cc - 1] + m[3 * cc]) + m[3 * cc + 1];
+  }
+}
+
+// Per (chunk, 64-frame tile): chroma = the 7 octave partial rows summed (ascending bins),
+// inf-norm per frame, f64 sum over the tile's frames (cqt_chroma_kernel's own tail).
+__global__ __launch_bounds__(256) void cqt_tail_kernel(const float* gpart, const int64_t* tf_base,
+                                                       const int* n_frames, double* partial) {
+  __shared__ float sh_ch[CM_FR * 12], sh_nv[CM_FR * 12];
+  const int c = blockIdx.y;
+  const int T = n_frames[c];
+  const int t0 = blockIdx.x * CM_FR;
+  if (t0 >= T) return;
+  const int nfr = min(CM_FR, T - t0);
+  const int tid = threadIdx.x;
+  const float* gp = gpart + (tf_base[c] + t0) * (7 * 12);
+  for (int q = tid; q < nfr * 12; q += 256) {
+    const int fl = q / 12, cc = q - 12 * fl;
+    const float* pt = gp + fl * (7 * 12) + cc;
     float ch = 0.0f;
 #pragma unroll
     for (int o = 0; o < 7; ++o) ch += pt[12 * o];
     sh_ch[q] = ch;
   }
   __syncthreads();
-  for (int q = tid; q < nfr * 12; q += CM_NTH) {
+  for (int q = tid; q < nfr * 12; q += 256) {
     const int fl = q / 12;
     float mx = 0.0f;
     for (int j = 0; j < 12; ++j) mx = fmaxf(mx, fabsf(sh_ch[fl * 12 + j]));
@@ -1157,7 +1117,7 @@ __global__ __launch_bounds__(CM_NTH) void cqt_mfma_kernel(CqmArgs a) {
   if (tid < 12) {
     double s = 0.0;
     for (int fl = 0; fl < nfr; ++fl) s += (double)sh_nv[fl * 12 + tid];
-    a.partial[(a.tf_base[c] / CM_FR + c + blockIdx.x) * 12 + tid] = s;
+    partial[(tf_base[c] / CM_FR + c + blockIdx.x) * 12 + tid] = s;
   }
 }
 
@@ -1220,6 +1180,7 @@ struct ChromaWs {
   double* partial;
   int* tuning_idx;
   float* xmax;  // decimate3 workgroup maxima of |level 0|
+  float* gpart; // [tuning frame][7][12] octave chroma partial rows (hybrid CQT)
 };
 
 static inline size_t al256(size_t n) { return (n + 255) & ~(size_t)255; }
@@ -1236,6 +1197,7 @@ size_t chroma_ws_bytes(int n, int64_t total_len) {
   b += al256(sizeof(double) * (size_t)(tfr / CQ_FR + n + 1) * 12);
   b += al256(sizeof(int64_t) * (n + 1));
   b += al256(sizeof(float) * (size_t)(n + (total_len + 64 * 7 * (int64_t)n) / 256 + 2));
+  b += al256(sizeof(float) * (size_t)tfr * 84);
   return b + 4096;
 }
 
@@ -1279,6 +1241,7 @@ int launch_chroma_mean(Context& ctx, const float* sig, const int64_t* chunk_off,
   w.partial = reinterpret_cast<double*>(take(sizeof(double) * (size_t)(tfr / CQ_FR + n + 1) * 12));
   int64_t* tp_base = reinterpret_cast<int64_t*>(take(sizeof(int64_t) * (n + 1)));
   w.xmax = reinterpret_cast<float*>(take(sizeof(float) * (size_t)(n + (total_len + 64 * 7 * (int64_t)n) / 256 + 2)));
+  w.gpart = reinterpret_cast<float*>(take(sizeof(float) * (size_t)tfr * 84));
   if (ext) {  // the caller's lists (zeroed counts): the window stage appends to them too
     w.peak_pitch = ext_pitch;
     w.peak_mag = ext_mag;
@@ -1334,34 +1297,6 @@ int launch_chroma_mean(Context& ctx, const float* sig, const int64_t* chunk_off,
     hipLaunchKernelGGL((tuning_select_kernel<NC_TS_NT>), dim3(n), dim3(NC_TS_NT), 0, st, w.peak_pitch, w.peak_mag,
                        w.chunk_npk, w.tf_base, w.tuning_idx, out_tuning, kt_.span());
   }
-#if NC_CQ_MFMA
-  {
-    CqmArgs ma;
-    ma.sig = sig;
-    ma.chunk_off = chunk_off;
-    ma.oct_off = w.oct_off;
-    ma.oct_len = w.oct_len;
-    ma.n_frames = w.n_frames;
-    ma.tuning_idx = w.tuning_idx;
-    ma.ws_oct = w.ws_oct;
-    ma.tf_base = w.tf_base;
-    ma.bfrag = ctx.t.cqm_b;
-    ma.bexp = ctx.t.cqm_bexp;
-    ma.cqt_isl = ctx.t.cqt_inv_sqrt_len;
-    ma.xmax = w.xmax;
-    ma.d3_span = D3_TPW * D3_T;
-    std::copy(ctx.t.cqm_gpow, ctx.t.cqm_gpow + 7, ma.gpow);
-    ma.partial = w.partial;
-    const int ntile = (int)((1 + max_chunk_len / 512 + CM_FR - 1) / CM_FR);
-    {
-      KTimer kt_(ctx, "cqt_chroma", st);
-      ma.span = kt_.span();
-      hipLaunchKernelGGL(cqt_mfma_kernel, dim3(ntile, n), dim3(CM_NTH), cqm_lds_bytes(), st, ma);
-    }
-    hipLaunchKernelGGL(chroma_finalize_kernel, dim3(n), dim3(64), 0, st, w.partial, w.tf_base, w.n_frames, n, CM_FR,
-                       out_chroma);
-  }
-#else
   CqtArgs ca;
   ca.sig = sig;
   ca.chunk_off = chunk_off;
@@ -1388,7 +1323,42 @@ int launch_chroma_mean(Context& ctx, const float* sig, const int64_t* chunk_off,
     return -2;
   }
   ca.partial = w.partial;
+#if NC_CQ_MFMA
+  // hybrid: octaves 0 .. CM_LO - 1 here, the others on the matrix cores, then the frame tail
+  ca.gpart = w.gpart;
+  ca.n_oct = CM_LO;
+#endif
   const int nblk = (int)((1 + max_chunk_len / 512 + CQ_FR - 1) / CQ_FR);
+#if NC_CQ_MFMA
+  CqmArgs ma;
+  ma.sig = sig;
+  ma.chunk_off = chunk_off;
+  ma.oct_off = w.oct_off;
+  ma.oct_len = w.oct_len;
+  ma.n_frames = w.n_frames;
+  ma.tuning_idx = w.tuning_idx;
+  ma.ws_oct = w.ws_oct;
+  ma.tf_base = w.tf_base;
+  ma.bfrag = ctx.t.cqm_b;
+  ma.bexp = ctx.t.cqm_bexp;
+  ma.cqt_isl = ctx.t.cqt_inv_sqrt_len;
+  ma.xmax = w.xmax;
+  ma.d3_span = D3_TPW * D3_T;
+  std::copy(ctx.t.cqm_gpow, ctx.t.cqm_gpow + 7, ma.gpow);
+  ma.gpart = w.gpart;
+  const int ntile = (int)((1 + max_chunk_len / 512 + CM_FR - 1) / CM_FR);
+  {
+    // one span over both CQT kernels (the timed "cqt_chroma" unit: 7 octaves of every chunk)
+    KTimer kt_(ctx, "cqt_chroma", st);
+    ca.span = kt_.span();
+    ma.span = kt_.span();
+    hipLaunchKernelGGL(cqt_chroma_kernel, dim3((nblk + CQ_BPW - 1) / CQ_BPW, n), dim3(CQ_WAVES * 64), cqt_lds_bytes(), st, ca);
+    hipLaunchKernelGGL(cqt_mfma_kernel, dim3(ntile, n), dim3(CM_NTH), cqm_lds_bytes(), st, ma);
+  }
+  hipLaunchKernelGGL(cqt_tail_kernel, dim3(ntile, n), dim3(256), 0, st, w.gpart, w.tf_base, w.n_frames, w.partial);
+  hipLaunchKernelGGL(chroma_finalize_kernel, dim3(n), dim3(64), 0, st, w.partial, w.tf_base, w.n_frames, n, CM_FR,
+                     out_chroma);
+#else
   {
     KTimer kt_(ctx, "cqt_chroma", st);
     ca.span = kt_.span();
