@@ -823,10 +823,12 @@ __global__ __launch_bounds__(CQ_WAVES * 64) void cqt_chroma_kernel(CqtArgs a) {
 }
 
 // ------------------------------------------------------------------------------ 4'. CQT on MFMA
-// Hybrid CQT: octaves 0 .. CM_LO - 1 run the FFT kernel above (hop >= 128: frames barely
-// overlap, so a GEMM would re-read every sample 2-8 times from HBM), octaves CM_LO .. 6
-// (hop <= 64) run here on the matrix cores; both write per-(frame, octave) chroma partial
-// rows and cqt_tail_kernel finishes the frames.
+// Hybrid CQT: octaves 0-2 run the FFT kernel above (hop >= 128: a 64-frame tile's span is
+// 9-33 K samples, too large to hold split in LDS, and streaming rows re-reads every sample
+// 2-8 times from HBM), octaves 3-6 (hop <= 64) run here on the matrix cores; both write
+// per-(frame, octave) chroma partial rows and cqt_tail_kernel finishes the frames.  Octaves
+// 3-6 share one workgroup (a wave each, 76 KB of LDS, two workgroups per CU).  Octave 2 on
+// the matrix cores in a workgroup of its own (NC_CM_SPLIT) measured no faster than its FFT.
 //
 // The CQT response is linear in the frame: C_j[t] = sum_b fb[j][b] rfft(x_t)[b] =
 // sum_n x_t[n] h_j[n] with h_j[n] = sum_b fb[j][b] e^{-2 pi i b n / 1024} (nc_tables.cpp).
@@ -888,6 +890,17 @@ constexpr int CM_BBYTES = CM_R * CM_SLICE * 16;
 constexpr int CM_KBYTES = CM_BBYTES + cm_aoff(7);
 constexpr int CM_MBYTES = CM_NW * CM_FR * kCqtFilt * 4;
 size_t cqm_lds_bytes() { return CM_KBYTES > CM_MBYTES ? CM_KBYTES : CM_MBYTES; }
+// the octave-split workgroup (octave CM_LO - 1, NC_CM_SPLIT waves): filter ring + one image
+#ifndef NC_CM_SPLIT  // waves of an octave CM_LO - 1 workgroup (0: that octave stays on the FFT kernel; per 224
+                     // chunks: 0 -> 879 us, 1 -> 1012, 2 -> 910, 4 -> 888)
+#define NC_CM_SPLIT 0
+#endif
+constexpr int CM_SW = NC_CM_SPLIT;
+constexpr int CM_FFT_OCT = CM_SW ? CM_LO - 1 : CM_LO;  // octaves on the FFT kernel
+size_t cqm_split_lds_bytes() {
+  const size_t k = CM_BBYTES + 4 * (size_t)cm_img(CM_LO - 1), m = (size_t)CM_FR * kCqtFilt * 4;
+  return k > m ? k : m;
+}
 
 struct CqmArgs {
   const float* sig;
@@ -936,7 +949,12 @@ __device__ __forceinline__ void cm_split(const float (&v)[8], float s, cm_half8&
   lo = __builtin_bit_cast(cm_half8, l);
 }
 
-__global__ __launch_bounds__(CM_NTH) void cqt_mfma_kernel(CqmArgs a) {
+// Two workgroup shapes: SPLIT < 0: NW waves, wave w = octave CM_LO + w over all 64 rows;
+// SPLIT = o: NW waves all on octave o, wave w on rows [16 RT w, 16 RT (w + 1)) of one image.
+template <int NW, int RT, int SPLIT>
+__global__ __launch_bounds__(NW * 64) void cqt_mfma_kernel(CqmArgs a) {
+  constexpr int GQ = (CM_NT * 2 + NW - 1) / NW;  // filter DMA pieces per wave per slice
+  static_assert(SPLIT >= 0 ? NW * RT * 16 == CM_FR : (NW == CM_NW && RT == CM_RT), "shape");
   const Span span_(a.span);
   extern __shared__ __attribute__((aligned(16))) char smem[];
   uint4* sB = reinterpret_cast<uint4*>(smem);  // [CM_R][CM_SLICE]
@@ -947,14 +965,15 @@ __global__ __launch_bounds__(CM_NTH) void cqt_mfma_kernel(CqmArgs a) {
   const int nfr = min(CM_FR, T - t0);
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int oct = CM_LO + wave;
+  const int oct = SPLIT >= 0 ? SPLIT : CM_LO + wave;
+  const int row0 = SPLIT >= 0 ? 16 * RT * wave : 0;
   const int ti = a.tuning_idx[c];
   const uint4* bsrc = a.bfrag + (size_t)ti * (CM_KS * CM_SLICE);
   // the first two filter slices are in flight while the image is built
   auto fetch_slice = [&](int ks) {
 #pragma unroll
-    for (int q = 0; q < CM_GQ; ++q) {
-      int i = wave + CM_NW * q;
+    for (int q = 0; q < GQ; ++q) {
+      int i = wave + NW * q;
       if (i >= CM_NT * 2) i = wave;  // duplicate of this wave's first piece (same bytes, same place)
       cm_dma16(bsrc + ks * CM_SLICE + i * 64 + lane, sB + (ks % CM_R) * CM_SLICE + i * 64);
     }
@@ -989,8 +1008,8 @@ __global__ __launch_bounds__(CM_NTH) void cqt_mfma_kernel(CqmArgs a) {
   constexpr int aoffs[8] = {cm_aoff(0), cm_aoff(1), cm_aoff(2), cm_aoff(3), cm_aoff(4), cm_aoff(5), cm_aoff(6), cm_aoff(7)};
   const int pad = cm_pad(oct);
   const int img = cm_img(oct);
-  _Float16* aimg = reinterpret_cast<_Float16*>(smem + CM_BBYTES + aoffs[oct]);
-  for (int i = lane; i < S / 8; i += 64) {
+  _Float16* aimg = reinterpret_cast<_Float16*>(smem + CM_BBYTES + (SPLIT >= 0 ? 0 : aoffs[oct]));
+  for (int i = SPLIT >= 0 ? tid : lane; i < S / 8; i += SPLIT >= 0 ? NW * 64 : 64) {
     float v[8];
     if (vec) {
       const float4 u0 = *reinterpret_cast<const float4*>(y + s0 + 8 * i);
@@ -1010,30 +1029,30 @@ __global__ __launch_bounds__(CM_NTH) void cqt_mfma_kernel(CqmArgs a) {
     *reinterpret_cast<cm_half8*>(aimg + pos) = h;
     *reinterpret_cast<cm_half8*>(aimg + img + pos) = l;
   }
-  int abase[CM_RT];
+  int abase[RT];
 #pragma unroll
-  for (int rt = 0; rt < CM_RT; ++rt) abase[rt] = (16 * rt + (lane & 15)) * (hop + pad) + kq + (kq / hop) * pad;
+  for (int rt = 0; rt < RT; ++rt) abase[rt] = (row0 + 16 * rt + (lane & 15)) * (hop + pad) + kq + (kq / hop) * pad;
   for (int ks = 1; ks < CM_R - 1; ++ks) fetch_slice(ks);
 
-  cm_f4 acc[CM_RT][CM_NT];
+  cm_f4 acc[RT][CM_NT];
 #pragma unroll
-  for (int rt = 0; rt < CM_RT; ++rt)
+  for (int rt = 0; rt < RT; ++rt)
 #pragma unroll
     for (int nt = 0; nt < CM_NT; ++nt) acc[rt][nt] = cm_f4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll 1
   for (int ks = 0; ks < CM_KS; ++ks) {
     // retire this wave's DMA of slice ks (the younger ones may stay in flight); the barrier
     // makes every wave's pieces visible and ends every read of the slot slice ks + R - 1 reuses
-    if (ks + CM_R - 2 < CM_KS) __builtin_amdgcn_s_waitcnt(cm_vmcnt(CM_GQ * (CM_R - 2)));
+    if (ks + CM_R - 2 < CM_KS) __builtin_amdgcn_s_waitcnt(cm_vmcnt(GQ * (CM_R - 2)));
     else __builtin_amdgcn_s_waitcnt(cm_vmcnt(0));
     __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the image writes (first step)
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
     if (ks + CM_R - 1 < CM_KS) fetch_slice(ks + CM_R - 1);
-    cm_half8 ah[CM_RT], al[CM_RT];
+    cm_half8 ah[RT], al[RT];
     const int kt = 32 * ks + (32 * ks / hop) * pad;
 #pragma unroll
-    for (int rt = 0; rt < CM_RT; ++rt) {
+    for (int rt = 0; rt < RT; ++rt) {
       ah[rt] = *reinterpret_cast<const cm_half8*>(aimg + abase[rt] + kt);
       al[rt] = *reinterpret_cast<const cm_half8*>(aimg + img + abase[rt] + kt);
     }
@@ -1043,7 +1062,7 @@ __global__ __launch_bounds__(CM_NTH) void cqt_mfma_kernel(CqmArgs a) {
       const cm_half8 bh = __builtin_bit_cast(cm_half8, sb[(nt * 2) * 64]);
       const cm_half8 bl = __builtin_bit_cast(cm_half8, sb[(nt * 2 + 1) * 64]);
 #pragma unroll
-      for (int rt = 0; rt < CM_RT; ++rt) {
+      for (int rt = 0; rt < RT; ++rt) {
         acc[rt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[rt], bh, acc[rt][nt], 0, 0, 0);
         acc[rt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[rt], bl, acc[rt][nt], 0, 0, 0);
         acc[rt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al[rt], bh, acc[rt][nt], 0, 0, 0);
@@ -1052,8 +1071,8 @@ __global__ __launch_bounds__(CM_NTH) void cqt_mfma_kernel(CqmArgs a) {
   }
   __syncthreads();  // every wave's last ring / image reads done before the rows overlay them
 
-  // |C| per (frame, row) into this wave's [CM_FR][36] region
-  float* mg = reinterpret_cast<float*>(smem) + wave * (CM_FR * kCqtFilt);
+  // |C| per (frame, row) into this wave's [16 RT][36] region
+  float* mg = reinterpret_cast<float*>(smem) + wave * (16 * RT * kCqtFilt);
   {
     const float oscale = (float)(1 << (oct >> 1)) * ((oct & 1) ? 0x1.6a09e6p+0f : 1.0f);
     const float* isl = a.cqt_isl + ti * kCqtBins + (kCqtBins - kCqtFilt * (oct + 1));
@@ -1063,10 +1082,10 @@ __global__ __launch_bounds__(CM_NTH) void cqt_mfma_kernel(CqmArgs a) {
     const float inv2 = ldexpf(1.0f, -(ex + bx[32 + (col & 3)]));
     const float il0 = isl[col], il1 = isl[16 + col], il2 = isl[32 + (col & 3)];
 #pragma unroll
-    for (int rt = 0; rt < CM_RT; ++rt)
+    for (int rt = 0; rt < RT; ++rt)
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        const int fr = 16 * rt + 4 * (lane >> 4) + i;
+        const int fr = 16 * rt + 4 * (lane >> 4) + i;  // row within this wave's rows
         float* m = mg + fr * kCqtFilt;
         m[col] = hypotf(acc[rt][0][i] * inv0 * oscale, acc[rt][1][i] * inv0 * oscale) * il0;
         m[16 + col] = hypotf(acc[rt][2][i] * inv1 * oscale, acc[rt][3][i] * inv1 * oscale) * il1;
@@ -1077,8 +1096,9 @@ __global__ __launch_bounds__(CM_NTH) void cqt_mfma_kernel(CqmArgs a) {
   __builtin_amdgcn_s_waitcnt(0xc07f);  // the wave reads back only its own rows
   __builtin_amdgcn_wave_barrier();
   // this octave's share of the 12 chroma bins: bins 3c-1, 3c, 3c+1 (mod 36), ascending
-  float* gp = a.gpart + (a.tf_base[c] + t0) * (7 * 12) + (6 - oct) * 12;
-  for (int q = lane; q < nfr * 12; q += 64) {
+  float* gp = a.gpart + (a.tf_base[c] + t0 + row0) * (7 * 12) + (6 - oct) * 12;
+  const int nrow = min(16 * RT, nfr - row0);
+  for (int q = lane; q < nrow * 12; q += 64) {
     const int fl = q / 12, cc = q - 12 * fl;
     const float* m = mg + fl * kCqtFilt;
     gp[fl * (7 * 12) + cc] = cc == 0 ? (m[0] + m[1]) + m[35] : (m[3 * cc - 1] + m[3 * cc]) + m[3 * cc + 1];
@@ -1326,7 +1346,7 @@ int launch_chroma_mean(Context& ctx, const float* sig, const int64_t* chunk_off,
 #if NC_CQ_MFMA
   // hybrid: octaves 0 .. CM_LO - 1 here, the others on the matrix cores, then the frame tail
   ca.gpart = w.gpart;
-  ca.n_oct = CM_LO;
+  ca.n_oct = CM_FFT_OCT;
 #endif
   const int nblk = (int)((1 + max_chunk_len / 512 + CQ_FR - 1) / CQ_FR);
 #if NC_CQ_MFMA
@@ -1353,7 +1373,10 @@ int launch_chroma_mean(Context& ctx, const float* sig, const int64_t* chunk_off,
     ca.span = kt_.span();
     ma.span = kt_.span();
     hipLaunchKernelGGL(cqt_chroma_kernel, dim3((nblk + CQ_BPW - 1) / CQ_BPW, n), dim3(CQ_WAVES * 64), cqt_lds_bytes(), st, ca);
-    hipLaunchKernelGGL(cqt_mfma_kernel, dim3(ntile, n), dim3(CM_NTH), cqm_lds_bytes(), st, ma);
+    hipLaunchKernelGGL((cqt_mfma_kernel<CM_NW, CM_RT, -1>), dim3(ntile, n), dim3(CM_NTH), cqm_lds_bytes(), st, ma);
+    if (CM_SW)
+      hipLaunchKernelGGL((cqt_mfma_kernel<(CM_SW ? CM_SW : 1), CM_FR / 16 / (CM_SW ? CM_SW : 1), CM_LO - 1>), dim3(ntile, n),
+                         dim3(64 * CM_SW), cqm_split_lds_bytes(), st, ma);
   }
   hipLaunchKernelGGL(cqt_tail_kernel, dim3(ntile, n), dim3(256), 0, st, w.gpart, w.tf_base, w.n_frames, w.partial);
   hipLaunchKernelGGL(chroma_finalize_kernel, dim3(n), dim3(64), 0, st, w.partial, w.tf_base, w.n_frames, n, CM_FR,
