@@ -42,6 +42,13 @@ VALU_PEAK_TFS = 157.3          # MI355X f32 vector (= f32 MFMA) peak, MI355X_MIC
 #   STFT->mel frame: rFFT 2048 (56 320) + power (3 075) + Slaney mel, ~2 050 taps x 2 (4 100)
 #   -> 63 495; a 10 s window has 431 frames.
 CHUNK_FLOP = 7 * 862 * 30400
+# The hybrid CQT (csrc/cqt.hip): octaves 0-2 on the f32 FFT kernel (3 x 862 x 30 400 per chunk),
+# octaves 3-6 on the f16 matrix cores as a [862 x 1024] . [1024 x 72] GEMM per octave with
+# hi/lo split operands (3 products): 4 x 862 x 1024 x 72 x 2 x 3 per chunk.  Both shares are
+# reported against their own peak over the whole CQT span (each fraction is a lower bound).
+CHUNK_FLOP_FFT = 3 * 862 * 30400
+CHUNK_FLOP_MFMA = 4 * 862 * 1024 * 72 * 2 * 3
+MFMA_F16_PEAK_TFS = 2500.0     # MI355X dense f16/bf16 MFMA peak, MI355X_MICROARCH.md
 WIN_FLOP = 431 * 63495
 # window_tg (csrc/nc_tgcorr.h) per 10 s window: the six lag correlations, 345 lags x 6 x
 # (T + acw = 775) f64 FMAs, plus the normalisers, 431 frames x 344 taps; its own I/O is the
@@ -263,12 +270,23 @@ def main():
         a = alg / (avg_ms * 1e-3) / 1e9
         c = flop / (avg_ms * 1e-3) / 1e12
         cb, cp = compute_roof.get(tag, ("valu_f32", VALU_PEAK_TFS))
-        return {"bound": "hbm", "kernel": tag, "achieved": a, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": a / HBM_PEAK_GBS, "traffic": None, "alg_bytes_per_launch": alg, "avg_launch_ms": avg_ms,
-                "launches_per_step": launches,
-                # the roof that actually binds: VALU, no MFMA on this path
-                "compute": {"bound": cb, "achieved": c, "peak": cp, "unit": "TFLOP/s",
-                            "frac": c / cp, "alg_flop_per_launch": flop}}
+        out = {"bound": "hbm", "kernel": tag, "achieved": a, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+               "frac": a / HBM_PEAK_GBS, "traffic": None, "alg_bytes_per_launch": alg, "avg_launch_ms": avg_ms,
+               "launches_per_step": launches,
+               # the roof that actually binds: VALU / f64 VALU / matrix cores
+               "compute": {"bound": cb, "achieved": c, "peak": cp, "unit": "TFLOP/s",
+                           "frac": c / cp, "alg_flop_per_launch": flop}}
+        if tag == "cqt_chroma":  # hybrid: the FFT share on the f32 VALU, the GEMM share on MFMA
+            shares = {}
+            for name, per_chunk, bound, peak in (("fft_octaves_0_2", CHUNK_FLOP_FFT, "valu_f32", VALU_PEAK_TFS),
+                                                 ("mfma_octaves_3_6", CHUNK_FLOP_MFMA, "mfma_f16", MFMA_F16_PEAK_TFS)):
+                f = table[tag][0] / launches * per_chunk
+                v = f / (avg_ms * 1e-3) / 1e12
+                shares[name] = {"bound": bound, "achieved": v, "peak": peak, "unit": "TFLOP/s", "frac": v / peak,
+                                "alg_flop_per_launch": f}
+            out["compute"] = {"bound": "hybrid (VALU FFT + MFMA GEMM)", "shares": shares,
+                              "note": "each share's flops over the whole CQT span: lower bounds"}
+        return out
 
     # the dominant kernel = the largest total execution time per step among the kernels with a
     # §8d unit (what rocprofv3 --stats ranks first); cqt_chroma (north_star's named target) is
