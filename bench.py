@@ -166,12 +166,20 @@ def main():
     # pairs, their windows split over the ranks (strong scaling)
     pairs = make_pairs(args.pairs, args.seconds, 1000 + (0 if win_mode else rank * args.pairs),
                        max(1, args.workers // max(1, world)))
+    # NC_BENCH_REHEARSE=1: rehearse the N > 1 path on fewer GPUs than ranks (ranks share devices
+    # round-robin; gloo instead of RCCL, which refuses two ranks on one device).  Never used for
+    # a reported number: the line then says so in "data".
+    rehearse = world > 1 and os.environ.get("NC_BENCH_REHEARSE") == "1"
+    dev = local % max(1, torch.cuda.device_count()) if rehearse else local
     if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        torch.cuda.set_device(dev)
+        if rehearse:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
     from nightcore_analyzer import engine as E
 
-    eng = E.get_engine(local)
+    eng = E.get_engine(dev)
     flat = []
     for nc, src in pairs:
         flat += [nc, src]
@@ -229,7 +237,7 @@ def main():
     spans = eng.kernel_spans()
     eng.kernel_profile(False)
     if world > 1:
-        t = torch.tensor([el], dtype=torch.float64, device="cuda")
+        t = torch.tensor([el], dtype=torch.float64, device="cpu" if rehearse else "cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
     step_ms = el / args.steps * 1e3
@@ -497,7 +505,8 @@ def main():
             "scaling": "strong" if win_mode else "weak",
             "vs_baseline": None,
             "dtype": "f32",
-            "data": "synthetic (SURVEY.md §8d chords+clicks+noise, nc = resample_poly(src, 4, 5)), resident in HBM",
+            "data": "synthetic (SURVEY.md §8d chords+clicks+noise, nc = resample_poly(src, 4, 5)), resident in HBM"
+                    + (f"; REHEARSAL: {world} ranks on {torch.cuda.device_count()} GPU(s), gloo" if rehearse else ""),
             "config": {"workload": "config 3: per GPU a batch of 64 x 3-min 22.05 kHz mono pairs; step = "
                                    "pipeline.run analysis of the batch without the hop-64 IBI pass"
                                    + ("; the K steps issued as one pipelined analyze_batches call (batch k+1's "
