@@ -54,6 +54,48 @@ def test_chroma_mean_and_tuning_match_oracle(gpu_ctx, seed):
         np.testing.assert_allclose(got[i], ref_c, rtol=0, atol=2e-5)
 
 
+@pytest.mark.parametrize("scale", [3e-7, 1e-3, 40.0, 3e4])
+def test_chroma_f16_split_scaling_across_amplitudes(gpu_ctx, scale):
+    """Octaves 3-6 run on the f16 matrix cores with hi/lo split operands at a per-chunk
+    power-of-two scale (cqt.hip cqt_mfma_kernel, decimate3's per-tile maxima): the chroma
+    must follow the oracle from quiet (-130 dB) to loud (+90 dB) chunks, and a chunk shorter
+    than one 64-frame tile.  A chunk whose first half is digital silence is checked for scale
+    invariance (power-of-two scaling: the GPU result at scale s equals the one at scale 1 to
+    f32 rounding) and against the oracle at 2e-3 only: its frames at the silence boundary
+    are ill-conditioned (a few edge samples projected on filters whose taps are ~0 there),
+    where any two f32 implementations differ by ~1e-3 in the mean -- the FFT-only build
+    (NC_CQ_MFMA=0) measured 7e-4 .. 1.2e-3 against the oracle on the same chunk."""
+    nc, src = synth.make_pair(30.0, 1007)
+    base = src[:441000].astype(np.float32)
+
+    def run(sc):
+        y = (base * sc).astype(np.float32)
+        half = y.copy()
+        half[:220500] = 0.0
+        sig = np.concatenate([y, half, y[:25000]]).astype(np.float32)
+        chunks = [(0, 441000), (441000, 441000), (882000, 25000)]
+        got, tun, _, _ = _chroma_gpu(gpu_ctx, sig, chunks)
+        return sig, chunks, got, tun
+
+    sig, chunks, got, tun = run(scale)
+    for i, (o, L) in enumerate(chunks):
+        yy = sig[o:o + L]
+        ref_c = ncref.chroma_cqt(yy, 22050, 512, 36, tuning=float(tun[i])).mean(axis=1)
+        tol = 2e-3 if i == 1 else 2e-5
+        np.testing.assert_allclose(got[i], ref_c, rtol=0, atol=tol, err_msg=f"scale {scale} chunk {i}")
+    if scale >= 1e-3:  # far from f32 subnormals
+        _, _, got1, _ = run(1.0)
+        np.testing.assert_allclose(got[1], got1[1], rtol=0, atol=1e-5)
+
+
+def test_chroma_silent_chunk_is_zero(gpu_ctx):
+    """All-zero chunk: decimate3's maximum is 0, the f16 scale stays 2^0 and every chroma is 0
+    (librosa's inf-norm leaves an all-zero frame at zero)."""
+    sig = np.zeros(441000, np.float32)
+    got, _, _, _ = _chroma_gpu(gpu_ctx, sig, [(0, 441000)])
+    assert np.all(got == 0.0)
+
+
 def test_chroma_ragged_chunks_across_decimator_tiles(gpu_ctx):
     """The fused octave chain (cqt.hip decimate3_kernel) owns 2048 level-0 samples per tile:
     chunk lengths one sample either side of a tile edge and at odd offsets (no aligned
