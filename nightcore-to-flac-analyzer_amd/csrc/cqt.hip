@@ -854,7 +854,10 @@ __global__ __launch_bounds__(CQ_WAVES * 64) void cqt_chroma_kernel(CqtArgs a) {
 #ifndef NC_CM_R  // filter-slice ring depth
 #define NC_CM_R 2
 #endif
-constexpr int CM_FR = 64;                          // frames per workgroup tile
+#ifndef NC_CM_FR
+#define NC_CM_FR 64
+#endif
+constexpr int CM_FR = NC_CM_FR;                    // frames per workgroup tile
 constexpr int CM_RT = CM_FR / 16;                  // row tiles per wave
 constexpr int CM_KS = kCqtNfft / 32;               // k-steps of 32 taps
 constexpr int CM_NT = 5;                           // column tiles (72 of 80 columns used)
@@ -929,7 +932,7 @@ __device__ __forceinline__ void cm_dma16(const void* gsrc, const void* lds_dst) 
   unsigned keep;
   asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
                : "=&s"(keep)
-               : "v"(gsrc), "s"(lds_addr(lds_dst))
+               : "v"(gsrc), "s"(__builtin_amdgcn_readfirstlane(lds_addr(lds_dst)))
                : "memory");
 }
 
@@ -1100,6 +1103,194 @@ __global__ __launch_bounds__(NW * 64) void cqt_mfma_kernel(CqmArgs a) {
   const int nrow = min(16 * RT, nfr - row0);
   for (int q = lane; q < nrow * 12; q += 64) {
     const int fl = q / 12, cc = q - 12 * fl;
+    const float* m = mg + fl * kCqtFilt;
+    gp[fl * (7 * 12) + cc] = cc == 0 ? (m[0] + m[1]) + m[35] : (m[3 * cc - 1] + m[3 * cc]) + m[3 * cc + 1];
+  }
+}
+
+// Octaves 0-2 on the matrix cores (NC_CM_LOW).  Their 64-frame spans (9-33 K samples) do
+// not fit LDS as images, but row t + 1 at k-step ks equals row t at k-step ks + G (G = hop /
+// 32): the M = 1024 / hop k-steps {g + G q : q < M} of "group" g read one block of 64 + M - 1
+// row pieces (32 samples each), row r of step q being block row r + q.  The k-steps run group
+// by group, so each sample is fetched once per tile (M = 2, 4, 8 times fewer bytes than
+// streaming rows per k-step).  Blocks arrive by LDS-DMA (raw f32, 16-byte pieces swizzled so
+// a fragment's 16 rows hit distinct bank groups), double buffered (issued at a group's first
+// step, retired at its second: see the wait below), and are split to f16 hi/lo at each
+// fragment read.  Four waves per workgroup: two 64-frame tiles, two waves per tile (32 rows
+// each) sharing its blocks; all four share the filter ring.  57 KB of LDS, two workgroups per
+// CU.  Per 224 chunks (tools/var_bench.py, one session): 816-856 us with octaves 0-2 here
+// against 866 us with them on the FFT kernel (NC_CM_LOW=0).
+#ifndef NC_CM_LOW  // octaves 0 .. NC_CM_LOW - 1 on cqt_mfma_low_kernel (0: on the FFT kernel)
+#define NC_CM_LOW 3
+#endif
+constexpr int CM_LOW = NC_CM_LOW;
+#ifndef NC_CL_DIAG  // diagnosis builds only: 1 every block through registers (no block DMA)
+#define NC_CL_DIAG 0
+#endif
+constexpr int CL_NW = 4;   // waves per workgroup
+constexpr int CL_TPW = 2;  // 64-frame tiles per workgroup (two waves each)
+constexpr int CL_RT = 2;   // row tiles per wave
+template <int OCT>
+struct CmLow {
+  static constexpr int H = 512 >> OCT, G = H / 32, M = 1024 / H, NR = CM_FR + M - 1, NI = (NR + 7) / 8;
+  static constexpr int QB = (NI + 1) / 2;  // block DMA pieces per wave (two waves per tile)
+  static constexpr int BLK = NI * 8 * 32;  // floats per block buffer
+};
+constexpr int CL_GQ = (CM_NT * 2 + CL_NW - 1) / CL_NW;  // filter DMA pieces per wave per slice
+size_t cql_lds_bytes() { return CM_BBYTES + CL_TPW * 2 * CmLow<2>::BLK * 4; }  // octave 2 has the largest block
+
+template <int OCT>
+__global__ __launch_bounds__(CL_NW * 64) void cqt_mfma_low_kernel(CqmArgs a) {
+  using L = CmLow<OCT>;
+  constexpr int H = L::H, G = L::G, M = L::M, NI = L::NI, QB = L::QB;
+  static_assert(G * M == CM_KS && CM_R == 2, "k-step groups; two-slot filter ring");
+  const Span span_(a.span);
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  uint4* sB = reinterpret_cast<uint4*>(smem);  // [2][CM_SLICE]
+  const int c = blockIdx.y;
+  const int T = a.n_frames[c];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int tw = wave >> 1, hw = wave & 1;  // tile of the workgroup, row half of the tile
+  if (blockIdx.x * (CL_TPW * CM_FR) >= T) return;
+  int t0 = (blockIdx.x * CL_TPW + tw) * CM_FR;
+  const bool active = t0 < T;  // an idle tile's waves still share the DMA and the barriers
+  if (!active) t0 = 0;
+  const int ti = a.tuning_idx[c];
+  const uint4* bsrc = a.bfrag + (size_t)ti * (CM_KS * CM_SLICE);
+  float* blk = reinterpret_cast<float*>(smem + CM_BBYTES) + tw * (2 * L::BLK);
+  auto kstep = [](int n) { return n / M + G * (n % M); };  // step n -> k-step (group n / M, shift n % M)
+  auto fetch_slice = [&](int n) {
+#pragma unroll
+    for (int q = 0; q < CL_GQ; ++q) {
+      int i = wave + CL_NW * q;
+      if (i >= CM_NT * 2) i = wave;  // duplicate of this wave's first piece
+      cm_dma16(bsrc + kstep(n) * CM_SLICE + i * 64 + lane, sB + (n & 1) * CM_SLICE + i * 64);
+    }
+  };
+  fetch_slice(0);
+
+  const float* y = OCT == 0 ? a.sig + a.chunk_off[c] : a.ws_oct + a.oct_off[c * 7 + OCT];
+  const int64_t Ly = a.oct_len[c * 7 + OCT];
+  int ex = 0;
+  {
+    const int64_t l3 = a.oct_len[c * 7 + 3];
+    const int ntl = (int)((l3 + a.d3_span - 1) / a.d3_span);
+    const float* xm = a.xmax + c + a.oct_off[c * 7 + 3] / 256;
+    float m0 = 0.0f;
+    for (int i = lane; i < ntl; i += 64) m0 = fmaxf(m0, xm[i]);
+    const float mx = wave_max_u(m0) * a.gpow[OCT];
+    if (mx > 0.0f) {
+      int e;
+      frexpf(mx, &e);
+      ex = min(13 - e, 100);
+    }
+  }
+  const float sx = ldexpf(1.0f, ex);
+  const int64_t s0 = (int64_t)t0 * H - 512;
+  // tile-uniform: both waves of a tile take the same path (their vmcnt bookkeeping agrees)
+  const bool vec = !NC_CL_DIAG && s0 >= 0 && s0 + (int64_t)(CM_FR - 1) * H + kCqtNfft <= Ly &&
+                   (reinterpret_cast<uintptr_t>(y) & 15) == 0;
+  // block g: row R (< NR) holds samples s0 + R H + 32 g + [0, 32), piece p at slot p ^ ((R >> 1) & 7);
+  // the tile's two waves each move half of the NI 8-row DMA groups (QB each, one repeated if odd)
+  const int dr = lane >> 3;
+  auto fetch_block = [&](int g) {
+    float* b = blk + (g & 1) * L::BLK;
+#pragma unroll
+    for (int k = 0; k < QB; ++k) {
+      int i = hw + 2 * k;
+      if (i >= NI) i = hw;
+      const int R = 8 * i + dr;
+      const int p = (lane & 7) ^ ((R >> 1) & 7);
+      if (vec) {
+        const int Rc = min(R, L::NR - 1);  // rows past NR: a valid address, never read
+        cm_dma16(y + s0 + (int64_t)Rc * H + 32 * g + 4 * p, b + i * 256);
+      } else {
+        const int64_t q = s0 + (int64_t)R * H + 32 * g + 4 * p;
+        float4 v;
+        v.x = (q >= 0 && q < Ly) ? y[q] : 0.0f;
+        v.y = (q + 1 >= 0 && q + 1 < Ly) ? y[q + 1] : 0.0f;
+        v.z = (q + 2 >= 0 && q + 2 < Ly) ? y[q + 2] : 0.0f;
+        v.w = (q + 3 >= 0 && q + 3 < Ly) ? y[q + 3] : 0.0f;
+        reinterpret_cast<float4*>(b)[i * 64 + lane] = v;
+      }
+    }
+  };
+  fetch_block(0);
+
+  cm_f4 acc[CL_RT][CM_NT];
+#pragma unroll
+  for (int rt = 0; rt < CL_RT; ++rt)
+#pragma unroll
+    for (int nt = 0; nt < CM_NT; ++nt) acc[rt][nt] = cm_f4{0.f, 0.f, 0.f, 0.f};
+  const int p0 = 2 * (lane >> 4);
+#pragma unroll 1
+  for (int n = 0; n < CM_KS; ++n) {
+    const int g = n / M, q = n - M * g;
+    // retire every DMA of this wave (slice n, and block g + 1 when issued at q == 0).  A counted
+    // vmcnt that leaves the block in flight is NOT safe here: LDS-DMA completions of an L2-hit
+    // slice and an HBM block can come back out of order (measured: run-to-run differences up to
+    // 2e-3 with vmcnt(QB) at q == 1, none with vmcnt(0)), so one step of latency is what
+    // either gets.
+    __builtin_amdgcn_s_waitcnt(cm_vmcnt(0));
+    __builtin_amdgcn_s_waitcnt(0xc07f);
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (n + 1 < CM_KS) fetch_slice(n + 1);         // into the slot step n - 1 read
+    if (q == 0 && g + 1 < G) fetch_block(g + 1);  // into the buffer group g - 1 read
+    const float4* b = reinterpret_cast<const float4*>(blk + (g & 1) * L::BLK);
+    cm_half8 ah[CL_RT], al[CL_RT];
+#pragma unroll
+    for (int rt = 0; rt < CL_RT; ++rt) {
+      const int R = 32 * hw + 16 * rt + (lane & 15) + q;
+      const int sw = (R >> 1) & 7;
+      const float4 u0 = b[R * 8 + (p0 ^ sw)], u1 = b[R * 8 + ((p0 + 1) ^ sw)];
+      const float v[8] = {u0.x, u0.y, u0.z, u0.w, u1.x, u1.y, u1.z, u1.w};
+      cm_split(v, sx, ah[rt], al[rt]);
+    }
+    const uint4* sb = sB + (n & 1) * CM_SLICE + lane;
+#pragma unroll
+    for (int nt = 0; nt < CM_NT; ++nt) {
+      const cm_half8 bh = __builtin_bit_cast(cm_half8, sb[(nt * 2) * 64]);
+      const cm_half8 bl = __builtin_bit_cast(cm_half8, sb[(nt * 2 + 1) * 64]);
+#pragma unroll
+      for (int rt = 0; rt < CL_RT; ++rt) {
+        acc[rt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[rt], bh, acc[rt][nt], 0, 0, 0);
+        acc[rt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[rt], bl, acc[rt][nt], 0, 0, 0);
+        acc[rt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al[rt], bh, acc[rt][nt], 0, 0, 0);
+      }
+    }
+  }
+  __syncthreads();  // the rows overlay the ring and blocks
+  if (!active) return;
+  const int nrow = min(32, T - t0 - 32 * hw);  // this wave's frames
+  if (nrow <= 0) return;
+  float* mg = reinterpret_cast<float*>(smem) + wave * (32 * kCqtFilt);
+  {
+    const float oscale = (float)(1 << (OCT >> 1)) * ((OCT & 1) ? 0x1.6a09e6p+0f : 1.0f);
+    const float* isl = a.cqt_isl + ti * kCqtBins + (kCqtBins - kCqtFilt * (OCT + 1));
+    const int* bx = a.bexp + ti * kCqtFilt;
+    const int col = lane & 15;
+    const float inv0 = ldexpf(1.0f, -(ex + bx[col])), inv1 = ldexpf(1.0f, -(ex + bx[16 + col]));
+    const float inv2 = ldexpf(1.0f, -(ex + bx[32 + (col & 3)]));
+    const float il0 = isl[col], il1 = isl[16 + col], il2 = isl[32 + (col & 3)];
+#pragma unroll
+    for (int rt = 0; rt < CL_RT; ++rt)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int fr = 16 * rt + 4 * (lane >> 4) + i;
+        float* m = mg + fr * kCqtFilt;
+        m[col] = hypotf(acc[rt][0][i] * inv0 * oscale, acc[rt][1][i] * inv0 * oscale) * il0;
+        m[16 + col] = hypotf(acc[rt][2][i] * inv1 * oscale, acc[rt][3][i] * inv1 * oscale) * il1;
+        const float im = __shfl_down(acc[rt][4][i], 4, 16);
+        if (col < 4) m[32 + col] = hypotf(acc[rt][4][i] * inv2 * oscale, im * inv2 * oscale) * il2;
+      }
+  }
+  __builtin_amdgcn_s_waitcnt(0xc07f);
+  __builtin_amdgcn_wave_barrier();
+  float* gp = a.gpart + (a.tf_base[c] + t0 + 32 * hw) * (7 * 12) + (6 - OCT) * 12;
+  for (int qq = lane; qq < nrow * 12; qq += 64) {
+    const int fl = qq / 12, cc = qq - 12 * fl;
     const float* m = mg + fl * kCqtFilt;
     gp[fl * (7 * 12) + cc] = cc == 0 ? (m[0] + m[1]) + m[35] : (m[3 * cc - 1] + m[3 * cc]) + m[3 * cc + 1];
   }
@@ -1346,7 +1537,7 @@ int launch_chroma_mean(Context& ctx, const float* sig, const int64_t* chunk_off,
 #if NC_CQ_MFMA
   // hybrid: octaves 0 .. CM_LO - 1 here, the others on the matrix cores, then the frame tail
   ca.gpart = w.gpart;
-  ca.n_oct = CM_FFT_OCT;
+  ca.n_oct = CM_LOW ? 0 : CM_FFT_OCT;
 #endif
   const int nblk = (int)((1 + max_chunk_len / 512 + CQ_FR - 1) / CQ_FR);
 #if NC_CQ_MFMA
@@ -1372,7 +1563,15 @@ int launch_chroma_mean(Context& ctx, const float* sig, const int64_t* chunk_off,
     KTimer kt_(ctx, "cqt_chroma", st);
     ca.span = kt_.span();
     ma.span = kt_.span();
-    hipLaunchKernelGGL(cqt_chroma_kernel, dim3((nblk + CQ_BPW - 1) / CQ_BPW, n), dim3(CQ_WAVES * 64), cqt_lds_bytes(), st, ca);
+    if (CM_LOW) {
+      static_assert(CM_LOW == 0 || (CM_LOW == CM_LO && CM_SW == 0), "octaves 0 .. CM_LO - 1 on the low kernel");
+      const dim3 lg((unsigned)((ntile + CL_TPW - 1) / CL_TPW), (unsigned)n);
+      hipLaunchKernelGGL((cqt_mfma_low_kernel<0>), lg, dim3(CL_NW * 64), cql_lds_bytes(), st, ma);
+      hipLaunchKernelGGL((cqt_mfma_low_kernel<1>), lg, dim3(CL_NW * 64), cql_lds_bytes(), st, ma);
+      hipLaunchKernelGGL((cqt_mfma_low_kernel<2>), lg, dim3(CL_NW * 64), cql_lds_bytes(), st, ma);
+    } else {
+      hipLaunchKernelGGL(cqt_chroma_kernel, dim3((nblk + CQ_BPW - 1) / CQ_BPW, n), dim3(CQ_WAVES * 64), cqt_lds_bytes(), st, ca);
+    }
     hipLaunchKernelGGL((cqt_mfma_kernel<CM_NW, CM_RT, -1>), dim3(ntile, n), dim3(CM_NTH), cqm_lds_bytes(), st, ma);
     if (CM_SW)
       hipLaunchKernelGGL((cqt_mfma_kernel<(CM_SW ? CM_SW : 1), CM_FR / 16 / (CM_SW ? CM_SW : 1), CM_LO - 1>), dim3(ntile, n),
