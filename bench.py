@@ -37,17 +37,12 @@ WIN_BYTES = 220500 * 4         # algorithmic bytes per 10 s window (SURVEY.md §
 CHUNK_BYTES = 441000 * 4       # algorithmic bytes per 20 s CQT chunk
 VALU_PEAK_TFS = 157.3          # MI355X f32 vector (= f32 MFMA) peak, MI355X_MICROARCH.md
 # Algorithmic FLOPs (a real N-point FFT counted as 2.5 N log2 N):
-#   CQT item (one frame of one octave): rFFT 1024 (25 600) + 36 sparse complex basis rows,
-#   ~600 complex taps x 8 (4 800) -> 30 400; a 20 s chunk has 7 octaves x 862 frames.
 #   STFT->mel frame: rFFT 2048 (56 320) + power (3 075) + Slaney mel, ~2 050 taps x 2 (4 100)
 #   -> 63 495; a 10 s window has 431 frames.
-CHUNK_FLOP = 7 * 862 * 30400
-# The hybrid CQT (csrc/cqt.hip): octaves 0-2 on the f32 FFT kernel (3 x 862 x 30 400 per chunk),
-# octaves 3-6 on the f16 matrix cores as a [862 x 1024] . [1024 x 72] GEMM per octave with
-# hi/lo split operands (3 products): 4 x 862 x 1024 x 72 x 2 x 3 per chunk.  Both shares are
-# reported against their own peak over the whole CQT span (each fraction is a lower bound).
-CHUNK_FLOP_FFT = 3 * 862 * 30400
-CHUNK_FLOP_MFMA = 4 * 862 * 1024 * 72 * 2 * 3
+# The CQT on the matrix cores (csrc/cqt.hip cqt_mfma_kernel + cqt_mfma_low_kernel): per octave
+# a [862 x 1024] . [1024 x 72] GEMM with hi/lo split f16 operands (3 products), 7 octaves:
+# 7 x 862 x 1024 x 72 x 2 x 3 per chunk, against the dense f16 MFMA peak over the CQT span.
+CHUNK_FLOP_MFMA = 7 * 862 * 1024 * 72 * 2 * 3
 MFMA_F16_PEAK_TFS = 2500.0     # MI355X dense f16/bf16 MFMA peak, MI355X_MICROARCH.md
 WIN_FLOP = 431 * 63495
 # window_tg (csrc/nc_tgcorr.h) per 10 s window: the six lag correlations, 345 lags x 6 x
@@ -264,9 +259,10 @@ def main():
     per = {k: (ms / n, n // ksteps) for k, (ms, n) in timers.items()}
 
     # algorithmic bytes / flops per launch = SURVEY.md §8d per-unit figure x units per launch
-    units = {"stft_mel": (win_per_step, WIN_BYTES, WIN_FLOP), "cqt_chroma": (chunks_per_step, CHUNK_BYTES, CHUNK_FLOP)}
+    units = {"stft_mel": (win_per_step, WIN_BYTES, WIN_FLOP),
+             "cqt_chroma": (chunks_per_step, CHUNK_BYTES, CHUNK_FLOP_MFMA)}
     # compute roof per kernel: f32 VALU for the FFT kernels, f64 VALU for the tempogram
-    compute_roof = {"window_tg": ("valu_f64", F64_PEAK_TFS)}
+    compute_roof = {"window_tg": ("valu_f64", F64_PEAK_TFS), "cqt_chroma": ("mfma_f16", MFMA_F16_PEAK_TFS)}
 
     def roof(tag, times, table=None):
         table = table or units
@@ -284,16 +280,6 @@ def main():
                # the roof that actually binds: VALU / f64 VALU / matrix cores
                "compute": {"bound": cb, "achieved": c, "peak": cp, "unit": "TFLOP/s",
                            "frac": c / cp, "alg_flop_per_launch": flop}}
-        if tag == "cqt_chroma":  # hybrid: the FFT share on the f32 VALU, the GEMM share on MFMA
-            shares = {}
-            for name, per_chunk, bound, peak in (("fft_octaves_0_2", CHUNK_FLOP_FFT, "valu_f32", VALU_PEAK_TFS),
-                                                 ("mfma_octaves_3_6", CHUNK_FLOP_MFMA, "mfma_f16", MFMA_F16_PEAK_TFS)):
-                f = table[tag][0] / launches * per_chunk
-                v = f / (avg_ms * 1e-3) / 1e12
-                shares[name] = {"bound": bound, "achieved": v, "peak": peak, "unit": "TFLOP/s", "frac": v / peak,
-                                "alg_flop_per_launch": f}
-            out["compute"] = {"bound": "hybrid (VALU FFT + MFMA GEMM)", "shares": shares,
-                              "note": "each share's flops over the whole CQT span: lower bounds"}
         return out
 
     # the dominant kernel = the largest total execution time per step among the kernels with a

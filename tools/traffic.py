@@ -12,16 +12,18 @@ import sys
 from pathlib import Path
 
 REPO = Path(__file__).resolve().parents[1]
-TAGS = {"cqt_chroma_kernel": "cqt_fft", "cqt_mfma_kernel": "cqt_mfma", "cqt_tail_kernel": "cqt_tail",
+TAGS = {"cqt_chroma_kernel": "cqt_fft", "cqt_mfma_kernel": "cqt_mfma", "cqt_mfma_low_kernel": "cqt_low",
+        "cqt_tail_kernel": "cqt_tail",
         "stft_mel_kernel": "stft_mel", "tuning_peaks_kernel": "tuning_peaks",
         "trim_blocks_kernel": "trim_blocks", "window_tg_kernel": "window_tg", "decimate_kernel": "decimate", "decimate3_kernel": "decimate"}
 # algorithmic bytes per step of the config-3 bench: 3968 windows x 882 000 B,
 # 896 chunks x 1 764 000 B, 64 pairs of 3 969 000 + 3 175 200 samples x 4 B for the trim pass;
 # the octave chain reads levels 0 and 3 and writes levels 1-6 once per 441 000-sample chunk
 # (441 000 + 55 125 read, 220 500 + 110 250 + 55 125 + 27 563 + 13 782 + 6 891 written, f32)
-# the hybrid CQT is three launches per chroma call (FFT octaves 0-2, MFMA octaves 3-6, frame
-# tail): their per-launch bytes are summed into "cqt_chroma", the unit bench.py times
-CQT_PARTS = ("cqt_fft", "cqt_mfma", "cqt_tail")
+# the CQT is several launches per chroma call (octaves 3-6, octaves 0-2 as three launches or
+# the FFT kernel, the frame tail): their bytes per call are summed into "cqt_chroma", the
+# unit bench.py times
+CQT_PARTS = ("cqt_fft", "cqt_low", "cqt_mfma", "cqt_tail")
 ALG_STEP = {"cqt_chroma": 896 * 1764000, "stft_mel": 3968 * 882000, "trim_blocks": 64 * (3969000 + 3175200) * 4,
             "decimate": 896 * 4 * (441000 + 55125 + 220500 + 110250 + 55125 + 27563 + 13782 + 6891)}
 
@@ -62,15 +64,16 @@ def main(out):
             # mean over launches of unequal groups: per-step bytes / launches per step
             k["alg_bytes_per_launch"] = int(ALG_STEP[tag] * calls / len(fetch[tag]))
         kern[tag] = k
-    if all(t in kern for t in CQT_PARTS):
-        parts = [kern[t] for t in CQT_PARTS]
-        k = {"launches": parts[0]["launches"], "parts": list(CQT_PARTS),
-             "fetch_size_kib_raw": round(sum(x["fetch_size_kib_raw"] for x in parts), 2),
-             "write_size_kib": round(sum(x["write_size_kib"] for x in parts), 2),
-             "hbm_bytes_per_launch": sum(x["hbm_bytes_per_launch"] for x in parts),
-             "launches_per_step": parts[0]["launches_per_step"]}
-        if fetch.get("cqt_fft"):
-            k["alg_bytes_per_launch"] = int(ALG_STEP["cqt_chroma"] * calls / len(fetch["cqt_fft"]))
+    present = [t for t in CQT_PARTS if t in kern]
+    if "cqt_tail" in present:
+        n_calls = kern["cqt_tail"]["launches"]  # one tail per chroma call
+        per_call = lambda key: sum(kern[t][key] * kern[t]["launches"] / n_calls for t in present)
+        k = {"launches": n_calls, "parts": present,
+             "fetch_size_kib_raw": round(per_call("fetch_size_kib_raw"), 2),
+             "write_size_kib": round(per_call("write_size_kib"), 2),
+             "hbm_bytes_per_launch": int(per_call("hbm_bytes_per_launch")),
+             "launches_per_step": kern["cqt_tail"]["launches_per_step"],
+             "alg_bytes_per_launch": int(ALG_STEP["cqt_chroma"] * calls / n_calls)}
         kern["cqt_chroma"] = k
     doc = {"workload": "config3-64pairs", "commit": commit, "analyze_calls": calls,
            "command": "tools/pmc_traffic.sh: rocprofv3 --pmc FETCH_SIZE, then a separate --pmc WRITE_SIZE pass, "
