@@ -35,6 +35,12 @@ def report(d: Path) -> None:
                 parts.append(f"ldsconf {100 * v['SQ_LDS_BANK_CONFLICT'] / max(1.0, v['SQ_LDS_IDX_ACTIVE']):4.1f}%")
                 nd = n[(k, "SQ_INSTS_VALU")]
                 parts.append(f"valu/disp {v['SQ_INSTS_VALU'] / nd:.3g} lds/disp {v['SQ_INSTS_LDS'] / nd:.3g}")
+            if v.get("SQ_VALU_MFMA_BUSY_CYCLES", 0.0) > 0 and v.get("GRBM_GUI_ACTIVE", 0.0) > 0:
+                # MFMA pipe busy cycles summed over the chip's 1024 SIMDs, against the dispatches'
+                # GPU-active cycles (MI355X_MICROARCH.md: 16 per 16x16x32 f16 MFMA)
+                nd = n[(k, "SQ_VALU_MFMA_BUSY_CYCLES")]
+                parts.append(f"mfma busy {100 * v['SQ_VALU_MFMA_BUSY_CYCLES'] / (1024 * v['GRBM_GUI_ACTIVE']):4.1f}% "
+                             f"mfma/disp {v.get('SQ_INSTS_MFMA', 0.0) / nd:.4g}")
             for c in ("FETCH_SIZE", "WRITE_SIZE"):
                 if c in v and v[c] > 1e4:
                     parts.append(f"{c} {v[c] / n[(k, c)]:.4g} KiB/disp")
