@@ -1140,7 +1140,7 @@ constexpr int CL_GQ = (CM_NT * 2 + CL_NW - 1) / CL_NW;  // filter DMA pieces per
 size_t cql_lds_bytes() { return CM_BBYTES + CL_TPW * 2 * CmLow<2>::BLK * 4; }  // octave 2 has the largest block
 
 template <int OCT>
-__global__ __launch_bounds__(CL_NW * 64) void cqt_mfma_low_kernel(CqmArgs a) {
+__device__ __forceinline__ void cqt_mfma_low(const CqmArgs& a) {
   using L = CmLow<OCT>;
   constexpr int H = L::H, G = L::G, M = L::M, NI = L::NI, QB = L::QB;
   static_assert(G * M == CM_KS && CM_R == 2, "k-step groups; two-slot filter ring");
@@ -1294,6 +1294,13 @@ __global__ __launch_bounds__(CL_NW * 64) void cqt_mfma_low_kernel(CqmArgs a) {
     const float* m = mg + fl * kCqtFilt;
     gp[fl * (7 * 12) + cc] = cc == 0 ? (m[0] + m[1]) + m[35] : (m[3 * cc - 1] + m[3 * cc]) + m[3 * cc + 1];
   }
+}
+
+// one launch for octaves 0-2 (blockIdx.z = octave), so their workgroups share the machine
+__global__ __launch_bounds__(CL_NW * 64) void cqt_mfma_low_kernel(CqmArgs a) {
+  if (blockIdx.z == 0) cqt_mfma_low<0>(a);
+  else if (blockIdx.z == 1) cqt_mfma_low<1>(a);
+  else cqt_mfma_low<2>(a);
 }
 
 // Per (chunk, 64-frame tile): chroma = the 7 octave partial rows summed (ascending bins),
@@ -1565,10 +1572,8 @@ int launch_chroma_mean(Context& ctx, const float* sig, const int64_t* chunk_off,
     ma.span = kt_.span();
     if (CM_LOW) {
       static_assert(CM_LOW == 0 || (CM_LOW == CM_LO && CM_SW == 0), "octaves 0 .. CM_LO - 1 on the low kernel");
-      const dim3 lg((unsigned)((ntile + CL_TPW - 1) / CL_TPW), (unsigned)n);
-      hipLaunchKernelGGL((cqt_mfma_low_kernel<0>), lg, dim3(CL_NW * 64), cql_lds_bytes(), st, ma);
-      hipLaunchKernelGGL((cqt_mfma_low_kernel<1>), lg, dim3(CL_NW * 64), cql_lds_bytes(), st, ma);
-      hipLaunchKernelGGL((cqt_mfma_low_kernel<2>), lg, dim3(CL_NW * 64), cql_lds_bytes(), st, ma);
+      const dim3 lg((unsigned)((ntile + CL_TPW - 1) / CL_TPW), (unsigned)n, 3u);
+      hipLaunchKernelGGL(cqt_mfma_low_kernel, lg, dim3(CL_NW * 64), cql_lds_bytes(), st, ma);
     } else {
       hipLaunchKernelGGL(cqt_chroma_kernel, dim3((nblk + CQ_BPW - 1) / CQ_BPW, n), dim3(CQ_WAVES * 64), cqt_lds_bytes(), st, ca);
     }
