@@ -88,6 +88,35 @@ def test_chroma_f16_split_scaling_across_amplitudes(gpu_ctx, scale):
         np.testing.assert_allclose(got[1], got1[1], rtol=0, atol=1e-5)
 
 
+def test_chroma_is_deterministic_across_workspace_contents(gpu_ctx):
+    """The CQT kernels stream operands by LDS-DMA with hand-counted waits (cqt.hip): a wait
+    that retires the wrong DMA reads stale LDS and shows up as run-to-run differences (a
+    counted vmcnt over mixed slice/block DMAs did, up to 2e-3).  Same chunks, workspaces
+    pre-filled with different bytes, results must be bit-identical."""
+    nc, src = synth.make_pair(60.0, 1011)
+    sig = np.concatenate([src, nc]).astype(np.float32)
+    chunks = [(i * 441000 // 2, 441000) for i in range(4)] + [(len(src) + 17, 441000), (len(src), 300000)]
+    dev = _dev.device(0)
+    d_sig = _dev.to_dev(sig, dev, np.float32)
+    off = np.array([c[0] for c in chunks], np.int64)
+    ln = np.array([c[1] for c in chunks], np.int64)
+    n = len(chunks)
+    d_off, d_len = _dev.to_dev(off, dev), _dev.to_dev(ln, dev)
+    wsb = gpu_ctx.lib.nc_chroma_workspace_bytes(gpu_ctx.h, n, int(ln.sum()))
+    outs = []
+    for fill in (0x00, 0x7f, 0xff, 0x3c):
+        ws = torch.full((wsb,), fill, dtype=torch.uint8, device=dev)
+        out = torch.full((n * 12,), float("nan"), dtype=torch.float32, device=dev)
+        tun = _dev.empty(n, torch.float32, dev)
+        gpu_ctx.call("nc_chroma_mean", d_sig.data_ptr(), d_off.data_ptr(), d_len.data_ptr(), n, int(ln.sum()),
+                     int(ln.max()), out.data_ptr(), tun.data_ptr(), None, ws.data_ptr(), wsb, _dev.stream_handle())
+        torch.cuda.synchronize()
+        outs.append(out.cpu().numpy())
+    for o in outs[1:]:
+        assert np.array_equal(o, outs[0])
+    assert not np.isnan(outs[0]).any()
+
+
 def test_chroma_silent_chunk_is_zero(gpu_ctx):
     """All-zero chunk: decimate3's maximum is 0, the f16 scale stays 2^0 and every chroma is 0
     (librosa's inf-norm leaves an all-zero frame at zero)."""
