@@ -1130,8 +1130,11 @@ constexpr int CM_LOW = NC_CM_LOW;
 #ifndef NC_CL_DIAG  // diagnosis builds only: 1 every block through registers (no block DMA)
 #define NC_CL_DIAG 0
 #endif
-constexpr int CL_NW = 4;   // waves per workgroup
-constexpr int CL_TPW = 2;  // 64-frame tiles per workgroup (two waves each)
+#ifndef NC_CL_TPW  // 64-frame tiles per workgroup (two waves each)
+#define NC_CL_TPW 2
+#endif
+constexpr int CL_TPW = NC_CL_TPW;
+constexpr int CL_NW = 2 * CL_TPW;  // waves per workgroup
 constexpr int CL_RT = 2;   // row tiles per wave
 template <int OCT>
 struct CmLow {
