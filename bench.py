@@ -363,6 +363,27 @@ def main():
         ibi = {"pairs": 2, "seconds_per_pair": (t_ibi - t_no) / 2, "hop64_frames_per_s": frames / max(1e-9, t_ibi - t_no),
                "ibi_ratio_pair0": o2[0].result.ibi_ratio}
 
+    # BASELINE configs[1]: one 3-min pair, the whole run() with its defaults (hop-64 IBI pass
+    # included), host arrays in: upload + analysis + result assembly, latency per call
+    cfg2 = None
+    if not args.no_config5 and rank == 0 and world == 1:
+        nc2, src2 = pairs[0]
+        for _ in range(2):
+            eng.analyze(signals=eng.upload_signals([nc2, src2]), params=E.Params())
+        torch.cuda.synchronize()
+        reps = 5
+        t1 = time.perf_counter()
+        for _ in range(reps):
+            o2c, = eng.analyze(signals=eng.upload_signals([nc2, src2]), params=E.Params())
+        torch.cuda.synchronize()
+        t2 = (time.perf_counter() - t1) / reps
+        nw2 = int(o2c.detail["energy_src"].size + o2c.detail["energy_nc"].size)
+        cfg2 = {"workload": "config 2: one 3-min pair (host arrays), run() defaults incl. the hop-64 IBI pass; "
+                            "upload + analysis + result assembly per call, 5 calls",
+                "seconds_per_pair": t2, "windows": nw2, "windows_per_s": nw2 / t2,
+                "tempo_ratio": o2c.result.tempo_ratio, "pitch_ratio": o2c.result.pitch_ratio,
+                "ibi_ratio": o2c.result.ibi_ratio}
+
     # BASELINE configs[4]: one 60-min pair, the whole run() incl. the hop-64 IBI pass, plus the
     # waveform xcorr verification search (xcorr.estimate_speed_xcorr) over the same signals
     cfg5 = None
@@ -512,6 +533,8 @@ def main():
             line["upload_included"] = upl
         if ibi is not None:
             line["ibi_pass"] = ibi
+        if cfg2 is not None:
+            line["config2"] = cfg2
         if cfg5 is not None:
             line["config5"] = cfg5
         if spec is not None:
