@@ -418,9 +418,8 @@ class Engine:
         # the chroma chain runs on its own stream, concurrently with the window/tempo chain
         # (NC_SERIAL_STREAMS=1 queues it on the launch stream instead: isolated per-kernel timings)
         # NC_STREAM_PRIO="chroma,tail" sets the two side streams' priorities (torch: lower = more
-        # urgent; the launch stream stays at 0).  Both side streams ahead of the window chain
-        # measured 14.20 ms per bench step against 14.26 at 0,0 (tools/prio_probe.sh, two
-        # alternated reps each: small, but the same sign in both)
+        # urgent; the launch stream stays at 0).  Round 1 measured -1,-1 against 0,0 at 14.20
+        # against 14.26 ms per step: within box-to-box spread, so the default is arbitrary
         prio = [int(v) for v in os.environ.get("NC_STREAM_PRIO", "-1,-1").split(",")]
         self.chroma_stream = torch.cuda.current_stream(self.dev) if os.environ.get("NC_SERIAL_STREAMS") == "1" \
             else torch.cuda.Stream(self.dev, priority=prio[0])
