@@ -893,6 +893,12 @@ __host__ __device__ constexpr int cm_aoff(int o) {  // byte offset of octave o's
 // K-loop LDS: filter ring [CM_R][CM_SLICE] uint4 | images.  Epilogue overlay: octave rows
 // [CM_NW][CM_FR][36] f32
 constexpr int CM_BBYTES = CM_R * CM_SLICE * 16;
+// Image pieces per lane whose loads are issued together (1: one at a time).  One session,
+// cqt_chroma per 224 chunks: 1 / 2 / 4 / 8 -> 751-753 / 739 / 744-745 / 743 us.
+#ifndef NC_CM_IMGU
+#define NC_CM_IMGU 4
+#endif
+constexpr int CM_IMGU = NC_CM_IMGU;
 constexpr int CM_KBYTES = CM_BBYTES + cm_aoff(7);
 constexpr int CM_MBYTES = CM_NW * CM_FR * kCqtFilt * 4;
 size_t cqm_lds_bytes() { return CM_KBYTES > CM_MBYTES ? CM_KBYTES : CM_MBYTES; }
@@ -1015,7 +1021,32 @@ __global__ __launch_bounds__(NW * 64) void cqt_mfma_kernel(CqmArgs a) {
   const int pad = cm_pad(oct);
   const int img = cm_img(oct);
   _Float16* aimg = reinterpret_cast<_Float16*>(smem + CM_BBYTES + (SPLIT >= 0 ? 0 : aoffs[oct]));
-  for (int i = SPLIT >= 0 ? tid : lane; i < S / 8; i += SPLIT >= 0 ? NW * 64 : 64) {
+  const int i0 = SPLIT >= 0 ? tid : lane, di = SPLIT >= 0 ? NW * 64 : 64;
+  int ib = i0;
+  if (CM_IMGU > 1 && vec) {
+    // CM_IMGU pieces per lane loaded before any is split: one load latency per batch instead
+    // of one per piece (the accumulators are not live yet, so the registers are free)
+    for (; ib + (CM_IMGU - 1) * di < S / 8; ib += CM_IMGU * di) {
+      float4 u[CM_IMGU][2];
+#pragma unroll
+      for (int k = 0; k < CM_IMGU; ++k) {
+        const float4* p = reinterpret_cast<const float4*>(y + s0 + 8 * (ib + k * di));
+        u[k][0] = p[0];
+        u[k][1] = p[1];
+      }
+#pragma unroll
+      for (int k = 0; k < CM_IMGU; ++k) {
+        const int i = ib + k * di;
+        const float v[8] = {u[k][0].x, u[k][0].y, u[k][0].z, u[k][0].w, u[k][1].x, u[k][1].y, u[k][1].z, u[k][1].w};
+        cm_half8 h, l;
+        cm_split(v, sx, h, l);
+        const int pos = 8 * i + (8 * i / hop) * pad;
+        *reinterpret_cast<cm_half8*>(aimg + pos) = h;
+        *reinterpret_cast<cm_half8*>(aimg + img + pos) = l;
+      }
+    }
+  }
+  for (int i = ib; i < S / 8; i += di) {
     float v[8];
     if (vec) {
       const float4 u0 = *reinterpret_cast<const float4*>(y + s0 + 8 * i);
