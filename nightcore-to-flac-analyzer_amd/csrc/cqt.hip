@@ -865,6 +865,16 @@ constexpr int CM_RT = CM_FR / 16;                  // row tiles per wave
 constexpr int CM_KS = kCqtNfft / 32;               // k-steps of 32 taps
 constexpr int CM_NT = 5;                           // column tiles (72 of 80 columns used)
 constexpr int CM_R = NC_CM_R;
+// Two tiles per workgroup with a 2 / 3 / 4-slot ring measure 809 / 822 / 812-822 against
+// 753-770 us per 224 chunks: one tile, two slots.
+#ifndef NC_CM_TPB  // 64-frame tiles per octave 3-6 workgroup (CM_NW waves each), sharing one filter ring
+#define NC_CM_TPB 1
+#endif
+constexpr int CM_TPB = NC_CM_TPB;
+#ifndef NC_CM_HR  // filter-slice ring depth of the octave 3-6 kernel
+#define NC_CM_HR NC_CM_R
+#endif
+constexpr int CM_HR = NC_CM_HR;
 constexpr int CM_SLICE = CM_NT * 2 * 64;           // uint4 fragments per k-step slice
 constexpr int CM_LO = NC_CM_LO;
 constexpr int CM_NW = 7 - CM_LO;                   // waves (octaves) per workgroup
@@ -899,8 +909,9 @@ constexpr int CM_BBYTES = CM_R * CM_SLICE * 16;
 #define NC_CM_IMGU 4
 #endif
 constexpr int CM_IMGU = NC_CM_IMGU;
-constexpr int CM_KBYTES = CM_BBYTES + cm_aoff(7);
-constexpr int CM_MBYTES = CM_NW * CM_FR * kCqtFilt * 4;
+constexpr int CM_HBBYTES = CM_HR * CM_SLICE * 16;  // the octave 3-6 kernel's ring
+constexpr int CM_KBYTES = CM_HBBYTES + CM_TPB * cm_aoff(7);
+constexpr int CM_MBYTES = CM_TPB * CM_NW * CM_FR * kCqtFilt * 4;
 size_t cqm_lds_bytes() { return CM_KBYTES > CM_MBYTES ? CM_KBYTES : CM_MBYTES; }
 // the octave-split workgroup (octave CM_LO - 1, NC_CM_SPLIT waves): filter ring + one image
 #ifndef NC_CM_SPLIT  // waves of an octave CM_LO - 1 workgroup (0: that octave stays on the FFT kernel; per 224
@@ -964,20 +975,27 @@ __device__ __forceinline__ void cm_split(const float (&v)[8], float s, cm_half8&
 // Two workgroup shapes: SPLIT < 0: NW waves, wave w = octave CM_LO + w over all 64 rows;
 // SPLIT = o: NW waves all on octave o, wave w on rows [16 RT w, 16 RT (w + 1)) of one image.
 template <int NW, int RT, int SPLIT>
-__global__ __launch_bounds__(NW * 64) void cqt_mfma_kernel(CqmArgs a) {
-  constexpr int GQ = (CM_NT * 2 + NW - 1) / NW;  // filter DMA pieces per wave per slice
+__global__ __launch_bounds__(NW * 64 * (SPLIT >= 0 ? 1 : CM_TPB)) void cqt_mfma_kernel(CqmArgs a) {
+  constexpr int TPB = SPLIT >= 0 ? 1 : CM_TPB;    // tiles per workgroup
+  constexpr int RB = SPLIT >= 0 ? CM_R : CM_HR;    // filter ring slots
+  constexpr int BB = RB * CM_SLICE * 16;
+  constexpr int NWT = NW * TPB;                    // waves per workgroup
+  constexpr int GQ = (CM_NT * 2 + NWT - 1) / NWT;  // filter DMA pieces per wave per slice
   static_assert(SPLIT >= 0 ? NW * RT * 16 == CM_FR : (NW == CM_NW && RT == CM_RT), "shape");
   const Span span_(a.span);
   extern __shared__ __attribute__((aligned(16))) char smem[];
   uint4* sB = reinterpret_cast<uint4*>(smem);  // [CM_R][CM_SLICE]
   const int c = blockIdx.y;
   const int T = a.n_frames[c];
-  const int t0 = blockIdx.x * CM_FR;
-  if (t0 >= T) return;
-  const int nfr = min(CM_FR, T - t0);
+  if (blockIdx.x * (TPB * CM_FR) >= T) return;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int oct = SPLIT >= 0 ? SPLIT : CM_LO + wave;
+  const int tw = wave / NW, wo = wave - NW * tw;  // tile of the workgroup, wave within the tile
+  int t0 = (blockIdx.x * TPB + tw) * CM_FR;
+  const bool active = t0 < T;  // an idle tile's waves still share the DMA and the barriers
+  if (!active) t0 = 0;
+  const int nfr = min(CM_FR, T - t0);
+  const int oct = SPLIT >= 0 ? SPLIT : CM_LO + wo;
   const int row0 = SPLIT >= 0 ? 16 * RT * wave : 0;
   const int ti = a.tuning_idx[c];
   const uint4* bsrc = a.bfrag + (size_t)ti * (CM_KS * CM_SLICE);
@@ -985,9 +1003,9 @@ __global__ __launch_bounds__(NW * 64) void cqt_mfma_kernel(CqmArgs a) {
   auto fetch_slice = [&](int ks) {
 #pragma unroll
     for (int q = 0; q < GQ; ++q) {
-      int i = wave + NW * q;
+      int i = wave + NWT * q;
       if (i >= CM_NT * 2) i = wave;  // duplicate of this wave's first piece (same bytes, same place)
-      cm_dma16(bsrc + ks * CM_SLICE + i * 64 + lane, sB + (ks % CM_R) * CM_SLICE + i * 64);
+      cm_dma16(bsrc + ks * CM_SLICE + i * 64 + lane, sB + (ks % RB) * CM_SLICE + i * 64);
     }
   };
   fetch_slice(0);
@@ -1020,7 +1038,7 @@ __global__ __launch_bounds__(NW * 64) void cqt_mfma_kernel(CqmArgs a) {
   constexpr int aoffs[8] = {cm_aoff(0), cm_aoff(1), cm_aoff(2), cm_aoff(3), cm_aoff(4), cm_aoff(5), cm_aoff(6), cm_aoff(7)};
   const int pad = cm_pad(oct);
   const int img = cm_img(oct);
-  _Float16* aimg = reinterpret_cast<_Float16*>(smem + CM_BBYTES + (SPLIT >= 0 ? 0 : aoffs[oct]));
+  _Float16* aimg = reinterpret_cast<_Float16*>(smem + BB + (SPLIT >= 0 ? 0 : tw * cm_aoff(7) + aoffs[oct]));
   const int i0 = SPLIT >= 0 ? tid : lane, di = SPLIT >= 0 ? NW * 64 : 64;
   int ib = i0;
   if (CM_IMGU > 1 && vec) {
@@ -1069,7 +1087,7 @@ __global__ __launch_bounds__(NW * 64) void cqt_mfma_kernel(CqmArgs a) {
   int abase[RT];
 #pragma unroll
   for (int rt = 0; rt < RT; ++rt) abase[rt] = (row0 + 16 * rt + (lane & 15)) * (hop + pad) + kq + (kq / hop) * pad;
-  for (int ks = 1; ks < CM_R - 1; ++ks) fetch_slice(ks);
+  for (int ks = 1; ks < RB - 1; ++ks) fetch_slice(ks);
 
   cm_f4 acc[RT][CM_NT];
 #pragma unroll
@@ -1080,12 +1098,12 @@ __global__ __launch_bounds__(NW * 64) void cqt_mfma_kernel(CqmArgs a) {
   for (int ks = 0; ks < CM_KS; ++ks) {
     // retire this wave's DMA of slice ks (the younger ones may stay in flight); the barrier
     // makes every wave's pieces visible and ends every read of the slot slice ks + R - 1 reuses
-    if (ks + CM_R - 2 < CM_KS) __builtin_amdgcn_s_waitcnt(cm_vmcnt(GQ * (CM_R - 2)));
+    if (ks + RB - 2 < CM_KS) __builtin_amdgcn_s_waitcnt(cm_vmcnt(GQ * (RB - 2)));
     else __builtin_amdgcn_s_waitcnt(cm_vmcnt(0));
     __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the image writes (first step)
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
-    if (ks + CM_R - 1 < CM_KS) fetch_slice(ks + CM_R - 1);
+    if (ks + RB - 1 < CM_KS) fetch_slice(ks + RB - 1);
     cm_half8 ah[RT], al[RT];
     const int kt = 32 * ks + (32 * ks / hop) * pad;
 #pragma unroll
@@ -1093,7 +1111,7 @@ __global__ __launch_bounds__(NW * 64) void cqt_mfma_kernel(CqmArgs a) {
       ah[rt] = *reinterpret_cast<const cm_half8*>(aimg + abase[rt] + kt);
       al[rt] = *reinterpret_cast<const cm_half8*>(aimg + img + abase[rt] + kt);
     }
-    const uint4* sb = sB + (ks % CM_R) * CM_SLICE + lane;
+    const uint4* sb = sB + (ks % RB) * CM_SLICE + lane;
 #pragma unroll
     for (int nt = 0; nt < CM_NT; ++nt) {
       const cm_half8 bh = __builtin_bit_cast(cm_half8, sb[(nt * 2) * 64]);
@@ -1107,6 +1125,7 @@ __global__ __launch_bounds__(NW * 64) void cqt_mfma_kernel(CqmArgs a) {
     }
   }
   __syncthreads();  // every wave's last ring / image reads done before the rows overlay them
+  if (!active) return;
 
   // |C| per (frame, row) into this wave's [16 RT][36] region
   float* mg = reinterpret_cast<float*>(smem) + wave * (16 * RT * kCqtFilt);
@@ -1616,7 +1635,8 @@ int launch_chroma_mean(Context& ctx, const float* sig, const int64_t* chunk_off,
     } else {
       hipLaunchKernelGGL(cqt_chroma_kernel, dim3((nblk + CQ_BPW - 1) / CQ_BPW, n), dim3(CQ_WAVES * 64), cqt_lds_bytes(), st, ca);
     }
-    hipLaunchKernelGGL((cqt_mfma_kernel<CM_NW, CM_RT, -1>), dim3(ntile, n), dim3(CM_NTH), cqm_lds_bytes(), st, ma);
+    hipLaunchKernelGGL((cqt_mfma_kernel<CM_NW, CM_RT, -1>), dim3((ntile + CM_TPB - 1) / CM_TPB, n),
+                       dim3(CM_NTH * CM_TPB), cqm_lds_bytes(), st, ma);
     if (CM_SW)
       hipLaunchKernelGGL((cqt_mfma_kernel<(CM_SW ? CM_SW : 1), CM_FR / 16 / (CM_SW ? CM_SW : 1), CM_LO - 1>), dim3(ntile, n),
                          dim3(64 * CM_SW), cqm_split_lds_bytes(), st, ma);
