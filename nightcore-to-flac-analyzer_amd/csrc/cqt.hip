@@ -909,6 +909,12 @@ constexpr int CM_BBYTES = CM_R * CM_SLICE * 16;
 #define NC_CM_IMGU 4
 #endif
 constexpr int CM_IMGU = NC_CM_IMGU;
+// 1: the next k-step's A fragments are read during this step's MFMAs: 748-765 against
+// 730-745 us per 224 chunks, so 0.
+#ifndef NC_CM_APF
+#define NC_CM_APF 0
+#endif
+constexpr int CM_APF = NC_CM_APF;
 constexpr int CM_HBBYTES = CM_HR * CM_SLICE * 16;  // the octave 3-6 kernel's ring
 constexpr int CM_KBYTES = CM_HBBYTES + CM_TPB * cm_aoff(7);
 constexpr int CM_MBYTES = CM_TPB * CM_NW * CM_FR * kCqtFilt * 4;
@@ -1094,6 +1100,18 @@ __global__ __launch_bounds__(NW * 64 * (SPLIT >= 0 ? 1 : CM_TPB)) void cqt_mfma_
   for (int rt = 0; rt < RT; ++rt)
 #pragma unroll
     for (int nt = 0; nt < CM_NT; ++nt) acc[rt][nt] = cm_f4{0.f, 0.f, 0.f, 0.f};
+  // A fragments of k-step ks (this wave's own image: written by this wave only, and LDS
+  // operations of one wave complete in order, so no barrier guards them)
+  auto load_a = [&](int ks, cm_half8* h, cm_half8* l) {
+    const int kt = 32 * ks + (32 * ks / hop) * pad;
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt) {
+      h[rt] = *reinterpret_cast<const cm_half8*>(aimg + abase[rt] + kt);
+      l[rt] = *reinterpret_cast<const cm_half8*>(aimg + img + abase[rt] + kt);
+    }
+  };
+  cm_half8 ah[RT], al[RT];
+  if (CM_APF) load_a(0, ah, al);
 #pragma unroll 1
   for (int ks = 0; ks < CM_KS; ++ks) {
     // retire this wave's DMA of slice ks (the younger ones may stay in flight); the barrier
@@ -1104,13 +1122,7 @@ __global__ __launch_bounds__(NW * 64 * (SPLIT >= 0 ? 1 : CM_TPB)) void cqt_mfma_
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
     if (ks + RB - 1 < CM_KS) fetch_slice(ks + RB - 1);
-    cm_half8 ah[RT], al[RT];
-    const int kt = 32 * ks + (32 * ks / hop) * pad;
-#pragma unroll
-    for (int rt = 0; rt < RT; ++rt) {
-      ah[rt] = *reinterpret_cast<const cm_half8*>(aimg + abase[rt] + kt);
-      al[rt] = *reinterpret_cast<const cm_half8*>(aimg + img + abase[rt] + kt);
-    }
+    if (!CM_APF) load_a(ks, ah, al);
     const uint4* sb = sB + (ks % RB) * CM_SLICE + lane;
 #pragma unroll
     for (int nt = 0; nt < CM_NT; ++nt) {
@@ -1123,6 +1135,7 @@ __global__ __launch_bounds__(NW * 64 * (SPLIT >= 0 ? 1 : CM_TPB)) void cqt_mfma_
         acc[rt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al[rt], bh, acc[rt][nt], 0, 0, 0);
       }
     }
+    if (CM_APF && ks + 1 < CM_KS) load_a(ks + 1, ah, al);  // under this step's MFMAs
   }
   __syncthreads();  // every wave's last ring / image reads done before the rows overlay them
   if (!active) return;
