@@ -30,6 +30,12 @@ namespace nc {
 #ifndef NC_SM_WAVES
 #define NC_SM_WAVES 14
 #endif
+// Workgroups per CU in the grid.  2 measures the same alone (585 against 582-591 us per 560
+// windows) but slower in the step (11.44-12.18 against 11.27-11.60 ms, 4 alternating runs):
+// the extra workgroups queue behind the chroma stream's kernels.
+#ifndef NC_SM_GRIDX
+#define NC_SM_GRIDX 1
+#endif
 #ifndef NC_SM_DIAG  // diagnosis variants only: 1 no mel, 2 no sample loads, 4 no S_db stores
 #define NC_SM_DIAG 0
 #endif
@@ -245,7 +251,7 @@ int launch_stft_mel(Context& ctx, const StftMelArgs& args, hipStream_t st) {
     return -2;
   }
   const int64_t n_groups = (a.total_frames + SM_WAVES - 1) / SM_WAVES;
-  const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(n_groups, (int64_t)ctx.num_cu * (lds <= 80 * 1024 ? 2 : 1)));
+  const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(n_groups, (int64_t)ctx.num_cu * NC_SM_GRIDX * (lds <= 80 * 1024 ? 2 : 1)));
   {
     KTimer kt_(ctx, "stft_mel", st);
     a.span = kt_.span();
