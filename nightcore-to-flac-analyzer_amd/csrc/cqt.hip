@@ -915,6 +915,12 @@ constexpr int CM_IMGU = NC_CM_IMGU;
 #define NC_CM_APF 0
 #endif
 constexpr int CM_APF = NC_CM_APF;
+// k-steps of the octave 3-6 kernel per workgroup barrier (needs NC_CM_HR >= 2 x).  2 with a
+// 4-slot ring: 869 us (one workgroup per CU), 780 us with two tiles, against 722-727 us.
+#ifndef NC_CM_KPB
+#define NC_CM_KPB 1
+#endif
+constexpr int CM_KPB = NC_CM_KPB;
 constexpr int CM_HBBYTES = CM_HR * CM_SLICE * 16;  // the octave 3-6 kernel's ring
 constexpr int CM_KBYTES = CM_HBBYTES + CM_TPB * cm_aoff(7);
 constexpr int CM_MBYTES = CM_TPB * CM_NW * CM_FR * kCqtFilt * 4;
@@ -986,6 +992,8 @@ __global__ __launch_bounds__(NW * 64 * (SPLIT >= 0 ? 1 : CM_TPB)) void cqt_mfma_
   constexpr int RB = SPLIT >= 0 ? CM_R : CM_HR;    // filter ring slots
   constexpr int BB = RB * CM_SLICE * 16;
   constexpr int NWT = NW * TPB;                    // waves per workgroup
+  constexpr int KPB = SPLIT >= 0 ? 1 : CM_KPB;     // k-steps per barrier
+  static_assert(RB >= 2 * KPB && CM_KS % KPB == 0, "ring holds two barrier groups");
   constexpr int GQ = (CM_NT * 2 + NWT - 1) / NWT;  // filter DMA pieces per wave per slice
   static_assert(SPLIT >= 0 ? NW * RT * 16 == CM_FR : (NW == CM_NW && RT == CM_RT), "shape");
   const Span span_(a.span);
@@ -1093,7 +1101,7 @@ __global__ __launch_bounds__(NW * 64 * (SPLIT >= 0 ? 1 : CM_TPB)) void cqt_mfma_
   int abase[RT];
 #pragma unroll
   for (int rt = 0; rt < RT; ++rt) abase[rt] = (row0 + 16 * rt + (lane & 15)) * (hop + pad) + kq + (kq / hop) * pad;
-  for (int ks = 1; ks < RB - 1; ++ks) fetch_slice(ks);
+  for (int ks = 1; ks < RB - KPB; ++ks) fetch_slice(ks);
 
   cm_f4 acc[RT][CM_NT];
 #pragma unroll
@@ -1112,16 +1120,7 @@ __global__ __launch_bounds__(NW * 64 * (SPLIT >= 0 ? 1 : CM_TPB)) void cqt_mfma_
   };
   cm_half8 ah[RT], al[RT];
   if (CM_APF) load_a(0, ah, al);
-#pragma unroll 1
-  for (int ks = 0; ks < CM_KS; ++ks) {
-    // retire this wave's DMA of slice ks (the younger ones may stay in flight); the barrier
-    // makes every wave's pieces visible and ends every read of the slot slice ks + R - 1 reuses
-    if (ks + RB - 2 < CM_KS) __builtin_amdgcn_s_waitcnt(cm_vmcnt(GQ * (RB - 2)));
-    else __builtin_amdgcn_s_waitcnt(cm_vmcnt(0));
-    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the image writes (first step)
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-    if (ks + RB - 1 < CM_KS) fetch_slice(ks + RB - 1);
+  auto do_step = [&](int ks) {
     if (!CM_APF) load_a(ks, ah, al);
     const uint4* sb = sB + (ks % RB) * CM_SLICE + lane;
 #pragma unroll
@@ -1136,6 +1135,22 @@ __global__ __launch_bounds__(NW * 64 * (SPLIT >= 0 ? 1 : CM_TPB)) void cqt_mfma_
       }
     }
     if (CM_APF && ks + 1 < CM_KS) load_a(ks + 1, ah, al);  // under this step's MFMAs
+  };
+#pragma unroll 1
+  for (int ks = 0; ks < CM_KS; ks += KPB) {
+    // retire this wave's DMA of slices ks .. ks + KPB - 1 (the younger ones may stay in
+    // flight); the barrier makes every wave's pieces visible and ends every read of the slots
+    // the next KPB slices reuse
+    if (ks + RB - KPB - 1 < CM_KS) __builtin_amdgcn_s_waitcnt(cm_vmcnt(GQ * (RB - 2 * KPB)));
+    else __builtin_amdgcn_s_waitcnt(cm_vmcnt(0));
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the image writes (first step)
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+#pragma unroll
+    for (int j = 0; j < KPB; ++j)
+      if (ks + RB - KPB + j < CM_KS) fetch_slice(ks + RB - KPB + j);
+#pragma unroll
+    for (int j = 0; j < KPB; ++j) do_step(ks + j);
   }
   __syncthreads();  // every wave's last ring / image reads done before the rows overlay them
   if (!active) return;
