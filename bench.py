@@ -11,9 +11,15 @@ per window, nc tempo prior, 20 s-chunk CQT chroma (14 per pair) + lag,
 tempo/pitch bootstraps, result assembly.  The hop-64 IBI pass is not part of
 the windows/sec metric and is reported beside it.
 
-N > 1: one process per GPU (torch.distributed.run), each rank owns its own 64
-pairs (pairs are independent objects: no data-path collective; weak scaling);
-barrier + synchronize around the K timed steps, max elapsed over ranks.
+N > 1 (BASELINE config 4 at N = 8): one process per GPU (torch.distributed.run); the
+batch is 64 pairs per GPU and its 10 s windows and 20 s chunk pairs are split over the
+ranks in pair-major blocks (nightcore_analyzer.sharded, north_star's window split; weak
+scaling).  A rank makes and uploads only the pairs its block touches; pairs cut by a
+block boundary exchange their per-window and chunk-pair records (RCCL all-gathers).
+With 64 equal pairs per rank the blocks fall on pair boundaries, so the headline has no
+cut pair; the line also times whole pairs per rank ("pairs") and the same split with every
+boundary moved half a pair ("windows_split": N - 1 cut pairs, both exchanges per step).
+Barrier + synchronize around the K timed steps, max elapsed over ranks.
 
     python bench.py [--gpus N] [--steps K] [--warmup W]
 """
@@ -62,6 +68,17 @@ def _gen(args):
 def make_pairs(n, seconds, base_seed, workers):
     with ProcessPoolExecutor(max_workers=workers) as ex:
         return list(ex.map(_gen, [(seconds, base_seed + i) for i in range(n)]))
+
+
+def make_pairs_ids(ids, seconds, base_seed, workers):
+    """The synthetic pairs with global indices `ids` (seed base_seed + index)."""
+    with ProcessPoolExecutor(max_workers=workers) as ex:
+        return list(ex.map(_gen, [(seconds, base_seed + i) for i in ids]))
+
+
+def synth_lengths(seconds):
+    from nightcore_analyzer import synth
+    return synth.pair_lengths(seconds)
 
 
 def _pmc_traffic(kernel_tag):
@@ -144,9 +161,10 @@ def main():
     ap.add_argument("--no-upload", action="store_true", help="skip the upload-included throughput")
     ap.add_argument("--no-pipeline", action="store_true",
                     help="time K separate analyze calls instead of one pipelined analyze_batches call")
-    ap.add_argument("--shard", choices=("pairs", "windows"), default="pairs",
-                    help="N > 1: whole pairs per rank (default), or every pair's windows split over the ranks "
-                         "(nightcore_analyzer.sharded; not yet measured on multi-GPU hardware)")
+    ap.add_argument("--shard", choices=("pairs", "windows"), default="windows",
+                    help="N > 1: the batch's windows and chunk pairs split over the ranks (default; "
+                         "nightcore_analyzer.sharded, BASELINE config 4), or whole pairs per rank; the other mode "
+                         "and the split-boundary variant are timed beside the headline")
     ap.add_argument("--workers", type=int, default=min(16, os.cpu_count() or 1))
     args = ap.parse_args()
 
@@ -155,12 +173,17 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    # the synthetic pairs are made (forked workers) before this process touches the GPU
-    win_mode = args.shard == "windows"
-    # pair mode: each rank its own pairs (weak scaling); window mode: every rank the same
-    # pairs, their windows split over the ranks (strong scaling)
-    pairs = make_pairs(args.pairs, args.seconds, 1000 + (0 if win_mode else rank * args.pairs),
-                       max(1, args.workers // max(1, world)))
+    # the synthetic pairs are made (forked workers) before this process touches the GPU.
+    # N > 1, window mode (BASELINE config 4, the default there): the batch is all ranks'
+    # pairs (64 per GPU, seeds 1000 + global pair index) and its items (windows, chunk pairs)
+    # are split over the ranks by sharded.shard_plan; a rank makes and uploads only the pairs
+    # its blocks touch (its own 64, plus the neighbour pairs the split-boundary variant cuts).
+    # Pair mode: each rank its own 64 pairs (weak scaling, no exchange).
+    win_mode = world > 1 and args.shard != "pairs"
+    P = args.pairs
+    own_ids = list(range(rank * P, (rank + 1) * P))
+    ids = sorted(set(own_ids) | ({rank * P - 1, (rank + 1) * P} & set(range(world * P)) if win_mode else set()))
+    pairs = dict(zip(ids, make_pairs_ids(ids, args.seconds, 1000, max(1, args.workers // max(1, world)))))
     # NC_BENCH_REHEARSE=1: rehearse the N > 1 path on fewer GPUs than ranks (ranks share devices
     # round-robin; gloo instead of RCCL, which refuses two ranks on one device).  Never used for
     # a reported number: the line then says so in "data".
@@ -176,21 +199,44 @@ def main():
 
     eng = E.get_engine(dev)
     flat = []
-    for nc, src in pairs:
-        flat += [nc, src]
+    for b in ids:
+        flat += list(pairs[b])
     signals = eng.upload_signals(flat)           # resident in HBM before timing
+    sel = np.array([f for j, b in enumerate(ids) if b in set(own_ids) for f in (2 * j, 2 * j + 1)], np.int64)
+    own = E.DeviceSignals(signals.buf, signals.off[sel], signals.length[sel])
     torch.cuda.synchronize()
     params = E.Params(compute_ibi=False)
 
-    if win_mode:
-        from nightcore_analyzer.sharded import DeviceStages, analyze_sharded
-        stages = DeviceStages(eng, signals)
+    def step():
+        return eng.analyze(signals=own, params=params)
 
-        def step():
-            return analyze_sharded(stages, params)
-    else:
-        def step():
-            return eng.analyze(signals=signals, params=params)
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
+    def max_over_ranks(v):
+        if world == 1:
+            return v
+        t = torch.tensor([v], dtype=torch.float64, device="cpu" if rehearse else "cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
+
+    def sum_over_ranks(v):
+        if world == 1:
+            return v
+        t = torch.tensor([float(v)], dtype=torch.float64, device="cpu" if rehearse else "cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+        return float(t.item())
+
+    lengths = [n for _ in range(world * P) for n in synth_lengths(args.seconds)]
+
+    def run_windows(k, split_offset=0.0):
+        """k steps of the window-sharded analysis (interior groups pipelined across steps)."""
+        from nightcore_analyzer.sharded import DeviceStages, analyze_sharded
+        res = analyze_sharded(DeviceStages(eng, signals), params, lengths=lengths, local_pairs=ids,
+                              split_offset=split_offset, gather=False, steps=k)
+        return [res] if k == 1 else res
+
     outs = step()
     bad = [i for i, o in enumerate(outs) if o.error is not None]
     if bad:
@@ -201,41 +247,78 @@ def main():
     pr = outs[0].result.pitch_ratio
     for _ in range(max(0, args.warmup - 1)):
         step()
+    if win_mode:
+        for off in (0.0, 0.5):
+            run_windows(max(1, args.warmup), off)
 
     # timed region: K steps with the kernels' own execution spans recorded (nc_profile mode 2:
     # two fire-and-forget atomics per wave, no host work per launch), so the per-kernel
     # durations below come from exactly the launches the headline number times
     eng.kernel_profile(2)
-    if world > 1:
-        dist.barrier()
+    barrier()
     torch.cuda.synchronize()
     # pair mode: the K steps are K complete analyses of the batch, issued as one pipelined
     # Engine.analyze_batches call (batch k + 1's trims and first groups are queued while batch
     # k's last groups run: no device idle at a batch's start-up); --no-pipeline times K
-    # separate analyze calls (reported beside it as single_call_ms_per_step)
-    pipelined = not win_mode and not args.no_pipeline
+    # separate analyze calls (reported beside it as single_call_ms_per_step).  Window mode:
+    # one analyze_sharded call of K steps (its interior groups pipelined the same way)
+    pipelined = not args.no_pipeline
     t0 = time.perf_counter()
-    if pipelined:
-        res = eng.analyze_batches([signals] * args.steps, params)
+    if win_mode:
+        res = run_windows(args.steps)
+    elif pipelined:
+        res = eng.analyze_batches([own] * args.steps, params)
     else:
         for _ in range(args.steps):
             step()
     torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
+    barrier()
     el = time.perf_counter() - t0
-    if pipelined:
+    if win_mode:
+        mine = [o for _, o in res[0]]
+        if any(o.error is not None for o in mine) or any(len(r) != len(res[0]) for r in res):
+            raise RuntimeError("a window-sharded step failed or returned an incomplete result")
+        win_total = sum_over_ranks(sum(o.detail["energy_src"].size + o.detail["energy_nc"].size for o in mine))
+        if rank == 0 and (mine[0].result.tempo_ratio != tr or mine[0].result.pitch_ratio != pr):
+            raise RuntimeError("the window-sharded result of pair 0 differs from the single-GPU engine's")
+    elif pipelined:
         if len(res) != args.steps or any(len(r) != len(outs) for r in res):
             raise RuntimeError("analyze_batches returned an incomplete result")
         if any(r[0].result.tempo_ratio != tr or r[0].result.pitch_ratio != pr for r in res):
             raise RuntimeError("a pipelined batch differs from the single-call result")
     spans = eng.kernel_spans()
     eng.kernel_profile(False)
-    if world > 1:
-        t = torch.tensor([el], dtype=torch.float64, device="cpu" if rehearse else "cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        el = float(t.item())
+    el = max_over_ranks(el)
     step_ms = el / args.steps * 1e3
+    value = (win_total if win_mode else world * win_per_step) * args.steps / el
+
+    # N > 1: the other modes beside the headline, K steps each, same clock
+    modes = None
+    if world > 1:
+        modes = {}
+        variants = [("pairs", None), ("windows_split", 0.5)] if win_mode else [("windows", 0.0),
+                                                                                ("windows_split", 0.5)]
+        for name, off in variants:
+            barrier()
+            torch.cuda.synchronize()
+            t1 = time.perf_counter()
+            if off is None:
+                eng.analyze_batches([own] * args.steps, params)
+                n_win = world * win_per_step
+            else:
+                r_ = run_windows(args.steps, off)
+                n_win = sum_over_ranks(sum(o.detail["energy_src"].size + o.detail["energy_nc"].size
+                                           for _, o in r_[0]))
+            torch.cuda.synchronize()
+            barrier()
+            e1 = max_over_ranks(time.perf_counter() - t1)
+            modes[name] = {"value": n_win * args.steps / e1, "ms_per_step": e1 / args.steps * 1e3}
+        from nightcore_analyzer.sharded import shard_plan
+        sp = shard_plan(lengths, params, world, 0.5)
+        modes["windows_split"].update(split_pairs=int(sp.split.sum()),
+                                      exchanged_rows_per_step=2 * sp.n_wrows + sp.n_crows,
+                                      how="every inner block boundary moved half a pair (split_offset 0.5): the "
+                                          "cut pairs' window and chunk-pair records all-gathered (C1a, C1b)")
     # {kernel: (average launch ms, launches per step)} from the spans of the timed region
     kper = {k: (ms / n, n / args.steps) for k, (ms, n) in spans.items()}
 
@@ -312,7 +395,7 @@ def main():
     # upload included: the same K steps with every step's 64 pairs copied host -> HBM from
     # pinned memory on a copy stream, double-buffered (step j + 1 uploads while step j runs)
     upl = None
-    if not args.no_upload and not win_mode:
+    if not args.no_upload and world == 1:
         host = signals.buf.cpu().pin_memory()
         bufs = [signals.buf, torch.empty_like(signals.buf)]
         cs = torch.cuda.Stream(eng.dev)
@@ -330,7 +413,7 @@ def main():
             if j + 1 < n_up:
                 upload(j + 1)
             torch.cuda.current_stream(eng.dev).wait_event(evs[j % 2])
-            eng.analyze(signals=E.DeviceSignals(bufs[j % 2], signals.off, signals.length), params=params)
+            eng.analyze(signals=E.DeviceSignals(bufs[j % 2], own.off, own.length), params=params)
         torch.cuda.synchronize()
         t_up = time.perf_counter() - t1
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -348,7 +431,7 @@ def main():
 
     ibi = None
     if not args.no_ibi and rank == 0:
-        sub = E.DeviceSignals(signals.buf, signals.off[:4], signals.length[:4])
+        sub = E.DeviceSignals(own.buf, own.off[:4], own.length[:4])
         eng.analyze(signals=sub, params=E.Params(compute_ibi=True))
         torch.cuda.synchronize()
         t1 = time.perf_counter()
@@ -367,7 +450,7 @@ def main():
     # included), host arrays in: upload + analysis + result assembly, latency per call
     cfg2 = None
     if not args.no_config5 and rank == 0 and world == 1:
-        nc2, src2 = pairs[0]
+        nc2, src2 = pairs[own_ids[0]]
         for _ in range(2):
             eng.analyze(signals=eng.upload_signals([nc2, src2]), params=E.Params())
         torch.cuda.synchronize()
@@ -399,10 +482,10 @@ def main():
         torch.cuda.synchronize()
         t_run = time.perf_counter() - t1
         t1 = time.perf_counter()
-        xr = X.estimate_speed_xcorr_arrays(src5, src5)
+        xr = X.estimate_speed_xcorr_arrays(src5, nc5)
         t_x = time.perf_counter() - t1
         cfg5 = {"workload": "config 5: one 60-min pair (src 3600 s, nc = resample_poly(src, 4, 5)), run() with "
-                            "the hop-64 IBI pass; xcorr search src vs src (host upload included)",
+                            "the hop-64 IBI pass; xcorr search src vs nc (host upload included)",
                 "seconds_run": t_run, "seconds_xcorr": t_x,
                 "hop64_frames": int((1 + len(nc5) // 64) + (1 + len(src5) // 64)),
                 "windows": int(o5.detail["energy_src"].size + o5.detail["energy_nc"].size),
@@ -412,28 +495,28 @@ def main():
     # call (spectral.py:52-94); per-kernel HIP events on the launch stream, the oracle beside it
     spec = None
     if not args.no_spectral and rank == 0:
-        srs = [22050] * signals.n_files
-        ev, h, keep = eng.spectral_frames(signals.buf, signals.off, signals.length, srs)
+        srs = [22050] * own.n_files
+        ev, h, keep = eng.spectral_frames(own.buf, own.off, own.length, srs)
         ev.synchronize()
         reps = 3
         torch.cuda.synchronize()
         t1 = time.perf_counter()
         for _ in range(reps):
-            ev, h, keep = eng.spectral_frames(signals.buf, signals.off, signals.length, srs)
+            ev, h, keep = eng.spectral_frames(own.buf, own.off, own.length, srs)
             ev.synchronize()
             res = eng.spectral_finish(h)
         t_spec = (time.perf_counter() - t1) / reps
         eng.kernel_profile(2)
         for _ in range(reps):
-            eng.spectral_frames(signals.buf, signals.off, signals.length, srs)[0].synchronize()
+            eng.spectral_frames(own.buf, own.off, own.length, srs)[0].synchronize()
         sk = {k: (ms / n, n / reps) for k, (ms, n) in eng.kernel_spans().items()}
         eng.kernel_profile(False)
         frames = int(h["T"].sum())
         fr_ms = sk["spectral_frames"][0]
         bins_ms = sk["spectral_bins"][0]
-        spec = {"workload": f"spectral.analyze of the {signals.n_files} resident 3-min files (22.05 kHz), one call",
-                "files": signals.n_files, "frames": frames, "ms_per_call": t_spec * 1e3,
-                "frames_per_s": frames / t_spec, "files_per_s": signals.n_files / t_spec,
+        spec = {"workload": f"spectral.analyze of the {own.n_files} resident 3-min files (22.05 kHz), one call",
+                "files": own.n_files, "frames": frames, "ms_per_call": t_spec * 1e3,
+                "frames_per_s": frames / t_spec, "files_per_s": own.n_files / t_spec,
                 "kernels_ms_per_call": {k: round(v[0] * v[1], 4) for k, v in sk.items()},
                 # spectral_frames: each input sample read once (512 x 4 B per frame hop);
                 # spectral_bins: the dB rows streamed once (1025 x 4 B per frame)
@@ -448,7 +531,7 @@ def main():
         if world == 1 and not args.no_cpu_baseline:
             sys.path.insert(0, str(REPO))
             from oracle import refglue
-            y0 = pairs[0][1]
+            y0 = pairs[own_ids[0]][1]
             t1 = time.perf_counter()
             refglue.spectral_analyze(y0, 22050)
             t_cpu = time.perf_counter() - t1
@@ -462,8 +545,8 @@ def main():
     if not args.no_resample and rank == 0:
         import scipy.signal
         from nightcore_analyzer.ops import poly_plan
-        n_files = min(16, len(pairs))
-        x44 = [scipy.signal.resample_poly(pairs[i][1], 2, 1).astype(np.float32) for i in range(n_files)]
+        n_files = min(16, len(own_ids))
+        x44 = [scipy.signal.resample_poly(pairs[own_ids[i]][1], 2, 1).astype(np.float32) for i in range(n_files)]
         sig44 = eng.upload_signals(x44)
         up_, down_, hh, pre = poly_plan(1, 2, int(sig44.length.max()))
         n_out = np.array([-(-int(n) * up_ // down_) for n in sig44.length], np.int64)
@@ -502,25 +585,29 @@ def main():
     if rank == 0:
         line = {
             "metric": "10 s windows/sec (CQT+onset, 22.05 kHz mono) at 1/2/4/8 GPUs; % HBM roofline",
-            "value": (1 if win_mode else world) * win_per_step * args.steps / el,
+            "value": value,
             "unit": "windows/s",
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": step_ms,
             "higher_is_better": True,
-            "scaling": "strong" if win_mode else "weak",
+            "scaling": "weak",
             "vs_baseline": None,
             "dtype": "f32",
             "data": "synthetic (SURVEY.md §8d chords+clicks+noise, nc = resample_poly(src, 4, 5)), resident in HBM"
                     + (f"; REHEARSAL: {world} ranks on {torch.cuda.device_count()} GPU(s), gloo" if rehearse else ""),
-            "config": {"workload": "config 3: per GPU a batch of 64 x 3-min 22.05 kHz mono pairs; step = "
-                                   "pipeline.run analysis of the batch without the hop-64 IBI pass"
-                                   + ("; the K steps issued as one pipelined analyze_batches call (batch k+1's "
-                                      "trim and first groups queued while batch k's last groups run)" if pipelined else ""),
+            "config": {"workload": ("config 3: per GPU a batch of 64 x 3-min 22.05 kHz mono pairs" if world == 1 else
+                                    f"config 4 shape: a batch of {world} x 64 x 3-min 22.05 kHz mono pairs, its windows "
+                                    "and chunk pairs split over the ranks (sharded.shard_plan)" if win_mode else
+                                    f"{world} x 64 x 3-min pairs, whole pairs per rank")
+                                   + "; step = pipeline.run analysis of the batch without the hop-64 IBI pass"
+                                   + ("; the K steps issued as one pipelined call (batch k+1's trim and first "
+                                      "groups queued while batch k's last groups run)" if pipelined else ""),
                        "single_call_ms_per_step": single_ms,
                        "pairs_per_gpu": args.pairs, "windows_per_gpu_step": win_per_step,
-                       "cqt_chunks_per_gpu_step": chunks_per_step, "parallelism": f"dp{world} (" + ("windows sharded, record all-gathers)" if win_mode else "pairs sharded)")},
+                       "cqt_chunks_per_gpu_step": chunks_per_step, "parallelism": f"dp{world} (" + ("windows sharded, split-pair record all-gathers)" if win_mode else
+                                                    "pairs sharded)")},
             # avg_launch_ms: the kernel's execution spans over the timed steps (rocprofv3's
             # kernel duration, sharing the chip with the concurrent chain); isolated: the same
             # kernels with the other streams idle
@@ -529,6 +616,8 @@ def main():
             "entry_points_ms_per_step": {k: round(v[0] * v[1], 4) for k, v in per.items()},
             "check": {"tempo_ratio_pair0": tr, "pitch_ratio_pair0": pr},
         }
+        if modes is not None:
+            line["modes"] = modes
         if upl is not None:
             line["upload_included"] = upl
         if ibi is not None:

@@ -176,6 +176,10 @@ int nc_chroma_lag(nc_ctx* ctx, const float* chroma, const int* src_idx, const in
  * lag decision is from a tie (no reference equivalent; diagnostics). */
 int nc_chroma_lag_margin(nc_ctx* ctx, const float* chroma, const int* src_idx, const int* nc_idx, int n_pairs,
                          int* lag_out, double* margin_out, void* stream);
+/* pitch._cyclic_xcorr_peak (pitch.py:67-85) for vectors of any length n >= 1: pair p is
+ * src[p*n .. p*n+n) against nc[p*n .. p*n+n); lag_out[p] = argmax_k dot(src, roll(nc, -k))
+ * (first maximum, first NaN wins as np.argmax), minus n when it exceeds n / 2. */
+int nc_xcorr_peak(nc_ctx* ctx, const float* src, const float* nc, int n, int n_pairs, int* lag_out, void* stream);
 
 /* ---------------------------------------------------------------------------
  * device glue between the kernels (so a batch needs no host round trip)

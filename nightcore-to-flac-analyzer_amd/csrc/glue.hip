@@ -9,6 +9,8 @@
 //                         finite positive tempo
 //   pitch_hz_kernel       pitch.py:95 + 161-164: shift = lag / 3.0 (the quirk),
 //                         nc_hz = 440 * 2^(shift/12), src_hz = 440
+//   xcorr_peak_kernel     pitch._cyclic_xcorr_peak (pitch.py:67-85) for vectors of any
+//                         length n (the 12-bin chroma_lag_kernel is the batch path)
 #include "nc_block.h"
 #include "nc_engine.h"
 
@@ -91,6 +93,66 @@ int launch_collect_valid(const double* bpm, const int* nbeats, const uint8_t* ac
 int launch_pitch_hz(const int* lags, int n, double* shift_out, double* nc_hz, double* src_hz, hipStream_t st) {
   if (n <= 0) return 0;
   hipLaunchKernelGGL(pitch_hz_kernel, dim3((n + 63) / 64), dim3(64), 0, st, lags, n, shift_out, nc_hz, src_hz);
+  NC_HIP(hipGetLastError());
+  return 0;
+}
+
+// pitch._cyclic_xcorr_peak for any n (pitch.py:67-85): xcorr[k] = sum_j a[j] b[(j + k) % n] as
+// an f32 fma chain in j order (the 12-bin chroma_lag_kernel's arithmetic), first argmax with
+// numpy's NaN rule (the first NaN wins), wrapped to lag - n when lag > n / 2.  One workgroup
+// per pair; each thread scans lags k = tid, tid + 256, ..., then a (value, k) tree in LDS.
+__device__ __forceinline__ bool xc_better(float v, int k, float bv, int bk) {
+  const bool vn = v != v, bn = bv != bv;
+  if (vn || bn) return vn && (!bn || k < bk);
+  return v > bv || (v == bv && k < bk);
+}
+
+__global__ __launch_bounds__(256) void xcorr_peak_kernel(const float* a, const float* b, int n, int* lag_out) {
+  __shared__ float sv[256];
+  __shared__ int sk[256];
+  const float* x = a + (size_t)blockIdx.x * n;
+  const float* y = b + (size_t)blockIdx.x * n;
+  float bv = 0.0f;
+  int bk = 0x7fffffff;
+  for (int k = threadIdx.x; k < n; k += 256) {
+    float d = 0.0f;
+    int i = k;
+    for (int j = 0; j < n; ++j) {
+      d = fmaf(x[j], y[i], d);
+      if (++i == n) i = 0;
+    }
+    if (bk == 0x7fffffff || xc_better(d, k, bv, bk)) {
+      bv = d;
+      bk = k;
+    }
+  }
+  sv[threadIdx.x] = bv;
+  sk[threadIdx.x] = bk;
+  __syncthreads();
+  for (int s = 128; s > 0; s >>= 1) {
+    if (threadIdx.x < s) {
+      const float v2 = sv[threadIdx.x + s];
+      const int k2 = sk[threadIdx.x + s];
+      if (k2 != 0x7fffffff && (sk[threadIdx.x] == 0x7fffffff || xc_better(v2, k2, sv[threadIdx.x], sk[threadIdx.x]))) {
+        sv[threadIdx.x] = v2;
+        sk[threadIdx.x] = k2;
+      }
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    const int lag = sk[0];
+    lag_out[blockIdx.x] = lag > n / 2 ? lag - n : lag;
+  }
+}
+
+int launch_xcorr_peak(const float* a, const float* b, int n, int n_pairs, int* lag_out, hipStream_t st) {
+  if (n_pairs <= 0) return 0;
+  if (n <= 0) {
+    set_error("xcorr_peak: n must be positive (np.argmax of an empty sequence raises)");
+    return -2;
+  }
+  hipLaunchKernelGGL(xcorr_peak_kernel, dim3(n_pairs), dim3(256), 0, st, a, b, n, lag_out);
   NC_HIP(hipGetLastError());
   return 0;
 }

@@ -42,6 +42,7 @@ int launch_chroma_mean(Context& ctx, const float* sig, const int64_t* chunk_off,
                        float* ext_mag, int* ext_npk, void* wait_event, void* ws, size_t ws_bytes, hipStream_t st);
 int launch_chroma_lag(const float* chroma, const int* src_idx, const int* nc_idx, int n_pairs, int* lag_out,
                       double* margin_out, hipStream_t st);
+int launch_xcorr_peak(const float* a, const float* b, int n, int n_pairs, int* lag_out, hipStream_t st);
 
 size_t bootstrap_job_bytes(int cap, int n_boot);
 int launch_bootstrap(const BootArgs& a, int n_jobs, hipStream_t st);
@@ -325,6 +326,12 @@ int nc_pitch_hz(nc_ctx* ctx, const int* lags, int n, double* shift_out, double* 
   CHECK_CTX(ctx);
   SET_DEVICE(ctx);
   return nc::launch_pitch_hz(lags, n, shift_out, nc_hz, src_hz, (hipStream_t)stream);
+}
+
+int nc_xcorr_peak(nc_ctx* ctx, const float* src, const float* nc, int n, int n_pairs, int* lag_out, void* stream) {
+  CHECK_CTX(ctx);
+  SET_DEVICE(ctx);
+  return nc::launch_xcorr_peak(src, nc, n, n_pairs, lag_out, (hipStream_t)stream);
 }
 
 size_t nc_bootstrap_job_bytes(int cap, int n_boot) { return nc::bootstrap_job_bytes(cap, n_boot); }

@@ -27,8 +27,9 @@ import math
 import os
 import threading
 import time
+import weakref
 from dataclasses import dataclass, field
-from typing import Dict, List, Optional, Sequence, Tuple
+from typing import Callable, Dict, List, Optional, Sequence, Tuple
 
 import numpy as np
 import torch
@@ -211,6 +212,10 @@ class Params:
     compute_pitch: bool = True
     compute_ibi: bool = True
     ibi_beats: bool = False      # also copy the hop-64 beat frames back (detail["ibi_beats"]: (nc, src))
+    # MELODIA refinement (pitch.py:246-291) where essentia is installed: melodia(pair, chroma
+    # shift, log) -> (src Hz, nc Hz) when accepted, else None (pipeline.run sets it; it runs
+    # essentia on the host arrays, as the reference does)
+    melodia: Optional[Callable] = None
 
 
 def _group_bounds(B: int, group_pairs, ) -> List[Tuple[int, int]]:
@@ -287,7 +292,10 @@ def beat_needs_workspace(T: int, acw: int) -> bool:
     return tab + T * 21 + 16 > 64 * 1024
 
 
-MAX_WINDOW_FRAMES = (160 * 1024 - 8 * (3 * 344)) // 16   # window_tg LDS (csrc/window_stage.hip): ~225 s
+# the longest window the per-window stage runs: window_tg_slide_kernel's LDS image of
+# 2 T + 3 acw doubles within kWinTgLdsCap = 160 KiB - 1 KiB (csrc/window_stage.hip
+# wtg_slide_lds_doubles): T <= 9660 frames, ~224 s at hop 512
+MAX_WINDOW_FRAMES = ((160 * 1024 - 1024) // 8 - 3 * 344) // 2
 
 
 def plan_batch(off: np.ndarray, length: np.ndarray, start: np.ndarray, end: np.ndarray, p: "Params",
@@ -436,6 +444,17 @@ class Engine:
         # NC_SHARE_TUNING=0 runs every tuning frame in the chroma chain instead (same results)
         self.share_tuning = os.environ.get("NC_SHARE_TUNING", "1") != "0"
 
+    def close(self) -> None:
+        """Wait for this engine's streams, then drop its workspaces and its context (tables)."""
+        if getattr(self, "ctx", None) is None:
+            return
+        for s_ in {self.chroma_stream, self.tail_stream, self.trim_stream}:
+            s_.synchronize()
+        torch.cuda.current_stream(self.dev).synchronize()
+        self._ws.clear()
+        self.ctx.close()
+        self.ctx = None
+
     def set_serial(self, on: bool) -> None:
         """Queue the chroma chain and the consensus tail on the launch stream too (on=True):
         every kernel then runs alone, so per-kernel timers measure its isolated speed rather
@@ -528,8 +547,9 @@ class Engine:
 
     # -------------------------------------------------------------- bootstrap (generic)
     def bootstrap(self, jobs: Sequence[Tuple[np.ndarray, Optional[np.ndarray]]], seed: int,
-                  n_boot: int = C.N_BOOTSTRAP, ci: float = C.CI_LEVEL):
-        """[(A, B|None)] -> [(point, (lo, hi))] with numpy default_rng(seed) semantics."""
+                  n_boot: int = C.N_BOOTSTRAP, ci: float = C.CI_LEVEL, ws_tag: str = ""):
+        """[(A, B|None)] -> [(point, (lo, hi))] with numpy default_rng(seed) semantics.
+        ``ws_tag`` prefixes the workspace name (work queued beside the pipelined groups)."""
         dev = self.dev
         vals, a_off, a_n, b_off, b_n, caps = [], [], [], [], [], []
         pos = 0
@@ -563,7 +583,7 @@ class Engine:
         d = up.commit(dev)
         n = len(jobs)
         out = torch.empty(3 * n, dtype=torch.float64, device=dev)
-        ws = self.workspace("boot", tot)
+        ws = self.workspace(ws_tag + "boot", tot)
         il, gl, ih, gh = percentile_params(n_boot, ci)
         self.call("nc_bootstrap_ratio", d["vals"].data_ptr(), d["a_off"].data_ptr(), d["a_n"].data_ptr(),
                   d["b_off"].data_ptr() if has_b else None, d["b_n"].data_ptr() if has_b else None, n,
@@ -764,6 +784,18 @@ class Engine:
         return p.silence_strip_db is not None and len(groups) > 1 and not (p.auto_align and p.src_trim_sec == 0.0)
 
     def _analyze_many(self, batches: List[DeviceSignals], p: Params, group_pairs, log=None) -> List[List[PairOutcome]]:
+        gen = self._analyze_gen(batches, p, group_pairs, log)
+        while True:
+            try:
+                next(gen)
+            except StopIteration as stop:
+                return stop.value
+
+    def _analyze_gen(self, batches: List[DeviceSignals], p: Params, group_pairs, log=None):
+        """The body of ``_analyze_many`` as a generator that yields after each pair group is
+        launched (the host is then free until the next ``next``): a caller can interleave
+        other host work — the window-sharded record exchanges — with the pipelined groups
+        while up to GROUPS_IN_FLIGHT of them keep the device busy.  Returns the results."""
         hs = self.host_stats
         launch = torch.cuda.current_stream(self.dev)
         # the signals are complete on the launch stream here; trims of later batches wait for
@@ -828,6 +860,7 @@ class Engine:
                 if len(pending) > self.GROUPS_IN_FLIGHT:
                     g = pending.pop(0)
                     results[g["bi"]] += self._finish_group(g, log)
+                yield
         for g in pending:
             results[g["bi"]] += self._finish_group(g, log)
         return results
@@ -1176,7 +1209,10 @@ class Engine:
                     align=align,
                     starts=starts, w0=w0, w1=w1, f_len=f_len,
                     strip_len=strip_len, lead=lead, trail=trail, intro=intro, win_n=win_n,
-                    pair_chunks=pair_chunks, n_cp=n_cp, nj=nj, n_pitch_jobs=n_pitch_jobs, B=B)
+                    pair_chunks=pair_chunks, n_cp=n_cp, nj=nj, n_pitch_jobs=n_pitch_jobs, B=B,
+                    spans=[((int(f_off[2 * b + 1] - signals.off[2 * b + 1]), int(f_len[2 * b + 1])),
+                            (int(f_off[2 * b] - signals.off[2 * b]), int(f_len[2 * b]))) for b in range(B)]
+                    if p.melodia is not None else None)
 
     def _finish_group(self, g: dict, log=None) -> List[PairOutcome]:
         """Wait for one group's results (sync 2 of that group) and assemble them on the host.
@@ -1198,7 +1234,8 @@ class Engine:
                 wait = _StageWaiter(o, g, h, lambda line, i=g["g0"] + b: log(i, line))
             assemble_pair(b, g["p"], h, ibi, g["starts_l"], g["w0"], g["w1"], g["f_len"], g["strip_len"], g["lead"],
                           g["trail"], g["intro"][b], g["win_n"], g["pair_chunks"], g["n_cp"], g["nj"],
-                          g["n_pitch_jobs"], g["align"][b] if g["align"] else None, out=o, wait=wait)
+                          g["n_pitch_jobs"], g["align"][b] if g["align"] else None, out=o, wait=wait,
+                          span=(g["g0"] + b, g["spans"][b]) if g.get("spans") else None)
             if wait is not None:
                 wait.flush()
             out.append(o)
@@ -1208,7 +1245,8 @@ class Engine:
         return out
 
     # -------------------------------------------------------------- IBI pass (tempo.py:120-173)
-    def ibi_core(self, buf, d_off, d_len, f_len, start_vals, pidx, hop: int = IBI_HOP, min_ibis: int = 4):
+    def ibi_core(self, buf, d_off, d_len, f_len, start_vals, pidx, hop: int = IBI_HOP, min_ibis: int = 4,
+                 ws_tag: str = ""):
         """onset(hop) -> streamed tempogram mean -> beat_track -> IBIs for every
         file (tempo.py:158-172); start bpm of file f = start_vals[pidx[f]]."""
         dev, st = self.dev, self.stream()
@@ -1218,14 +1256,14 @@ class Engine:
         onset = torch.empty(max(1, total), dtype=torch.float32, device=dev)
         fbase = torch.empty(nF + 1, dtype=torch.int64, device=dev)
         wsb = self.ctx.lib.nc_ibi_onset_workspace_bytes(self.ctx.h, nF, total)
-        ws = self.workspace("ibi_on", wsb)
+        ws = self.workspace(ws_tag + "ibi_on", wsb)
         self.call("nc_ibi_onset", buf.data_ptr(), d_off.data_ptr(), d_len.data_ptr(), nF, total, hop,
                   onset.data_ptr(), fbase.data_ptr(), ws.data_ptr(), ws.numel(), st)
         acw = int(int(8.0 * SR) // hop)
         tg = torch.empty(nF * acw, dtype=torch.float64, device=dev)
         fmax = int(frames.max())
         wsb = self.ctx.lib.nc_ibi_tempogram_workspace_bytes(self.ctx.h, nF, total, fmax, hop)
-        ws = self.workspace("ibi_tg", wsb)
+        ws = self.workspace(ws_tag + "ibi_tg", wsb)
         self.call("nc_ibi_tempogram", onset.data_ptr(), fbase.data_ptr(), nF, total, fmax, hop, tg.data_ptr(),
                   ws.data_ptr(), ws.numel(), st)
         lens = h2d(frames, np.int32, dev)
@@ -1235,7 +1273,7 @@ class Engine:
         mg = torch.zeros(nF, dtype=torch.float64, device=dev)
         beats = torch.empty(max(1, total), dtype=torch.int32, device=dev)
         wsb = self.ctx.lib.nc_tempo_beats_workspace_bytes(total)
-        ws = self.workspace("ibi_beats", wsb)
+        ws = self.workspace(ws_tag + "ibi_beats", wsb)
         self.call("nc_tempo_beats", onset.data_ptr(), fbase.data_ptr(), lens.data_ptr(), nF, int(frames.max()),
                   tg.data_ptr(), acw, start_vals.data_ptr(), pidx.data_ptr(), None, hop, 1, bpm.data_ptr(),
                   lag.data_ptr(), nb.data_ptr(), mg.data_ptr(), beats.data_ptr(), total, ws.data_ptr(), ws.numel(),
@@ -1288,7 +1326,7 @@ class Engine:
 # ------------------------------------------------------------------------------ host assembly + logs
 def assemble_pair(b, p: Params, h, ibi, starts, w0, w1, f_len, strip_len, lead, trail, intro,
                   win_n, pair_chunks, n_cp, nj, n_pitch_jobs, align=None, out: Optional[PairOutcome] = None,
-                  wait=None) -> PairOutcome:
+                  wait=None, span=None) -> PairOutcome:
     """One pair's AnalysisResult (or run()'s exception) and its log lines, in the order of
     pipeline.py:77-215, from the host views of its group.  ``wait(stage)`` ("gate",
     "pitch", "src", "nc", "final") is called before the lines that need a stage's
@@ -1351,9 +1389,18 @@ def assemble_pair(b, p: Params, h, ibi, starts, w0, w1, f_len, strip_len, lead, 
               "pitch CI is degenerate; estimate may be less reliable.")
         L(lambda: f"    Chroma xcorr: {point_st:+.3f} st  95% CI [{lo_st:+.3f}, {hi_st:+.3f}] st"
                   f"  ({n} chunk{'s' if n != 1 else ''})")
-        L("    essentia not available — skipping MELODIA refinement")
-        L("  Pitch method: chroma_xcorr")
-        method = "chroma_xcorr"
+        pick = None
+        if p.melodia is None or span is None:
+            L("    essentia not available — skipping MELODIA refinement")
+        else:
+            lines: List[str] = []
+            pick = p.melodia(span[0], point_st, lines.append, span[1])   # batch pair index, trimmed spans
+            for x in lines:
+                L(x)
+        method = "chroma+melodia" if pick is not None else "chroma_xcorr"
+        if pick is not None:
+            src_p, nc_p = pick
+        L(f"  Pitch method: {method}")
         margins = h["cmargin"][c0:c1].copy()
         out.detail.update(chunk_lags=lags, chunk_lag_margin=margins, tuning=h["tuning"][2 * c0:2 * c1].copy(),
                           chroma=h["chroma"][24 * c0:24 * c1].reshape(-1, 12).copy())
@@ -1401,7 +1448,11 @@ def assemble_pair(b, p: Params, h, ibi, starts, w0, w1, f_len, strip_len, lead, 
                       tempo_margin_src=h["margin"][src_w].copy(), tempo_margin_nc=h["margin"][nc_w].copy())
     L("Computing consensus…")
     wait("final")
-    if p.compute_pitch:
+    if p.compute_pitch and method == "chroma+melodia":
+        vs, vn = C._valid(src_p), C._valid(nc_p)
+        if len(vs) >= C.MIN_VALID and len(vn) >= C.MIN_VALID:
+            pitch_boot = C._bootstrap_ratio(vn, vs)      # consensus.py:550-553 on the MELODIA lists
+    elif p.compute_pitch:
         pj = len(w0) // 2 + b     # pitch job index: after the B tempo jobs
         bo = h["bout_l"]
         pitch_boot = (bo[pj], (bo[nj + pj], bo[2 * nj + pj]))
@@ -1437,18 +1488,37 @@ def assemble_pair(b, p: Params, h, ibi, starts, w0, w1, f_len, strip_len, lead, 
     return out
 
 
-_engines: Dict[Tuple[int, int], Engine] = {}
-_elock = threading.Lock()
+_tls = threading.local()
+_live: "weakref.WeakSet[Engine]" = weakref.WeakSet()     # engines not yet collected (tests, diagnostics)
 
 
 def get_engine(device: Optional[int] = None) -> Engine:
-    """One engine per (device, thread) — contexts are not shared across threads."""
+    """This thread's engine for ``device`` — contexts are not shared across threads.  The
+    engine lives in thread-local storage, so it (its context, streams and HBM workspaces) is
+    released when the thread ends: the reference's GUI starts a fresh QThread per analysis
+    (gui/worker.py:16-56), and a long session must not keep one engine per finished thread.
+    ``release_engine`` frees it earlier."""
     if device is None:
         device = torch.cuda.current_device() if torch.cuda.is_available() else 0
-    key = (device, threading.get_ident())
-    with _elock:
-        e = _engines.get(key)
-        if e is None:
-            e = Engine(device)
-            _engines[key] = e
-        return e
+    engines = getattr(_tls, "engines", None)
+    if engines is None:
+        engines = _tls.engines = {}
+    e = engines.get(device)
+    if e is None:
+        e = engines[device] = Engine(device)
+        _live.add(e)
+    return e
+
+
+def release_engine(device: Optional[int] = None) -> None:
+    """Close this thread's engine for ``device`` (every device when None) after its queued
+    work: the next get_engine on this thread builds a new one."""
+    engines = getattr(_tls, "engines", None) or {}
+    for d in [d for d in engines if device is None or d == device]:
+        engines.pop(d).close()
+
+
+def live_engines() -> int:
+    """Engines still alive in this process (every thread's)."""
+    gc.collect()
+    return len(_live)

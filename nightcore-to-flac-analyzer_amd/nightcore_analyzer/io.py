@@ -71,7 +71,12 @@ def _read_wav(path: Path):
     sr, bits = int.from_bytes(fmt[4:8], "little"), int.from_bytes(fmt[14:16], "little")
     if tag == _WAVE_EXTENSIBLE and len(fmt) >= 26:
         tag = int.from_bytes(fmt[24:26], "little")          # SubFormat GUID data1 (low 16 bits)
-    width = bits // 8
+    block_align = int.from_bytes(fmt[12:14], "little")
+    if ch <= 0 or block_align <= 0 or block_align % ch:
+        raise ValueError(f"{path}: invalid WAVE header (channels={ch}, block_align={block_align})")
+    # the container width, not bits // 8: 12- or 20-bit samples sit left-justified in 2 or 3
+    # bytes, so the bytes split into samples at block_align / channels
+    width = block_align // ch
     n = len(raw) // (width * ch) * width * ch
     raw = raw[:n]
     if tag == _WAVE_FLOAT and width in (4, 8):
@@ -116,6 +121,50 @@ def load_audio(path: str, sr: Optional[int] = SAMPLE_RATE) -> tuple[np.ndarray, 
         g = math.gcd(int(sr), int(file_sr))
         y, = resample_poly(get_engine(), [y], int(sr) // g, int(file_sr) // g)
     return np.ascontiguousarray(y, dtype=np.float32), sr
+
+
+def decoded_length(x, sr: int = SAMPLE_RATE) -> int:
+    """Samples ``load_audio(x, sr)`` returns, read from the file header alone (a decoded
+    array: its length): the window-sharded runs plan every rank's items from the lengths
+    of all files before each rank decodes only the files it touches."""
+    if isinstance(x, np.ndarray):
+        return len(x)
+    p = Path(x)
+    if p.suffix.lower() == ".npy":
+        a = np.load(p, mmap_mode="r", allow_pickle=False)
+        return int(a.shape[1] if a.ndim > 1 else a.shape[0])
+    if p.suffix.lower() != ".wav":
+        return len(load_audio(x, sr)[0])          # raises the same NotImplementedError
+    size = p.stat().st_size
+    fmt = None
+    frames = None
+    with open(p, "rb") as fh:
+        head = fh.read(12)
+        if len(head) < 12 or head[:4] not in (b"RIFF", b"RF64") or head[8:12] != b"WAVE":
+            raise ValueError(f"{p}: not a RIFF/WAVE file")
+        pos = 12
+        while pos + 8 <= size:
+            fh.seek(pos)
+            ck = fh.read(8)
+            cid, n = ck[:4], int.from_bytes(ck[4:8], "little")
+            if cid == b"fmt ":
+                fmt = fh.read(n)
+            elif cid == b"data":
+                frames = min(n, size - pos - 8)
+            pos += 8 + n + (n & 1)
+    if fmt is None or frames is None or len(fmt) < 16:
+        raise ValueError(f"{p}: WAVE file without fmt/data chunks")
+    ch, block_align = int.from_bytes(fmt[2:4], "little"), int.from_bytes(fmt[12:14], "little")
+    if ch <= 0 or block_align <= 0 or block_align % ch:
+        raise ValueError(f"{p}: invalid WAVE header (channels={ch}, block_align={block_align})")
+    n = frames // block_align
+    file_sr = int.from_bytes(fmt[4:8], "little")
+    if sr is None or file_sr == sr:
+        return n
+    import math
+    g = math.gcd(int(sr), file_sr)
+    up, down = int(sr) // g, file_sr // g
+    return -(-n * up // down)                   # resample_poly's output length
 
 
 def strip_silence(audio: np.ndarray, sr: int, top_db: float = SILENCE_STRIP_DB) -> tuple[np.ndarray, float, float]:

@@ -135,6 +135,17 @@ def chroma_lags(eng: Engine, chroma_dev: torch.Tensor, src_idx: Sequence[int], n
     return lag.cpu().numpy()[:n].astype(int).tolist()
 
 
+def xcorr_peaks(eng: Engine, src: np.ndarray, nc: np.ndarray) -> List[int]:
+    """pitch._cyclic_xcorr_peak (pitch.py:67-85) for rows of [pairs, n] (any n >= 1)."""
+    a = np.ascontiguousarray(src, np.float32)
+    b = np.ascontiguousarray(nc, np.float32)
+    n_pairs, n = a.shape
+    d = torch.from_numpy(np.concatenate([a.reshape(-1), b.reshape(-1)])).to(eng.dev)
+    lag = torch.empty(max(1, n_pairs), dtype=torch.int32, device=eng.dev)
+    eng.call("nc_xcorr_peak", d[:a.size].data_ptr(), d[a.size:].data_ptr(), n, n_pairs, lag.data_ptr(), eng.stream())
+    return lag.cpu().numpy()[:n_pairs].astype(int).tolist()
+
+
 def xcorr_speed(eng: Engine, ya: np.ndarray, yb: np.ndarray, sr: int = SR, n_windows: int = 20,
                 window_sec: float = 3.0, search_range: float = 0.05,
                 skip_edges: float = 0.10) -> Tuple[float, float]:

@@ -52,17 +52,34 @@ def run(nightcore_path: str, source_path: str, *, window_sec: float = WINDOW_SEC
     nc = _load(nightcore_path, _log, "nightcore")
     src = _load(source_path, _log, "source")
     from .engine import get_engine
+    p = _params(window_sec, hop_sec, energy_gate_db, silence_strip_db, src_trim_sec, auto_align, compute_pitch)
+    if compute_pitch:
+        p.melodia = _melodia_hook([(nc, src)])
     # log lines stream out as the device stages complete (pipeline.py:77-215 logs as it goes;
     # the GUI worker forwards each line live, gui/worker.py:46-53)
-    outcome, = get_engine().analyze([(nc, src)], _params(window_sec, hop_sec, energy_gate_db, silence_strip_db,
-                                                         src_trim_sec, auto_align, compute_pitch),
-                                    log=(lambda i, line: _log(line)) if log is not None else None)
+    outcome, = get_engine().analyze([(nc, src)], p, log=(lambda i, line: _log(line)) if log is not None else None)
     if outcome.error is not None:
         raise outcome.error
     return outcome.result
 
 
 analyze = run
+
+
+def _melodia_hook(pairs):
+    """Params.melodia for pairs of host arrays (nc, src) when essentia is installed (None
+    otherwise, the case in this image): MELODIA on the pair's trimmed signals, then
+    estimate_pitch_combined's acceptance rule (pitch.py:246-291)."""
+    from . import pitch
+    if pitch._try_import_essentia() is None:
+        return None
+
+    def hook(b, chroma_st, log, span):         # b: pair index in `pairs`; span: trimmed (src, nc)
+        (so, sl), (no, nl) = span
+        nc, src = pairs[b]
+        mel = pitch.estimate_pitch_melodia(src[so:so + sl], nc[no:no + nl], 22050, log=log)
+        return pitch.melodia_choice(mel, chroma_st, log)
+    return hook
 
 
 def run_batch(pairs: Sequence[Tuple[PathOrArray, PathOrArray]], *, window_sec: float = WINDOW_SEC,
@@ -75,7 +92,10 @@ def run_batch(pairs: Sequence[Tuple[PathOrArray, PathOrArray]], *, window_sec: f
     quiet = (lambda m: None)
     arrays = [(_load(n, quiet, "nightcore"), _load(s, quiet, "source")) for n, s in pairs]
     from .engine import get_engine
-    outs = get_engine().analyze(arrays, _params(window_sec, hop_sec, energy_gate_db, silence_strip_db,
-                                                src_trim_sec, auto_align, compute_pitch, compute_ibi),
+    p = _params(window_sec, hop_sec, energy_gate_db, silence_strip_db, src_trim_sec, auto_align, compute_pitch,
+                compute_ibi)
+    if compute_pitch:
+        p.melodia = _melodia_hook(arrays)
+    outs = get_engine().analyze(arrays, p,
                                 log=(lambda i, line: log(f"[pair {i}] {line}")) if log is not None else None)
     return [o.error if o.error is not None else o.result for o in outs]

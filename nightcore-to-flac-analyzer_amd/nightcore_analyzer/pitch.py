@@ -28,25 +28,27 @@ def _mean_chroma(audio: np.ndarray, sr: int) -> np.ndarray:
     """Time-averaged 12-bin CQT chroma (pitch.py:55-64)."""
     from .engine import get_engine
     from .ops import chroma_means
+    from .tempo import require_rate
+    require_rate(sr, "_mean_chroma")
     return chroma_means(get_engine(), [audio])[0][0]
 
 
 def _cyclic_xcorr_peak(src_chroma: np.ndarray, nc_chroma: np.ndarray) -> int:
-    """Wrapped argmax_k dot(src, roll(nc, -k)) (pitch.py:67-85), on the device."""
-    import torch
+    """Wrapped argmax_k dot(src, roll(nc, -k)) (pitch.py:67-85) for vectors of any length,
+    on the device (nc_xcorr_peak)."""
     from .engine import get_engine
-    from .ops import chroma_lags
-    eng = get_engine()
-    n = len(src_chroma)
-    if n != 12:
-        raise ValueError("the engine's cross-correlation kernel is 12-bin (n_chroma = 12)")
-    d = torch.tensor(np.concatenate([src_chroma, nc_chroma]).astype(np.float32), device=eng.dev)
-    return chroma_lags(eng, d, [0], [1])[0]
+    from .ops import xcorr_peaks
+    a, b = np.asarray(src_chroma), np.asarray(nc_chroma)
+    if a.ndim != 1 or a.shape != b.shape:
+        raise ValueError(f"_cyclic_xcorr_peak: vectors of equal length expected, got {a.shape} and {b.shape}")
+    return xcorr_peaks(get_engine(), a[None, :], b[None, :])[0]
 
 
 def _chroma_shift_for_chunk(src_chunk: np.ndarray, nc_chunk: np.ndarray, sr: int) -> float:
     from .engine import get_engine
     from .ops import chroma_means, chroma_lags
+    from .tempo import require_rate
+    require_rate(sr, "_chroma_shift_for_chunk")
     eng = get_engine()
     _, _, dev_chroma = chroma_means(eng, [src_chunk, nc_chunk])
     return chroma_lags(eng, dev_chroma, [0], [1])[0] / 3.0
@@ -65,6 +67,8 @@ def estimate_pitch_chroma(src_audio: np.ndarray, nc_audio: np.ndarray, sr: int,
     """pitch.py:100-173: per-20 s-chunk lags, median shift, seed-0 bootstrap CI, Hz lists."""
     from .engine import get_engine
     from .ops import chroma_means, chroma_lags, shift_bootstrap
+    from .tempo import require_rate
+    require_rate(sr, "estimate_pitch_chroma")
     eng = get_engine()
     plan = _chunk_plan(len(src_audio), len(nc_audio), sr)
     arrays = []
@@ -99,26 +103,67 @@ def _try_import_essentia():
 
 
 def estimate_pitch_melodia(src_audio, nc_audio, sr, log=None):
-    """pitch.py:187-241 — requires essentia; absent here, so skipped (returns None)."""
+    """pitch.py:187-241: essentia's PredominantPitchMelodia (frame 2048, hop 128) on both
+    signals -> voiced F0 lists (Hz), each thinned to at most MAX_MELODIA_FRAMES by a fixed
+    stride; None when essentia is absent (the case in this image), when extraction fails or
+    when a side has no voiced frame.  MELODIA is not rebuilt on the device: like the
+    reference, this step is essentia's own CPU algorithm and runs only where essentia is
+    installed."""
     es = _try_import_essentia()
     if es is None:
         if log:
             log("    essentia not available — skipping MELODIA refinement")
         return None
-    raise NotImplementedError("MELODIA refinement (essentia) is outside the MI355X engine (SURVEY.md §8f)")
+
+    def voiced_f0(audio):
+        try:
+            f0, _ = es.PredominantPitchMelodia(frameSize=2048, hopSize=128, sampleRate=float(sr))(
+                np.asarray(audio, dtype=np.float32))
+            f0 = np.asarray(f0)
+            v = f0[f0 > 0.0]
+            if v.size == 0:
+                return None
+            if v.size > MAX_MELODIA_FRAMES:
+                v = v[::v.size // MAX_MELODIA_FRAMES]
+            return v
+        except Exception as exc:           # noqa: BLE001 - reported, never raised (pitch.py:223-226)
+            if log:
+                log(f"    MELODIA extraction failed: {exc}")
+            return None
+
+    vs = voiced_f0(src_audio)
+    vn = voiced_f0(nc_audio)
+    if vs is None or vn is None:
+        return None
+    if log:
+        st = 12.0 * math.log2(float(np.median(vn)) / float(np.median(vs)))
+        log(f"    MELODIA: {st:+.6f} st  ({len(vs)} src / {len(vn)} nc voiced frames)")
+    return [float(v) for v in vs], [float(v) for v in vn]
+
+
+def melodia_choice(mel, chroma_st: float, log: Optional[Callable[[str], None]] = None):
+    """estimate_pitch_combined's acceptance rule (pitch.py:272-291): the MELODIA lists when
+    their median shift is within MELODIA_AGREE_ST of the chroma shift, else None (logged)."""
+    if mel is None:
+        return None
+    src_m, nc_m = mel
+    sm = float(np.median([v for v in src_m if v is not None]))
+    nm = float(np.median([v for v in nc_m if v is not None]))
+    if sm > 0 and nm > 0:
+        mst = 12.0 * math.log2(nm / sm)
+        if abs(mst - chroma_st) <= MELODIA_AGREE_ST:
+            return src_m, nc_m
+        if log:
+            log(f"    MELODIA ({mst:+.3f} st) disagrees with chroma ({chroma_st:+.3f} st) by "
+                f"{abs(mst - chroma_st):.2f} st > {MELODIA_AGREE_ST} st threshold — using chroma only")
+    return None
 
 
 def estimate_pitch_combined(src_audio: np.ndarray, nc_audio: np.ndarray, sr: int,
                             log: Optional[Callable[[str], None]] = None
                             ) -> Tuple[List[Optional[float]], List[Optional[float]], str]:
     src_hz, nc_hz, chroma_st, _, _ = estimate_pitch_chroma(src_audio, nc_audio, sr, log=log)
-    mel = estimate_pitch_melodia(src_audio, nc_audio, sr, log=log)
-    if mel is not None:
-        src_m, nc_m = mel
-        sm = float(np.median([v for v in src_m if v is not None]))
-        nm = float(np.median([v for v in nc_m if v is not None]))
-        if sm > 0 and nm > 0:
-            mst = 12.0 * math.log2(nm / sm)
-            if abs(mst - chroma_st) <= MELODIA_AGREE_ST:
-                return src_m, nc_m, "chroma+melodia"
+    pick = melodia_choice(estimate_pitch_melodia(src_audio, nc_audio, sr, log=log), chroma_st, log)
+    if pick is not None:
+        return pick[0], pick[1], "chroma+melodia"
     return src_hz, nc_hz, "chroma_xcorr"

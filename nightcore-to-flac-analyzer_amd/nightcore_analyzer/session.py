@@ -3,7 +3,7 @@ from __future__ import annotations
 
 import json
 from pathlib import Path
-from typing import Any
+from typing import Any, Optional
 
 _SESSION_FILE = Path.home() / ".nightcore_analyzer_session.json"
 
@@ -32,7 +32,10 @@ def set(key: str, value: Any) -> None:  # noqa: A001 - reference API name
     _save(data)
 
 
-def set_many(**kwargs: Any) -> None:
+def set_many(updates: Optional[dict] = None, **kwargs: Any) -> None:
+    """Persist every pair of ``updates`` in one write (session.py:37-41); keyword pairs are
+    accepted too."""
     data = _load()
+    data.update(updates or {})
     data.update(kwargs)
     _save(data)

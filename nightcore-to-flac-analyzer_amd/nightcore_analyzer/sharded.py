@@ -1,40 +1,58 @@
-"""Window-sharded analysis across ranks: one (nightcore, source) pair can span GPUs.
+"""Window-sharded analysis across ranks: the items of a batch of (nightcore, source)
+pairs — 10 s windows and 20 s chunk pairs — are split over the GPUs of a node, so one
+pair can span GPUs.
 
 north_star: "the 10 s / 5 s-hop windows over both input files are the natural shard
-unit: partition them across the GPUs with an RCCL gather of per-window estimates
-over xGMI before consensus".  SURVEY.md §8(e) lays the split out; this module follows
-it.  Every rank holds the same decoded pairs and derives the same host plan (silence
-trim, windows, 20 s chunk pairs: ``engine.plan_batch``); then
+unit: partition them across the GPUs with an RCCL gather of per-window estimates over
+xGMI before consensus".  SURVEY.md §8(e) lays the split out and this module follows it:
 
-  1. rank r runs the per-window stage (energy, onset, tempogram mean: K1-K5) on its
-     contiguous block of windows;                        C1a: all-gather energies
-  2. every rank applies the energy gate (io.py:115-126) to the whole batch; rank r
-     tracks its source windows with start_bpm 120 (tempo.py:27-77, K6-K8);
-                                                         C1b: all-gather window records
-  3. every rank forms the nc prior of every pair from the gathered source records
-     (median of valid source tempos x duration ratio, pipeline.py:174-183) and tracks
-     its nightcore windows with their pair's prior;
-     rank r also runs its contiguous block of 20 s chunk pairs (K9-K11, pitch.py:121-138);
-                                                         C1c: all-gather window + chunk records
-  4. the owner of each pair (pairs are blocked over ranks) runs the bootstraps
-     (consensus.py:243-267, pitch.py:143-150), the hop-64 IBI pass of the pair's two
-     files (tempo.py:120-173, consensus.py:270-312) and the host assembly (report,
-     warnings, logs), then the finished results are gathered to every rank.
+* **Item plan** (``shard_plan``, host, identical on every rank, from the untrimmed file
+  lengths alone).  Every pair contributes, in pair-major order, its source window slots,
+  its nightcore window slots and its chunk-pair slots (a chunk pair weighs CP_COST
+  windows: its CQT chain costs about that much device time).  Slot counts come from the
+  untrimmed lengths; silence trimming only shortens a file, so a slot past the trimmed
+  count is simply empty.  The weighted item line is cut into one contiguous block per
+  rank.  A pair belongs to the rank holding its first item (its *owner*: consensus, IBI,
+  report).  Most pairs lie inside one block (*interior*); only the pairs a block boundary
+  cuts (*split pairs*, at most world - 1 of them when there are more pairs than ranks)
+  need an exchange.
+* **Rank r loads, uploads and trims only the pairs it touches.**
+* **Interior pairs** run through the pipelined single-GPU engine (``Engine._analyze_gen``:
+  pair groups on three HIP streams, up to three in flight), with no collective at all.
+* **Split pairs** run stage by stage on a fourth stream, interleaved with the interior
+  groups (the host advances the engine's group pipeline between stages, so the device
+  always has queued work while the host waits on an exchange):
+    1. windows of this rank's slots: energy, onset, tempogram mean (K1-K5), and the tempo
+       of its source windows at start_bpm 120 (tempo.py:27-77, K6-K8);
+                                           C1a: all-gather of the split pairs' window records
+    2. energy gate of each file over its gathered energies (io.py:115-126); nc prior of
+       each pair from its gathered source records (pipeline.py:174-183); tempo of this
+       rank's nightcore windows with their pair's prior; this rank's chunk pairs
+       (tuning, CQT chroma, lag: K9-K11, pitch.py:121-138);
+                                           C1b: all-gather of window + chunk-pair records
+    3. the owner runs the bootstraps (consensus.py:243-312, pitch.py:143-150), the hop-64
+       IBI pass (tempo.py:120-173) and the host assembly (report, warnings, logs).
+* The results of every pair are gathered to every rank (``gather=True``, the API
+  default; the benchmark leaves it off, as its pair mode does).
 
-The records are fixed-size f64 rows (``all_gather_into_tensor``: RCCL over xGMI with the
-"nccl" backend, CPU tensors with gloo); shards of unequal size are padded to the
-largest one, and every gathered block carries its rank's error flag, so a failure on
-one rank raises on every rank instead of leaving the others blocked in a collective.
+The records are fixed-size f64 rows (``all_gather_into_tensor`` of device tensors over
+RCCL with the "nccl" backend — no host hop before the collective — or of CPU tensors with
+gloo); blocks of unequal size are padded to the largest, and every gathered block carries
+its rank's error flag, so a failure on one rank raises on every rank (``ShardError`` on
+the others) instead of leaving them blocked in a collective.  When no pair is split
+(equal pairs, B divisible by the world size: BASELINE config 4) the plan has no exchange
+on the data path.
 
-The device work is behind a small stage interface (``DeviceStages``: libncgpu on this
-rank's GPU).  The same orchestration runs over any object with that interface; the
-multi-process CPU tests drive it with the oracle, so the exchange, the prior and the
+The split-pair stages run over a small stage interface: ``DeviceStages`` (libncgpu on
+this rank's GPU) or, in the multi-process CPU tests, the oracle
+(``tests/sharded_oracle.OracleStages``), so the plan, the exchange, the prior and the
 consensus placement are tested without a GPU.  Every result equals the single-rank
 ``Engine.analyze`` result of the same batch.
 """
 from __future__ import annotations
 
 import math
+from dataclasses import dataclass
 from typing import List, Optional, Sequence, Tuple
 
 import numpy as np
@@ -42,19 +60,120 @@ import torch
 import torch.distributed as dist
 
 from . import consensus as C
-from .distributed import shard_range
-from .engine import (ALIGN_MIN_OFFSET, CHUNK_SEC, HOP_LENGTH, IBI_HOP, MIN_BEATS, MIN_CHUNKS, REF_HZ, SR,
-                     DeviceSignals, Engine, PairOutcome, Params, _Upload, assemble_pair, plan_batch)
+from .engine import (CHUNK_SEC, HOP_LENGTH, MIN_BEATS, MIN_CHUNKS, REF_HZ, SR, DeviceSignals, Engine, PairOutcome,
+                     Params, _Upload, assemble_pair, plan_batch)
 
-# per-window record: energy_db, bpm, nbeats, tempo lag, decision margin
-W_ENERGY, W_BPM, W_NBEATS, W_LAG, W_MARGIN = range(5)
-W_FIELDS = 5
-# per-chunk-pair record: lag, tuning (src, nc), mean chroma (src 12, nc 12), lag margin
-CP_FIELDS = 3 + 24 + 1
+# exchanged window record: exists, energy_db, bpm, nbeats, tempo lag, decision margin
+R_EXISTS, R_ENERGY, R_BPM, R_NBEATS, R_LAG, R_MARGIN = range(6)
+W_FIELDS = 6
+# chunk-pair record: exists, lag, tuning (src, nc), mean chroma (src 12, nc 12), lag margin
+CP_FIELDS = 1 + 3 + 24 + 1
+CP_COST = 8          # a chunk pair's weight in the item line, in windows
 
 
 class ShardError(RuntimeError):
     """Another rank of a window-sharded run failed (its own exception is raised there)."""
+
+
+# ------------------------------------------------------------------------------ item plan
+def n_window_slots(L: int, win_n: int, hop_n: int) -> int:
+    """io.slice_windows' count for a file of L samples (io.py:82-112)."""
+    return (L - win_n) // hop_n + 1 if L >= win_n and hop_n > 0 else 0
+
+
+@dataclass
+class ShardPlan:
+    """Item blocks of every rank (see the module docstring).  rng[b, s, r] = slot range
+    [lo, hi) of segment s (0 source windows, 1 nightcore windows, 2 chunk pairs) of pair b
+    on rank r."""
+    world: int
+    B: int
+    slots: np.ndarray          # [B, 3]
+    rng: np.ndarray            # [B, 3, world, 2]
+    owner: np.ndarray          # [B]
+    split: np.ndarray          # [B] bool
+    wrow: np.ndarray           # [B] first exchange-table window row of a split pair (-1 otherwise)
+    crow: np.ndarray           # [B] first exchange-table chunk row of a split pair (-1 otherwise)
+    n_wrows: int
+    n_crows: int
+
+    def on_rank(self, b: int, r: int) -> bool:
+        return bool(np.any(self.rng[b, :, r, 1] > self.rng[b, :, r, 0]))
+
+    def touched(self, r: int) -> List[int]:
+        return [b for b in range(self.B) if self.owner[b] == r or self.on_rank(b, r)]
+
+    def owned(self, r: int) -> List[int]:
+        return [b for b in range(self.B) if self.owner[b] == r]
+
+    def window_row(self, b: int, side: int, k: int) -> int:
+        return int(self.wrow[b] + (k if side == 0 else self.slots[b, 0] + k))
+
+    def contrib_w(self, r: int) -> np.ndarray:
+        """Exchange-table window rows rank r computes (split pairs, ascending)."""
+        rows = []
+        for b in np.flatnonzero(self.split):
+            for side in (0, 1):
+                lo, hi = self.rng[b, side, r]
+                rows += [self.window_row(b, side, k) for k in range(lo, hi)]
+        return np.asarray(rows, np.int64)
+
+    def contrib_c(self, r: int) -> np.ndarray:
+        rows = []
+        for b in np.flatnonzero(self.split):
+            lo, hi = self.rng[b, 2, r]
+            rows += [int(self.crow[b] + k) for k in range(lo, hi)]
+        return np.asarray(rows, np.int64)
+
+
+def shard_plan(lengths: Sequence[int], p: Params, world: int, split_offset: float = 0.0) -> ShardPlan:
+    """The item blocks of a batch whose files (nc_0, src_0, nc_1, src_1, ...) have the given
+    untrimmed lengths.  ``split_offset`` moves every inner block boundary by that fraction
+    of a mean pair (0: plain equal blocks; 0.5 cuts every boundary through a pair's middle,
+    which is how the exchange is measured on batches whose blocks would otherwise align)."""
+    L = np.asarray(lengths, np.int64)
+    B = len(L) // 2
+    win_n, hop_n = int(p.window_sec * SR), int(p.hop_sec * SR)
+    cn = int(CHUNK_SEC * SR)
+    slots = np.zeros((B, 3), np.int64)
+    for b in range(B):
+        ln, ls = int(L[2 * b]), int(L[2 * b + 1])
+        slots[b] = (n_window_slots(ls, win_n, hop_n), n_window_slots(ln, win_n, hop_n),
+                    max(1, min(ls // cn, ln // cn)) if p.compute_pitch else 0)
+    cost = slots[:, 0] + slots[:, 1] + CP_COST * slots[:, 2]
+    base = np.concatenate([[0], np.cumsum(cost)]).astype(np.int64)
+    T = int(base[-1])
+    bounds = np.array([T * r // world for r in range(world + 1)], np.int64)
+    if split_offset and B:
+        shift = int(round(split_offset * T / B))
+        bounds[1:world] = np.clip(bounds[1:world] + shift, 0, T)
+    bounds = np.maximum.accumulate(bounds)
+    bounds[world] = np.iinfo(np.int64).max // 4          # every unit < T lies in some block
+
+    def rank_of(u: int) -> int:
+        return int(min(world - 1, max(0, np.searchsorted(bounds, u, side="right") - 1)))
+
+    rng = np.zeros((B, 3, world, 2), np.int64)
+    for b in range(B):
+        u0 = (base[b], base[b] + slots[b, 0], base[b] + slots[b, 0] + slots[b, 1])
+        for s, stride in ((0, 1), (1, 1), (2, CP_COST)):
+            n = int(slots[b, s])
+            for r in range(world):
+                lo = -(-(int(bounds[r]) - int(u0[s])) // stride)
+                hi = -(-(int(bounds[r + 1]) - int(u0[s])) // stride)
+                rng[b, s, r] = (min(n, max(0, lo)), min(n, max(0, hi)))
+    owner = np.array([rank_of(min(int(base[b]), max(T - 1, 0))) for b in range(B)], np.int64)
+    split = np.zeros(B, bool)
+    for b in range(B):
+        split[b] = any(rng[b, s, r, 1] > rng[b, s, r, 0] for s in range(3) for r in range(world) if r != owner[b])
+    wrow = np.full(B, -1, np.int64)
+    crow = np.full(B, -1, np.int64)
+    nw = nc_ = 0
+    for b in np.flatnonzero(split):
+        wrow[b], crow[b] = nw, nc_
+        nw += int(slots[b, 0] + slots[b, 1])
+        nc_ += int(slots[b, 2])
+    return ShardPlan(world, B, slots, rng, owner, split, wrow, crow, nw, nc_)
 
 
 # ------------------------------------------------------------------------------ exchange
@@ -67,22 +186,34 @@ class Exchange:
         self.world = dist.get_world_size(group) if self.on else 1
         self.rank = dist.get_rank(group) if self.on else 0
         backend = dist.get_backend(group) if self.on else "gloo"
+        # RCCL gathers device tensors (no host hop before the collective); gloo CPU tensors
         self.dev = torch.device("cuda", torch.cuda.current_device()) if backend == "nccl" else torch.device("cpu")
 
-    def gather_rows(self, local: np.ndarray, n_total: int, failed: Optional[BaseException]) -> np.ndarray:
-        """Rank r contributes rows [lo_r, hi_r) of an n_total x k table (lo/hi from
-        shard_range); returns the whole table on every rank.  One all_gather_into_tensor of
-        (largest shard + 1 flag row) x k f64 per rank."""
+    stream: Optional[torch.cuda.Stream] = None    # RCCL: the stream the exchanged records live on
+
+    def gather_blocks(self, local: np.ndarray, counts: Sequence[int], failed: Optional[BaseException]) -> np.ndarray:
+        """Rank r contributes counts[r] rows of k f64; returns the rows of every rank in rank
+        order (one all_gather_into_tensor of (max count + 1 flag row) x k per rank).  A
+        failure anywhere raises on every rank.  With RCCL the collective is ordered on
+        ``stream`` (the split-pair stream), not behind the interior groups of the launch
+        stream."""
+        if self.dev.type == "cuda" and self.stream is not None:
+            with torch.cuda.stream(self.stream):
+                return self._gather_blocks(local, counts, failed)
+        return self._gather_blocks(local, counts, failed)
+
+    def _gather_blocks(self, local: np.ndarray, counts: Sequence[int], failed: Optional[BaseException]) -> np.ndarray:
         k = local.shape[1]
         if not self.on or self.world == 1:
             if failed is not None:
                 raise failed
             return np.ascontiguousarray(local, np.float64)
-        S = -(-n_total // self.world)
+        S = int(max(counts)) if len(counts) else 0
         mine = np.zeros((S + 1, k), np.float64)
-        mine[:local.shape[0]] = local
+        if failed is None:
+            mine[:local.shape[0]] = local
         mine[S, 0] = 1.0 if failed is not None else 0.0
-        t = torch.from_numpy(mine).to(self.dev)
+        t = torch.from_numpy(mine).to(self.dev, non_blocking=self.dev.type == "cuda")
         out = torch.empty((self.world * (S + 1), k), dtype=torch.float64, device=self.dev)
         dist.all_gather_into_tensor(out, t, group=self.group)
         allr = out.cpu().numpy().reshape(self.world, S + 1, k)
@@ -91,11 +222,11 @@ class Exchange:
             raise failed
         if bad:
             raise ShardError(f"window-sharded analysis failed on rank(s) {bad}")
-        rows = []
-        for r in range(self.world):
-            lo, hi = shard_range(n_total, self.world, r)
-            rows.append(allr[r, :hi - lo])
-        return np.concatenate(rows, axis=0) if rows else np.zeros((0, k))
+        return np.concatenate([allr[r, :counts[r]] for r in range(self.world)], axis=0) if S else np.zeros((0, k))
+
+    def check(self, failed: Optional[BaseException]) -> None:
+        """Fail together: one flag gather."""
+        self.gather_blocks(np.zeros((0, 1)), [0] * self.world, failed)
 
     def gather_objects(self, local: list) -> list:
         if not self.on or self.world == 1:
@@ -117,23 +248,56 @@ def _try(fn, *args):
 
 # ------------------------------------------------------------------------------ device stages
 class DeviceStages:
-    """The stage operations of one rank on its GPU (libncgpu), over signals resident in
-    HBM: files nc_0, src_0, nc_1, src_1, ... in one buffer."""
+    """The stage operations of one rank on its GPU (libncgpu), over signals resident in HBM
+    (files nc_0, src_0, nc_1, src_1, ... of the pairs this rank touches, one buffer).  The
+    stages run on their own HIP stream with their own workspaces ("sp_*"), so they overlap
+    the engine's pipelined interior groups without sharing scratch with them."""
 
-    def __init__(self, eng: Engine, signals: DeviceSignals):
+    def __init__(self, eng: Engine, signals: DeviceSignals, stream: Optional[torch.cuda.Stream] = None):
         self.eng = eng
         self.sig = signals
         self.off = signals.off
         self.length = signals.length
         self._win = None
+        if stream is None:
+            stream = getattr(eng, "_split_stream", None) or torch.cuda.Stream(eng.dev)
+            eng._split_stream = stream
+        self.stream = stream
+        self.stream.wait_stream(torch.cuda.current_stream(eng.dev))   # the upload of the signals
+
+    def restrict(self, files: Sequence[int]) -> "DeviceStages":
+        f = np.asarray(files, np.int64)
+        return DeviceStages(self.eng, DeviceSignals(self.sig.buf, self.off[f], self.length[f]), self.stream)
+
+    def pipeline(self, files: Sequence[int], p: Params, steps: int = 1):
+        """The engine's pipelined group generator over the pairs of `files` (interior pairs),
+        ``steps`` complete analyses back to back (Engine.analyze_batches)."""
+        f = np.asarray(files, np.int64)
+        return self.eng._analyze_gen([DeviceSignals(self.sig.buf, self.off[f], self.length[f])] * steps, p, None,
+                                     None)
 
     def trim(self, p: Params) -> Tuple[np.ndarray, np.ndarray]:
-        return self.eng._trim_all(self.sig, p)
+        with torch.cuda.stream(self.stream):
+            eng = self.eng
+            nF = self.sig.n_files
+            up = _Upload()
+            up.add("off", self.off, np.int64)
+            up.add("len", self.length, np.int64)
+            d0 = up.commit(eng.dev)
+            lens = np.ascontiguousarray(self.length, np.int64)
+            ws = eng.workspace("sp_trim", eng.ctx.lib.nc_trim_workspace_bytes(lens.ctypes.data, nF))
+            se = torch.empty(2 * nF, dtype=torch.int64, device=eng.dev)
+            eng.call("nc_trim_bounds", self.sig.buf.data_ptr(), d0["off"].data_ptr(), d0["len"].data_ptr(), nF,
+                     int(np.sum(1 + lens // 512)), float(p.silence_strip_db), se[:nF].data_ptr(), se[nF:].data_ptr(),
+                     ws.data_ptr(), ws.numel(), eng.stream())
+            h = se.cpu().numpy()
+        return h[:nF].copy(), h[nF:].copy()
 
     def align(self, start: np.ndarray, end: np.ndarray) -> List[Tuple[float, float]]:
         o, s = self.sig.off, start
-        return self.eng.align_offsets(self.sig.buf, o[1::2] + s[1::2], end[1::2] - s[1::2], o[0::2] + s[0::2],
-                                      end[0::2] - s[0::2])
+        with torch.cuda.stream(self.stream):
+            return self.eng.align_offsets(self.sig.buf, o[1::2] + s[1::2], end[1::2] - s[1::2], o[0::2] + s[0::2],
+                                          end[0::2] - s[0::2])
 
     def windows(self, win_abs: np.ndarray, win_n: int) -> np.ndarray:
         """Per-window stage (nc_window_stage: energy, onset, tempogram mean) -> energies."""
@@ -143,15 +307,16 @@ class DeviceStages:
             return np.zeros(0)
         T = 1 + win_n // HOP_LENGTH
         acw = int(int(8.0 * SR) // HOP_LENGTH)
-        off = torch.from_numpy(np.ascontiguousarray(win_abs, np.int64)).to(eng.dev)
-        onset = torch.empty(n * T, dtype=torch.float32, device=eng.dev)
-        tg = torch.empty(n * acw, dtype=torch.float64, device=eng.dev)
-        en = torch.empty(n, dtype=torch.float64, device=eng.dev)
-        ws = eng.workspace("win", eng.ctx.lib.nc_window_stage_workspace_bytes(eng.ctx.h, n, win_n, HOP_LENGTH))
-        eng.call("nc_window_stage", self.sig.buf.data_ptr(), off.data_ptr(), None, n, win_n, HOP_LENGTH,
-                 onset.data_ptr(), tg.data_ptr(), en.data_ptr(), ws.data_ptr(), ws.numel(), eng.stream())
-        self._win = dict(onset=onset, tg=tg, T=T, acw=acw)
-        return en.cpu().numpy()
+        with torch.cuda.stream(self.stream):
+            off = torch.from_numpy(np.ascontiguousarray(win_abs, np.int64)).to(eng.dev)
+            onset = torch.empty(n * T, dtype=torch.float32, device=eng.dev)
+            tg = torch.empty(n * acw, dtype=torch.float64, device=eng.dev)
+            en = torch.empty(n, dtype=torch.float64, device=eng.dev)
+            ws = eng.workspace("sp_win", eng.ctx.lib.nc_window_stage_workspace_bytes(eng.ctx.h, n, win_n, HOP_LENGTH))
+            eng.call("nc_window_stage", self.sig.buf.data_ptr(), off.data_ptr(), None, n, win_n, HOP_LENGTH,
+                     onset.data_ptr(), tg.data_ptr(), en.data_ptr(), ws.data_ptr(), ws.numel(), eng.stream())
+            self._win = dict(onset=onset, tg=tg, T=T, acw=acw)
+            return en.cpu().numpy()
 
     def tempo(self, sel: np.ndarray, start_bpm: np.ndarray) -> np.ndarray:
         """beat_track of the selected local windows (indices into the last windows() call)
@@ -162,59 +327,59 @@ class DeviceStages:
             return out
         w = self._win
         T, acw = w["T"], w["acw"]
-        up = _Upload()
-        up.add("on_off", np.asarray(sel, np.int64) * T, np.int64)
-        up.add("on_len", np.full(n, T), np.int32)
-        up.add("start", start_bpm, np.float64)
-        d = up.commit(eng.dev)
-        tg = w["tg"].view(-1, acw)[torch.from_numpy(np.asarray(sel, np.int64)).to(eng.dev)].contiguous()
-        bpm = torch.zeros(n, dtype=torch.float64, device=eng.dev)
-        lag = torch.zeros(n, dtype=torch.int32, device=eng.dev)
-        nb = torch.zeros(n, dtype=torch.int32, device=eng.dev)
-        mg = torch.zeros(n, dtype=torch.float64, device=eng.dev)
-        ws = eng.workspace("beats", eng.ctx.lib.nc_tempo_beats_workspace_bytes(n * T))   # any window length
-        eng.call("nc_tempo_beats", w["onset"].data_ptr(), d["on_off"].data_ptr(), d["on_len"].data_ptr(), n, T,
-                 tg.data_ptr(), acw, d["start"].data_ptr(), None, None, HOP_LENGTH, 1, bpm.data_ptr(),
-                 lag.data_ptr(), nb.data_ptr(), mg.data_ptr(), None, n * T, ws.data_ptr(), ws.numel(), eng.stream())
-        out[:, 0] = bpm.cpu().numpy()
-        out[:, 1] = nb.cpu().numpy()
-        out[:, 2] = lag.cpu().numpy()
-        out[:, 3] = mg.cpu().numpy()
-        return out
+        with torch.cuda.stream(self.stream):
+            up = _Upload()
+            up.add("on_off", np.asarray(sel, np.int64) * T, np.int64)
+            up.add("on_len", np.full(n, T), np.int32)
+            up.add("start", start_bpm, np.float64)
+            up.add("sel", np.asarray(sel, np.int64), np.int64)
+            d = up.commit(eng.dev)
+            tg = w["tg"].view(-1, acw)[d["sel"]].contiguous()
+            res = torch.zeros(4 * n, dtype=torch.float64, device=eng.dev)
+            lag = torch.zeros(n, dtype=torch.int32, device=eng.dev)
+            nb = torch.zeros(n, dtype=torch.int32, device=eng.dev)
+            ws = eng.workspace("sp_beats", eng.ctx.lib.nc_tempo_beats_workspace_bytes(n * T))  # any window length
+            eng.call("nc_tempo_beats", w["onset"].data_ptr(), d["on_off"].data_ptr(), d["on_len"].data_ptr(), n, T,
+                     tg.data_ptr(), acw, d["start"].data_ptr(), None, None, HOP_LENGTH, 1, res[:n].data_ptr(),
+                     lag.data_ptr(), nb.data_ptr(), res[3 * n:].data_ptr(), None, n * T, ws.data_ptr(), ws.numel(),
+                     eng.stream())
+            res[n:2 * n] = nb.to(torch.float64)
+            res[2 * n:3 * n] = lag.to(torch.float64)
+            return res.cpu().numpy().reshape(4, n).T.copy()        # one read-back for the four fields
 
     def chunks(self, chunk_off: Sequence[int], chunk_len: Sequence[int]) -> np.ndarray:
         """Mean chroma of every chunk (files interleaved src, nc per chunk pair) and the
-        pair lags -> [n_pairs, CP_FIELDS]."""
+        pair lags -> [n_pairs, 28]: lag, tuning (src, nc), chroma (src 12, nc 12), margin."""
         eng, n = self.eng, len(chunk_off)
-        out = np.zeros((n // 2, CP_FIELDS), np.float64)
         if n == 0:
-            return out
-        up = _Upload()
-        up.add("off", chunk_off, np.int64)
-        up.add("len", chunk_len, np.int64)
-        up.add("si", np.arange(0, n, 2), np.int32)
-        up.add("ni", np.arange(1, n, 2), np.int32)
-        d = up.commit(eng.dev)
-        chroma = torch.empty(n * 12, dtype=torch.float32, device=eng.dev)
-        tun = torch.empty(n, dtype=torch.float32, device=eng.dev)
-        lag = torch.empty(n // 2, dtype=torch.int32, device=eng.dev)
-        tot = int(np.sum(chunk_len))
-        ws = eng.workspace("chroma", eng.ctx.lib.nc_chroma_workspace_bytes(eng.ctx.h, n, tot))
-        eng.call("nc_chroma_mean", self.sig.buf.data_ptr(), d["off"].data_ptr(), d["len"].data_ptr(), n, tot,
-                 int(max(chunk_len)), chroma.data_ptr(), tun.data_ptr(), None, ws.data_ptr(), ws.numel(),
-                 eng.stream())
-        mg = torch.empty(n // 2, dtype=torch.float64, device=eng.dev)
-        eng.call("nc_chroma_lag_margin", chroma.data_ptr(), d["si"].data_ptr(), d["ni"].data_ptr(), n // 2,
-                 lag.data_ptr(), mg.data_ptr(), eng.stream())
-        out[:, 0] = lag.cpu().numpy()
-        t = tun.cpu().numpy().reshape(-1, 2)
-        out[:, 1:3] = t
-        out[:, 3:27] = chroma.cpu().numpy().reshape(-1, 24)
-        out[:, 27] = mg.cpu().numpy()
-        return out
+            return np.zeros((0, CP_FIELDS - 1), np.float64)
+        with torch.cuda.stream(self.stream):
+            up = _Upload()
+            up.add("off", chunk_off, np.int64)
+            up.add("len", chunk_len, np.int64)
+            up.add("si", np.arange(0, n, 2), np.int32)
+            up.add("ni", np.arange(1, n, 2), np.int32)
+            d = up.commit(eng.dev)
+            chroma = torch.empty(n * 12, dtype=torch.float32, device=eng.dev)
+            tun = torch.empty(n, dtype=torch.float32, device=eng.dev)
+            lag = torch.empty(n // 2, dtype=torch.int32, device=eng.dev)
+            tot = int(np.sum(chunk_len))
+            ws = eng.workspace("sp_chroma", eng.ctx.lib.nc_chroma_workspace_bytes(eng.ctx.h, n, tot))
+            eng.call("nc_chroma_mean", self.sig.buf.data_ptr(), d["off"].data_ptr(), d["len"].data_ptr(), n, tot,
+                     int(max(chunk_len)), chroma.data_ptr(), tun.data_ptr(), None, ws.data_ptr(), ws.numel(),
+                     eng.stream())
+            mg = torch.empty(n // 2, dtype=torch.float64, device=eng.dev)
+            eng.call("nc_chroma_lag_margin", chroma.data_ptr(), d["si"].data_ptr(), d["ni"].data_ptr(), n // 2,
+                     lag.data_ptr(), mg.data_ptr(), eng.stream())
+            rec = torch.cat([lag.to(torch.float64)[:, None], tun.to(torch.float64).view(-1, 2),
+                             chroma.to(torch.float64).view(-1, 24), mg[:, None]], dim=1)
+            return rec.cpu().numpy()
 
     def bootstrap(self, jobs, seed: int):
-        return self.eng.bootstrap(jobs, seed=seed) if jobs else []
+        if not jobs:
+            return []
+        with torch.cuda.stream(self.stream):
+            return self.eng.bootstrap(jobs, seed=seed, ws_tag="sp_")
 
     def ibi(self, f_off: np.ndarray, f_len: np.ndarray, start_bpm: np.ndarray):
         """estimate_ibis_global of each file span -> (ibis (array, or None under 4), IBI
@@ -223,17 +388,18 @@ class DeviceStages:
         if n == 0:
             z = np.zeros(0, np.int64)
             return [], z, z, z
-        up = _Upload()
-        up.add("off", f_off, np.int64)
-        up.add("len", f_len, np.int64)
-        up.add("start", start_bpm, np.float64)
-        d = up.commit(eng.dev)
-        core = eng.ibi_core(self.sig.buf, d["off"], d["len"], np.asarray(f_len, np.int64), d["start"],
-                            torch.arange(n, dtype=torch.int32, device=eng.dev))
-        vals, nibi = core["ibis"].cpu().numpy(), core["nibi"].cpu().numpy()
-        fb = core["fbase_h"]
-        ibis = [vals[fb[i]:fb[i] + nibi[i]].copy() if nibi[i] >= 4 else None for i in range(n)]
-        return ibis, nibi, core["nbeats"].cpu().numpy(), core["lag"].cpu().numpy()
+        with torch.cuda.stream(self.stream):
+            up = _Upload()
+            up.add("off", f_off, np.int64)
+            up.add("len", f_len, np.int64)
+            up.add("start", start_bpm, np.float64)
+            d = up.commit(eng.dev)
+            core = eng.ibi_core(self.sig.buf, d["off"], d["len"], np.asarray(f_len, np.int64), d["start"],
+                                torch.arange(n, dtype=torch.int32, device=eng.dev), ws_tag="sp_")
+            vals, nibi = core["ibis"].cpu().numpy(), core["nibi"].cpu().numpy()
+            fb = core["fbase_h"]
+            ibis = [vals[fb[i]:fb[i] + nibi[i]].copy() if nibi[i] >= 4 else None for i in range(n)]
+            return ibis, nibi, core["nbeats"].cpu().numpy(), core["lag"].cpu().numpy()
 
 
 # ------------------------------------------------------------------------------ orchestration
@@ -247,68 +413,237 @@ def _gate(energy: np.ndarray, w0, w1, threshold_db: float) -> np.ndarray:
     return act
 
 
-def analyze_sharded(stages, p: Optional[Params] = None, group=None) -> List[PairOutcome]:
-    """pipeline.run's analysis of every pair held by ``stages`` with the windows and chunk
-    pairs split over the ranks of ``group``; every rank returns all outcomes in pair
-    order (module docstring)."""
+def _files(pairs: Sequence[int]) -> List[int]:
+    return [f for j in pairs for f in (2 * j, 2 * j + 1)]
+
+
+class _Pump:
+    """Advances the engine's interior group pipeline one group at a time (no-op without one)."""
+
+    def __init__(self, gen):
+        self.gen, self.value = gen, None
+
+    def __call__(self, n: int = 1) -> None:
+        for _ in range(n):
+            if self.gen is None:
+                return
+            try:
+                next(self.gen)
+            except StopIteration as stop:
+                self.value, self.gen = stop.value, None
+
+    def drain(self):
+        while self.gen is not None:
+            self()
+        return self.value
+
+
+def analyze_sharded(stages, p: Optional[Params] = None, group=None, *, lengths: Optional[Sequence[int]] = None,
+                    local_pairs: Optional[Sequence[int]] = None, split_offset: float = 0.0, gather: bool = True,
+                    steps: int = 1):
+    """pipeline.run's analysis of a batch with its windows and chunk pairs split over the
+    ranks of ``group`` (module docstring).
+
+    ``stages`` holds the signals of the pairs ``local_pairs`` (global pair indices, in
+    order; None: every pair of the batch), and ``lengths`` the untrimmed lengths of all
+    2B files (None: those of ``stages``, which then holds the whole batch).  With
+    ``gather`` every rank returns all outcomes in pair order; without, this rank's owned
+    pairs as [(pair index, outcome)].  ``steps`` > 1 analyses the batch that many times
+    back to back, the interior groups pipelined across steps as Engine.analyze_batches
+    does (the benchmark's timed region), and returns one such list per step."""
     p = p or Params()
     ex = Exchange(group)
-    rank, world = ex.rank, ex.world
-    start, end = stages.trim(p) if p.silence_strip_db is not None else \
-        (np.zeros(len(stages.off), np.int64), np.asarray(stages.length, np.int64).copy())
-    align = stages.align(start, end) if (p.auto_align and p.src_trim_sec == 0.0) else None
-    pl = plan_batch(stages.off, stages.length, start, end, p, align)
-    B, n_win, n_src_w = pl.B, pl.n_win, pl.n_src_w
-    w0, w1 = pl.w0, pl.w1
-    pair_of = np.zeros(max(1, n_win), np.int64)            # pair of each window
-    for b in range(B):
-        pair_of[w0[2 * b]:w1[2 * b]] = b
-        pair_of[w0[2 * b + 1]:w1[2 * b + 1]] = b
-
-    # 1. per-window stage on this rank's block; C1a
-    lo, hi = shard_range(n_win, world, rank)
-    rec = np.zeros((hi - lo, W_FIELDS), np.float64)
-    e_loc, err = _try(stages.windows, pl.win_abs[lo:hi], pl.win_n)
-    if err is None:
-        rec[:, W_ENERGY] = e_loc
-    energy = ex.gather_rows(rec[:, :1], n_win, err)[:, 0]
-    active = _gate(energy, w0, w1, p.energy_gate_db)
-
-    # 2. source windows with start_bpm 120; C1b
-    src_sel = np.array([i - lo for i in range(lo, min(hi, n_src_w)) if active[i]], np.int64)
-    r, err = _try(stages.tempo, src_sel, np.full(len(src_sel), 120.0))
-    if err is None and len(src_sel):
-        rec[src_sel, W_BPM:] = r
-    table = ex.gather_rows(rec, n_win, err)
-
-    # 3. nc prior of every pair (pipeline.py:174-183), nightcore windows; chunk pairs; C1c
-    prior = np.full(B, 120.0)
-    for b in range(B):
-        valid = [table[w, W_BPM] for w in range(w0[2 * b + 1], w1[2 * b + 1])
-                 if active[w] and table[w, W_NBEATS] >= MIN_BEATS]
-        nc_dur, src_dur = pl.f_len[2 * b] / SR, pl.f_len[2 * b + 1] / SR
-        if valid and nc_dur > 0 and src_dur > 0:
-            prior[b] = C._median(valid) * (src_dur / nc_dur)
-    nc_sel = np.array([i - lo for i in range(max(lo, n_src_w), hi) if active[i]], np.int64)
-    r, err = _try(stages.tempo, nc_sel, prior[pair_of[nc_sel + lo]] if len(nc_sel) else np.zeros(0))
-    if err is None and len(nc_sel):
-        rec[nc_sel, W_BPM:] = r
-    table = ex.gather_rows(rec, n_win, err)
-    clo, chi = shard_range(pl.n_cp, world, rank)
-    cp, err = _try(stages.chunks, pl.chunk_off[2 * clo:2 * chi], pl.chunk_len[2 * clo:2 * chi])
-    cps = ex.gather_rows(cp if err is None else np.zeros((chi - clo, CP_FIELDS)), pl.n_cp, err)
-
-    # 4. consensus on the owner of each pair
-    plo, phi = shard_range(B, world, rank)
-    outs, err = _try(_consensus, stages, p, pl, align, active, energy, table, prior, cps, plo, phi)
-    ex.gather_rows(np.zeros((phi - plo, 1)), B, err)     # fail together before the result gather
-    for o in outs:
-        o.logs                          # render the deferred log lines (plain strings travel)
-    return ex.gather_objects(outs)
+    r, world = ex.rank, ex.world
+    L = np.asarray(stages.length if lengths is None else lengths, np.int64)
+    sp = shard_plan(L, p, world, split_offset)
+    local_pairs = list(range(sp.B)) if local_pairs is None else list(local_pairs)
+    pos = {b: j for j, b in enumerate(local_pairs)}
+    touched = sp.touched(r)
+    missing = [b for b in touched if b not in pos]
+    if missing:
+        raise ValueError(f"rank {r} touches pairs {missing} that its stages do not hold")
+    ex.stream = getattr(stages, "stream", None)
+    interior = [b for b in touched if not sp.split[b]]
+    fast = hasattr(stages, "pipeline") and bool(interior)
+    stage_pairs = [b for b in touched if sp.split[b]] if fast else touched
+    pump = _Pump(stages.pipeline(_files([pos[b] for b in interior]), p, steps) if fast else None)
+    pump(3)                                     # Engine.GROUPS_IN_FLIGHT groups queued before any wait
+    split_st = stages.restrict(_files([pos[b] for b in stage_pairs]))
+    per_step, err = [], None
+    for _ in range(steps):
+        outs, err = _try(_split_stages, split_st, p, ex, sp, r, stage_pairs, pump)
+        if err is not None:
+            break
+        per_step.append(outs)
+    if err is None and fast:
+        res, err = _try(pump.drain)
+        if err is None:
+            for k in range(steps):
+                per_step[k] = per_step[k] + list(zip(interior, res[k]))
+    if world > 1:
+        ex.check(err)                           # fail together before the result gather
+    elif err is not None:
+        raise err
+    result = []
+    for outs in per_step:
+        outs.sort(key=lambda t: t[0])
+        if not gather:
+            result.append(outs)
+            continue
+        for _, o in outs:
+            o.logs                              # render the deferred log lines (plain strings travel)
+        result.append([o for _, o in sorted(ex.gather_objects(outs), key=lambda t: t[0])])
+    return result[0] if steps == 1 else result
 
 
-def _consensus(stages, p: Params, pl, align, active, energy, table, prior, cps, plo: int, phi: int) -> list:
-    """Bootstraps, IBI pass and host assembly of pairs [plo, phi) (this rank's)."""
+def _split_stages(stages, p: Params, ex: Exchange, sp: ShardPlan, r: int, pairs: List[int], pump) -> list:
+    """Stages 1-3 of the module docstring for ``pairs`` (global indices) held by ``stages``
+    (files nc, src per pair, in that order); returns [(pair, outcome)] of the owned ones.
+    Every exception between two exchanges is carried into the next one, so all ranks meet
+    every collective and a failure raises everywhere."""
+    nP = len(pairs)
+    exchange = sp.n_wrows > 0 or sp.n_crows > 0          # identical on every rank
+    cw_cnt = [len(sp.contrib_w(q)) for q in range(sp.world)] if exchange else []
+    cc_cnt = [len(sp.contrib_c(q)) for q in range(sp.world)] if exchange else []
+    cw_all = np.concatenate([sp.contrib_w(q) for q in range(sp.world)]) if exchange else None
+    cc_all = np.concatenate([sp.contrib_c(q) for q in range(sp.world)]) if exchange else None
+    cw, cc = sp.contrib_w(r), sp.contrib_c(r)
+    st = {}                                              # phase state
+
+    def gather(table_rows, local_rows, local_vals, cnt, all_rows, n_rows, width, failed):
+        """Exchange-table rows of the split pairs: this rank's `local_rows` (values
+        `local_vals`) in, the whole table out (None without an exchange)."""
+        if not exchange:
+            if failed is not None:
+                raise failed
+            return None
+        mine = np.zeros((len(table_rows), width), np.float64)   # slots past a trimmed count stay empty
+        if failed is None:
+            row_of = {int(rw): i for i, rw in enumerate(local_rows) if rw >= 0}
+            for i, rw in enumerate(table_rows):
+                if int(rw) in row_of:
+                    mine[i] = local_vals[row_of[int(rw)]]
+        rows = ex.gather_blocks(mine, cnt, failed)
+        table = np.zeros((n_rows, width), np.float64)
+        table[all_rows.astype(np.int64)] = rows
+        return table
+
+    # ---- phase 0: trim, plan, this rank's items; windows + source tempo (start_bpm 120)
+    def phase0():
+        start, end = stages.trim(p) if (p.silence_strip_db is not None and nP) else \
+            (np.zeros(2 * nP, np.int64), np.asarray(stages.length, np.int64).copy())
+        align = stages.align(start, end) if (p.auto_align and p.src_trim_sec == 0.0 and nP) else None
+        pl = plan_batch(stages.off, stages.length, start, end, p, align)
+        pump()
+        # this rank's windows (plan indices) and chunk pairs: its slot ranges within the
+        # trimmed counts, with the exchange row of each (-1 for pairs whose items are all local)
+        wl, wl_src, wl_row, cpl, cpl_row = [], [], [], [], []
+        for j, b in enumerate(pairs):
+            for side, f in ((0, 2 * j + 1), (1, 2 * j)):
+                lo, hi = sp.rng[b, side, r]
+                for k in range(lo, min(hi, int(pl.w1[f] - pl.w0[f]))):
+                    wl.append(int(pl.w0[f]) + k)
+                    wl_src.append(side == 0)
+                    wl_row.append(sp.window_row(b, side, k) if sp.split[b] else -1)
+            lo, hi = sp.rng[b, 2, r]
+            c0, c1 = pl.pair_chunks[j] if p.compute_pitch else (0, 0)
+            for k in range(lo, min(hi, c1 - c0)):
+                cpl.append(c0 + k)
+                cpl_row.append(int(sp.crow[b] + k) if sp.split[b] else -1)
+        wl = np.asarray(wl, np.int64)
+        wl_src = np.asarray(wl_src, bool)
+        rec = np.zeros((len(wl), W_FIELDS), np.float64)
+        rec[:, R_EXISTS] = 1.0
+        rec[:, R_ENERGY] = stages.windows(pl.win_abs[wl] if len(wl) else np.zeros(0, np.int64), pl.win_n)
+        src_sel = np.flatnonzero(wl_src)
+        if len(src_sel):
+            rec[src_sel, R_BPM:] = stages.tempo(src_sel, np.full(len(src_sel), 120.0))
+        pump()
+        st.update(pl=pl, align=align, wl=wl, wl_src=wl_src, wl_row=wl_row, cpl=cpl, cpl_row=cpl_row, rec=rec)
+
+    _, err = _try(phase0)
+    gtab = gather(cw, st.get("wl_row", []), st.get("rec"), cw_cnt, cw_all, sp.n_wrows, W_FIELDS, err)       # C1a
+
+    def fill(full, have, table):
+        """Plan-order rows of the split pairs' windows held by other ranks, from `table`."""
+        pl = st["pl"]
+        for j, b in enumerate(pairs):
+            if not sp.split[b]:
+                continue
+            for side, f in ((0, 2 * j + 1), (1, 2 * j)):
+                for w in range(int(pl.w0[f]), int(pl.w1[f])):
+                    if not have[w]:
+                        row = table[sp.window_row(b, side, w - int(pl.w0[f]))]
+                        if row[R_EXISTS] != 1.0:
+                            raise ShardError(f"window record of pair {b} missing from the exchange")
+                        full[w] = row
+
+    # ---- phase 1: gate, nc prior (pipeline.py:174-183), nightcore tempo, chunk pairs
+    def phase1():
+        pl, wl, wl_src, rec = st["pl"], st["wl"], st["wl_src"], st["rec"]
+        full = np.zeros((pl.n_win, W_FIELDS), np.float64)
+        have = np.zeros(pl.n_win, bool)
+        full[wl] = rec
+        have[wl] = True
+        if gtab is not None:
+            fill(full, have, gtab)
+        energy = full[:, R_ENERGY].copy()
+        active = _gate(energy, pl.w0, pl.w1, p.energy_gate_db)
+        prior = np.full(nP, 120.0)
+        pair_of = np.zeros(max(1, pl.n_win), np.int64)
+        for j in range(nP):
+            fs, fn = 2 * j + 1, 2 * j
+            pair_of[pl.w0[fn]:pl.w1[fn]] = j
+            pair_of[pl.w0[fs]:pl.w1[fs]] = j
+            valid = [full[w, R_BPM] for w in range(int(pl.w0[fs]), int(pl.w1[fs]))
+                     if active[w] and full[w, R_NBEATS] >= MIN_BEATS]
+            nc_dur, src_dur = pl.f_len[fn] / SR, pl.f_len[fs] / SR
+            if valid and nc_dur > 0 and src_dur > 0:
+                prior[j] = C._median(valid) * (src_dur / nc_dur)
+        nc_sel = np.flatnonzero(~wl_src & active[wl]) if len(wl) else np.zeros(0, np.int64)
+        if len(nc_sel):
+            rec[nc_sel, R_BPM:] = stages.tempo(nc_sel, prior[pair_of[wl[nc_sel]]])
+        pump()
+        cpl = st["cpl"]
+        crec = np.zeros((len(cpl), CP_FIELDS), np.float64)
+        if len(cpl):
+            crec[:, 0] = 1.0
+            crec[:, 1:] = stages.chunks([pl.chunk_off[2 * c + k] for c in cpl for k in (0, 1)],
+                                        [pl.chunk_len[2 * c + k] for c in cpl for k in (0, 1)])
+        pump()
+        st.update(full=full, have=have, energy=energy, active=active, prior=prior, crec=crec)
+
+    _, err = _try(phase1) if err is None else (None, err)
+    gtab = gather(cw, st.get("wl_row", []), st.get("rec"), cw_cnt, cw_all, sp.n_wrows, W_FIELDS, err)       # C1b
+    ctab = gather(cc, st.get("cpl_row", []), st.get("crec"), cc_cnt, cc_all, sp.n_crows, CP_FIELDS, None)
+    pump()
+
+    # ---- phase 2: every record in plan order, then consensus on the owner of each pair
+    pl, full, have = st["pl"], st["full"], st["have"]
+    full[st["wl"]] = st["rec"]
+    if gtab is not None:
+        fill(full, have, gtab)
+    cps = np.zeros((pl.n_cp, CP_FIELDS - 1), np.float64)
+    got = np.zeros(pl.n_cp, bool)
+    if len(st["cpl"]):
+        cps[st["cpl"]] = st["crec"][:, 1:]
+        got[st["cpl"]] = True
+    for j, b in enumerate(pairs):
+        if sp.split[b] and p.compute_pitch:
+            c0, c1 = pl.pair_chunks[j]
+            for k in range(c1 - c0):
+                if not got[c0 + k]:
+                    row = ctab[sp.crow[b] + k]
+                    if row[0] != 1.0:
+                        raise ShardError(f"chunk-pair record of pair {b} missing from the exchange")
+                    cps[c0 + k] = row[1:]
+    owned = [j for j, b in enumerate(pairs) if sp.owner[b] == r]
+    res = _consensus(stages, p, pl, st["align"], st["active"], st["energy"], full, st["prior"], cps, owned)
+    return [(pairs[j], o) for j, o in zip(owned, res)]
+
+
+def _consensus(stages, p: Params, pl, align, active, energy, full, prior, cps, owned: List[int]) -> list:
+    """Bootstraps, IBI pass and host assembly of the held pairs ``owned`` (plan indices)."""
     B, n_cp = pl.B, pl.n_cp
     w0, w1 = pl.w0, pl.w1
     lags = [int(v) for v in cps[:, 0]] if n_cp else []
@@ -319,14 +654,14 @@ def _consensus(stages, p: Params, pl, align, active, energy, table, prior, cps, 
     nj = B + n_pj
     bout = np.full(3 * nj, np.nan)
     sout = np.full(3 * max(1, n_pj), np.nan)
-    bpm, nbeats = table[:, W_BPM], table[:, W_NBEATS]
+    bpm, nbeats = full[:, R_BPM], full[:, R_NBEATS]
 
     def valid_tempos(f):
         return [bpm[w] for w in range(w0[f], w1[f]) if active[w] and nbeats[w] >= MIN_BEATS and bpm[w] > 0
                 and math.isfinite(bpm[w])]
 
     tempo_jobs, pitch_jobs, shift_jobs = [], [], []
-    for b in range(plo, phi):
+    for b in owned:
         nt, st = valid_tempos(2 * b), valid_tempos(2 * b + 1)
         if len(nt) >= C.MIN_VALID and len(st) >= C.MIN_VALID:
             tempo_jobs.append((b, (np.array(nt), np.array(st))))
@@ -344,7 +679,7 @@ def _consensus(stages, p: Params, pl, align, active, energy, table, prior, cps, 
     ibi = None
     if p.compute_ibi:
         # hop-64 pass of the owned pairs' files (nc with the pair prior, src with 120)
-        files = [f for b in range(plo, phi) for f in (2 * b, 2 * b + 1)]
+        files = [f for b in owned for f in (2 * b, 2 * b + 1)]
         sb = np.array([prior[f // 2] if f % 2 == 0 else 120.0 for f in files])
         ibis, nibi, nb, lg = stages.ibi(pl.f_off[files], pl.f_len[files], sb)
         nF = 2 * B
@@ -353,8 +688,8 @@ def _consensus(stages, p: Params, pl, align, active, energy, table, prior, cps, 
         for k, f in enumerate(files):
             ibi["nibi"][f] = nibi[k]
             ibi["nbeats"][f], ibi["lag"][f] = nb[k], lg[k]
-        jobs = [(b, (ibis[2 * (b - plo) + 1], ibis[2 * (b - plo)])) for b in range(plo, phi)
-                if ibis[2 * (b - plo)] is not None and ibis[2 * (b - plo) + 1] is not None]
+        jobs = [(b, (ibis[2 * i + 1], ibis[2 * i])) for i, b in enumerate(owned)
+                if ibis[2 * i] is not None and ibis[2 * i + 1] is not None]
         for (b, _), (pt, (lo_, hi_)) in zip(jobs, stages.bootstrap([j for _, j in jobs], 42)):
             ibi["out"][b], ibi["out"][B + b], ibi["out"][2 * B + b] = pt, lo_, hi_
 
@@ -365,20 +700,28 @@ def _consensus(stages, p: Params, pl, align, active, energy, table, prior, cps, 
          "sout_l": sout.tolist(), "bout_l": bout.tolist(), "tuning": tun, "chroma": chroma,
          "cmargin": cps[:, 27].copy() if n_cp else np.zeros(0),
          "bpm_l": bpm.tolist(), "nbeats_l": [int(v) for v in nbeats], "prior_l": prior.tolist(),
-         "margin": table[:, W_MARGIN]}
+         "margin": full[:, R_MARGIN]}
     starts_l = [s.tolist() for s in pl.starts]
     w0l, w1l = [int(v) for v in w0], [int(v) for v in w1]
     return [assemble_pair(b, p, h, ibi, starts_l, w0l, w1l, pl.f_len, pl.strip_len, pl.lead, pl.trail,
                           pl.intro[b], pl.win_n, pl.pair_chunks, n_cp, nj, n_pj, align[b] if align else None)
-            for b in range(plo, phi)]
+            for b in owned]
 
 
 def run_window_sharded(pairs: Sequence[Tuple[np.ndarray, np.ndarray]], p: Optional[Params] = None,
-                       group=None, device: Optional[int] = None) -> List[PairOutcome]:
-    """Upload every (nc, src) pair to this rank's GPU and run ``analyze_sharded``."""
+                       group=None, device: Optional[int] = None, split_offset: float = 0.0,
+                       gather: bool = True):
+    """Upload the (nc, src) pairs this rank touches to its GPU and run ``analyze_sharded``
+    (``pairs`` may hold every pair of the batch; only the touched ones are uploaded)."""
     from .engine import get_engine
     eng = get_engine(device)
-    flat = []
-    for nc, src in pairs:
-        flat += [np.asarray(nc, np.float32), np.asarray(src, np.float32)]
-    return analyze_sharded(DeviceStages(eng, eng.upload_signals(flat)), p, group)
+    p = p or Params()
+    world = dist.get_world_size(group) if dist.is_available() and dist.is_initialized() else 1
+    rank = dist.get_rank(group) if dist.is_available() and dist.is_initialized() else 0
+    lengths = [len(a) for nc, src in pairs for a in (nc, src)]
+    touched = shard_plan(lengths, p, world, split_offset).touched(rank)
+    flat = [np.asarray(a, np.float32) for b in touched for a in pairs[b]]
+    sig = eng.upload_signals(flat) if flat else DeviceSignals(torch.zeros(64, device=eng.dev),
+                                                             np.zeros(0, np.int64), np.zeros(0, np.int64))
+    return analyze_sharded(DeviceStages(eng, sig), p, group, lengths=lengths, local_pairs=touched,
+                           split_offset=split_offset, gather=gather)

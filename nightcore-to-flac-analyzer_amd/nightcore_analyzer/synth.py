@@ -86,6 +86,12 @@ def make_pair(seconds: float = 180.0, seed: int = 1000, kind: str = "chords",
     return nc, src
 
 
+def pair_lengths(seconds: float = 180.0, up: int = 4, down: int = 5):
+    """(nightcore, source) lengths of make_pair(seconds, ...) without making the pair."""
+    n = int(round(seconds * SR))
+    return -(-n * up // down), n
+
+
 def make_batch(n_pairs: int, seconds: float = 180.0, base_seed: int = 1000, kind: str = "chords"):
     """Config-3/4 style batch: pair i uses seed base_seed + i."""
     return [make_pair(seconds, base_seed + i, kind) for i in range(n_pairs)]

@@ -14,7 +14,7 @@ from typing import Callable, List, Optional
 
 import numpy as np
 
-from .io import AudioWindow
+from .io import SAMPLE_RATE, AudioWindow
 
 MIN_BEATS: int = 4
 AGREEMENT_TOLERANCE: float = 0.08
@@ -23,9 +23,21 @@ IBI_HOP_LENGTH: int = 64
 IBI_MIN_IBIS: int = 4
 
 
+def require_rate(sr, what: str) -> None:
+    """The engine's STFT / mel / tempogram / CQT tables are built for io.SAMPLE_RATE (the
+    rate io.load_audio returns, io.py:44-55).  Another rate raises instead of being
+    analysed with the wrong tables."""
+    if int(sr) != SAMPLE_RATE:
+        raise ValueError(f"{what}: sample rate {sr} Hz is not supported by the MI355X engine, whose tables "
+                         f"are built for {SAMPLE_RATE} Hz; load or resample the audio at {SAMPLE_RATE} Hz "
+                         f"(io.load_audio(path, sr={SAMPLE_RATE}))")
+
+
 def estimate_tempo(window: AudioWindow, start_bpm: float = 120.0) -> Optional[float]:
+    """tempo.py:27-77 for one window, at window.sample_rate."""
     from .engine import get_engine
     from .ops import window_tempos
+    require_rate(window.sample_rate, "estimate_tempo")
     return window_tempos(get_engine(), [window.audio], [start_bpm])[0]
 
 
@@ -35,6 +47,8 @@ def batch_estimate_tempo(windows: List[AudioWindow], log: Optional[Callable[[str
     from .engine import get_engine
     from .ops import window_tempos
     n = len(windows)
+    for w in windows:
+        require_rate(w.sample_rate, "batch_estimate_tempo")
     res = window_tempos(get_engine(), [w.audio for w in windows], [start_bpm] * n) if n else []
     if log:
         for i, w in enumerate(windows):
@@ -47,6 +61,5 @@ def estimate_ibis_global(y: np.ndarray, sr: int, hop_length: int = IBI_HOP_LENGT
                          min_ibis: int = IBI_MIN_IBIS, start_bpm: float = 120.0) -> Optional[np.ndarray]:
     from .engine import get_engine
     from .ops import ibis
-    if sr != 22050:
-        raise NotImplementedError("the engine's tables are built for sr = 22050 (io.SAMPLE_RATE)")
+    require_rate(sr, "estimate_ibis_global")
     return ibis(get_engine(), [y], [start_bpm], hop=hop_length, min_ibis=min_ibis)[0]

@@ -20,6 +20,13 @@ class OracleStages:
         self._wins = []
         self.fail_in = fail_in            # stage name that raises (error-propagation test)
 
+    def restrict(self, files):
+        """The same stages over a subset of the files (the pairs a rank touches)."""
+        o = OracleStages.__new__(OracleStages)
+        f = np.asarray(files, np.int64)
+        o.buf, o.off, o.length, o._wins, o.fail_in = self.buf, self.off[f], self.length[f], [], self.fail_in
+        return o
+
     def _check(self, name):
         if self.fail_in == name:
             raise RuntimeError(f"injected failure in {name}")
@@ -51,6 +58,7 @@ class OracleStages:
         return out
 
     def chunks(self, chunk_off, chunk_len):
+        self._check("chunks")
         out = np.zeros((len(chunk_off) // 2, 28))
         for k in range(len(chunk_off) // 2):
             a = self.buf[chunk_off[2 * k]:chunk_off[2 * k] + chunk_len[2 * k]]

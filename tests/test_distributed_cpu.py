@@ -72,3 +72,46 @@ def test_run_batch_distributed_failing_rank_delivers_its_exception():
         assert res[r][:4] == [("rank", 0, i * 10) for i in range(4)]
         assert all(isinstance(e, ValueError) and str(e) == "rank 1 failed" for e in res[r][4:])
         assert len(res[r]) == 7
+
+
+def test_run_batch_distributed_rejects_unknown_arguments():
+    from nightcore_analyzer.distributed import run_batch_distributed
+    with pytest.raises(ValueError, match="shard must be"):
+        run_batch_distributed([("a.wav", "b.wav")], shard="frames")
+    with pytest.raises(TypeError, match="unexpected keyword"):
+        run_batch_distributed([("a.wav", "b.wav")], shard="windows", windowsec=3.0)
+    with pytest.raises(ValueError, match="pair mode only"):
+        run_batch_distributed([("a.wav", "b.wav")], analyze_fn=len, shard="windows")
+
+
+def _win_worker(rank, world, port, q, paths):
+    import torch.distributed as dist
+    from nightcore_analyzer.distributed import run_batch_distributed
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        out = run_batch_distributed(paths, shard="windows", log=None)
+        q.put((rank, [(type(e).__name__, str(e)) for e in out]))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_window_mode_run_failure_is_every_pairs_result(tmp_path):
+    """Window mode: a file that does not decode (here on every rank, no device needed)
+    comes back as each pair's result on every rank, not as an exception."""
+    import numpy as np
+    good = tmp_path / "ok.npy"
+    np.save(good, np.zeros(22050 * 40, np.float32))
+    paths = [(str(tmp_path / "missing.wav"), str(good)), (str(good), str(good)), (str(good), str(good))]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_win_worker, args=(r, 2, port, q, paths)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in range(2))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert res[0] == res[1]
+    assert len(res[0]) == 3 and all(name == "FileNotFoundError" for name, _ in res[0])

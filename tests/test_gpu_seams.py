@@ -1,0 +1,86 @@
+"""GPU side of the drop-in seams: pitch._cyclic_xcorr_peak for any vector length
+(pitch.py:67-85, nc_xcorr_peak) against a numpy restatement of the reference's loop,
+and the engine lifetime across the sequential analysis threads of the reference's GUI
+(gui/worker.py:16-56: one QThread per analysis)."""
+import threading
+
+import numpy as np
+import pytest
+import torch
+
+from nightcore_analyzer import engine as E
+from nightcore_analyzer import pipeline, pitch, synth
+
+pytestmark = pytest.mark.gpu
+
+
+def _ref_peak(a, b):
+    """pitch.py:76-85 restated: f32 dot products (one f32 FMA chain in j order; the f32 x f32
+    product is exact in f64, so the f64 sum rounded to f32 is the FMA barring a double
+    rounding tie), first argmax."""
+    n = len(a)
+    xc = []
+    for k in range(n):
+        d = np.float32(0.0)
+        r = np.roll(b, -k)
+        for j in range(n):
+            d = np.float32(np.float64(a[j]) * np.float64(r[j]) + np.float64(d))
+        xc.append(d)
+    lag = int(np.argmax(np.array(xc, np.float32)))
+    return lag - n if lag > n // 2 else lag
+
+
+@pytest.fixture(scope="module")
+def eng():
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    return E.get_engine(0)
+
+
+@pytest.mark.parametrize("n", [1, 2, 3, 7, 12, 36, 37, 300, 1000])
+def test_cyclic_xcorr_peak_any_length(eng, n):
+    rng = np.random.default_rng(n)
+    for t in range(6):
+        a = rng.random(n).astype(np.float32)
+        b = np.roll(a, rng.integers(n)) + np.float32(0.01) * rng.random(n).astype(np.float32) if t % 2 else \
+            rng.random(n).astype(np.float32)
+        b = b.astype(np.float32)
+        assert pitch._cyclic_xcorr_peak(a, b) == _ref_peak(a, b), (n, t)
+
+
+def test_cyclic_xcorr_peak_ties_and_nan(eng):
+    a = np.ones(12, np.float32)
+    assert pitch._cyclic_xcorr_peak(a, a) == 0                   # all lags tie: the first (k = 0)
+    b = np.zeros(12, np.float32)
+    b[5] = np.nan
+    assert pitch._cyclic_xcorr_peak(a, b) == 0                   # every xcorr is NaN: np.argmax -> 0
+    a2 = np.zeros(12, np.float32)
+    a2[3] = 1.0
+    b2 = np.zeros(12, np.float32)
+    b2[10] = 1.0                                                  # peak at k = 7 -> wrapped to -5
+    assert pitch._cyclic_xcorr_peak(a2, b2) == _ref_peak(a2, b2) == -5
+
+
+def test_engine_released_with_its_thread():
+    """pipeline.run from 20 sequential threads: one engine per live thread, released when
+    the thread ends; HBM reserved by the caching allocator stays flat."""
+    nc, src = synth.make_pair(40.0, 1003)
+    reserved, live, errs = [], [], []
+    base = E.live_engines()                            # other tests' engines on this (main) thread
+
+    def work():
+        try:
+            pipeline.run(nc, src, log=None)
+        except BaseException as exc:                 # noqa: BLE001 - reported below
+            errs.append(exc)
+
+    for i in range(20):
+        t = threading.Thread(target=work)
+        t.start()
+        t.join()
+        torch.cuda.synchronize()
+        reserved.append(torch.cuda.memory_reserved())
+        live.append(E.live_engines())
+    assert not errs, errs[0]
+    assert max(live) == base, (base, live)             # each thread's engine went with its thread
+    assert reserved[-1] <= reserved[2], reserved      # flat after the first threads warmed the allocator

@@ -1,10 +1,15 @@
 """GPU runs of the window-sharded path (nightcore_analyzer.sharded with DeviceStages):
 
 * one rank: every outcome equals Engine.analyze of the same batch (results, report,
-  logs, per-window detail) — the stage-by-stage path is the same computation;
+  logs, per-window detail) — interior pairs through the pipelined engine;
 * two ranks on the one GPU of the box (gloo for the record exchange, libncgpu for the
   stages): a single pair split over both ranks reproduces the reference's own
-  pipeline.run goldens, on both ranks.
+  pipeline.run goldens, on both ranks;
+* four ranks on the one GPU over a 17-pair batch (3 golden pairs + 14 synthetic pairs of
+  90-200 s) with every block boundary moved into a pair (split_offset): interior pairs
+  through the engine pipeline, split pairs through the stage path and the C1a/C1b
+  exchanges; every outcome equals Engine.analyze of the whole batch on one rank, field
+  for field, on every rank.
 
 The 8-GPU RCCL run is the driver's; here the exchange is the same all_gather_into_tensor
 call on CPU tensors.
@@ -74,35 +79,48 @@ def _free_port():
     return port
 
 
-def _worker(rank, world, port, names, q):
+def _worker(rank, world, port, names, q, split_offset=0.0, full=False):
     import torch.distributed as dist
     from nightcore_analyzer.sharded import run_window_sharded
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        pairs = [make_case(synth, n)[:2] for n in names]
-        outs = run_window_sharded(pairs, E.Params(), device=0)
-        q.put((rank, [(None if o.error is None else str(o.error),
-                       None if o.result is None else _norm(dataclasses.asdict(o.result)),
-                       None if o.result is None else str(o.result), o.logs) for o in outs]))
+        pairs = _batch(names)
+        outs = run_window_sharded(pairs, E.Params(), device=0, split_offset=split_offset)
+        if full:
+            q.put((rank, [_key(o) for o in outs]))
+        else:
+            q.put((rank, [(None if o.error is None else str(o.error),
+                           None if o.result is None else _norm(dataclasses.asdict(o.result)),
+                           None if o.result is None else str(o.result), o.logs) for o in outs]))
     except Exception as exc:     # noqa: BLE001
         q.put((rank, repr(exc)))
     finally:
         dist.destroy_process_group()
 
 
-def test_sharded_two_ranks_one_pair_matches_reference(eng, golden_pipeline):
-    names = ["chords80"]
+def _batch(names):
+    """Golden cases by name; ("syn", seconds, seed) entries are synthetic pairs."""
+    return [synth.make_pair(n[1], n[2]) if isinstance(n, tuple) else make_case(synth, n)[:2] for n in names]
+
+
+def _spawn(world, names, split_offset=0.0, full=False, timeout=240):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, names, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, names, q, split_offset, full)) for r in range(world)]
     for p in procs:
         p.start()
-    res = dict(q.get(timeout=240) for _ in range(2))
+    res = dict(q.get(timeout=timeout) for _ in range(world))
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
+    return res
+
+
+def test_sharded_two_ranks_one_pair_matches_reference(eng, golden_pipeline):
+    names = ["chords80"]
+    res = _spawn(2, names)
     g = golden_pipeline["chords80"]
     for r in (0, 1):
         assert isinstance(res[r], list), res[r]
@@ -112,3 +130,24 @@ def test_sharded_two_ranks_one_pair_matches_reference(eng, golden_pipeline):
         for k, v in g["result"].items():
             assert result[k] == v, k
         assert text == g["str"]
+
+
+SEVENTEEN = ["chords80", "sweep30", "sweep30_nc_tail_quiet"] + \
+    [("syn", float(s), 1100 + i) for i, s in enumerate((180, 90, 200, 120, 180, 150, 95, 180, 130, 175, 110, 160, 180,
+                                                        140))]
+
+
+def test_sharded_four_ranks_seventeen_pairs_equal_engine(eng):
+    """four ranks (gloo) on the one GPU, split pairs at every block
+    boundary; all 17 outcomes equal Engine.analyze of the batch, field for field."""
+    from nightcore_analyzer.sharded import shard_plan
+    pairs = _batch(SEVENTEEN)
+    sp = shard_plan([len(a) for pr in pairs for a in pr], E.Params(), 4, 0.45)
+    assert sp.split.sum() == 3 and len(set(sp.owner.tolist())) == 4
+    ref = [_key(o) for o in eng.analyze(pairs, E.Params())]
+    res = _spawn(4, SEVENTEEN, split_offset=0.45, full=True, timeout=110)
+    for r in range(4):
+        assert isinstance(res[r], list), res[r]
+        assert len(res[r]) == len(ref)
+        for i, (a, b) in enumerate(zip(res[r], ref)):
+            assert _norm(list(a)) == _norm(list(b)), (r, i)

@@ -11,6 +11,7 @@ import math
 import os
 import socket
 
+import numpy as np
 import pytest
 import torch.multiprocessing as mp
 
@@ -38,7 +39,7 @@ def _norm(x):
     return x
 
 
-def _worker(rank, world, port, names, q, fail_rank, fail_in):
+def _worker(rank, world, port, names, q, fail_rank, fail_in, split_offset=0.0):
     import torch.distributed as dist
     from nightcore_analyzer.engine import Params
     from nightcore_analyzer.sharded import analyze_sharded
@@ -48,7 +49,7 @@ def _worker(rank, world, port, names, q, fail_rank, fail_in):
     try:
         pairs = [make_case(synth, n)[:2] for n in names]
         st = OracleStages(pairs, fail_in=fail_in if rank == fail_rank else None)
-        outs = analyze_sharded(st, Params())
+        outs = analyze_sharded(st, Params(), split_offset=split_offset)
         q.put((rank, "ok", [(None if o.error is None else (type(o.error).__name__, str(o.error)),
                              None if o.result is None else _norm(dataclasses.asdict(o.result)),
                              None if o.result is None else str(o.result), o.logs) for o in outs]))
@@ -58,11 +59,12 @@ def _worker(rank, world, port, names, q, fail_rank, fail_in):
         dist.destroy_process_group()
 
 
-def _run(world, names, fail_rank=-1, fail_in=None):
+def _run(world, names, fail_rank=-1, fail_in=None, split_offset=0.0):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, names, q, fail_rank, fail_in)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, names, q, fail_rank, fail_in,
+                                                                split_offset)) for r in range(world)]
     for p in procs:
         p.start()
     res = dict((r, (kind, v)) for r, kind, v in (q.get(timeout=300) for _ in range(world)))
@@ -77,6 +79,9 @@ def _check_golden(outs, names, golden):
     for (err, res, text, logs), n in zip(outs, names):
         g = golden[n]
         assert logs == g["log"][N_LOAD_LINES:], n
+        if "error" in g:                      # run() raises: the outcome carries the same exception
+            assert err == (g["error"]["type"], g["error"]["message"]), (n, err)
+            continue
         assert err is None, (n, err)
         for k, v in g["result"].items():
             assert res[k] == v, (n, k)
@@ -93,6 +98,50 @@ def test_window_sharded_matches_reference_goldens(golden_pipeline, world, names)
 
 
 def test_window_sharded_failure_raises_on_every_rank():
-    res = _run(2, ["sweep30"], fail_rank=1, fail_in="tempo")
-    assert res[1] == ("raised", ("RuntimeError", "injected failure in tempo"))
+    # sweep30 on 2 ranks: rank 0 holds the 8 windows, rank 1 the chunk pair (shard_plan)
+    res = _run(2, ["sweep30"], fail_rank=1, fail_in="chunks")
+    assert res[1] == ("raised", ("RuntimeError", "injected failure in chunks"))
     assert res[0][0] == "raised" and res[0][1][0] == "ShardError"
+
+
+def test_shard_plan_blocks():
+    """The item plan: every slot on exactly one rank, contiguous pair-major blocks of nearly
+    equal cost, owners non-decreasing, and no split pair when the blocks align with pairs."""
+    from nightcore_analyzer.engine import Params
+    from nightcore_analyzer.sharded import CP_COST, shard_plan
+    p = Params()
+    L = [3175200, 3969000] * 16                    # 16 equal 3-min pairs (config 3/4 shape)
+    for world in (1, 2, 4, 8):
+        sp = shard_plan(L, p, world)
+        assert not sp.split.any() and sp.n_wrows == 0
+        assert [len(sp.owned(r)) for r in range(world)] == [16 // world] * world
+    sp = shard_plan(L, p, 4, split_offset=0.5)     # every inner boundary through a pair's middle
+    assert sp.split.sum() == 3 and sp.n_wrows == 3 * 62 and sp.n_crows == 3 * 7
+    lens = [int(x) for x in np.random.default_rng(5).integers(200_000, 4_000_000, 22)]
+    for world, off in ((3, 0.0), (5, 0.3), (7, 0.9)):
+        sp = shard_plan(lens, p, world, off)
+        cover = np.zeros_like(sp.slots)
+        for r in range(world):
+            cover += sp.rng[:, :, r, 1] - sp.rng[:, :, r, 0]
+        assert np.array_equal(cover, sp.slots)
+        assert np.all(np.diff(sp.owner) >= 0)
+        rows = np.concatenate([sp.contrib_w(r) for r in range(world)])
+        assert np.array_equal(np.sort(rows), np.arange(sp.n_wrows))
+        cost = [(sp.rng[:, 0, r, 1] - sp.rng[:, 0, r, 0] + sp.rng[:, 1, r, 1] - sp.rng[:, 1, r, 0]).sum()
+                + CP_COST * (sp.rng[:, 2, r, 1] - sp.rng[:, 2, r, 0]).sum() for r in range(world)]
+        if off == 0.0:
+            assert max(cost) - min(cost) <= 2 * CP_COST, cost
+        for b in range(sp.B):
+            assert sp.owner[b] in [r for r in range(world) if sp.on_rank(b, r)] or sp.slots[b].sum() == 0
+
+
+def test_window_sharded_split_pairs_match_reference_goldens(golden_pipeline):
+    """Four pairs on three ranks with every block boundary moved into a pair: split pairs
+    exchange their window and chunk-pair records (C1a, C1b); an error-path pair raises the
+    reference's ValueError with its logs."""
+    names = ["chords80", "sweep30", "sweep30_nc_tail_quiet", "chords80"]
+    res = _run(3, names, split_offset=0.37)
+    for r in range(3):
+        kind, outs = res[r]
+        assert kind == "ok", (r, outs)
+        _check_golden(outs, names, golden_pipeline)
