@@ -82,11 +82,11 @@ def synth_lengths(seconds):
 
 
 def _pmc_traffic(kernel_tag):
-    """HBM bytes per launch of the dominant kernel from the committed rocprofv3 PMC pass
-    (profiles/*_traffic.json, FETCH_SIZE x 2 + WRITE_SIZE per MI355X_MICROARCH.md), if one
+    """HBM bytes per launch of a kernel from the newest committed rocprofv3 PMC pass
+    (profiles/r*_traffic.json, FETCH_SIZE x 2 + WRITE_SIZE per MI355X_MICROARCH.md), if one
     exists for this workload; counters cannot be read from inside a timed run."""
     best = None
-    for f in sorted((REPO / "profiles").glob("*_traffic.json")):
+    for f in sorted((REPO / "profiles").glob("r*_traffic.json")):
         try:
             d = json.loads(f.read_text())
         except ValueError:
@@ -357,12 +357,21 @@ def main():
         a = alg / (avg_ms * 1e-3) / 1e9
         c = flop / (avg_ms * 1e-3) / 1e12
         cb, cp = compute_roof.get(tag, ("valu_f32", VALU_PEAK_TFS))
+        tr = _pmc_traffic(tag)
         out = {"bound": "hbm", "kernel": tag, "achieved": a, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-               "frac": a / HBM_PEAK_GBS, "traffic": None, "alg_bytes_per_launch": alg, "avg_launch_ms": avg_ms,
+               "frac": a / HBM_PEAK_GBS, "traffic": tr["bytes_per_launch"] if tr else None,
+               "traffic_source": tr["source"] if tr else None, "alg_bytes_per_launch": alg, "avg_launch_ms": avg_ms,
                "launches_per_step": launches,
                # the roof that actually binds: VALU / f64 VALU / matrix cores
                "compute": {"bound": cb, "achieved": c, "peak": cp, "unit": "TFLOP/s",
                            "frac": c / cp, "alg_flop_per_launch": flop}}
+        if tag == "cqt_chroma":
+            # the MFMA figures count the three split products; the useful contraction is one of
+            # them (7 x 862 x 1024 x 72 x 2 flop per chunk)
+            out["cqt_dtype"] = "f16x3 split operands (hi/lo, ~22-bit), f32 accumulate"
+            out["compute"]["useful_frac"] = c / 3.0 / cp
+            out["compute"]["useful_achieved"] = c / 3.0
+            out["parts_ms"] = {k: times[k][0] for k in ("cqt_low", "cqt_high") if k in times}
         return out
 
     # the dominant kernel = the largest total execution time per step among the kernels with a
@@ -370,9 +379,6 @@ def main():
     # always reported beside it
     dom = max(units, key=lambda k: kper.get(k, (0, 0))[0] * kper.get(k, (0, 0))[1])
     roofline = roof(dom, kper)
-    traffic = _pmc_traffic(dom)
-    if traffic:
-        roofline.update(traffic=traffic["bytes_per_launch"], traffic_source=traffic["source"])
     if dom != "cqt_chroma" and "cqt_chroma" in kper:
         roofline["cqt_chroma"] = roof("cqt_chroma", kper)
     # the per-window tempogram kernel against its f64 roof (its bytes are the S_db scratch)
@@ -595,6 +601,8 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "f32",
+            "arithmetic": {"stft_mel / tuning FFTs": "f32 (VALU)", "tempogram, decisions, bootstrap": "f64",
+                           "cqt": "f16x3 split operands (hi/lo, ~22-bit) on the matrix cores, f32 accumulate"},
             "data": "synthetic (SURVEY.md §8d chords+clicks+noise, nc = resample_poly(src, 4, 5)), resident in HBM"
                     + (f"; REHEARSAL: {world} ranks on {torch.cuda.device_count()} GPU(s), gloo" if rehearse else ""),
             "config": {"workload": ("config 3: per GPU a batch of 64 x 3-min 22.05 kHz mono pairs" if world == 1 else

@@ -35,7 +35,7 @@ extern "C" {
 
 typedef struct nc_ctx nc_ctx;
 
-#define NCGPU_ABI_VERSION 2
+#define NCGPU_ABI_VERSION 3  /* 3: tuning decision margin outputs (nc_chroma_mean*), nc_xcorr_peak */
 
 int nc_abi_version(void);
 const char* nc_last_error(void);
@@ -134,13 +134,17 @@ int nc_ibi_from_beats(nc_ctx* ctx, const int* beats, const int64_t* off, const i
  * octave decimation by the engine's half-band FIR in place of soxr_hq) ->
  * 12-bin chroma (n_chroma = 12: the reference's lag/3 quirk) ->
  * per-frame inf-norm -> mean.  out_chroma[c*12 + k] (f32), out_tuning[c]
- * (f32, bins), out_tuning_idx[c] (nullable; index on the 0.01 grid).
+ * (f32, bins), out_tuning_idx[c] (nullable; index on the 0.01 grid),
+ * out_tuning_margin[c] (nullable; the tuning decision's margin: the argmax bin's
+ * residual count minus the runner-up's, 0 on a tie broken by np.argmax's first-index
+ * rule, 0 when no peak passes the threshold).
  * total_len = sum of chunk_len; max_chunk_len = max of chunk_len.
  * ------------------------------------------------------------------------- */
 size_t nc_chroma_workspace_bytes(const nc_ctx* ctx, int n_chunks, int64_t total_len);
 int nc_chroma_mean(nc_ctx* ctx, const float* sig, const int64_t* chunk_off, const int64_t* chunk_len,
                    int n_chunks, int64_t total_len, int64_t max_chunk_len, float* out_chroma,
-                   float* out_tuning, int* out_tuning_idx, void* ws, size_t ws_bytes, void* stream);
+                   float* out_tuning, int* out_tuning_idx, int* out_tuning_margin, void* ws, size_t ws_bytes,
+                   void* stream);
 
 /* ---------------------------------------------------------------------------
  * K9-K11 with shared tuning frames (optional fusion; same results as the pair
@@ -165,7 +169,8 @@ int nc_window_stage_tuning(nc_ctx* ctx, const float* sig, const int64_t* win_off
                            void* stft_done_event, void* ws, size_t ws_bytes, void* stream);
 int nc_chroma_mean_shared(nc_ctx* ctx, const float* sig, const int64_t* chunk_off, const int64_t* chunk_len,
                           int n_chunks, int64_t total_len, int64_t max_chunk_len, float* out_chroma,
-                          float* out_tuning, int* out_tuning_idx, const int* tf_skip, int64_t tf_skip_total,
+                          float* out_tuning, int* out_tuning_idx, int* out_tuning_margin, const int* tf_skip,
+                          int64_t tf_skip_total,
                           float* peak_pitch, float* peak_mag, int* chunk_npk, void* wait_event, void* ws,
                           size_t ws_bytes, void* stream);
 /* pitch._cyclic_xcorr_peak (pitch.py:67-85): lag_out[p] = wrapped argmax_k

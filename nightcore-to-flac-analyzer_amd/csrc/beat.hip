@@ -290,10 +290,7 @@ __global__ __launch_bounds__(NT) void tempo_beat_kernel(BeatArgs a) {
   const int B = max(1, min(dmin, NT / 2));
   const int D = dmax - dmin + 1;
   // chunk length and fold length both ~sqrt(D): the scan and the fold are serial per thread
-#ifndef NC_BEAT_GCAP
-#define NC_BEAT_GCAP 64
-#endif
-  const int Gn = max(1, min(min(NT / B, NC_BEAT_GCAP), (int)ceil(sqrt((double)D))));
+  const int Gn = max(1, min(min(NT / B, 64), (int)ceil(sqrt((double)D))));
   const int C = (D + Gn - 1) / Gn;
   // long sequences: the DP reads cum[i - d] for d in [dmin, dmax] only, so the last ring_cap
   // (>= dmax + B) scores are kept in an LDS ring instead of being re-read from L2 per candidate

@@ -11,10 +11,10 @@
 //   1. decimate3_kernel x2    y_{i+1} = sqrt(2) * halfband(y_i)[::2], three levels per launch
 //   2. tuning_peaks_kernel    STFT 2048/512 (Hann) -> piptrack peaks, appended per chunk
 //   3. tuning_select_kernel   median(mag) -> residual histogram (0.01 bins) -> tuning index
-//   4. cqt_chroma_kernel      (frame pair, octave) items per wave: two rect 1024 frames as one
-//                             complex FFT 1024, separated in registers -> sparse basis[tuning]
-//                             (register weights) -> |C|/sqrt(len) -> 12-bin chroma -> inf-norm
-//                             -> per-block partial sums (f64)
+//   4. cqt_mfma_low_kernel    octaves 0-2, cqt_mfma_kernel octaves 3-6: per octave the GEMM
+//                             [frames x 1024] . [1024 x 72] on the f16 matrix cores (hi/lo split
+//                             operands) -> |C|/sqrt(len) -> per-octave chroma partial rows;
+//                             cqt_tail_kernel: 12-bin chroma -> inf-norm -> per-tile f64 sums
 //   5. chroma_finalize_kernel mean over frames -> f32[12] per chunk
 //   6. chroma_lag_kernel      argmax_k dot(src, roll(nc, -k)), wrapped to [-5, 6]
 #include <algorithm>
@@ -97,10 +97,7 @@ __global__ __launch_bounds__(256) void chroma_plan_kernel(const int64_t* chunk_l
 // 0.77 ms per bench step (isolated); 512-output tiles (26 KB LDS) were as fast alone but
 // co-resided worse with stft_mel on the other stream (step 14.5 -> 15.5 ms); 256 (14 KB)
 // gave 14.1 ms.
-#ifndef NC_D3_T  // level-(base + 3) outputs per decimate3 workgroup
-#define NC_D3_T 256
-#endif
-constexpr int D3_T = NC_D3_T;
+constexpr int D3_T = 256;               // level-(base + 3) outputs per decimate3 workgroup
 constexpr int D3_N1 = 4 * D3_T + 144;  // level base+1 values computed (from 4 m0 - 72)
 constexpr int D3_N2 = 2 * D3_T + 48;   // level base+2 values computed (from 2 m0 - 24)
 constexpr int D3_P0 = 4 * D3_T + 168;  // level base pairs staged (values from 8 m0 - 168)
@@ -169,14 +166,9 @@ __device__ __forceinline__ void d3_level(const float* E, const float* O, int cnt
 // The level-base input of a tile is requested as D3_LD float4 loads per thread, all issued
 // before any is staged (one global latency per tile instead of one per load; 276 -> 242 us
 // per 224 chunks).  Walking several tiles per workgroup with the next tile's loads in
-// flight during the levels (NC_D3_TPW > 1) measures slower, 355 against 228 us: the tile
-// loop moves the taps out of SGPRs and the kernel to 105 VGPRs, four waves per SIMD
-// instead of eight.
+// flight during the levels measured slower (round 2: 355 against 228 us; the tile loop moves
+// the taps out of SGPRs and the kernel to 105 VGPRs, four waves per SIMD instead of eight).
 constexpr int D3_LD = (D3_P0 / 2 + 255) / 256;  // float4 input loads per thread per tile
-#ifndef NC_D3_TPW  // consecutive tiles per workgroup, the next one's input loaded during the levels
-#define NC_D3_TPW 1
-#endif
-constexpr int D3_TPW = NC_D3_TPW;
 
 // the f32 taps by value: kernel arguments are scalar loads, so the taps stay in SGPRs
 // (v_fmac takes one SGPR operand) instead of holding ~37 VGPRs for the whole kernel
@@ -195,8 +187,8 @@ __global__ __launch_bounds__(256) void decimate3_kernel(const float* sig, const 
   __shared__ float wmax[4];
   const int c = blockIdx.y;
   const int64_t* len = oct_len + c * 7 + base;
-  const int64_t mb = (int64_t)blockIdx.x * (D3_TPW * D3_T);
-  if (mb >= len[3]) return;
+  const int64_t m0 = (int64_t)blockIdx.x * D3_T;
+  if (m0 >= len[3]) return;
   const float (&h)[2 * kHalfbandK + 1] = taps.h;
   const float* in = base == 0 ? sig + chunk_off[c] : ws_oct + oct_off[c * 7 + base];
   const int64_t L0 = len[0];
@@ -226,13 +218,8 @@ __global__ __launch_bounds__(256) void decimate3_kernel(const float* sig, const 
     }
   };
   float4 pf[D3_LD];
-  float bmax = 0.0f;
-  load_tile(mb, pf);
-#pragma unroll 1
-  for (int tt = 0; tt < D3_TPW; ++tt) {
-    const int64_t m0 = mb + (int64_t)tt * D3_T;
-    if (m0 >= len[3]) break;
-    if (tt) __syncthreads();  // the previous tile's last level has read e0/o0
+  load_tile(m0, pf);
+  {
     float m = 0.0f;  // max |level 0| over the tile's input (the MFMA CQT's f16 scale)
 #pragma unroll
     for (int k = 0; k < D3_LD; ++k) {
@@ -250,12 +237,8 @@ __global__ __launch_bounds__(256) void decimate3_kernel(const float* sig, const 
     __syncthreads();
     // one maximum per workgroup, no atomics: slot c + oct_off[c][3] / 256 + blockIdx.x (distinct
     // per chunk; read back by cqt_mfma_kernel)
-    if (base == 0 && xmax && threadIdx.x == 0) {
-      bmax = fmaxf(bmax, fmaxf(fmaxf(wmax[0], wmax[1]), fmaxf(wmax[2], wmax[3])));
-      xmax[c + oct_off[c * 7 + 3] / 256 + blockIdx.x] = bmax;
-    }
-    // the next tile's input is in flight while this one's levels run
-    if (tt + 1 < D3_TPW && m0 + D3_T < len[3]) load_tile(m0 + D3_T, pf);
+    if (base == 0 && xmax && threadIdx.x == 0)
+      xmax[c + oct_off[c * 7 + 3] / 256 + blockIdx.x] = fmaxf(fmaxf(wmax[0], wmax[1]), fmaxf(wmax[2], wmax[3]));
     // level base+1: [4 m0 - 72, +D3_N1), owned [4 m0, 4 m0 + 4 T); phases -> e1/o1
     d3_level(e0, o0, D3_N1, 4 * m0 - 72, len[1], h, e1, o1, out1, 72, 4 * D3_T);
     __syncthreads();
@@ -274,10 +257,7 @@ __global__ __launch_bounds__(256) void decimate3_kernel(const float* sig, const 
 // peaks of a frame are appended to its chunk's region (peak_*[tf_base[c] * kPeakSlots ..])
 // at an atomically reserved position: the median and the histogram that consume them
 // do not depend on the order, so the result stays deterministic.
-#ifndef NC_TP_WAVES
-#define NC_TP_WAVES 16  // 14 -> 16 waves: 537 -> 495 us per 224 chunks (with the LDS Hann window)
-#endif
-constexpr int TP_WAVES = NC_TP_WAVES;
+constexpr int TP_WAVES = 16;  // 14 -> 16 waves: 537 -> 495 us per 224 chunks (with the LDS Hann window)
 using TpTw = StagedTw<1024>;
 
 struct PeakArgs {
@@ -382,9 +362,7 @@ __global__ __launch_bounds__(TP_WAVES * 64) void tuning_peaks_kernel(PeakArgs a)
 // 1024 threads per chunk: 79.8 -> 34.9 us per 224 chunks against 256 (the passes are
 // latency-bound loops over the peak list; wave-aggregated top-byte counts, which remove
 // the LDS same-address conflicts, measured no better)
-#ifndef NC_TS_NT
-#define NC_TS_NT 1024
-#endif
+constexpr int TS_NT = 1024;
 __device__ __forceinline__ int tuning_bin(float r) {
   // np.histogram(residual, linspace(-0.5, 0.5, 101)) bin of r (exact edge comparisons in f64)
   const double rd = (double)r;
@@ -421,7 +399,7 @@ __device__ __forceinline__ int wave_incl_scan_i(int v) {
 template <int NT>
 __global__ __launch_bounds__(NT) void tuning_select_kernel(const float* peak_pitch, const float* peak_mag,
                                                            const int* chunk_npk, const int64_t* tf_base,
-                                                           int* tuning_idx, float* tuning_val,
+                                                           int* tuning_idx, float* tuning_val, int* tuning_margin,
                                                            unsigned long long* span) {
   const Span span_(span);
   __shared__ BlockScratch<NT> bs;
@@ -511,375 +489,49 @@ __global__ __launch_bounds__(NT) void tuning_select_kernel(const float* peak_pit
     }
     tuning_idx[c] = best;
     tuning_val[c] = (float)((double)best * (1.0 / 100.0) + (-0.5));
+    if (tuning_margin) {  // decision margin: argmax count minus the runner-up's (0 = tie, first index won)
+      int second = -1;
+      for (int j = 0; j < 100; ++j)
+        if (j != best) second = max(second, counts[j]);
+      tuning_margin[c] = nsel > 0 ? counts[best] - second : 0;
+    }
   }
 }
 
-// ------------------------------------------------------------------------------ 4. CQT + chroma
-// One workgroup per (chunk, CQ_FR frames).  Work items are (frame pair, octave), one per
-// wave: the two real 1024-sample rect frames t, t+1 of the octave signal are packed as
-// z = x_t + i x_{t+1} into ONE 1024-point complex FFT (Stockham 16.16 through the wave's
-// LDS slot, then the last radix-4 stage on the lane's butterfly set
-// J = {l, 128-l, 128+l, 256-l} (lane 0: {0, 64, 192, 128}), which holds every output
-// k < 256 together with its mirror 1024 - k, so the two spectra separate in registers:
-//   X_t[k] = (Z[k] + conj Z[N-k]) / 2,   X_{t+1}[k] = (Z[k] - conj Z[N-k]) / 2i.
-// Only the bins the basis rows touch, [klo, khi], are written back (one float4 per bin
-// holding both frames, doubled: the row weights carry the 1/2); each lane's piece of a sparse row (weights in registers, loaded
-// once per workgroup for the chunk's tuning) reads them with 16-byte loads.  Per row
-// |C| sqrt(sr/my_sr) / sqrt(len) goes to an LDS row tile; then per frame the 12-bin
-// chroma (bins 3c-1, 3c, 3c+1 of each octave, ascending), its inf-norm and the f64 sum
-// over the workgroup's frames.
-#ifndef NC_CQ_WAVES
-#define NC_CQ_WAVES 16
-#endif
-#ifndef NC_CQ_DIAG  // diagnostic variants only (tools/var_build.sh): 1 no basis, 2 no loads, 4 no chroma tail
-#define NC_CQ_DIAG 0  // 8 no D writes, 16 constant stage-3 twiddles, 32 stage-3 inputs from registers
-#endif
-#ifndef NC_CQ_PREFETCH
-#define NC_CQ_PREFETCH 0
-#endif
-#ifndef NC_CQ_FR
-#define NC_CQ_FR 32
-#endif
-#ifndef NC_CQ_TB  // basis taps per batch of LDS loads (0: one tap at a time, per-lane guarded)
-#define NC_CQ_TB 2  // measured per 224 chunks: 0 -> 1158-1171 us, 2 -> 1144, 4/8 -> 1152
-#endif
-#ifndef NC_CQ_BPW
-#define NC_CQ_BPW 3
-#endif
-constexpr int CQ_WAVES = NC_CQ_WAVES;
-constexpr int CQ_FR = NC_CQ_FR;    // frames per block: CQ_FR / 2 * 7 (frame pair, octave) items
-constexpr int CQ_BPW = NC_CQ_BPW;  // consecutive blocks of one chunk per workgroup (persistent)
-constexpr int CQ_PMAX = 16;          // register-resident taps per lane piece (checked at launch)
-constexpr int CQ_TW2 = 15 * 16;      // stage-2 twiddles W_256^{k r}, [r - 1][k]
-
-struct CqtArgs {
-  const float* sig;
-  const int64_t* chunk_off;
-  const int64_t* oct_off;
-  const int64_t* oct_len;
-  const int* n_frames;
-  const int* tuning_idx;
-  const float* ws_oct;
-  const int64_t* tf_base;  // partial rows of chunk c start at tf_base[c] / CQ_FR + c
-  const float2* tw;        // exp(-2 pi i m / 8192)
-  const float* cqt_isl;
-  const int* cqt_plo;      // [tuning][64] lane pieces (nc_tables.cpp)
-  const int* cqt_plen;
-  const int* cqt_partner;  // [tuning][64]
-  const int* cqt_pfilt;    // [tuning][64]
-  const float2* cqt_wcol;  // [tuning][pmax][64]
-  int pmax;
-  int klo, khi;            // FFT bins the rows touch
-  double* partial;  // [n][nblk][12]
-  // hybrid mode (gpart non-null): only octaves 0 .. n_oct - 1, whose chroma partial rows go to
-  // gpart[(tf_base[c] + t)][7][12] for cqt_tail_kernel (the MFMA kernel writes the others)
-  float* gpart = nullptr;
-  int n_oct = 7;
-  unsigned long long* span = nullptr;  // nc_profile execution span (nc_device.h)
-};
-
-// butterfly b of lane l in the last stage: {l, 128-l, 128+l, 256-l}, lane 0 {0, 64, 192, 128}
-__device__ __forceinline__ int Jb(int l, int b) {
-  return b == 0 ? l : b == 1 ? (l ? 128 - l : 64) : b == 2 ? (l ? 128 + l : 192) : (l ? 256 - l : 128);
-}
-
-// LDS: stage-2 twiddles | per-lane stage-3 twiddles | row tile [CQ_FR][252] | FFT slots (the
-// chroma tail's [CQ_FR][12] scratch reuses the slots once a block's items are done)
-constexpr int CQ_TILE = 7 * 12;  // per frame: octave partials [bin octave][chroma]
-size_t cqt_lds_bytes() {
-  static_assert(2 * CQ_FR * 12 * sizeof(float) <= LdsSize<1024>::value * sizeof(float2), "tail scratch");
-  return sizeof(float2) * (CQ_TW2 + 12 * 64) + sizeof(float) * (CQ_FR * CQ_TILE + CQ_WAVES * 72) + 16 +
-         sizeof(float2) * (size_t)CQ_WAVES * LdsSize<1024>::value;
-}
-
-__global__ __launch_bounds__(CQ_WAVES * 64) void cqt_chroma_kernel(CqtArgs a) {
-  const Span span_(a.span);
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  constexpr int NT = CQ_WAVES * 64;
-  const int c = blockIdx.y;
-  const int T = a.n_frames[c];
-  const int nb = (T + CQ_FR - 1) / CQ_FR;
-  const int fb0 = blockIdx.x * CQ_BPW;
-  if (fb0 >= nb) return;
-  const int fb1 = min(nb, fb0 + CQ_BPW);
-  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform (SGPR)
-  float2* sh_tw = reinterpret_cast<float2*>(smem);
-  float2* sh_tw3 = sh_tw + CQ_TW2;                // [12][64] per-lane stage-3 twiddles
-  float* sh_part = reinterpret_cast<float*>(sh_tw3 + 12 * 64);  // [CQ_FR][7][12] octave chroma partials
-  float* sh_mag = sh_part + CQ_FR * CQ_TILE + wave * 72;         // [2][36] this wave's item rows
-  const int fft_f = (int)(sh_part + CQ_FR * CQ_TILE + CQ_WAVES * 72 - reinterpret_cast<float*>(smem) + 3) & ~3;
-  float2* slots = reinterpret_cast<float2*>(reinterpret_cast<float*>(smem) + fft_f);
-  float2* fftbuf = slots + wave * LdsSize<1024>::value;
-  float* sh_ch = reinterpret_cast<float*>(slots);  // [CQ_FR][12], tail only
-  float* sh_nv = sh_ch + CQ_FR * 12;               // [CQ_FR][12], tail only
-  const int ti = a.tuning_idx[c];
-  for (int i = tid; i < CQ_TW2; i += NT) {
-    const int r = i / 16 + 1, k = i % 16;
-    sh_tw[i] = a.tw[(k * r * 32) & 8191];
-  }
-  const float* isl = a.cqt_isl + ti * kCqtBins;
-  // per-lane constants for the whole workgroup: butterfly set, stage-3 twiddles W_1024^{J r},
-  // the lane's row piece and its weights
-  for (int i = tid; i < 12 * 64; i += NT) {  // sh_tw3[(3 b + r - 1) * 64 + l] = W_1024^{J_b(l) r}
-    const int l = i & 63, br = i >> 6, b = br / 3, r = br % 3 + 1;
-    sh_tw3[i] = a.tw[(Jb(l, b) * r * 8) & 8191];
-  }
-  const int plo = a.cqt_plo[ti * 64 + lane] - a.klo, plen = a.cqt_plen[ti * 64 + lane];
-  const int partner = a.cqt_partner[ti * 64 + lane], pfilt = a.cqt_pfilt[ti * 64 + lane];
-  float2 w[CQ_PMAX];
-#pragma unroll
-  for (int j = 0; j < CQ_PMAX; ++j)
-    w[j] = j < plen ? a.cqt_wcol[((size_t)ti * a.pmax + j) * 64 + lane] : make_float2(0.f, 0.f);
-  __syncthreads();
-
-  for (int fb = fb0; fb < fb1; ++fb) {
-  const int t0 = fb * CQ_FR;
-  const int nfr = min(CQ_FR, T - t0);
-  const int npair = (nfr + 1) >> 1;
-  const int no = a.n_oct;  // octaves per frame pair (7, or the FFT share in hybrid mode)
-  const int n_items = npair * no;
-  // the two frames of item `item` in the stage-1 register layout z[l + 64 r]
-  auto load_item = [&](int item, int ln, FftIn<1024>& in) {
-    const int oct = item % no;
-    const int t = t0 + 2 * (item / no);
-    const float* y = oct == 0 ? a.sig + a.chunk_off[c] : a.ws_oct + a.oct_off[c * 7 + oct];
-    const int64_t Ly = a.oct_len[c * 7 + oct];
-    const int hop = 512 >> oct;
-    const int64_t sA = (int64_t)t * hop - 512, sB = sA + hop;
-    if (NC_CQ_DIAG & 2) {
-#pragma unroll
-      for (int r = 0; r < 16; ++r) in[0][r] = make_float2((float)(ln + r), (float)(item - r));
-    } else if (sA >= 0 && sB + 1024 <= Ly) {
-      const float* pa = y + (sA + ln);  // 64 r floats = immediate offsets of one base address
-      const float* pb = pa + hop;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) in[0][r] = make_float2(pa[64 * r], pb[64 * r]);
-    } else {
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int64_t ia = sA + ln + 64 * r, ib = sB + ln + 64 * r;
-        in[0][r] = make_float2((ia >= 0 && ia < Ly) ? y[ia] : 0.0f, (ib >= 0 && ib < Ly) ? y[ib] : 0.0f);
-      }
-    }
-  };
-  FftIn<1024> in;
-  if (NC_CQ_PREFETCH && wave < n_items) load_item(wave, lane, in);
-  for (int it = wave; it < n_items; it += CQ_WAVES) {
-    // opaque lane id: per-lane addresses are recomputed per item instead of being hoisted
-    // out of the loop into registers (which would spill)
-    int ln = lane;
-    asm volatile("" : "+v"(ln));
-    const int pr = it / no, oct = it - no * pr;
-    const int fl = 2 * pr;
-    if (!NC_CQ_PREFETCH) load_item(it, ln, in);
-    // the row's 1/sqrt(len), requested with the samples so its latency hides under the FFT
-    const float il = isl[kCqtBins - kCqtFilt * (oct + 1) + max(pfilt, 0)];
-    stockham_stage_regs<1024, 16, 1, 64, false, 0, 0>(in, fftbuf, sh_tw, ln);
-    // with NC_CQ_PREFETCH the next item's samples stream in while this one finishes
-    if (NC_CQ_PREFETCH && it + CQ_WAVES < n_items) load_item(it + CQ_WAVES, ln, in);
-    stockham_stage<1024, 16, 16, 64, false, 0, 0>(fftbuf, sh_tw, ln);
-    float2 v[4][4];
-    if constexpr (NC_LDS_SPLIT && !(NC_CQ_DIAG & 48)) {
-      // lpad(J + 256 r) = lpad(J) + 272 r: four bases, immediate offsets, one wait
-      float2 o[16];
-      lds_read16<0, 2176, 4352, 6528, 0, 2176, 4352, 6528, 0, 2176, 4352, 6528, 0, 2176, 4352, 6528>(
-          o, lds_addr(fftbuf + lpad(Jb(ln, 0))), lds_addr(fftbuf + lpad(Jb(ln, 1))),
-          lds_addr(fftbuf + lpad(Jb(ln, 2))), lds_addr(fftbuf + lpad(Jb(ln, 3))));
-#pragma unroll
-      for (int b = 0; b < 4; ++b)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) v[b][r] = o[4 * b + r];
-      // (the twiddles stay compiler-scheduled here: batching them needs registers this kernel
-      // does not have)
-#pragma unroll
-      for (int b = 0; b < 4; ++b) {
-#pragma unroll
-        for (int r = 1; r < 4; ++r) v[b][r] = cmul(v[b][r], sh_tw3[(3 * b + r - 1) * 64 + ln]);
-        DFT<4>::run(v[b]);
-      }
-    } else {
-#pragma unroll
-    for (int b = 0; b < 4; ++b)
-#pragma unroll
-      for (int r = 0; r < 4; ++r)
-        v[b][r] = (NC_CQ_DIAG & 32) ? make_float2(in[0][4 * b + r].y, in[0][(4 * b + r + 1) & 15].x)
-                                    : fftbuf[lpad(Jb(ln, b) + 256 * r)];
-#pragma unroll
-    for (int b = 0; b < 4; ++b) {
-#pragma unroll
-      for (int r = 1; r < 4; ++r)
-        v[b][r] = cmul(v[b][r], (NC_CQ_DIAG & 16) ? make_float2(0.7f, 0.3f * r) : sh_tw3[(3 * b + r - 1) * 64 + ln]);
-      DFT<4>::run(v[b]);
-    }
-    }
-    // v[b][r] = Z[J[b] + 256 r]; the mirror of k = J[b] is Z[(256 - J[b]) + 768]
-    float4* D = reinterpret_cast<float4*>(fftbuf);  // D[k - klo] = (X_t[k], X_{t+1}[k]); all reads above precede
-#pragma unroll
-    for (int b = 0; b < 4; ++b) {
-      const int k = Jb(ln, b);
-      if (!(NC_CQ_DIAG & 8) && k >= a.klo && k <= a.khi) {
-        const float2 m = b == 0 ? v[3][3] : b == 1 ? v[2][3] : b == 2 ? v[1][3] : (ln ? v[0][3] : v[3][3]);
-        const float2 za = v[b][0], zb = cconj(m);
-        const float2 s = csub(za, zb);
-        // 2 X_t[k] and 2 X_t+1[k]: the weights carry the 1/2 (exact, so the row sums are unchanged)
-        D[k - a.klo] = make_float4(za.x + zb.x, za.y + zb.y, s.y, -s.x);
-      }
-    }
-    // lane piece of a sparse row (complex64 accumulation in row order) for both frames; the
-    // row's second half (partner lane) is then added to its first half
-    float ar = 0.0f, ai = 0.0f, br = 0.0f, bi = 0.0f;
-#if NC_CQ_TB
-    // taps in batches of NC_CQ_TB loads issued together (one LDS wait per batch); taps past
-    // the piece have zero weights and read its last bin, so they add exactly 0; a scheduling
-    // barrier per batch keeps the compiler from hoisting every load at once (VGPR spills)
-    if (!(NC_CQ_DIAG & 1)) {
-      const int plast = plo + max(plen, 1) - 1;
-#pragma unroll
-      for (int j0 = 0; j0 < CQ_PMAX; j0 += NC_CQ_TB) {
-        float4 d[NC_CQ_TB];
-#pragma unroll
-        for (int q = 0; q < NC_CQ_TB; ++q) d[q] = D[min(plo + j0 + q, plast)];
-#pragma unroll
-        for (int q = 0; q < NC_CQ_TB; ++q) {
-          const float2 wj = w[j0 + q];
-          ar = fmaf(wj.x, d[q].x, fmaf(-wj.y, d[q].y, ar));
-          ai = fmaf(wj.x, d[q].y, fmaf(wj.y, d[q].x, ai));
-          br = fmaf(wj.x, d[q].z, fmaf(-wj.y, d[q].w, br));
-          bi = fmaf(wj.x, d[q].w, fmaf(wj.y, d[q].z, bi));
-        }
-        __builtin_amdgcn_sched_barrier(0);
-      }
-    }
-#else
-#pragma unroll
-    for (int j = 0; j < CQ_PMAX; ++j) {
-      if (!(NC_CQ_DIAG & 1) && j < plen) {
-        const float4 d = D[plo + j];
-        ar = fmaf(w[j].x, d.x, fmaf(-w[j].y, d.y, ar));
-        ai = fmaf(w[j].x, d.y, fmaf(w[j].y, d.x, ai));
-        br = fmaf(w[j].x, d.z, fmaf(-w[j].y, d.w, br));
-        bi = fmaf(w[j].x, d.w, fmaf(w[j].y, d.z, bi));
-      }
-    }
-#endif
-    const int src = partner < 0 ? ln : partner;
-    const float ar2 = __shfl(ar, src, 64), ai2 = __shfl(ai, src, 64);
-    const float br2 = __shfl(br, src, 64), bi2 = __shfl(bi, src, 64);
-    if (partner >= 0) {
-      ar += ar2;
-      ai += ai2;
-      br += br2;
-      bi += bi2;
-    }
-    if (pfilt >= 0) {
-      // fft_basis *= sqrt(sr / my_sr) = sqrtf(2^oct), correctly rounded: 2^(oct/2), times
-      // sqrtf(2) for odd octaves (exact power-of-two products)
-      const float oscale = (float)(1 << (oct >> 1)) * ((oct & 1) ? 0x1.6a09e6p+0f : 1.0f);
-      const float xr = ar * oscale, xi = ai * oscale, yr = br * oscale, yi = bi * oscale;
-      sh_mag[pfilt] = hypotf(xr, xi) * il;  // numpy's abs of complex64
-      sh_mag[36 + pfilt] = hypotf(yr, yi) * il;
-    }
-    // this octave's share of the 12 chroma bins of both frames: bins 3c-1, 3c, 3c+1 (mod 36),
-    // in ascending order (c = 0: 0, 1, 35); tile row = bin octave 6 - oct (ascending bins)
-    if (ln < 24) {
-      const int f = ln >= 12, cc = ln - 12 * f;
-      const float* m = sh_mag + 36 * f;
-      const float p = cc == 0 ? (m[0] + m[1]) + m[35] : (m[3 * cc - 1] + m[3 * cc]) + m[3 * cc + 1];
-      if (fl + f < nfr) sh_part[(fl + f) * CQ_TILE + (6 - oct) * 12 + cc] = p;
-    }
-  }
-  __syncthreads();
-  if (NC_CQ_DIAG & 4) continue;
-  if (a.gpart) {  // hybrid: this kernel's octave rows out, the tail runs in cqt_tail_kernel
-    for (int q = tid; q < nfr * no * 12; q += NT) {
-      const int fl = q / (no * 12), r = q - fl * (no * 12), o = r / 12, cc = r - 12 * o;
-      a.gpart[((a.tf_base[c] + t0 + fl) * 7 + (6 - o)) * 12 + cc] = sh_part[fl * CQ_TILE + (6 - o) * 12 + cc];
-    }
-    __syncthreads();  // the slots are reused by the next block's items
-    continue;
-  }
-  // chroma c = sum over the 7 octaves (ascending bins) of the octave partials
-  for (int q = tid; q < nfr * 12; q += NT) {
-    const int fl = q / 12, cc = q - 12 * fl;
-    const float* pt = sh_part + fl * CQ_TILE + cc;
-    float ch = 0.0f;
-#pragma unroll
-    for (int o = 0; o < 7; ++o) ch += pt[12 * o];
-    sh_ch[q] = ch;
-  }
-  __syncthreads();
-  for (int q = tid; q < nfr * 12; q += NT) {
-    const int fl = q / 12;
-    float mx = 0.0f;
-    for (int j = 0; j < 12; ++j) mx = fmaxf(mx, fabsf(sh_ch[fl * 12 + j]));
-    const double len = (mx < 1.17549435e-38f) ? 1.0 : (double)mx;
-    sh_nv[q] = (float)((double)sh_ch[q] / len);
-  }
-  __syncthreads();
-  if (tid < 12) {
-    double acc = 0.0;
-    for (int fl = 0; fl < nfr; ++fl) acc += (double)sh_nv[fl * 12 + tid];
-    a.partial[(a.tf_base[c] / CQ_FR + c + fb) * 12 + tid] = acc;
-  }
-  __syncthreads();  // the slots are reused by the next block's items
-  }
-}
-
-// ------------------------------------------------------------------------------ 4'. CQT on MFMA
-// Hybrid CQT: octaves 0-2 run the FFT kernel above (hop >= 128: a 64-frame tile's span is
-// 9-33 K samples, too large to hold split in LDS, and streaming rows re-reads every sample
-// 2-8 times from HBM), octaves 3-6 (hop <= 64) run here on the matrix cores; both write
-// per-(frame, octave) chroma partial rows and cqt_tail_kernel finishes the frames.  Octaves
-// 3-6 share one workgroup (a wave each, 76 KB of LDS, two workgroups per CU).  Octave 2 on
-// the matrix cores in a workgroup of its own (NC_CM_SPLIT) measured no faster than its FFT.
-//
+// ------------------------------------------------------------------------------ 4. CQT on MFMA
 // The CQT response is linear in the frame: C_j[t] = sum_b fb[j][b] rfft(x_t)[b] =
 // sum_n x_t[n] h_j[n] with h_j[n] = sum_b fb[j][b] e^{-2 pi i b n / 1024} (nc_tables.cpp).
 // Per octave that is a real GEMM [frames x 1024] . [1024 x 72] (Re and Im of the 36 rows),
 // run on the f16 matrix cores with both operands split into hi + lo halves (x = xh + xl,
 // products xh.hh + xh.hl + xl.hh, f32 accumulation): 22 significant bits per operand, so
-// |C| matches the f32 FFT path to ~1e-6 of the frame's largest bin.  The frame operand is
-// scaled by 2^ex with max|y_o| * 2^ex < 2^13 (max|y_0| from decimate3, bounded per octave by
+// |C| matches an f32 FFT to ~1e-6 of the frame's largest bin.  The frame operand is scaled
+// by 2^ex with max|y_o| * 2^ex < 2^13 (max|y_0| from decimate3, bounded per octave by
 // (sqrt(2) sum|h|)^o) and the filters by 2^e_j; C = acc * 2^-(ex + e_j) exactly.
 //
-// One workgroup per (chunk, 64-frame tile), one wave per octave: 4 row tiles x 5 column
-// tiles x 3 products = 60 MFMA 16x16x32 per k-step of 32 taps, 32 k-steps.  The tile's span
-// (63 hop + 1024 samples) is split once into an LDS image that every k-step's fragments
-// read; the filter slices (one k-step: 10 fragments x 1 KB) stream through a CM_R-deep LDS
-// ring by LDS-DMA, with one raw s_barrier per k-step.  76 KB of LDS: two workgroups per CU,
-// whose k-steps interleave freely.
-#ifndef NC_CQ_MFMA
-#define NC_CQ_MFMA 1
-#endif
-#ifndef NC_CM_LO  // first octave on the matrix cores
-#define NC_CM_LO 3
-#endif
-#ifndef NC_CM_R  // filter-slice ring depth
-#define NC_CM_R 2
-#endif
-#ifndef NC_CM_FR
-#define NC_CM_FR 64
-#endif
-constexpr int CM_FR = NC_CM_FR;                    // frames per workgroup tile
+// Octaves 3-6 (hop <= 64, cqt_mfma_kernel): one workgroup per (chunk, 64-frame tile), one
+// wave per octave: 4 row tiles x 5 column tiles x 3 products = 60 MFMA 16x16x32 per k-step
+// of 32 taps, 32 k-steps.  The tile's span (63 hop + 1024 samples) is split once into an LDS
+// image that every k-step's fragments read; the filter slices (one k-step: 10 fragments x
+// 1 KB) stream through a two-slot LDS ring by LDS-DMA, with one raw s_barrier per k-step.
+// 76 KB of LDS: two workgroups per CU, whose k-steps interleave freely.  Octaves 0-2 (hop
+// >= 128, cqt_mfma_low_kernel below): their spans do not fit LDS as images.  Both write
+// per-(frame, octave) chroma partial rows; cqt_tail_kernel finishes the frames.
+//
+// Measured and not kept (round 2, per 224 chunks): two tiles per workgroup
+// sharing a 2 / 3 / 4-slot ring 809 / 822 / 812-822 against 753-770 us; two or four k-steps
+// per barrier 780-869 against 722-727 us; the next k-step's A fragments read under this
+// step's MFMAs 748-765 against 730-745 us; octave 2 in a workgroup of its own 888-1012
+// against 879 us; the FFT CQT kernel for octaves 0-2 866 against 816-856 us (removed in
+// round 3).
+constexpr int CM_FR = 64;                          // frames per workgroup tile
 constexpr int CM_RT = CM_FR / 16;                  // row tiles per wave
 constexpr int CM_KS = kCqtNfft / 32;               // k-steps of 32 taps
 constexpr int CM_NT = 5;                           // column tiles (72 of 80 columns used)
-constexpr int CM_R = NC_CM_R;
-// Two tiles per workgroup with a 2 / 3 / 4-slot ring measure 809 / 822 / 812-822 against
-// 753-770 us per 224 chunks: one tile, two slots.
-#ifndef NC_CM_TPB  // 64-frame tiles per octave 3-6 workgroup (CM_NW waves each), sharing one filter ring
-#define NC_CM_TPB 1
-#endif
-constexpr int CM_TPB = NC_CM_TPB;
-#ifndef NC_CM_HR  // filter-slice ring depth of the octave 3-6 kernel
-#define NC_CM_HR NC_CM_R
-#endif
-constexpr int CM_HR = NC_CM_HR;
+constexpr int CM_R = 2;                            // filter-slice ring slots
 constexpr int CM_SLICE = CM_NT * 2 * 64;           // uint4 fragments per k-step slice
-constexpr int CM_LO = NC_CM_LO;
+constexpr int CM_LO = 3;                           // first octave of cqt_mfma_kernel
 constexpr int CM_NW = 7 - CM_LO;                   // waves (octaves) per workgroup
 constexpr int CM_NTH = CM_NW * 64;
-static_assert(CM_LO >= 1 && CM_LO <= 6 && CM_R >= 2, "hybrid split");
 constexpr int CM_GQ = (CM_NT * 2 + CM_NW - 1) / CM_NW;  // filter DMA pieces per wave per slice
 typedef _Float16 cm_half8 __attribute__((ext_vector_type(8)));
 typedef float cm_f4 __attribute__((ext_vector_type(4)));
@@ -903,39 +555,12 @@ __host__ __device__ constexpr int cm_aoff(int o) {  // byte offset of octave o's
 // K-loop LDS: filter ring [CM_R][CM_SLICE] uint4 | images.  Epilogue overlay: octave rows
 // [CM_NW][CM_FR][36] f32
 constexpr int CM_BBYTES = CM_R * CM_SLICE * 16;
-// Image pieces per lane whose loads are issued together (1: one at a time).  One session,
-// cqt_chroma per 224 chunks: 1 / 2 / 4 / 8 -> 751-753 / 739 / 744-745 / 743 us.
-#ifndef NC_CM_IMGU
-#define NC_CM_IMGU 4
-#endif
-constexpr int CM_IMGU = NC_CM_IMGU;
-// 1: the next k-step's A fragments are read during this step's MFMAs: 748-765 against
-// 730-745 us per 224 chunks, so 0.
-#ifndef NC_CM_APF
-#define NC_CM_APF 0
-#endif
-constexpr int CM_APF = NC_CM_APF;
-// k-steps of the octave 3-6 kernel per workgroup barrier (needs NC_CM_HR >= 2 x).  2 with a
-// 4-slot ring: 869 us (one workgroup per CU), 780 us with two tiles, against 722-727 us.
-#ifndef NC_CM_KPB
-#define NC_CM_KPB 1
-#endif
-constexpr int CM_KPB = NC_CM_KPB;
-constexpr int CM_HBBYTES = CM_HR * CM_SLICE * 16;  // the octave 3-6 kernel's ring
-constexpr int CM_KBYTES = CM_HBBYTES + CM_TPB * cm_aoff(7);
-constexpr int CM_MBYTES = CM_TPB * CM_NW * CM_FR * kCqtFilt * 4;
+// Image pieces per lane whose loads are issued together.  One session, cqt_chroma per 224
+// chunks: 1 / 2 / 4 / 8 -> 751-753 / 739 / 744-745 / 743 us.
+constexpr int CM_IMGU = 4;
+constexpr int CM_KBYTES = CM_BBYTES + cm_aoff(7);
+constexpr int CM_MBYTES = CM_NW * CM_FR * kCqtFilt * 4;
 size_t cqm_lds_bytes() { return CM_KBYTES > CM_MBYTES ? CM_KBYTES : CM_MBYTES; }
-// the octave-split workgroup (octave CM_LO - 1, NC_CM_SPLIT waves): filter ring + one image
-#ifndef NC_CM_SPLIT  // waves of an octave CM_LO - 1 workgroup (0: that octave stays on the FFT kernel; per 224
-                     // chunks: 0 -> 879 us, 1 -> 1012, 2 -> 910, 4 -> 888)
-#define NC_CM_SPLIT 0
-#endif
-constexpr int CM_SW = NC_CM_SPLIT;
-constexpr int CM_FFT_OCT = CM_SW ? CM_LO - 1 : CM_LO;  // octaves on the FFT kernel
-size_t cqm_split_lds_bytes() {
-  const size_t k = CM_BBYTES + 4 * (size_t)cm_img(CM_LO - 1), m = (size_t)CM_FR * kCqtFilt * 4;
-  return k > m ? k : m;
-}
 
 struct CqmArgs {
   const float* sig;
@@ -984,42 +609,27 @@ __device__ __forceinline__ void cm_split(const float (&v)[8], float s, cm_half8&
   lo = __builtin_bit_cast(cm_half8, l);
 }
 
-// Two workgroup shapes: SPLIT < 0: NW waves, wave w = octave CM_LO + w over all 64 rows;
-// SPLIT = o: NW waves all on octave o, wave w on rows [16 RT w, 16 RT (w + 1)) of one image.
-template <int NW, int RT, int SPLIT>
-__global__ __launch_bounds__(NW * 64 * (SPLIT >= 0 ? 1 : CM_TPB)) void cqt_mfma_kernel(CqmArgs a) {
-  constexpr int TPB = SPLIT >= 0 ? 1 : CM_TPB;    // tiles per workgroup
-  constexpr int RB = SPLIT >= 0 ? CM_R : CM_HR;    // filter ring slots
-  constexpr int BB = RB * CM_SLICE * 16;
-  constexpr int NWT = NW * TPB;                    // waves per workgroup
-  constexpr int KPB = SPLIT >= 0 ? 1 : CM_KPB;     // k-steps per barrier
-  static_assert(RB >= 2 * KPB && CM_KS % KPB == 0, "ring holds two barrier groups");
-  constexpr int GQ = (CM_NT * 2 + NWT - 1) / NWT;  // filter DMA pieces per wave per slice
-  static_assert(SPLIT >= 0 ? NW * RT * 16 == CM_FR : (NW == CM_NW && RT == CM_RT), "shape");
+__global__ __launch_bounds__(CM_NTH) void cqt_mfma_kernel(CqmArgs a) {
   const Span span_(a.span);
   extern __shared__ __attribute__((aligned(16))) char smem[];
   uint4* sB = reinterpret_cast<uint4*>(smem);  // [CM_R][CM_SLICE]
   const int c = blockIdx.y;
   const int T = a.n_frames[c];
-  if (blockIdx.x * (TPB * CM_FR) >= T) return;
+  const int t0 = blockIdx.x * CM_FR;
+  if (t0 >= T) return;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int tw = wave / NW, wo = wave - NW * tw;  // tile of the workgroup, wave within the tile
-  int t0 = (blockIdx.x * TPB + tw) * CM_FR;
-  const bool active = t0 < T;  // an idle tile's waves still share the DMA and the barriers
-  if (!active) t0 = 0;
   const int nfr = min(CM_FR, T - t0);
-  const int oct = SPLIT >= 0 ? SPLIT : CM_LO + wo;
-  const int row0 = SPLIT >= 0 ? 16 * RT * wave : 0;
+  const int oct = CM_LO + wave;
   const int ti = a.tuning_idx[c];
   const uint4* bsrc = a.bfrag + (size_t)ti * (CM_KS * CM_SLICE);
-  // the first two filter slices are in flight while the image is built
+  // the first filter slice is in flight while the image is built
   auto fetch_slice = [&](int ks) {
 #pragma unroll
-    for (int q = 0; q < GQ; ++q) {
-      int i = wave + NWT * q;
+    for (int q = 0; q < CM_GQ; ++q) {
+      int i = wave + CM_NW * q;
       if (i >= CM_NT * 2) i = wave;  // duplicate of this wave's first piece (same bytes, same place)
-      cm_dma16(bsrc + ks * CM_SLICE + i * 64 + lane, sB + (ks % RB) * CM_SLICE + i * 64);
+      cm_dma16(bsrc + ks * CM_SLICE + i * 64 + lane, sB + (ks % CM_R) * CM_SLICE + i * 64);
     }
   };
   fetch_slice(0);
@@ -1052,23 +662,22 @@ __global__ __launch_bounds__(NW * 64 * (SPLIT >= 0 ? 1 : CM_TPB)) void cqt_mfma_
   constexpr int aoffs[8] = {cm_aoff(0), cm_aoff(1), cm_aoff(2), cm_aoff(3), cm_aoff(4), cm_aoff(5), cm_aoff(6), cm_aoff(7)};
   const int pad = cm_pad(oct);
   const int img = cm_img(oct);
-  _Float16* aimg = reinterpret_cast<_Float16*>(smem + BB + (SPLIT >= 0 ? 0 : tw * cm_aoff(7) + aoffs[oct]));
-  const int i0 = SPLIT >= 0 ? tid : lane, di = SPLIT >= 0 ? NW * 64 : 64;
-  int ib = i0;
-  if (CM_IMGU > 1 && vec) {
+  _Float16* aimg = reinterpret_cast<_Float16*>(smem + CM_BBYTES + aoffs[oct]);
+  int ib = lane;
+  if (vec) {
     // CM_IMGU pieces per lane loaded before any is split: one load latency per batch instead
     // of one per piece (the accumulators are not live yet, so the registers are free)
-    for (; ib + (CM_IMGU - 1) * di < S / 8; ib += CM_IMGU * di) {
+    for (; ib + (CM_IMGU - 1) * 64 < S / 8; ib += CM_IMGU * 64) {
       float4 u[CM_IMGU][2];
 #pragma unroll
       for (int k = 0; k < CM_IMGU; ++k) {
-        const float4* p = reinterpret_cast<const float4*>(y + s0 + 8 * (ib + k * di));
+        const float4* p = reinterpret_cast<const float4*>(y + s0 + 8 * (ib + k * 64));
         u[k][0] = p[0];
         u[k][1] = p[1];
       }
 #pragma unroll
       for (int k = 0; k < CM_IMGU; ++k) {
-        const int i = ib + k * di;
+        const int i = ib + k * 64;
         const float v[8] = {u[k][0].x, u[k][0].y, u[k][0].z, u[k][0].w, u[k][1].x, u[k][1].y, u[k][1].z, u[k][1].w};
         cm_half8 h, l;
         cm_split(v, sx, h, l);
@@ -1078,7 +687,7 @@ __global__ __launch_bounds__(NW * 64 * (SPLIT >= 0 ? 1 : CM_TPB)) void cqt_mfma_
       }
     }
   }
-  for (int i = ib; i < S / 8; i += di) {
+  for (int i = ib; i < S / 8; i += 64) {
     float v[8];
     if (vec) {
       const float4 u0 = *reinterpret_cast<const float4*>(y + s0 + 8 * i);
@@ -1098,65 +707,51 @@ __global__ __launch_bounds__(NW * 64 * (SPLIT >= 0 ? 1 : CM_TPB)) void cqt_mfma_
     *reinterpret_cast<cm_half8*>(aimg + pos) = h;
     *reinterpret_cast<cm_half8*>(aimg + img + pos) = l;
   }
-  int abase[RT];
+  int abase[CM_RT];
 #pragma unroll
-  for (int rt = 0; rt < RT; ++rt) abase[rt] = (row0 + 16 * rt + (lane & 15)) * (hop + pad) + kq + (kq / hop) * pad;
-  for (int ks = 1; ks < RB - KPB; ++ks) fetch_slice(ks);
+  for (int rt = 0; rt < CM_RT; ++rt) abase[rt] = (16 * rt + (lane & 15)) * (hop + pad) + kq + (kq / hop) * pad;
 
-  cm_f4 acc[RT][CM_NT];
+  cm_f4 acc[CM_RT][CM_NT];
 #pragma unroll
-  for (int rt = 0; rt < RT; ++rt)
+  for (int rt = 0; rt < CM_RT; ++rt)
 #pragma unroll
     for (int nt = 0; nt < CM_NT; ++nt) acc[rt][nt] = cm_f4{0.f, 0.f, 0.f, 0.f};
-  // A fragments of k-step ks (this wave's own image: written by this wave only, and LDS
-  // operations of one wave complete in order, so no barrier guards them)
-  auto load_a = [&](int ks, cm_half8* h, cm_half8* l) {
+#pragma unroll 1
+  for (int ks = 0; ks < CM_KS; ++ks) {
+    // retire this wave's DMA of slice ks (vmcnt(0): nothing younger is in flight, and a
+    // counted wait over mixed LDS-DMA raced in round 2); the barrier makes
+    // every wave's pieces visible and ends every read of the slot slice ks + 1 reuses
+    __builtin_amdgcn_s_waitcnt(cm_vmcnt(0));
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the image writes (first step)
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (ks + 1 < CM_KS) fetch_slice(ks + 1);
+    // A fragments of k-step ks (this wave's own image: written by this wave only, and LDS
+    // operations of one wave complete in order, so no barrier guards them)
+    cm_half8 ah[CM_RT], al[CM_RT];
     const int kt = 32 * ks + (32 * ks / hop) * pad;
 #pragma unroll
-    for (int rt = 0; rt < RT; ++rt) {
-      h[rt] = *reinterpret_cast<const cm_half8*>(aimg + abase[rt] + kt);
-      l[rt] = *reinterpret_cast<const cm_half8*>(aimg + img + abase[rt] + kt);
+    for (int rt = 0; rt < CM_RT; ++rt) {
+      ah[rt] = *reinterpret_cast<const cm_half8*>(aimg + abase[rt] + kt);
+      al[rt] = *reinterpret_cast<const cm_half8*>(aimg + img + abase[rt] + kt);
     }
-  };
-  cm_half8 ah[RT], al[RT];
-  if (CM_APF) load_a(0, ah, al);
-  auto do_step = [&](int ks) {
-    if (!CM_APF) load_a(ks, ah, al);
-    const uint4* sb = sB + (ks % RB) * CM_SLICE + lane;
+    const uint4* sb = sB + (ks % CM_R) * CM_SLICE + lane;
 #pragma unroll
     for (int nt = 0; nt < CM_NT; ++nt) {
       const cm_half8 bh = __builtin_bit_cast(cm_half8, sb[(nt * 2) * 64]);
       const cm_half8 bl = __builtin_bit_cast(cm_half8, sb[(nt * 2 + 1) * 64]);
 #pragma unroll
-      for (int rt = 0; rt < RT; ++rt) {
+      for (int rt = 0; rt < CM_RT; ++rt) {
         acc[rt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[rt], bh, acc[rt][nt], 0, 0, 0);
         acc[rt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[rt], bl, acc[rt][nt], 0, 0, 0);
         acc[rt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al[rt], bh, acc[rt][nt], 0, 0, 0);
       }
     }
-    if (CM_APF && ks + 1 < CM_KS) load_a(ks + 1, ah, al);  // under this step's MFMAs
-  };
-#pragma unroll 1
-  for (int ks = 0; ks < CM_KS; ks += KPB) {
-    // retire this wave's DMA of slices ks .. ks + KPB - 1 (the younger ones may stay in
-    // flight); the barrier makes every wave's pieces visible and ends every read of the slots
-    // the next KPB slices reuse
-    if (ks + RB - KPB - 1 < CM_KS) __builtin_amdgcn_s_waitcnt(cm_vmcnt(GQ * (RB - 2 * KPB)));
-    else __builtin_amdgcn_s_waitcnt(cm_vmcnt(0));
-    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the image writes (first step)
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-#pragma unroll
-    for (int j = 0; j < KPB; ++j)
-      if (ks + RB - KPB + j < CM_KS) fetch_slice(ks + RB - KPB + j);
-#pragma unroll
-    for (int j = 0; j < KPB; ++j) do_step(ks + j);
   }
   __syncthreads();  // every wave's last ring / image reads done before the rows overlay them
-  if (!active) return;
 
-  // |C| per (frame, row) into this wave's [16 RT][36] region
-  float* mg = reinterpret_cast<float*>(smem) + wave * (16 * RT * kCqtFilt);
+  // |C| per (frame, row) into this wave's [64][36] region
+  float* mg = reinterpret_cast<float*>(smem) + wave * (CM_FR * kCqtFilt);
   {
     const float oscale = (float)(1 << (oct >> 1)) * ((oct & 1) ? 0x1.6a09e6p+0f : 1.0f);
     const float* isl = a.cqt_isl + ti * kCqtBins + (kCqtBins - kCqtFilt * (oct + 1));
@@ -1166,10 +761,10 @@ __global__ __launch_bounds__(NW * 64 * (SPLIT >= 0 ? 1 : CM_TPB)) void cqt_mfma_
     const float inv2 = ldexpf(1.0f, -(ex + bx[32 + (col & 3)]));
     const float il0 = isl[col], il1 = isl[16 + col], il2 = isl[32 + (col & 3)];
 #pragma unroll
-    for (int rt = 0; rt < RT; ++rt)
+    for (int rt = 0; rt < CM_RT; ++rt)
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        const int fr = 16 * rt + 4 * (lane >> 4) + i;  // row within this wave's rows
+        const int fr = 16 * rt + 4 * (lane >> 4) + i;  // row within the tile
         float* m = mg + fr * kCqtFilt;
         m[col] = hypotf(acc[rt][0][i] * inv0 * oscale, acc[rt][1][i] * inv0 * oscale) * il0;
         m[16 + col] = hypotf(acc[rt][2][i] * inv1 * oscale, acc[rt][3][i] * inv1 * oscale) * il1;
@@ -1180,40 +775,29 @@ __global__ __launch_bounds__(NW * 64 * (SPLIT >= 0 ? 1 : CM_TPB)) void cqt_mfma_
   __builtin_amdgcn_s_waitcnt(0xc07f);  // the wave reads back only its own rows
   __builtin_amdgcn_wave_barrier();
   // this octave's share of the 12 chroma bins: bins 3c-1, 3c, 3c+1 (mod 36), ascending
-  float* gp = a.gpart + (a.tf_base[c] + t0 + row0) * (7 * 12) + (6 - oct) * 12;
-  const int nrow = min(16 * RT, nfr - row0);
-  for (int q = lane; q < nrow * 12; q += 64) {
+  float* gp = a.gpart + (a.tf_base[c] + t0) * (7 * 12) + (6 - oct) * 12;
+  for (int q = lane; q < nfr * 12; q += 64) {
     const int fl = q / 12, cc = q - 12 * fl;
     const float* m = mg + fl * kCqtFilt;
     gp[fl * (7 * 12) + cc] = cc == 0 ? (m[0] + m[1]) + m[35] : (m[3 * cc - 1] + m[3 * cc]) + m[3 * cc + 1];
   }
 }
 
-// Octaves 0-2 on the matrix cores (NC_CM_LOW).  Their 64-frame spans (9-33 K samples) do
-// not fit LDS as images, but row t + 1 at k-step ks equals row t at k-step ks + G (G = hop /
-// 32): the M = 1024 / hop k-steps {g + G q : q < M} of "group" g read one block of 64 + M - 1
-// row pieces (32 samples each), row r of step q being block row r + q.  The k-steps run group
-// by group, so each sample is fetched once per tile (M = 2, 4, 8 times fewer bytes than
+// Octaves 0-2 on the matrix cores.  Their 64-frame spans (9-33 K samples) do not fit LDS as
+// images, but row t + 1 at k-step ks equals row t at k-step ks + G (G = hop / 32): the
+// M = 1024 / hop k-steps {g + G q : q < M} of "group" g read one block of 64 + M - 1 row
+// pieces (32 samples each), row r of step q being block row r + q.  The k-steps run group by
+// group, so each sample is fetched once per tile (M = 2, 4, 8 times fewer bytes than
 // streaming rows per k-step).  Blocks arrive by LDS-DMA (raw f32, 16-byte pieces swizzled so
 // a fragment's 16 rows hit distinct bank groups), double buffered (issued at a group's first
 // step, retired at its second: see the wait below), and are split to f16 hi/lo at each
 // fragment read.  Four waves per workgroup: two 64-frame tiles, two waves per tile (32 rows
 // each) sharing its blocks; all four share the filter ring.  57 KB of LDS, two workgroups per
-// CU.  Per 224 chunks (tools/var_bench.py, one session): 816-856 us with octaves 0-2 here
-// against 866 us with them on the FFT kernel (NC_CM_LOW=0).
-#ifndef NC_CM_LOW  // octaves 0 .. NC_CM_LOW - 1 on cqt_mfma_low_kernel (0: on the FFT kernel)
-#define NC_CM_LOW 3
-#endif
-constexpr int CM_LOW = NC_CM_LOW;
-#ifndef NC_CL_DIAG  // diagnosis builds only: 1 every block through registers (no block DMA)
-#define NC_CL_DIAG 0
-#endif
-// 64-frame tiles per workgroup (two waves each).  One session, cqt_chroma per 224 chunks:
-// 1 / 3 / 4 tiles 778 / 782-797 / 989 us against 761 us at 2 (2 workgroups per CU).
-#ifndef NC_CL_TPW
-#define NC_CL_TPW 2
-#endif
-constexpr int CL_TPW = NC_CL_TPW;
+// CU.  Per 224 chunks (round 2, one session): 816-856 us with octaves 0-2 here against 866 us
+// on the FFT kernel; 1 / 3 / 4 tiles per workgroup 778 / 782-797 / 989 us against 761 us at
+// 2; the waits below removed (a timing-only build that races, round 3) 922-954 against
+// 733-758 us, so the exposed DMA latency is not what bounds this kernel.
+constexpr int CL_TPW = 2;          // 64-frame tiles per workgroup (two waves each)
 constexpr int CL_NW = 2 * CL_TPW;  // waves per workgroup
 constexpr int CL_RT = 2;   // row tiles per wave
 template <int OCT>
@@ -1275,7 +859,7 @@ __device__ __forceinline__ void cqt_mfma_low(const CqmArgs& a) {
   const float sx = ldexpf(1.0f, ex);
   const int64_t s0 = (int64_t)t0 * H - 512;
   // tile-uniform: both waves of a tile take the same path (their vmcnt bookkeeping agrees)
-  const bool vec = !NC_CL_DIAG && s0 >= 0 && s0 + (int64_t)(CM_FR - 1) * H + kCqtNfft <= Ly &&
+  const bool vec = s0 >= 0 && s0 + (int64_t)(CM_FR - 1) * H + kCqtNfft <= Ly &&
                    (reinterpret_cast<uintptr_t>(y) & 15) == 0;
   // block g: row R (< NR) holds samples s0 + R H + 32 g + [0, 32), piece p at slot p ^ ((R >> 1) & 7);
   // the tile's two waves each move half of the NI 8-row DMA groups (QB each, one repeated if odd)
@@ -1390,7 +974,7 @@ __global__ __launch_bounds__(CL_NW * 64) void cqt_mfma_low_kernel(CqmArgs a) {
 }
 
 // Per (chunk, 64-frame tile): chroma = the 7 octave partial rows summed (ascending bins),
-// inf-norm per frame, f64 sum over the tile's frames (cqt_chroma_kernel's own tail).
+// inf-norm per frame, f64 sum over the tile's frames.
 __global__ __launch_bounds__(256) void cqt_tail_kernel(const float* gpart, const int64_t* tf_base,
                                                        const int* n_frames, double* partial) {
   __shared__ float sh_ch[CM_FR * 12], sh_nv[CM_FR * 12];
@@ -1498,7 +1082,7 @@ size_t chroma_ws_bytes(int n, int64_t total_len) {
   b += al256(sizeof(int64_t) * (n + 1)) * 2;
   b += al256(sizeof(float) * (size_t)(total_len + 64 * 7 * (int64_t)n));
   b += al256(sizeof(float) * (size_t)tfr * kPeakSlots) * 2;
-  b += al256(sizeof(double) * (size_t)(tfr / CQ_FR + n + 1) * 12);
+  b += al256(sizeof(double) * (size_t)(tfr / CM_FR + n + 1) * 12);
   b += al256(sizeof(int64_t) * (n + 1));
   b += al256(sizeof(float) * (size_t)(n + (total_len + 64 * 7 * (int64_t)n) / 256 + 2));
   b += al256(sizeof(float) * (size_t)tfr * 84);
@@ -1507,7 +1091,8 @@ size_t chroma_ws_bytes(int n, int64_t total_len) {
 
 int launch_chroma_mean(Context& ctx, const float* sig, const int64_t* chunk_off, const int64_t* chunk_len, int n,
                        int64_t total_len, int64_t max_chunk_len, float* out_chroma, float* out_tuning,
-                       int* out_tuning_idx, const int* tf_skip, int64_t tf_skip_total, float* ext_pitch,
+                       int* out_tuning_idx, int* out_tuning_margin, const int* tf_skip, int64_t tf_skip_total,
+                       float* ext_pitch,
                        float* ext_mag, int* ext_npk, void* wait_event, void* ws, size_t ws_bytes, hipStream_t st) {
   if (n <= 0) return 0;
   const bool ext = ext_pitch && ext_mag && ext_npk;
@@ -1542,7 +1127,7 @@ int launch_chroma_mean(Context& ctx, const float* sig, const int64_t* chunk_off,
   w.ws_oct = reinterpret_cast<float*>(take(sizeof(float) * (size_t)(total_len + 64 * 7 * (int64_t)n)));
   w.peak_pitch = reinterpret_cast<float*>(take(sizeof(float) * (size_t)tfr * kPeakSlots));
   w.peak_mag = reinterpret_cast<float*>(take(sizeof(float) * (size_t)tfr * kPeakSlots));
-  w.partial = reinterpret_cast<double*>(take(sizeof(double) * (size_t)(tfr / CQ_FR + n + 1) * 12));
+  w.partial = reinterpret_cast<double*>(take(sizeof(double) * (size_t)(tfr / CM_FR + n + 1) * 12));
   int64_t* tp_base = reinterpret_cast<int64_t*>(take(sizeof(int64_t) * (n + 1)));
   w.xmax = reinterpret_cast<float*>(take(sizeof(float) * (size_t)(n + (total_len + 64 * 7 * (int64_t)n) / 256 + 2)));
   w.gpart = reinterpret_cast<float*>(take(sizeof(float) * (size_t)tfr * 84));
@@ -1560,13 +1145,13 @@ int launch_chroma_mean(Context& ctx, const float* sig, const int64_t* chunk_off,
   // gain: the chip is already full with the window chain on the caller's other stream.)
   for (int base = 0; base < 6; base += 3) {
     const int64_t mo = (max_chunk_len >> (base + 3)) + 1;  // >= the longest chunk's level base + 3
-    dim3 grid((unsigned)((mo + D3_TPW * D3_T - 1) / (D3_TPW * D3_T)), (unsigned)n);
+    dim3 grid((unsigned)((mo + D3_T - 1) / D3_T), (unsigned)n);
     {
       KTimer kt_(ctx, "decimate", st);
       D3Taps taps;
       std::copy(ctx.t.halfband_f32, ctx.t.halfband_f32 + 2 * kHalfbandK + 1, taps.h);
       hipLaunchKernelGGL(decimate3_kernel, grid, dim3(256), 0, st, sig, chunk_off, w.oct_off, w.oct_len, w.ws_oct,
-                         base, taps, NC_CQ_MFMA ? w.xmax : nullptr, kt_.span());
+                         base, taps, w.xmax, kt_.span());
     }
   }
   PeakArgs pa;
@@ -1598,42 +1183,9 @@ int launch_chroma_mean(Context& ctx, const float* sig, const int64_t* chunk_off,
   if (wait_event) NC_HIP(hipStreamWaitEvent(st, static_cast<hipEvent_t>(wait_event), 0));
   {
     KTimer kt_(ctx, "tuning_select", st);
-    hipLaunchKernelGGL((tuning_select_kernel<NC_TS_NT>), dim3(n), dim3(NC_TS_NT), 0, st, w.peak_pitch, w.peak_mag,
-                       w.chunk_npk, w.tf_base, w.tuning_idx, out_tuning, kt_.span());
+    hipLaunchKernelGGL((tuning_select_kernel<TS_NT>), dim3(n), dim3(TS_NT), 0, st, w.peak_pitch, w.peak_mag,
+                       w.chunk_npk, w.tf_base, w.tuning_idx, out_tuning, out_tuning_margin, kt_.span());
   }
-  CqtArgs ca;
-  ca.sig = sig;
-  ca.chunk_off = chunk_off;
-  ca.oct_off = w.oct_off;
-  ca.oct_len = w.oct_len;
-  ca.n_frames = w.n_frames;
-  ca.tuning_idx = w.tuning_idx;
-  ca.ws_oct = w.ws_oct;
-  ca.tf_base = w.tf_base;
-  ca.tw = ctx.t.tw;
-  ca.cqt_isl = ctx.t.cqt_inv_sqrt_len;
-  ca.cqt_plo = ctx.t.cqt_plo;
-  ca.cqt_plen = ctx.t.cqt_plen;
-  ca.cqt_partner = ctx.t.cqt_partner;
-  ca.cqt_pfilt = ctx.t.cqt_pfilt;
-  ca.cqt_wcol = ctx.t.cqt_wcol;
-  ca.pmax = ctx.t.cqt_pmax;
-  ca.klo = ctx.t.cqt_klo;
-  ca.khi = ctx.t.cqt_khi;
-  // the mirror pairs (k, 1024 - k) of the packed FFT cover k in [1, 255]; D must fit a slot
-  if (ca.klo < 1 || ca.khi > 255 || ca.pmax > CQ_PMAX ||
-      (size_t)(ca.khi - ca.klo + 1) * sizeof(float4) > LdsSize<1024>::value * sizeof(float2)) {
-    set_error("chroma: CQT basis bin range / piece length outside the kernel's schedule");
-    return -2;
-  }
-  ca.partial = w.partial;
-#if NC_CQ_MFMA
-  // hybrid: octaves 0 .. CM_LO - 1 here, the others on the matrix cores, then the frame tail
-  ca.gpart = w.gpart;
-  ca.n_oct = CM_LOW ? 0 : CM_FFT_OCT;
-#endif
-  const int nblk = (int)((1 + max_chunk_len / 512 + CQ_FR - 1) / CQ_FR);
-#if NC_CQ_MFMA
   CqmArgs ma;
   ma.sig = sig;
   ma.chunk_off = chunk_off;
@@ -1647,40 +1199,26 @@ int launch_chroma_mean(Context& ctx, const float* sig, const int64_t* chunk_off,
   ma.bexp = ctx.t.cqm_bexp;
   ma.cqt_isl = ctx.t.cqt_inv_sqrt_len;
   ma.xmax = w.xmax;
-  ma.d3_span = D3_TPW * D3_T;
+  ma.d3_span = D3_T;
   std::copy(ctx.t.cqm_gpow, ctx.t.cqm_gpow + 7, ma.gpow);
   ma.gpart = w.gpart;
   const int ntile = (int)((1 + max_chunk_len / 512 + CM_FR - 1) / CM_FR);
   {
-    // one span over both CQT kernels (the timed "cqt_chroma" unit: 7 octaves of every chunk)
-    KTimer kt_(ctx, "cqt_chroma", st);
-    ca.span = kt_.span();
+    // the two CQT kernels are timed apart ("cqt_low", "cqt_high": one rocprof row each); the
+    // bench's cqt_chroma unit (7 octaves of every chunk) is their sum
+    KTimer kt_(ctx, "cqt_low", st);
     ma.span = kt_.span();
-    if (CM_LOW) {
-      static_assert(CM_LOW == 0 || (CM_LOW == CM_LO && CM_SW == 0), "octaves 0 .. CM_LO - 1 on the low kernel");
-      const dim3 lg((unsigned)((ntile + CL_TPW - 1) / CL_TPW), (unsigned)n, 3u);
-      hipLaunchKernelGGL(cqt_mfma_low_kernel, lg, dim3(CL_NW * 64), cql_lds_bytes(), st, ma);
-    } else {
-      hipLaunchKernelGGL(cqt_chroma_kernel, dim3((nblk + CQ_BPW - 1) / CQ_BPW, n), dim3(CQ_WAVES * 64), cqt_lds_bytes(), st, ca);
-    }
-    hipLaunchKernelGGL((cqt_mfma_kernel<CM_NW, CM_RT, -1>), dim3((ntile + CM_TPB - 1) / CM_TPB, n),
-                       dim3(CM_NTH * CM_TPB), cqm_lds_bytes(), st, ma);
-    if (CM_SW)
-      hipLaunchKernelGGL((cqt_mfma_kernel<(CM_SW ? CM_SW : 1), CM_FR / 16 / (CM_SW ? CM_SW : 1), CM_LO - 1>), dim3(ntile, n),
-                         dim3(64 * CM_SW), cqm_split_lds_bytes(), st, ma);
+    const dim3 lg((unsigned)((ntile + CL_TPW - 1) / CL_TPW), (unsigned)n, 3u);
+    hipLaunchKernelGGL(cqt_mfma_low_kernel, lg, dim3(CL_NW * 64), cql_lds_bytes(), st, ma);
+  }
+  {
+    KTimer kt_(ctx, "cqt_high", st);
+    ma.span = kt_.span();
+    hipLaunchKernelGGL(cqt_mfma_kernel, dim3(ntile, n), dim3(CM_NTH), cqm_lds_bytes(), st, ma);
   }
   hipLaunchKernelGGL(cqt_tail_kernel, dim3(ntile, n), dim3(256), 0, st, w.gpart, w.tf_base, w.n_frames, w.partial);
   hipLaunchKernelGGL(chroma_finalize_kernel, dim3(n), dim3(64), 0, st, w.partial, w.tf_base, w.n_frames, n, CM_FR,
                      out_chroma);
-#else
-  {
-    KTimer kt_(ctx, "cqt_chroma", st);
-    ca.span = kt_.span();
-    hipLaunchKernelGGL(cqt_chroma_kernel, dim3((nblk + CQ_BPW - 1) / CQ_BPW, n), dim3(CQ_WAVES * 64), cqt_lds_bytes(), st, ca);
-  }
-  hipLaunchKernelGGL(chroma_finalize_kernel, dim3(n), dim3(64), 0, st, w.partial, w.tf_base, w.n_frames, n,
-                     CQ_FR, out_chroma);
-#endif
   NC_HIP(hipGetLastError());
   return 0;
 }

@@ -38,7 +38,8 @@ int launch_trim(Context& ctx, const float* sig, const int64_t* file_off, const i
 size_t chroma_ws_bytes(int n, int64_t total_len);
 int launch_chroma_mean(Context& ctx, const float* sig, const int64_t* chunk_off, const int64_t* chunk_len, int n,
                        int64_t total_len, int64_t max_chunk_len, float* out_chroma, float* out_tuning,
-                       int* out_tuning_idx, const int* tf_skip, int64_t tf_skip_total, float* ext_pitch,
+                       int* out_tuning_idx, int* out_tuning_margin, const int* tf_skip, int64_t tf_skip_total,
+                       float* ext_pitch,
                        float* ext_mag, int* ext_npk, void* wait_event, void* ws, size_t ws_bytes, hipStream_t st);
 int launch_chroma_lag(const float* chroma, const int* src_idx, const int* nc_idx, int n_pairs, int* lag_out,
                       double* margin_out, hipStream_t st);
@@ -265,23 +266,23 @@ size_t nc_chroma_workspace_bytes(const nc_ctx* ctx, int n_chunks, int64_t total_
 
 int nc_chroma_mean(nc_ctx* ctx, const float* sig, const int64_t* chunk_off, const int64_t* chunk_len, int n_chunks,
                    int64_t total_len, int64_t max_chunk_len, float* out_chroma, float* out_tuning,
-                   int* out_tuning_idx, void* ws, size_t ws_bytes, void* stream) {
+                   int* out_tuning_idx, int* out_tuning_margin, void* ws, size_t ws_bytes, void* stream) {
   CHECK_CTX(ctx);
   SET_DEVICE(ctx);
   return nc::launch_chroma_mean(ctx->c, sig, chunk_off, chunk_len, n_chunks, total_len, max_chunk_len, out_chroma,
-                                out_tuning, out_tuning_idx, nullptr, 0, nullptr, nullptr, nullptr, nullptr, ws,
+                                out_tuning, out_tuning_idx, out_tuning_margin, nullptr, 0, nullptr, nullptr, nullptr, nullptr, ws,
                                 ws_bytes, (hipStream_t)stream);
 }
 
 int nc_chroma_mean_shared(nc_ctx* ctx, const float* sig, const int64_t* chunk_off, const int64_t* chunk_len,
                           int n_chunks, int64_t total_len, int64_t max_chunk_len, float* out_chroma,
-                          float* out_tuning, int* out_tuning_idx, const int* tf_skip, int64_t tf_skip_total,
-                          float* peak_pitch, float* peak_mag, int* chunk_npk, void* wait_event, void* ws,
-                          size_t ws_bytes, void* stream) {
+                          float* out_tuning, int* out_tuning_idx, int* out_tuning_margin, const int* tf_skip,
+                          int64_t tf_skip_total, float* peak_pitch, float* peak_mag, int* chunk_npk,
+                          void* wait_event, void* ws, size_t ws_bytes, void* stream) {
   CHECK_CTX(ctx);
   SET_DEVICE(ctx);
   return nc::launch_chroma_mean(ctx->c, sig, chunk_off, chunk_len, n_chunks, total_len, max_chunk_len, out_chroma,
-                                out_tuning, out_tuning_idx, tf_skip, tf_skip_total, peak_pitch, peak_mag, chunk_npk,
+                                out_tuning, out_tuning_idx, out_tuning_margin, tf_skip, tf_skip_total, peak_pitch, peak_mag, chunk_npk,
                                 wait_event, ws, ws_bytes, (hipStream_t)stream);
 }
 

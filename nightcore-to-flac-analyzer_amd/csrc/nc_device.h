@@ -236,9 +236,6 @@ __device__ __forceinline__ void static_for(F&& f) { static_for_impl<0, N_>(f); }
 // ds_read_b64 cost 2 + 2 (MI355X_MICROARCH.md, LDS table); for the FFT exchanges that is a
 // fifth of the kernels' LDS time.  An asm block is never merged; its outputs are defined
 // only after its own s_waitcnt, so no consumer can see a pending register.
-#ifndef NC_LDS_SPLIT
-#define NC_LDS_SPLIT 1
-#endif
 typedef float nc_f2v __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ uint32_t lds_addr(const void* p) {
   return (uint32_t)(uintptr_t)p;  // generic LDS pointer: aperture | offset
@@ -324,7 +321,7 @@ __device__ __forceinline__ void stockham_stage_regs(float2 (&v)[N / (R * NT)][R]
   for (int b = 0; b < NB; ++b) {
     const int j = tid + NT * b;
     const int k = j % NS;
-    if constexpr (NC_LDS_SPLIT && NS > 1 && TWN == 0 && R == 16) {
+    if constexpr (NS > 1 && TWN == 0 && R == 16) {
       // 15 twiddles from the LDS table in five batches of three ds_read_b64
       const uint32_t ta = lds_addr(tw + STO + k);
       tw_batch3<0, NS * 8>(v[b] + 1, ta);
@@ -366,7 +363,7 @@ __device__ __forceinline__ void stockham_stage(float2* lds, const float2* __rest
   float2 v[NB][R];
   if constexpr (NT % 16 == 0 && (N / R) % 16 == 0) {
     const float2* p = lds + lpad(tid);
-    if constexpr (NC_LDS_SPLIT && NB == 1 && R == 16) {
+    if constexpr (NB == 1 && R == 16) {
       lds_read16_strided<0, (N / R) * 17 / 16 * 8>(v[0], lds_addr(p));
     } else {
 #pragma unroll
@@ -515,39 +512,26 @@ __device__ __forceinline__ int mirror_J(int l, int b) {
 // (spectral_frames) keeps them compiler-scheduled, or the compiler homes v in scratch.
 template <int STW3, bool TWB = false>
 __device__ __forceinline__ void fft1024_last_mirror(const float2* lds, const float2* tw, int l, float2 (&v)[4][4]) {
-  if constexpr (NC_LDS_SPLIT) {
-    // lpad(J + 256 r) = lpad(J) + 272 r: four bases, immediate offsets
-    float2 o[16];
-    lds_read16<0, 2176, 4352, 6528, 0, 2176, 4352, 6528, 0, 2176, 4352, 6528, 0, 2176, 4352, 6528>(
-        o, lds_addr(lds + lpad(mirror_J(l, 0))), lds_addr(lds + lpad(mirror_J(l, 1))),
-        lds_addr(lds + lpad(mirror_J(l, 2))), lds_addr(lds + lpad(mirror_J(l, 3))));
+  // lpad(J + 256 r) = lpad(J) + 272 r: four bases, immediate offsets
+  float2 o[16];
+  lds_read16<0, 2176, 4352, 6528, 0, 2176, 4352, 6528, 0, 2176, 4352, 6528, 0, 2176, 4352, 6528>(
+      o, lds_addr(lds + lpad(mirror_J(l, 0))), lds_addr(lds + lpad(mirror_J(l, 1))),
+      lds_addr(lds + lpad(mirror_J(l, 2))), lds_addr(lds + lpad(mirror_J(l, 3))));
 #pragma unroll
-    for (int b = 0; b < 4; ++b)
+  for (int b = 0; b < 4; ++b)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) v[b][r] = o[4 * b + r];
-    if constexpr (TWB) {
-      static_for<4>([&](auto bc) {
-        constexpr int b = decltype(bc)::value;
-        float2 w[3];
-        const uint32_t a = lds_addr(tw + STW3 + mirror_J(l, b));
-        lds_read3<0, 2048, 4096>(w, a, a, a);
+    for (int r = 0; r < 4; ++r) v[b][r] = o[4 * b + r];
+  if constexpr (TWB) {
+    static_for<4>([&](auto bc) {
+      constexpr int b = decltype(bc)::value;
+      float2 w[3];
+      const uint32_t a = lds_addr(tw + STW3 + mirror_J(l, b));
+      lds_read3<0, 2048, 4096>(w, a, a, a);
 #pragma unroll
-        for (int r = 1; r < 4; ++r) v[b][r] = cmul(v[b][r], w[r - 1]);
-        DFT<4>::run(v[b]);
-      });
-    } else {
-#pragma unroll
-      for (int b = 0; b < 4; ++b) {
-#pragma unroll
-        for (int r = 1; r < 4; ++r) v[b][r] = cmul(v[b][r], tw[STW3 + (r - 1) * 256 + mirror_J(l, b)]);
-        DFT<4>::run(v[b]);
-      }
-    }
+      for (int r = 1; r < 4; ++r) v[b][r] = cmul(v[b][r], w[r - 1]);
+      DFT<4>::run(v[b]);
+    });
   } else {
-#pragma unroll
-    for (int b = 0; b < 4; ++b)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) v[b][r] = lds[lpad(mirror_J(l, b) + 256 * r)];
 #pragma unroll
     for (int b = 0; b < 4; ++b) {
 #pragma unroll

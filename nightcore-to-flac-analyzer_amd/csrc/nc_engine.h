@@ -49,13 +49,6 @@ struct Tables {
   float* cqt_inv_sqrt_len = nullptr;  // [kNTunings][252]  1/sqrt(lengths)
   int cqt_maxlen = 0;
   int cqt_maxnnz = 0;           // max over tunings of the 36 rows' total length
-  int* cqt_plo = nullptr;       // [kNTunings][64] lane pieces of the rows (see nc_tables.cpp)
-  int* cqt_plen = nullptr;
-  int* cqt_partner = nullptr;   // [kNTunings][64] lane holding this row's second half, or -1
-  int* cqt_pfilt = nullptr;     // [kNTunings][64] row completed by this lane, or -1
-  float2* cqt_wcol = nullptr;   // [kNTunings][cqt_pmax][64] piece weights / 2, column-major per tap
-  int cqt_pmax = 0;
-  int cqt_klo = 0, cqt_khi = 0; // FFT bins any row touches (over all tunings)
   double* halfband = nullptr;   // 2K+1 taps
   float halfband_f32[2 * kHalfbandK + 1] = {};  // host copy, rounded to f32 (decimate3 kernel argument)
   // MFMA CQT (cqt_mfma_kernel): the 36 rows as 1024-tap time-domain filters, split into f16

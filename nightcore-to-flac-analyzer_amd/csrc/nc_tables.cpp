@@ -299,64 +299,6 @@ void build_tables(Context& ctx) {
     }
     for (int ti = 0; ti < kNTunings; ++ti)
       t.cqt_maxnnz = std::max(t.cqt_maxnnz, coff[ti * nf + nf - 1] + clen[ti * nf + nf - 1] - coff[ti * nf]);
-    // 64-lane schedule of the 36 sparse rows: the (64 - 36) longest rows are split in two
-    // halves; the 64 pieces are given to lanes in ascending order of their first bin, so the
-    // 32 lanes of each half-wave read D[lo + j] from a narrow bin window (at most 2-way LDS
-    // bank collisions instead of 4); weights are stored column-major per tap, w[j][lane],
-    // so the weight reads are contiguous.  Per lane: first bin, length, the lane holding the
-    // row's second half (or -1) and the row it completes (or -1 for a second half).
-    struct Piece {
-      int lo, len, off, filt, half;
-    };
-    std::vector<int> plo(kNTunings * 64, 0), plen(kNTunings * 64, 0), ppart(kNTunings * 64, -1),
-        pfilt(kNTunings * 64, -1);
-    t.cqt_klo = nbin;
-    t.cqt_khi = 0;
-    t.cqt_pmax = 0;
-    std::vector<std::vector<Piece>> sched(kNTunings);
-    for (int ti = 0; ti < kNTunings; ++ti) {
-      std::vector<int> order(nf);
-      for (int f = 0; f < nf; ++f) order[f] = f;
-      std::stable_sort(order.begin(), order.end(),
-                       [&](int x, int y) { return clen[ti * nf + x] > clen[ti * nf + y]; });
-      std::vector<char> split(nf, 0);
-      for (int i = 0; i < 64 - nf && i < nf; ++i) split[order[i]] = 1;
-      std::vector<Piece>& P = sched[ti];
-      for (int f = 0; f < nf; ++f) {
-        const int lo = clo[ti * nf + f], len = clen[ti * nf + f], off = coff[ti * nf + f];
-        t.cqt_klo = std::min(t.cqt_klo, lo);
-        t.cqt_khi = std::max(t.cqt_khi, lo + len - 1);
-        if (split[f]) {
-          const int h = (len + 1) / 2;
-          P.push_back({lo, h, off, f, 0});
-          P.push_back({lo + h, len - h, off + h, f, 1});
-        } else {
-          P.push_back({lo, len, off, f, 0});
-        }
-      }
-      std::stable_sort(P.begin(), P.end(), [](const Piece& x, const Piece& y) { return x.lo < y.lo; });
-      for (const Piece& q : P) t.cqt_pmax = std::max(t.cqt_pmax, q.len);
-      for (int l = 0; l < (int)P.size(); ++l) {
-        plo[ti * 64 + l] = P[l].lo;
-        plen[ti * 64 + l] = P[l].len;
-        if (P[l].half == 0) pfilt[ti * 64 + l] = P[l].filt;
-      }
-      for (int l = 0; l < (int)P.size(); ++l)
-        if (P[l].half == 1)
-          for (int m = 0; m < (int)P.size(); ++m)
-            if (P[m].half == 0 && P[m].filt == P[l].filt) ppart[ti * 64 + m] = l;
-    }
-    std::vector<float2> wcol((size_t)kNTunings * t.cqt_pmax * 64, make_float2(0.f, 0.f));
-    for (int ti = 0; ti < kNTunings; ++ti)
-      for (int l = 0; l < (int)sched[ti].size(); ++l)
-        for (int j = 0; j < sched[ti][l].len; ++j)
-          wcol[((size_t)ti * t.cqt_pmax + j) * 64 + l] =  // x 1/2: the frame-pair separation's halving
-              make_float2(0.5f * cw[sched[ti][l].off + j].x, 0.5f * cw[sched[ti][l].off + j].y);
-    t.cqt_plo = upload(plo);
-    t.cqt_plen = upload(plen);
-    t.cqt_partner = upload(ppart);
-    t.cqt_pfilt = upload(pfilt);
-    t.cqt_wcol = upload(wcol);
     t.cqt_lo = upload(clo);
     t.cqt_len = upload(clen);
     t.cqt_off = upload(coff);
@@ -439,7 +381,7 @@ void free_tables(Context& ctx) {
   Tables& t = ctx.t;
   void* ptrs[] = {t.tw, t.hann2048, t.hann_ac512, t.hann_ac64, t.wsq512, t.wsq64, t.mel_lo,  t.mel_len, t.mel_off,
                   t.mel_w,  t.cqt_lo,   t.cqt_len,    t.cqt_off,  t.cqt_w,   t.cqt_inv_sqrt_len, t.halfband,
-                  t.cqt_plo, t.cqt_plen, t.cqt_partner, t.cqt_pfilt, t.cqt_wcol, t.mel_w4, t.mel_lo4, t.mel_nj4,
+                  t.mel_w4, t.mel_lo4, t.mel_nj4,
                   t.cqm_b,   t.cqm_bexp};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);

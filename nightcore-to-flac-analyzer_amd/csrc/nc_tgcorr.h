@@ -31,13 +31,8 @@
 
 namespace nc {
 
-#ifndef NC_TGC_LB
-#define NC_TGC_LB 3
-#endif
-constexpr int TGC_LB = NC_TGC_LB;
-#ifndef NC_TGC_UNROLL
-#define NC_TGC_UNROLL 1  // 0: one sample per iteration with register moves (diagnosis)
-#endif  // consecutive lags per thread (odd: 6-dword lane stride, no LDS bank conflicts; 5 spills)
+// consecutive lags per thread (odd: 6-dword lane stride, no LDS bank conflicts; 5 spills)
+constexpr int TGC_LB = 3;
 
 __host__ __device__ inline int tgc_extent(int T, int N) { return T + N; }       // u range
 __host__ __device__ inline int tgc_pad(int N) { return N + TGC_LB + 1; }        // zeros either side of x
@@ -172,23 +167,11 @@ __device__ __forceinline__ void tgc_correlate(const double* x, const double* seq
       }
     };
     int u = ua;
-#if NC_TGC_UNROLL
 #pragma unroll 1
     for (; u + LB <= ub; u += LB) tgc_static_for<LB>([&](auto rot) { step(u + decltype(rot)::value, rot); });
     tgc_static_for<LB>([&](auto rot) {
       if (u + decltype(rot)::value < ub) step(u + decltype(rot)::value, rot);
     });
-#else
-#pragma unroll 1
-    for (; u < ub; ++u) {
-      step(u, std::integral_constant<int, 0>{});
-#pragma unroll
-      for (int q = 0; q < LB - 1; ++q) {
-        xp[q] = xp[q + 1];
-        xm[q] = xm[q + 1];
-      }
-    }
-#endif
     const double inv_half = 2.0 / (double)N;
 #pragma unroll
     for (int q = 0; q < LB; ++q) {

@@ -23,7 +23,7 @@
 // Everything is deterministic (no float atomics).
 #include <algorithm>
 
-// the asm LDS batches of nc_device.h (NC_LDS_SPLIT) push this kernel's band arrays into
+// the asm LDS batches of nc_device.h (lds_read16) push this kernel's band arrays into
 // scratch; it keeps the compiler-scheduled FFT reads
 #define NC_LDS_SPLIT 0
 

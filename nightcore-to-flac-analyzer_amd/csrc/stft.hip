@@ -20,35 +20,42 @@
 #include "nc_engine.h"
 #include "nc_piptrack.h"
 
-#ifndef NC_SM_TWB  // stage-3 twiddles as asm batches too
-#define NC_SM_TWB 1
-#endif
 #include "stft_args.h"
 
 namespace nc {
 
-#ifndef NC_SM_WAVES
-#define NC_SM_WAVES 14
-#endif
-// Workgroups per CU in the grid.  2 measures the same alone (585 against 582-591 us per 560
-// windows) but slower in the step (11.44-12.18 against 11.27-11.60 ms, 4 alternating runs):
-// the extra workgroups queue behind the chroma stream's kernels.
-#ifndef NC_SM_GRIDX
-#define NC_SM_GRIDX 1
-#endif
-#ifndef NC_SM_DIAG  // diagnosis variants only: 1 no mel, 2 no sample loads, 4 no S_db stores
-#define NC_SM_DIAG 0
-#endif
-#ifndef NC_SM_MEL_GLOBAL  // 1: mel lane weights read through L1 instead of staged in LDS
-#define NC_SM_MEL_GLOBAL 0
-#endif
-#ifndef NC_SM_HANN_LDS  // 1: the 2048-tap Hann window staged in LDS (else read through L1 per frame)
-#define NC_SM_HANN_LDS 1
-#endif
-constexpr int SM_HANN2 = NC_SM_HANN_LDS ? 1024 : 0;  // float2 elements of the staged window
-constexpr int SM_WAVES = NC_SM_WAVES;
+// Measured and not kept (rounds 2-3): two workgroups per CU (the same alone,
+// slower in the step: the extra workgroups queue behind the chroma stream's kernels); the
+// mel weights read through L1 instead of LDS (16 waves: 625 against 579 us per 560 windows);
+// the Hann window through L1 (607 against 566 us).
+constexpr int SM_HANN2 = 1024;  // float2 elements of the staged Hann window
+constexpr int SM_WAVES = 14;
 constexpr int SM_THREADS = SM_WAVES * 64;
 using SmTw = StagedTw<1024>;  // per-stage twiddle table in LDS (conflict-free reads)
+
+// Mel band loops with compile-time trip counts, unrolled in load batches: 562-576 against
+// 577-596 us per 560 windows (round 3, same session), bit-identical.
+constexpr int kMelJ0 = 3, kMelJ1 = 14;  // float4 steps of the short / long band of a lane (nc_tables.cpp)
+constexpr int kMelB = 7;                // steps per load batch
+
+// acc = the fmaf chain of mel_loop over j < nj (< J), in the same order: batches of kMelB
+// steps, loads first (predicated per lane), then the chain
+template <int J>
+__device__ __forceinline__ void mel_unrolled(const float* pw, const float4* w4, int lo, int nj, int lane, float& acc) {
+#pragma unroll
+  for (int j0 = 0; j0 < J; j0 += kMelB) {
+    float4 p[kMelB], w[kMelB];
+#pragma unroll
+    for (int j = 0; j < kMelB; ++j)
+      if (j0 + j < J && j0 + j < nj) {
+        p[j] = *reinterpret_cast<const float4*>(pw + lo + 4 * (j0 + j));
+        w[j] = w4[(j0 + j) * 64 + lane];
+      }
+#pragma unroll
+    for (int j = 0; j < kMelB; ++j)
+      if (j0 + j < J && j0 + j < nj) acc = fmaf(w[j].w, p[j].w, fmaf(w[j].z, p[j].z, fmaf(w[j].y, p[j].y, fmaf(w[j].x, p[j].x, acc))));
+  }
+}
 
 __device__ __forceinline__ int seq_of_frame(const int64_t* base, int n, int64_t g) {
   int lo = 0, hi = n - 1;
@@ -63,7 +70,7 @@ __device__ __forceinline__ int seq_of_frame(const int64_t* base, int n, int64_t 
 __host__ __device__ __forceinline__ int al4(int n) { return (n + 3) & ~3; }
 
 size_t stft_mel_lds_bytes(int mel_j) {
-  return (size_t)al4(SmTw::size) * sizeof(float2) + (NC_SM_MEL_GLOBAL ? 0 : (size_t)mel_j * 64 * sizeof(float4)) +
+  return (size_t)al4(SmTw::size) * sizeof(float2) + (size_t)mel_j * 64 * sizeof(float4) +
          (size_t)SM_HANN2 * sizeof(float2) + (size_t)SM_WAVES * LdsSize<1024>::value * sizeof(float2);
 }
 
@@ -73,14 +80,13 @@ __global__ __launch_bounds__(SM_THREADS) void stft_mel_kernel(StftMelArgs a) {
   float2* sh_tw = reinterpret_cast<float2*>(smem);
   float4* sh_w4 = reinterpret_cast<float4*>(sh_tw + al4(SmTw::size));  // [mel_j0 + mel_j1][64]
   const int lane0 = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform (SGPR)
-  float2* sh_hann = reinterpret_cast<float2*>(sh_w4 + (NC_SM_MEL_GLOBAL ? 0 : (a.mel_j0 + a.mel_j1) * 64));
+  float2* sh_hann = reinterpret_cast<float2*>(sh_w4 + (a.mel_j0 + a.mel_j1) * 64);
   float2* fftbuf = sh_hann + SM_HANN2 + wave * LdsSize<1024>::value;
 
   fill_staged_tw<1024>(sh_tw, a.tw, threadIdx.x, SM_THREADS);
   for (int i = threadIdx.x; i < SM_HANN2; i += SM_THREADS) sh_hann[i] = reinterpret_cast<const float2*>(a.hann2048)[i];
-  if (!NC_SM_MEL_GLOBAL)
-    for (int i = threadIdx.x; i < (a.mel_j0 + a.mel_j1) * 64; i += SM_THREADS) sh_w4[i] = a.mel_w4[i];
-  const float4* mw4 = NC_SM_MEL_GLOBAL ? a.mel_w4 : sh_w4;
+  for (int i = threadIdx.x; i < (a.mel_j0 + a.mel_j1) * 64; i += SM_THREADS) sh_w4[i] = a.mel_w4[i];
+  const float4* mw4 = sh_w4;
   __syncthreads();
 
   const int64_t n_groups = (a.total_frames + SM_WAVES - 1) / SM_WAVES;
@@ -114,20 +120,12 @@ __global__ __launch_bounds__(SM_THREADS) void stft_mel_kernel(StftMelArgs a) {
     FftIn<1024> in;
     double e = 0.0;
     const bool interior = s0 >= 0 && s0 + 2048 <= L && ((off & 1) == 0);
-    if (NC_SM_DIAG & 2) {
-#pragma unroll
-      for (int r = 0; r < 16; ++r) in[0][r] = make_float2((float)(lane + r), (float)(g - r));
-    } else if (interior) {
+    if (interior) {
       const float2* x2 = reinterpret_cast<const float2*>(x + s0);
       float2 xv[16], hw[16];  // samples and window pairs (h[2n], h[2n + 1]), n = lane + 64 r
 #pragma unroll
       for (int r = 0; r < 16; ++r) xv[r] = x2[lane + 64 * r];  // issued first: the LDS batch hides under them
-      if constexpr (NC_SM_HANN_LDS) {
-        lds_read16_strided<0, 64 * 8>(hw, lds_addr(sh_hann + lane));
-      } else {
-#pragma unroll
-        for (int r = 0; r < 16; ++r) hw[r] = reinterpret_cast<const float2*>(hann)[lane + 64 * r];
-      }
+      lds_read16_strided<0, 64 * 8>(hw, lds_addr(sh_hann + lane));
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int n = lane + 64 * r;
@@ -168,7 +166,7 @@ __global__ __launch_bounds__(SM_THREADS) void stft_mel_kernel(StftMelArgs a) {
     stockham_stage_regs<1024, 16, 1, 64, false, 0, 0>(in, fftbuf, twl, lane);
     stockham_stage<1024, 16, 16, 64, false, 0, 0>(fftbuf, twl, lane);
     float2 v[4][4];
-    fft1024_last_mirror<SmTw::s3, NC_SM_TWB>(fftbuf, twl, lane, v);
+    fft1024_last_mirror<SmTw::s3, true>(fftbuf, twl, lane, v);
     float* pw = reinterpret_cast<float*>(fftbuf);  // power P[k], k in [0, 1024] (all Z reads precede)
     rsplit_mirror<SmTw::split>(v, twl, lane, [&](int k, float2 X, float2 XN) {
       pw[k] = fmaf(X.x, X.x, X.y * X.y);
@@ -192,35 +190,13 @@ __global__ __launch_bounds__(SM_THREADS) void stft_mel_kernel(StftMelArgs a) {
     // Slaney mel: lane l owns bands l and 127 - l, read as float4 steps from a 16-byte aligned
     // first bin with zero-padded weights (fmaf chain in bin order, as the CSR form)
     float acc0 = 0.0f, acc1 = 0.0f;
-    if (NC_SM_DIAG & 1) {
-      acc0 = pw[lane];
-      acc1 = pw[1023 - lane];
-    } else {
-      const int lo = a.mel_lo4[lane], nj = a.mel_nj4[lane];
-      for (int j = 0; j < a.mel_j0; ++j)
-        if (j < nj) {
-          const float4 p = *reinterpret_cast<const float4*>(pw + lo + 4 * j);
-          const float4 w = mw4[j * 64 + lane];
-          acc0 = fmaf(w.w, p.w, fmaf(w.z, p.z, fmaf(w.y, p.y, fmaf(w.x, p.x, acc0))));
-        }
-    }
-    if (!(NC_SM_DIAG & 1)) {
-      const int lo = a.mel_lo4[64 + lane], nj = a.mel_nj4[64 + lane];
-      const float4* w1 = mw4 + a.mel_j0 * 64;
-      for (int j = 0; j < a.mel_j1; ++j)
-        if (j < nj) {
-          const float4 p = *reinterpret_cast<const float4*>(pw + lo + 4 * j);
-          const float4 w = w1[j * 64 + lane];
-          acc1 = fmaf(w.w, p.w, fmaf(w.z, p.z, fmaf(w.y, p.y, fmaf(w.x, p.x, acc1))));
-        }
-    }
+    mel_unrolled<kMelJ0>(pw, mw4, a.mel_lo4[lane], a.mel_nj4[lane], lane, acc0);
+    mel_unrolled<kMelJ1>(pw, mw4 + kMelJ0 * 64, a.mel_lo4[64 + lane], a.mel_nj4[64 + lane], lane, acc1);
     const float db0 = 10.0f * log10f(fmaxf(1e-10f, acc0));
     const float db1 = 10.0f * log10f(fmaxf(1e-10f, acc1));
     float* row = a.sdb + g * 128;
-    if (!(NC_SM_DIAG & 4) || db0 == 12345.0f) {
-      row[lane] = db0;
-      row[127 - lane] = db1;
-    }
+    row[lane] = db0;
+    row[127 - lane] = db1;
     const float mx = wave_max_u(fmaxf(db0, db1));
     if (lane == 0) a.frame_max[g] = mx;
   }
@@ -245,13 +221,17 @@ int launch_stft_mel(Context& ctx, const StftMelArgs& args, hipStream_t st) {
     set_error("stft_mel: hop must be even and <= 512");
     return -2;
   }
+  if (a.mel_j0 != kMelJ0 || a.mel_j1 != kMelJ1) {
+    set_error("stft_mel: mel table trip counts differ from the kernel's compile-time ones");
+    return -2;
+  }
   const size_t lds = stft_mel_lds_bytes(a.mel_j0 + a.mel_j1);
   if (lds > 160 * 1024) {
     set_error("stft_mel: LDS layout exceeds 160 KiB");
     return -2;
   }
   const int64_t n_groups = (a.total_frames + SM_WAVES - 1) / SM_WAVES;
-  const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(n_groups, (int64_t)ctx.num_cu * NC_SM_GRIDX * (lds <= 80 * 1024 ? 2 : 1)));
+  const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(n_groups, (int64_t)ctx.num_cu * (lds <= 80 * 1024 ? 2 : 1)));
   {
     KTimer kt_(ctx, "stft_mel", st);
     a.span = kt_.span();

@@ -27,18 +27,7 @@ namespace nc {
 //   T tg_mean[k] = sum_{i<3} phi_i(k) (Hank_i(k) - Toep_i(k)),  phi = (1, cos theta k, sin theta k),
 //   Hank_i(k) = sum_u a_i[u] x[u + k],  Toep_i(k) = sum_u b_i[u] x[u - k],
 // with a_i / b_i built from prefix sums of the frame normalisers (derivation in nc_tgcorr.h).
-// Diagnosis knobs (tools/wtg_variants.sh): NC_WT_THREADS workgroup size, NC_WT_STAGE
-// stops after 1 onset, 2 normalisers, 3 prefix sums + sequences (4 = the whole kernel).
-#ifndef NC_WT_THREADS
-#define NC_WT_THREADS 512
-#endif
-#ifndef NC_WT_RINV_BLOCKED
-#define NC_WT_RINV_BLOCKED 1
-#endif
-#ifndef NC_WT_STAGE
-#define NC_WT_STAGE 4
-#endif
-constexpr int WT_THREADS = NC_WT_THREADS;  // 8 waves; ~78 KB LDS -> two windows per CU
+constexpr int WT_THREADS = 512;  // 8 waves; ~78 KB LDS -> two windows per CU
 constexpr size_t kWinTgLdsCap = 160 * 1024 - 1024;  // dynamic LDS; the rest holds BlockScratch
 
 struct WinTgArgs {
@@ -253,20 +242,14 @@ __global__ __launch_bounds__(WT_THREADS) __attribute__((amdgpu_waves_per_eu(4)))
     sh_cs[2 * j + 1] = s;
   }
   wtg_onset<WT_THREADS>(a, w, sh_x, red);
-#if NC_WT_RINV_BLOCKED
-  if (NC_WT_STAGE >= 2) wtg_rinv_blocked<WT_THREADS>(sh_x, sh_wsq, T, acw, seq, sh_q, sh_rinv);
-#else
-  if (NC_WT_STAGE >= 2) wtg_rinv<WT_THREADS>(sh_x, sh_wsq, T, acw, sh_rinv);
-#endif
+  wtg_rinv_blocked<WT_THREADS>(sh_x, sh_wsq, T, acw, seq, sh_q, sh_rinv);
   __syncthreads();
-  if (NC_WT_STAGE >= 3) {
-    tgc_prefix(sh_rinv, sh_cs, T, acw, sh_q, tid, WT_THREADS);
-    __syncthreads();
-    tgc_sequences(sh_x, sh_q, sh_cs, T, acw, L.U, seq, tid, WT_THREADS);
-  }
+  tgc_prefix(sh_rinv, sh_cs, T, acw, sh_q, tid, WT_THREADS);
+  __syncthreads();
+  tgc_sequences(sh_x, sh_q, sh_cs, T, acw, L.U, seq, tid, WT_THREADS);
   __syncthreads();
   double* part = lds + L.scr;  // [segments][blocks * LB], over the normaliser scratch
-  if (NC_WT_STAGE >= 4) tgc_correlate(sh_x, seq, acw, L.U, part, tid, WT_THREADS);
+  tgc_correlate(sh_x, seq, acw, L.U, part, tid, WT_THREADS);
   __syncthreads();
   const int nseg = tgc_segments(acw, WT_THREADS), stride = tgc_blocks(acw) * TGC_LB;
   for (int k = tid; k < acw; k += WT_THREADS) {

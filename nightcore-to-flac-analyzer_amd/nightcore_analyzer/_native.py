@@ -44,12 +44,12 @@ SIGNATURES = {
     "nc_tempo_prior": (I32, [P, P, P, P, P, P, P, P, I32, P, P]),
     "nc_ibi_from_beats": (I32, [P, P, P, P, I32, I32, I32, P, P, P]),
     "nc_chroma_workspace_bytes": (SZ, [P, I32, I64]),
-    "nc_chroma_mean": (I32, [P, P, P, P, I32, I64, I64, P, P, P, P, SZ, P]),
+    "nc_chroma_mean": (I32, [P, P, P, P, I32, I64, I64, P, P, P, P, P, SZ, P]),
     "nc_chroma_lag": (I32, [P, P, P, P, I32, P, P]),
     "nc_chroma_lag_margin": (I32, [P, P, P, P, I32, P, P, P]),
     "nc_xcorr_peak": (I32, [P, P, P, I32, I32, P, P]),
     "nc_window_stage_tuning": (I32, [P, P, P, P, I32, I32, I32, P, P, P, P, P, I32, P, P, P, P, P, SZ, P]),
-    "nc_chroma_mean_shared": (I32, [P, P, P, P, I32, I64, I64, P, P, P, P, I64, P, P, P, P, P, SZ, P]),
+    "nc_chroma_mean_shared": (I32, [P, P, P, P, I32, I64, I64, P, P, P, P, P, I64, P, P, P, P, P, SZ, P]),
     "nc_window_energy": (I32, [P, P, P, I32, I32, P, P]),
     "nc_energy_gate": (I32, [P, P, P, P, I32, D, P, P]),
     "nc_collect_valid": (I32, [P, P, P, P, P, P, I32, I32, P, P, P]),

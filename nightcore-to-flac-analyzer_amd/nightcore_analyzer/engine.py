@@ -79,6 +79,7 @@ def percentile_params(n_boot: int, ci: float) -> Tuple[float, float, float, floa
 
 PEAK_SLOTS = 192   # piptrack peak slots per tuning frame (csrc/nc_piptrack.h kPeakSlots)
 NEAR_TIE = 1e-3    # chroma-lag decisions closer than this (relative xcorr gap) are reported
+TUNING_NEAR_TIE = 1  # tuning decisions whose histogram argmax leads by at most this many residuals
 _logger = logging.getLogger("nightcore_analyzer")
 
 
@@ -501,7 +502,7 @@ class Engine:
 
     GROUPS_IN_FLIGHT = 3    # pair groups queued ahead of the host's oldest wait (analyze)
 
-    KERNEL_TAGS = ("stft_mel", "window_tg", "tuning_peaks", "decimate", "cqt_chroma", "trim_blocks", "tempo_beat",
+    KERNEL_TAGS = ("stft_mel", "window_tg", "tuning_peaks", "decimate", "cqt_low", "cqt_high", "trim_blocks", "tempo_beat",
                    "tg_slide", "spectral_frames", "spectral_bins")
 
     def kernel_profile(self, on) -> None:
@@ -518,6 +519,10 @@ class Engine:
             self.ctx.call(fn, tag.encode(), C.byref(ms), C.byref(n))
             if n.value:
                 out[tag] = (ms.value, n.value)
+        if "cqt_low" in out and "cqt_high" in out:
+            # the CQT unit of the roofline (7 octaves of every chunk of a chroma call): the two
+            # kernels' times summed, as rocprofv3 --stats lists them (two rows)
+            out["cqt_chroma"] = (out["cqt_low"][0] + out["cqt_high"][0], out["cqt_low"][1])
         return out
 
     def kernel_times(self) -> Dict[str, Tuple[float, int]]:
@@ -1030,6 +1035,7 @@ class Engine:
         # one zero-filled output arena, copied back in one D2H
         ar = _Arena()
         for name, n, dt in (("chroma", n_chunks * 12, np.float32), ("tuning", n_chunks, np.float32),
+                            ("tmargin", n_chunks, np.int32),
                             ("clag", n_cp, np.int32), ("cmargin", n_cp, np.float64), ("vals", TV + PV, np.float64), ("energy", n_win, np.float64),
                             ("active", n_win, np.uint8), ("bpm", n_win, np.float64), ("lag", n_win, np.int32),
                             ("nbeats", n_win, np.int32), ("margin", n_win, np.float64), ("prior", B, np.float64),
@@ -1103,13 +1109,14 @@ class Engine:
             if share:
                 self.call("nc_chroma_mean_shared", signals.buf.data_ptr(), d["chunk_off"].data_ptr(),
                           d["chunk_len"].data_ptr(), n_chunks, tot_len, int(max(chunk_len)), o["chroma"].data_ptr(),
-                          o["tuning"].data_ptr(), None, d["tf_skip"].data_ptr(), int(tf_skip.sum()),
+                          o["tuning"].data_ptr(), None, o["tmargin"].data_ptr(), d["tf_skip"].data_ptr(),
+                          int(tf_skip.sum()),
                           peaks[0].data_ptr(), peaks[1].data_ptr(), o["npk"].data_ptr(), ev_stft.cuda_event,
                           ws_c.data_ptr(), ws_c.numel(), st2)
             else:
                 self.call("nc_chroma_mean", signals.buf.data_ptr(), d["chunk_off"].data_ptr(),
                           d["chunk_len"].data_ptr(), n_chunks, tot_len, int(max(chunk_len)), o["chroma"].data_ptr(),
-                          o["tuning"].data_ptr(), None, ws_c.data_ptr(), ws_c.numel(), st2)
+                          o["tuning"].data_ptr(), None, o["tmargin"].data_ptr(), ws_c.data_ptr(), ws_c.numel(), st2)
             self.call("nc_chroma_lag_margin", o["chroma"].data_ptr(), d["lag_src"].data_ptr(),
                       d["lag_nc"].data_ptr(), n_cp, o["clag"].data_ptr(), o["cmargin"].data_ptr(), st2)
             self.call("nc_pitch_hz", o["clag"].data_ptr(), n_cp, pvals[0:n_cp].data_ptr(),
@@ -1126,7 +1133,7 @@ class Engine:
                       sout[0:n_pitch_jobs].data_ptr(), sout[n_pitch_jobs:2 * n_pitch_jobs].data_ptr(),
                       sout[2 * n_pitch_jobs:3 * n_pitch_jobs].data_ptr(), None, d["s_wsoff"].data_ptr(),
                       d["s_cap"].data_ptr(), ws2.data_ptr(), ws2.numel(), st2)
-        stage_copy("pitch", s2, ["clag", "cmargin", ("vals", TV, TV + PV), "sout", "chroma", "tuning"])
+        stage_copy("pitch", s2, ["clag", "cmargin", ("vals", TV, TV + PV), "sout", "chroma", "tuning", "tmargin"])
         ev_chroma = torch.cuda.Event()
         ev_chroma.record(s2)
 
@@ -1402,12 +1409,19 @@ def assemble_pair(b, p: Params, h, ibi, starts, w0, w1, f_len, strip_len, lead, 
             src_p, nc_p = pick
         L(f"  Pitch method: {method}")
         margins = h["cmargin"][c0:c1].copy()
+        tmargins = h["tmargin"][2 * c0:2 * c1].copy() if "tmargin" in h else None
         out.detail.update(chunk_lags=lags, chunk_lag_margin=margins, tuning=h["tuning"][2 * c0:2 * c1].copy(),
-                          chroma=h["chroma"][24 * c0:24 * c1].reshape(-1, 12).copy())
+                          chroma=h["chroma"][24 * c0:24 * c1].reshape(-1, 12).copy(), tuning_margin=tmargins)
         if len(margins) and margins.min() < NEAR_TIE:
             # not in the reference's log stream (kept identical); Python logging only
             _logger.info("chroma lag near-tie in pair %d: chunk(s) %s, relative margin %s", b,
                          np.flatnonzero(margins < NEAR_TIE).tolist(), np.round(margins[margins < NEAR_TIE], 6).tolist())
+        if tmargins is not None and len(tmargins) and tmargins.min() <= TUNING_NEAR_TIE:
+            # a tuning histogram whose best bin leads by <= 1 residual: one peak decides the
+            # CQT's fmin shift, so an f32 / f64 difference in a single peak could flip it
+            _logger.info("tuning near-tie in pair %d: chunk(s) %s (src, nc interleaved), count margin %s", b,
+                         np.flatnonzero(tmargins <= TUNING_NEAR_TIE).tolist(),
+                         tmargins[tmargins <= TUNING_NEAR_TIE].tolist())
     else:
         L("Skipping pitch estimation.")
         src_p, nc_p, method = [], [], None

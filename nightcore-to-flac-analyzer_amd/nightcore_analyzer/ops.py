@@ -121,7 +121,7 @@ def chroma_means(eng: Engine, audios: Sequence[np.ndarray]) -> Tuple[np.ndarray,
     tot = int(sig.length.sum())
     ws = eng.workspace("chroma", eng.ctx.lib.nc_chroma_workspace_bytes(eng.ctx.h, n, tot))
     eng.call("nc_chroma_mean", sig.buf.data_ptr(), d["off"].data_ptr(), d["len"].data_ptr(), n, tot,
-             int(sig.length.max()), out.data_ptr(), tun.data_ptr(), None, ws.data_ptr(), ws.numel(), eng.stream())
+             int(sig.length.max()), out.data_ptr(), tun.data_ptr(), None, None, ws.data_ptr(), ws.numel(), eng.stream())
     return out.cpu().numpy().reshape(n, 12), tun.cpu().numpy(), out
 
 

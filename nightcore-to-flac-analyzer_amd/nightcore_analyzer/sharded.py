@@ -66,8 +66,9 @@ from .engine import (CHUNK_SEC, HOP_LENGTH, MIN_BEATS, MIN_CHUNKS, REF_HZ, SR, D
 # exchanged window record: exists, energy_db, bpm, nbeats, tempo lag, decision margin
 R_EXISTS, R_ENERGY, R_BPM, R_NBEATS, R_LAG, R_MARGIN = range(6)
 W_FIELDS = 6
-# chunk-pair record: exists, lag, tuning (src, nc), mean chroma (src 12, nc 12), lag margin
-CP_FIELDS = 1 + 3 + 24 + 1
+# chunk-pair record: exists, lag, tuning (src, nc), mean chroma (src 12, nc 12), lag margin,
+# tuning decision margins (src, nc)
+CP_FIELDS = 1 + 3 + 24 + 1 + 2
 CP_COST = 8          # a chunk pair's weight in the item line, in windows
 
 
@@ -349,7 +350,8 @@ class DeviceStages:
 
     def chunks(self, chunk_off: Sequence[int], chunk_len: Sequence[int]) -> np.ndarray:
         """Mean chroma of every chunk (files interleaved src, nc per chunk pair) and the
-        pair lags -> [n_pairs, 28]: lag, tuning (src, nc), chroma (src 12, nc 12), margin."""
+        pair lags -> [n_pairs, 30]: lag, tuning (src, nc), chroma (src 12, nc 12), lag margin,
+        tuning margins (src, nc)."""
         eng, n = self.eng, len(chunk_off)
         if n == 0:
             return np.zeros((0, CP_FIELDS - 1), np.float64)
@@ -363,16 +365,18 @@ class DeviceStages:
             chroma = torch.empty(n * 12, dtype=torch.float32, device=eng.dev)
             tun = torch.empty(n, dtype=torch.float32, device=eng.dev)
             lag = torch.empty(n // 2, dtype=torch.int32, device=eng.dev)
+            tmg = torch.empty(n, dtype=torch.int32, device=eng.dev)
             tot = int(np.sum(chunk_len))
             ws = eng.workspace("sp_chroma", eng.ctx.lib.nc_chroma_workspace_bytes(eng.ctx.h, n, tot))
             eng.call("nc_chroma_mean", self.sig.buf.data_ptr(), d["off"].data_ptr(), d["len"].data_ptr(), n, tot,
-                     int(max(chunk_len)), chroma.data_ptr(), tun.data_ptr(), None, ws.data_ptr(), ws.numel(),
+                     int(max(chunk_len)), chroma.data_ptr(), tun.data_ptr(), None, tmg.data_ptr(), ws.data_ptr(), ws.numel(),
                      eng.stream())
             mg = torch.empty(n // 2, dtype=torch.float64, device=eng.dev)
             eng.call("nc_chroma_lag_margin", chroma.data_ptr(), d["si"].data_ptr(), d["ni"].data_ptr(), n // 2,
                      lag.data_ptr(), mg.data_ptr(), eng.stream())
             rec = torch.cat([lag.to(torch.float64)[:, None], tun.to(torch.float64).view(-1, 2),
-                             chroma.to(torch.float64).view(-1, 24), mg[:, None]], dim=1)
+                             chroma.to(torch.float64).view(-1, 24), mg[:, None], tmg.to(torch.float64).view(-1, 2)],
+                            dim=1)
             return rec.cpu().numpy()
 
     def bootstrap(self, jobs, seed: int):
@@ -699,6 +703,7 @@ def _consensus(stages, p: Params, pl, align, active, energy, full, prior, cps, o
     h = {"active_l": active.tolist(), "energy": energy, "clag_l": lags, "pvals": pvals, "pvals_l": pvals.tolist(),
          "sout_l": sout.tolist(), "bout_l": bout.tolist(), "tuning": tun, "chroma": chroma,
          "cmargin": cps[:, 27].copy() if n_cp else np.zeros(0),
+         "tmargin": cps[:, 28:30].reshape(-1).astype(np.int32) if n_cp else np.zeros(0, np.int32),
          "bpm_l": bpm.tolist(), "nbeats_l": [int(v) for v in nbeats], "prior_l": prior.tolist(),
          "margin": full[:, R_MARGIN]}
     starts_l = [s.tolist() for s in pl.starts]

@@ -666,23 +666,41 @@ def tuning_edges(resolution=0.01):
     return np.linspace(-0.5, 0.5, int(np.ceil(1.0 / resolution)) + 1)
 
 
-def pitch_tuning(freqs, resolution=0.01, bins_per_octave=36):
+def tuning_counts(freqs, resolution=0.01, bins_per_octave=36):
+    """The residual histogram of librosa.pitch_tuning (None when no frequency is > 0)."""
     freqs = np.atleast_1d(freqs)
     freqs = freqs[freqs > 0]
     if not np.any(freqs):
-        return 0.0
+        return None
     octs = np.log2(freqs / (440.0 / 16))
     residual = np.mod(bins_per_octave * octs, 1.0)
     residual[residual >= 0.5] -= 1.0
-    counts, edges = np.histogram(residual, tuning_edges(resolution))
-    return float(edges[np.argmax(counts)])
+    counts, _ = np.histogram(residual, tuning_edges(resolution))
+    return counts
 
 
-def estimate_tuning(y, sr=22050, n_fft=2048, bins_per_octave=36):
+def pitch_tuning(freqs, resolution=0.01, bins_per_octave=36):
+    counts = tuning_counts(freqs, resolution, bins_per_octave)
+    if counts is None:
+        return 0.0
+    return float(tuning_edges(resolution)[np.argmax(counts)])
+
+
+def estimate_tuning_detail(y, sr=22050, n_fft=2048, bins_per_octave=36):
+    """(tuning, bin index, decision margin): estimate_tuning with the histogram's argmax bin
+    and its lead over the runner-up bin (test diagnostics; 0 when no peak passes)."""
     pitch, mag = piptrack(y, sr, n_fft)
     pm = pitch > 0
     thr = np.median(mag[pm]) if pm.any() else 0.0
-    return pitch_tuning(pitch[(mag >= thr) & pm], 0.01, bins_per_octave)
+    counts = tuning_counts(pitch[(mag >= thr) & pm], 0.01, bins_per_octave)
+    if counts is None:
+        return 0.0, 50, 0
+    best = int(np.argmax(counts))
+    return float(tuning_edges(0.01)[best]), best, int(counts[best] - np.max(np.delete(counts, best)))
+
+
+def estimate_tuning(y, sr=22050, n_fft=2048, bins_per_octave=36):
+    return estimate_tuning_detail(y, sr, n_fft, bins_per_octave)[0]
 
 
 def cq_to_chroma(n_input=252, bins_per_octave=36, n_chroma=12) -> np.ndarray:

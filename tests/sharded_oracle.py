@@ -59,12 +59,15 @@ class OracleStages:
 
     def chunks(self, chunk_off, chunk_len):
         self._check("chunks")
-        out = np.zeros((len(chunk_off) // 2, 28))
+        out = np.zeros((len(chunk_off) // 2, 30))
         for k in range(len(chunk_off) // 2):
             a = self.buf[chunk_off[2 * k]:chunk_off[2 * k] + chunk_len[2 * k]]
             b = self.buf[chunk_off[2 * k + 1]:chunk_off[2 * k + 1] + chunk_len[2 * k + 1]]
             ca, cb = refglue.mean_chroma(a), refglue.mean_chroma(b)
             out[k, 0] = refglue.cyclic_xcorr_peak(ca, cb)
+            ta, tb = ncref.estimate_tuning_detail(a), ncref.estimate_tuning_detail(b)
+            out[k, 1:3] = ta[0], tb[0]
+            out[k, 28:30] = ta[2], tb[2]
             out[k, 3:15], out[k, 15:27] = ca, cb
             xc = np.sort([float(np.dot(ca, np.roll(cb, -j))) for j in range(12)])
             out[k, 27] = (xc[-1] - xc[-2]) / abs(xc[-1]) if xc[-1] else 0.0

@@ -21,7 +21,7 @@ def runs(path, csig, coff, clen, cn, CL, R=6):
     lib.nc_create.argtypes = [I32, C.POINTER(P)]
     lib.nc_chroma_workspace_bytes.restype = SZ
     lib.nc_chroma_workspace_bytes.argtypes = [P, I32, I64]
-    lib.nc_chroma_mean.argtypes = [P, P, P, P, I32, I64, I64, P, P, P, P, SZ, P]
+    lib.nc_chroma_mean.argtypes = [P, P, P, P, I32, I64, I64, P, P, P, P, P, SZ, P]
     ctx = P()
     assert lib.nc_create(0, C.byref(ctx)) == 0
     st = torch.cuda.current_stream().cuda_stream
@@ -32,7 +32,7 @@ def runs(path, csig, coff, clen, cn, CL, R=6):
         chroma = torch.full((cn * 12,), float("nan"), device="cuda")
         tun = torch.empty(cn, device="cuda")
         assert lib.nc_chroma_mean(ctx, csig.data_ptr(), coff.data_ptr(), clen.data_ptr(), cn, cn * CL, CL,
-                                  chroma.data_ptr(), tun.data_ptr(), None, cws.data_ptr(), cwsb, st) == 0
+                                  chroma.data_ptr(), tun.data_ptr(), None, None, cws.data_ptr(), cwsb, st) == 0
         torch.cuda.synchronize()
         outs.append(chroma.cpu().numpy().reshape(cn, 12).copy())
     return outs

@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round measurement in one GPU call: PMC traffic passes (-> profiles/r2_traffic.json, copied to
+# Round measurement in one GPU call: PMC traffic passes (-> profiles/r3_traffic.json, copied to
 # the output dir), the default bench line (which reads that traffic file), and a rocprofv3
 # kernel-stats summary of the timed region.     usage: tools/gpu_round.sh TAG
 set -o pipefail
@@ -9,7 +9,7 @@ R=$GRAFT_REPO_ROOT
 mkdir -p $O
 export TMPDIR=/tmp
 bash tools/pmc_traffic.sh $O/pmc > $O/traffic.log 2>&1 || { echo "traffic failed"; tail -20 $O/traffic.log; exit 1; }
-cp profiles/r2_traffic.json $O/
+cp profiles/r3_traffic.json $O/
 timeout -k 10 500 python -u bench.py > $O/bench.json 2> $O/bench.err || { echo "bench failed"; tail -20 $O/bench.err; exit 1; }
 cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $R/$O/prof -o run --output-format csv -- \
   python3 $R/bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-config5 --no-spectral --no-resample --no-upload \

@@ -1,7 +1,7 @@
 #!/bin/bash
 # HBM traffic per launch of the bench's kernels: two rocprofv3 counter passes (FETCH_SIZE, then
 # WRITE_SIZE: they do not fit one pass) over the bench command, each under its own limit, then
-# tools/traffic.py -> profiles/r2_traffic.json.     usage: tools/pmc_traffic.sh OUTDIR
+# tools/traffic.py -> profiles/r3_traffic.json.     usage: tools/pmc_traffic.sh OUTDIR
 set -o pipefail
 OUT=$1
 R=$GRAFT_REPO_ROOT

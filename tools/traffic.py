@@ -2,8 +2,8 @@
 """Per-launch HBM traffic of the bench kernels from the two counter passes of
 tools/pmc_traffic.sh, corrected per MI355X_MICROARCH.md (FETCH_SIZE reports half the
 bytes of a wide coalesced read on gfx950: hbm = 2 x FETCH_SIZE + WRITE_SIZE, KiB -> B),
-written to profiles/r2_traffic.json for bench.py's roofline.traffic.
-    python3 tools/traffic.py OUTDIR"""
+written to profiles/<NAME> (default r3_traffic.json) for bench.py's roofline.traffic.
+    python3 tools/traffic.py OUTDIR [NAME]"""
 import collections
 import csv
 import json
@@ -12,7 +12,7 @@ import sys
 from pathlib import Path
 
 REPO = Path(__file__).resolve().parents[1]
-TAGS = {"cqt_chroma_kernel": "cqt_fft", "cqt_mfma_kernel": "cqt_mfma", "cqt_mfma_low_kernel": "cqt_low",
+TAGS = {"cqt_mfma_kernel": "cqt_high", "cqt_mfma_low_kernel": "cqt_low",
         "cqt_tail_kernel": "cqt_tail",
         "stft_mel_kernel": "stft_mel", "tuning_peaks_kernel": "tuning_peaks",
         "trim_blocks_kernel": "trim_blocks", "window_tg_kernel": "window_tg", "decimate_kernel": "decimate", "decimate3_kernel": "decimate"}
@@ -20,10 +20,10 @@ TAGS = {"cqt_chroma_kernel": "cqt_fft", "cqt_mfma_kernel": "cqt_mfma", "cqt_mfma
 # 896 chunks x 1 764 000 B, 64 pairs of 3 969 000 + 3 175 200 samples x 4 B for the trim pass;
 # the octave chain reads levels 0 and 3 and writes levels 1-6 once per 441 000-sample chunk
 # (441 000 + 55 125 read, 220 500 + 110 250 + 55 125 + 27 563 + 13 782 + 6 891 written, f32)
-# the CQT is several launches per chroma call (octaves 3-6, octaves 0-2 as three launches or
-# the FFT kernel, the frame tail): their bytes per call are summed into "cqt_chroma", the
-# unit bench.py times
-CQT_PARTS = ("cqt_fft", "cqt_low", "cqt_mfma", "cqt_tail")
+# the CQT is two launches per chroma call (octaves 0-2, octaves 3-6): their bytes per call
+# are summed into "cqt_chroma", the unit bench.py times (the sum of the two kernels' times);
+# the frame tail (cqt_tail) is listed on its own
+CQT_PARTS = ("cqt_low", "cqt_high")
 ALG_STEP = {"cqt_chroma": 896 * 1764000, "stft_mel": 3968 * 882000, "trim_blocks": 64 * (3969000 + 3175200) * 4,
             "decimate": 896 * 4 * (441000 + 55125 + 220500 + 110250 + 55125 + 27563 + 13782 + 6891)}
 
@@ -65,14 +65,14 @@ def main(out):
             k["alg_bytes_per_launch"] = int(ALG_STEP[tag] * calls / len(fetch[tag]))
         kern[tag] = k
     present = [t for t in CQT_PARTS if t in kern]
-    if "cqt_tail" in present:
-        n_calls = kern["cqt_tail"]["launches"]  # one tail per chroma call
+    if len(present) == len(CQT_PARTS):
+        n_calls = kern["cqt_low"]["launches"]  # one of each per chroma call
         per_call = lambda key: sum(kern[t][key] * kern[t]["launches"] / n_calls for t in present)
         k = {"launches": n_calls, "parts": present,
              "fetch_size_kib_raw": round(per_call("fetch_size_kib_raw"), 2),
              "write_size_kib": round(per_call("write_size_kib"), 2),
              "hbm_bytes_per_launch": int(per_call("hbm_bytes_per_launch")),
-             "launches_per_step": kern["cqt_tail"]["launches_per_step"],
+             "launches_per_step": kern["cqt_low"]["launches_per_step"],
              "alg_bytes_per_launch": int(ALG_STEP["cqt_chroma"] * calls / n_calls)}
         kern["cqt_chroma"] = k
     doc = {"workload": "config3-64pairs", "commit": commit, "analyze_calls": calls,
@@ -83,7 +83,8 @@ def main(out):
                          "the bytes of a wide coalesced read (MI355X_MICROARCH.md; calibrated with "
                          "tools/calib_fetch.hip: a 1 GiB stream read reports 0.500 GiB)",
            "kernels": kern}
-    (REPO / "profiles" / "r2_traffic.json").write_text(json.dumps(doc, indent=1) + "\n")
+    name = sys.argv[2] if len(sys.argv) > 2 else "r3_traffic.json"
+    (REPO / "profiles" / name).write_text(json.dumps(doc, indent=1) + "\n")
     print(json.dumps(doc, indent=1))
 
 

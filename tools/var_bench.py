@@ -15,7 +15,7 @@ REPO = Path(__file__).resolve().parents[1]
 sys.path.insert(0, str(REPO / "nightcore-to-flac-analyzer_amd"))
 from nightcore_analyzer import synth  # noqa: E402
 
-TAGS = (b"stft_mel", b"window_tg", b"decimate", b"tuning_peaks", b"tuning_select", b"cqt_chroma")
+TAGS = (b"stft_mel", b"window_tg", b"decimate", b"tuning_peaks", b"tuning_select", b"cqt_low", b"cqt_high")
 
 
 def bench(path, src):
@@ -28,7 +28,7 @@ def bench(path, src):
     lib.nc_window_stage.argtypes = [P, P, P, P, I32, I32, I32, P, P, P, P, SZ, P]
     lib.nc_chroma_workspace_bytes.restype = SZ
     lib.nc_chroma_workspace_bytes.argtypes = [P, I32, I64]
-    lib.nc_chroma_mean.argtypes = [P, P, P, P, I32, I64, I64, P, P, P, P, SZ, P]
+    lib.nc_chroma_mean.argtypes = [P, P, P, P, I32, I64, I64, P, P, P, P, P, SZ, P]
     lib.nc_profile_enable.argtypes = [P, I32]
     lib.nc_profile_read.argtypes = [P, C.c_char_p, C.POINTER(C.c_double), C.POINTER(I32)]
     ctx = P()
@@ -60,7 +60,7 @@ def bench(path, src):
         assert lib.nc_window_stage(ctx, sig.data_ptr(), off.data_ptr(), None, n, L, 512, onset.data_ptr(),
                                    tg.data_ptr(), en.data_ptr(), ws.data_ptr(), wsb, st) == 0
         assert lib.nc_chroma_mean(ctx, csig.data_ptr(), coff.data_ptr(), clen.data_ptr(), cn, cn * CL, CL,
-                                  chroma.data_ptr(), tun.data_ptr(), None, cws.data_ptr(), cwsb, st) == 0
+                                  chroma.data_ptr(), tun.data_ptr(), None, None, cws.data_ptr(), cwsb, st) == 0
     for _ in range(2):
         run()
     torch.cuda.synchronize()
