@@ -250,6 +250,35 @@ size_t nc_ibi_tempogram_workspace_bytes(const nc_ctx* ctx, int n_files, int64_t 
 int nc_ibi_tempogram(nc_ctx* ctx, const float* onset, const int64_t* frame_base, int n_files,
                      int64_t total_frames, int max_frames, int hop, double* tg_out, void* ws, size_t ws_bytes,
                      void* stream);
+/* The same pass split over ranks (window-sharded runs); one rank's
+ * share of file f is frames [t0[f], t1[f]) and tempogram tiles [b0[f], b1[f]) (2048 frames
+ * each); t0 / t1 / b0 / b1 are device int64 arrays.
+ * nc_ibi_mel_range:   the mel dB rows the onsets of [t0, t1) need (STFT frames
+ *                     [t0 - pad, t1 - pad + 1) within the file, pad = 1 + 1024 / hop) into ws,
+ *                     and max_out[f] = their largest dB value (-inf for none): this rank's
+ *                     share of power_to_db's top_db reference (C2: all-reduce MAX).
+ *                     total_rows = the host's count of those rows over all files.
+ * nc_ibi_onset_range: onset_out[obase[f] + t - t0[f]] for t in [t0[f], t1[f]) (obase =
+ *                     prefix of t1 - t0; total_out = its sum) against the file's global
+ *                     maximum gmax[f]; ws and total_rows as in the nc_ibi_mel_range call.
+ *                     (C4: the segments are gathered into each file's full onset.)
+ * nc_ibi_tempogram_tiles:  partial rows slab[(f * n_tblk + b) * N + k] of tiles
+ *                     b in [b0[f], b1[f]) from the FULL onset (n_tblk = ceil(max_frames / 2048),
+ *                     N = tempogram window); ws sized by nc_ibi_tempogram_workspace_bytes.
+ * nc_ibi_tempogram_reduce: tg_out[f * N + k] = (sum over b of slab rows, in order) / T_f
+ *                     once every tile's row is in slab (C3: the rows are gathered) -- the
+ *                     same bits as nc_ibi_tempogram. */
+size_t nc_ibi_range_workspace_bytes(const nc_ctx* ctx, int n_files, int64_t total_rows);
+int nc_ibi_mel_range(nc_ctx* ctx, const float* sig, const int64_t* file_off, const int64_t* file_len,
+                     int n_files, const int64_t* t0, const int64_t* t1, int hop, int64_t total_rows,
+                     float* max_out, void* ws, size_t ws_bytes, void* stream);
+int nc_ibi_onset_range(nc_ctx* ctx, int n_files, const int64_t* t0, int hop, int64_t total_out,
+                       const float* gmax, float* onset_out, void* ws, int64_t total_rows, void* stream);
+int nc_ibi_tempogram_tiles(nc_ctx* ctx, const float* onset, const int64_t* frame_base, int n_files,
+                           int64_t total_frames, int max_frames, int hop, const int64_t* b0, const int64_t* b1,
+                           double* slab, void* ws, size_t ws_bytes, void* stream);
+int nc_ibi_tempogram_reduce(nc_ctx* ctx, const double* slab, const int64_t* frame_base, int n_files,
+                            int max_frames, int hop, double* tg_out, void* stream);
 
 /* ---------------------------------------------------------------------------
  * K13  windowed waveform cross-correlation — the search loop of

@@ -101,10 +101,14 @@ __global__ void tg_pad_kernel(const float* onset, const int64_t* frame_base, int
 
 __global__ __launch_bounds__(256) void tg_rinv_kernel(const float* xpad, const int64_t* frame_base, int n_files,
                                                       int64_t total_frames, int N, const double* __restrict__ wsq,
-                                                      double* rinv) {
+                                                      const int64_t* b0, const int64_t* b1, double* rinv) {
   const int64_t g = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (g >= total_frames) return;
   const int f = find_file(frame_base, n_files, g);
+  if (b0) {  // only the frames of this rank's tiles
+    const int64_t tb = (g - frame_base[f]) / TG_TB;
+    if (tb < b0[f] || tb >= b1[f]) return;
+  }
   const float* x = xpad + g + (int64_t)f * N;  // xbase(f) + t
   double s = 0.0;
   for (int j = 0; j < N; ++j) {
@@ -120,6 +124,8 @@ struct TgSlideArgs {
   const int64_t* frame_base;
   int N;
   int n_tblk;     // tiles per file along frames (max over files)
+  const int64_t* b0 = nullptr;  // nullable [n_files]: only tiles [b0, b1) of each file
+  const int64_t* b1 = nullptr;
   double* slab;   // [n_files][n_tblk][N]
   unsigned long long* span = nullptr;  // nc_profile execution span (nc_device.h)
 };
@@ -133,7 +139,7 @@ __global__ __launch_bounds__(TG_KB) void tg_slide_kernel(TgSlideArgs a) {
   const int64_t base = a.frame_base[f];
   const int T = (int)(a.frame_base[f + 1] - base);
   const int t0 = tb * TG_TB;
-  if (t0 >= T) return;
+  if (t0 >= T || (a.b0 && (tb < a.b0[f] || tb >= a.b1[f]))) return;
   const int t1 = min(T, t0 + TG_TB);
   const int N = a.N;
   const float* xf = a.xpad + base + (int64_t)f * N + t0;
@@ -164,8 +170,118 @@ __global__ void tg_reduce_kernel(const double* slab, const int64_t* frame_base, 
   tg_out[(size_t)f * N + k] = s / (double)T;
 }
 
+// ------------------------------------------------------------------------------ D: one rank's share
+// The window-sharded runs split the hop-64 pass of a file over the ranks (SURVEY.md §8e
+// C2-C4): rank r computes the onsets of its frames [t0, t1) -- the mel dB rows they need,
+// [t0 - pad, t1 - pad + 1), then the onsets against the file's GLOBAL dB maximum (the
+// power_to_db top_db clamp, all-reduced with MAX between the two calls) -- and the tempogram
+// partial rows of its 2048-frame tiles [b0, b1) from the gathered full onset; the fixed-order
+// sum of every tile's row (tg_reduce_kernel) then equals the one-GPU result bit for bit.
+__global__ __launch_bounds__(256) void ibi_range_plan_kernel(const int64_t* file_len, const int64_t* t0,
+                                                             const int64_t* t1, int n_files, int hop, int pad,
+                                                             int64_t* row0, int64_t* row_base, int64_t* obase) {
+  // rows [row0, row1) of file f: its STFT frames [t0 - pad, t1 - pad + 1) within [0, T_f)
+  auto rows = [&](int f) -> int64_t {
+    const int64_t T = 1 + file_len[f] / hop;
+    const int64_t r0 = max((int64_t)0, t0[f] - pad), r1 = min(T, t1[f] - pad + 1);
+    return r1 > r0 ? r1 - r0 : 0;
+  };
+  block_prefix_table<256>(n_files, row_base, rows);
+  block_prefix_table<256>(n_files, obase, [&](int f) { return t1[f] > t0[f] ? t1[f] - t0[f] : (int64_t)0; });
+  __syncthreads();
+  for (int f = threadIdx.x; f < n_files; f += 256) row0[f] = max((int64_t)0, t0[f] - pad);
+}
+
+__global__ __launch_bounds__(256) void ibi_onset_range_kernel(const float* sdb, const int64_t* row_base,
+                                                              const int64_t* row0, const int64_t* t0,
+                                                              const int64_t* obase, const float* gmax, int n_files,
+                                                              int64_t total_out, int pad, float* onset) {
+  const int lane = threadIdx.x & 63;
+  const int64_t g = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (g >= total_out) return;
+  const int f = find_file(obase, n_files, g);
+  const int64_t t = t0[f] + (g - obase[f]);
+  float val = 0.0f;
+  if (t >= pad) {
+    const float c = gmax[f] - 80.0f;
+    const int64_t j = row_base[f] + (t - pad - row0[f]);
+    const float a0 = fmaxf(sdb[j * 128 + lane], c), a1 = fmaxf(sdb[(j + 1) * 128 + lane], c);
+    const float b0 = fmaxf(sdb[j * 128 + lane + 64], c), b1 = fmaxf(sdb[(j + 1) * 128 + lane + 64], c);
+    const float part = fmaxf(0.0f, a1 - a0) + fmaxf(0.0f, b1 - b0);
+    val = wave_sum(part) * (1.0f / 128.0f);
+  }
+  if (lane == 0) onset[g] = val;
+}
+
 // ------------------------------------------------------------------------------ host
 static inline size_t a256(size_t n) { return (n + 255) & ~(size_t)255; }
+
+size_t ibi_range_ws_bytes(int n_files, int64_t total_rows) {
+  return 4 * a256(sizeof(int64_t) * (n_files + 1)) + a256(sizeof(float) * (size_t)total_rows) +
+         a256(sizeof(float) * (size_t)total_rows * 128) + 4096;
+}
+
+struct IbiRangeWs {
+  int64_t *row0, *row_base, *obase;
+  float *fmax_, *sdb;
+};
+static IbiRangeWs ibi_range_ws(void* ws, int n_files, int64_t total_rows) {
+  char* p = static_cast<char*>(ws);
+  IbiRangeWs w;
+  w.row0 = reinterpret_cast<int64_t*>(p);
+  p += a256(sizeof(int64_t) * (n_files + 1));
+  w.row_base = reinterpret_cast<int64_t*>(p);
+  p += a256(sizeof(int64_t) * (n_files + 1));
+  w.obase = reinterpret_cast<int64_t*>(p);
+  p += 2 * a256(sizeof(int64_t) * (n_files + 1));
+  w.fmax_ = reinterpret_cast<float*>(p);
+  p += a256(sizeof(float) * (size_t)total_rows);
+  w.sdb = reinterpret_cast<float*>(p);
+  return w;
+}
+
+int launch_ibi_mel_range(Context& ctx, const float* sig, const int64_t* file_off, const int64_t* file_len,
+                         int n_files, const int64_t* t0, const int64_t* t1, int hop, int64_t total_rows,
+                         float* max_out, void* ws, size_t ws_bytes, hipStream_t st) {
+  if (n_files <= 0) return 0;
+  if (ws_bytes < ibi_range_ws_bytes(n_files, total_rows)) {
+    set_error("ibi_mel_range: workspace too small");
+    return -3;
+  }
+  IbiRangeWs w = ibi_range_ws(ws, n_files, total_rows);
+  const int pad = 1 + kNFFT / (2 * hop);
+  hipLaunchKernelGGL(ibi_range_plan_kernel, dim3(1), dim3(256), 0, st, file_len, t0, t1, n_files, hop, pad, w.row0,
+                     w.row_base, w.obase);
+  if (total_rows > 0) {
+    StftMelArgs s{};
+    s.sig = sig;
+    s.seq_off = file_off;
+    s.seq_len = file_len;
+    s.frame_base = w.row_base;
+    s.seq_t0 = w.row0;
+    s.n_seq = n_files;
+    s.total_frames = total_rows;
+    s.hop = hop;
+    s.sdb = w.sdb;
+    s.frame_max = w.fmax_;
+    s.frame_energy = nullptr;
+    const int rc = launch_stft_mel(ctx, s, st);
+    if (rc) return rc;
+  }
+  hipLaunchKernelGGL(seq_max_kernel, dim3(n_files), dim3(256), 0, st, w.fmax_, w.row_base, max_out);
+  NC_HIP(hipGetLastError());
+  return 0;
+}
+
+int launch_ibi_onset_range(int n_files, const int64_t* t0, int hop, int64_t total_out, const float* gmax,
+                           float* onset_out, void* ws, int64_t total_rows, hipStream_t st) {
+  if (n_files <= 0 || total_out <= 0) return 0;
+  IbiRangeWs w = ibi_range_ws(ws, n_files, total_rows);
+  hipLaunchKernelGGL(ibi_onset_range_kernel, dim3((unsigned)((total_out + 3) / 4)), dim3(256), 0, st, w.sdb,
+                     w.row_base, w.row0, t0, w.obase, gmax, n_files, total_out, 1 + kNFFT / (2 * hop), onset_out);
+  NC_HIP(hipGetLastError());
+  return 0;
+}
 
 size_t ibi_onset_ws_bytes(int n_files, int64_t total_frames) {
   return a256(sizeof(int64_t) * (n_files + 1)) + a256(sizeof(float) * n_files) +
@@ -219,9 +335,36 @@ size_t ibi_tg_ws_bytes(const Context& ctx, int n_files, int64_t total_frames, in
          a256(sizeof(double) * (size_t)total_frames) + a256(sizeof(double) * (size_t)n_files * n_tblk * N) + 256;
 }
 
+int launch_ibi_tempogram_tiles(Context& ctx, const float* onset, const int64_t* frame_base, int n_files,
+                               int64_t total_frames, int max_frames, int hop, const int64_t* b0, const int64_t* b1,
+                               double* slab_out, double* tg_out, void* ws, size_t ws_bytes, hipStream_t st);
+
 int launch_ibi_tempogram(Context& ctx, const float* onset, const int64_t* frame_base, int n_files,
                          int64_t total_frames, int max_frames, int hop, double* tg_out, void* ws, size_t ws_bytes,
                          hipStream_t st) {
+  return launch_ibi_tempogram_tiles(ctx, onset, frame_base, n_files, total_frames, max_frames, hop, nullptr, nullptr,
+                                    nullptr, tg_out, ws, ws_bytes, st);
+}
+
+int launch_ibi_tempogram_reduce(Context& ctx, const double* slab, const int64_t* frame_base, int n_files,
+                                int max_frames, int hop, double* tg_out, hipStream_t st) {
+  const int N = tg_acw(ctx, hop);
+  if (N <= 0 || n_files <= 0 || max_frames <= 0) {
+    set_error("ibi_tempogram_reduce: bad shape");
+    return -2;
+  }
+  const int n_tblk = (max_frames + TG_TB - 1) / TG_TB;
+  hipLaunchKernelGGL(tg_reduce_kernel, dim3((N + 255) / 256, n_files), dim3(256), 0, st, slab, frame_base, n_tblk,
+                     N, tg_out);
+  NC_HIP(hipGetLastError());
+  return 0;
+}
+
+// slab_out (nullable): the caller's [n_files][n_tblk][N] rows instead of the workspace's;
+// tg_out (nullable): the reduce (every tile must then be in the slab)
+int launch_ibi_tempogram_tiles(Context& ctx, const float* onset, const int64_t* frame_base, int n_files,
+                               int64_t total_frames, int max_frames, int hop, const int64_t* b0, const int64_t* b1,
+                               double* slab_out, double* tg_out, void* ws, size_t ws_bytes, hipStream_t st) {
   if (n_files <= 0 || total_frames <= 0) return 0;
   const int N = tg_acw(ctx, hop);
   if (N <= 0 || (N & 1)) {
@@ -243,17 +386,19 @@ int launch_ibi_tempogram(Context& ctx, const float* onset, const int64_t* frame_
   p += a256(sizeof(float) * (size_t)total_padded);
   double* rinv = reinterpret_cast<double*>(p);
   p += a256(sizeof(double) * (size_t)total_frames);
-  double* slab = reinterpret_cast<double*>(p);
+  double* slab = slab_out ? slab_out : reinterpret_cast<double*>(p);
   hipLaunchKernelGGL(tg_pad_kernel, dim3((unsigned)((total_padded + 255) / 256)), dim3(256), 0, st, onset,
                      frame_base, n_files, total_padded, N, xpad);
   hipLaunchKernelGGL(tg_rinv_kernel, dim3((unsigned)((total_frames + 255) / 256)), dim3(256), 0, st, xpad,
-                     frame_base, n_files, total_frames, N, hop == 64 ? ctx.t.wsq64 : ctx.t.wsq512, rinv);
+                     frame_base, n_files, total_frames, N, hop == 64 ? ctx.t.wsq64 : ctx.t.wsq512, b0, b1, rinv);
   TgSlideArgs a;
   a.xpad = xpad;
   a.rinv = rinv;
   a.frame_base = frame_base;
   a.N = N;
   a.n_tblk = n_tblk;
+  a.b0 = b0;
+  a.b1 = b1;
   a.slab = slab;
   const size_t lds = TG_TB * sizeof(double) + (size_t)(TG_TB + N) * sizeof(float);
   {
@@ -262,8 +407,9 @@ int launch_ibi_tempogram(Context& ctx, const float* onset, const int64_t* frame_
     hipLaunchKernelGGL(tg_slide_kernel, dim3(((N + 1) / 2 + TG_KB - 1) / TG_KB, n_tblk, n_files), dim3(TG_KB), lds, st,
                      a);
   }
-  hipLaunchKernelGGL(tg_reduce_kernel, dim3((N + 255) / 256, n_files), dim3(256), 0, st, slab, frame_base, n_tblk,
-                     N, tg_out);
+  if (tg_out)
+    hipLaunchKernelGGL(tg_reduce_kernel, dim3((N + 255) / 256, n_files), dim3(256), 0, st, slab, frame_base, n_tblk,
+                       N, tg_out);
   NC_HIP(hipGetLastError());
   return 0;
 }

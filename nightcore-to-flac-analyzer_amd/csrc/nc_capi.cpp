@@ -57,6 +57,18 @@ int launch_ibi_tempogram(Context& ctx, const float* onset, const int64_t* frame_
                          int64_t total_frames, int max_frames, int hop,
                          double* tg_out, void* ws, size_t ws_bytes, hipStream_t st);
 
+size_t ibi_range_ws_bytes(int n_files, int64_t total_rows);
+int launch_ibi_mel_range(Context& ctx, const float* sig, const int64_t* file_off, const int64_t* file_len,
+                         int n_files, const int64_t* t0, const int64_t* t1, int hop, int64_t total_rows,
+                         float* max_out, void* ws, size_t ws_bytes, hipStream_t st);
+int launch_ibi_onset_range(int n_files, const int64_t* t0, int hop, int64_t total_out, const float* gmax,
+                           float* onset_out, void* ws, int64_t total_rows, hipStream_t st);
+int launch_ibi_tempogram_tiles(Context& ctx, const float* onset, const int64_t* frame_base, int n_files,
+                               int64_t total_frames, int max_frames, int hop, const int64_t* b0, const int64_t* b1,
+                               double* slab_out, double* tg_out, void* ws, size_t ws_bytes, hipStream_t st);
+int launch_ibi_tempogram_reduce(Context& ctx, const double* slab, const int64_t* frame_base, int n_files,
+                                int max_frames, int hop, double* tg_out, hipStream_t st);
+
 size_t align_ws_bytes(int n_pairs, int n_speeds, int64_t total_len, int64_t max_len, int max_off_frames);
 int launch_align_offsets(Context& ctx, const float* sig, const int64_t* src_off, const int64_t* src_len,
                          const int64_t* nc_off, const int64_t* nc_len, int n_pairs, const double* speeds,
@@ -395,6 +407,49 @@ int nc_ibi_tempogram(nc_ctx* ctx, const float* onset, const int64_t* frame_base,
   SET_DEVICE(ctx);
   return nc::launch_ibi_tempogram(ctx->c, onset, frame_base, n_files, total_frames, max_frames, hop, tg_out, ws,
                                   ws_bytes, (hipStream_t)stream);
+}
+
+size_t nc_ibi_range_workspace_bytes(const nc_ctx* ctx, int n_files, int64_t total_rows) {
+  (void)ctx;
+  return nc::ibi_range_ws_bytes(n_files, total_rows);
+}
+
+int nc_ibi_mel_range(nc_ctx* ctx, const float* sig, const int64_t* file_off, const int64_t* file_len, int n_files,
+                     const int64_t* t0, const int64_t* t1, int hop, int64_t total_rows, float* max_out, void* ws,
+                     size_t ws_bytes, void* stream) {
+  CHECK_CTX(ctx);
+  SET_DEVICE(ctx);
+  return nc::launch_ibi_mel_range(ctx->c, sig, file_off, file_len, n_files, t0, t1, hop, total_rows, max_out, ws,
+                                  ws_bytes, (hipStream_t)stream);
+}
+
+int nc_ibi_onset_range(nc_ctx* ctx, int n_files, const int64_t* t0, int hop, int64_t total_out, const float* gmax,
+                       float* onset_out, void* ws, int64_t total_rows, void* stream) {
+  CHECK_CTX(ctx);
+  SET_DEVICE(ctx);
+  return nc::launch_ibi_onset_range(n_files, t0, hop, total_out, gmax, onset_out, ws, total_rows,
+                                    (hipStream_t)stream);
+}
+
+int nc_ibi_tempogram_tiles(nc_ctx* ctx, const float* onset, const int64_t* frame_base, int n_files,
+                           int64_t total_frames, int max_frames, int hop, const int64_t* b0, const int64_t* b1,
+                           double* slab, void* ws, size_t ws_bytes, void* stream) {
+  CHECK_CTX(ctx);
+  SET_DEVICE(ctx);
+  if (!b0 || !b1 || !slab) {
+    nc::set_error("ibi_tempogram_tiles: b0, b1 and slab are required");
+    return -2;
+  }
+  return nc::launch_ibi_tempogram_tiles(ctx->c, onset, frame_base, n_files, total_frames, max_frames, hop, b0, b1,
+                                        slab, nullptr, ws, ws_bytes, (hipStream_t)stream);
+}
+
+int nc_ibi_tempogram_reduce(nc_ctx* ctx, const double* slab, const int64_t* frame_base, int n_files, int max_frames,
+                            int hop, double* tg_out, void* stream) {
+  CHECK_CTX(ctx);
+  SET_DEVICE(ctx);
+  return nc::launch_ibi_tempogram_reduce(ctx->c, slab, frame_base, n_files, max_frames, hop, tg_out,
+                                         (hipStream_t)stream);
 }
 
 int nc_xcorr_search(nc_ctx* ctx, const float* sig, const int64_t* item_a, const int64_t* item_b, int n_items,

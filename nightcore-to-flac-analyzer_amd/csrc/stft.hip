@@ -98,7 +98,7 @@ __global__ __launch_bounds__(SM_THREADS) void stft_mel_kernel(StftMelArgs a) {
     int64_t t, L;
     if (a.frame_base) {
       s = seq_of_frame(a.frame_base, a.n_seq, g);
-      t = g - a.frame_base[s];
+      t = g - a.frame_base[s] + (a.seq_t0 ? a.seq_t0[s] : 0);
     } else {
       s = (int)(g / a.uniform_T);
       t = g - (int64_t)s * a.uniform_T;

@@ -12,6 +12,8 @@ struct StftMelArgs {
   const int64_t* seq_off;     // [n_seq] sample offsets into sig
   const int64_t* seq_len;     // [n_seq] or nullptr: every sequence is uniform_len long
   const int64_t* frame_base;  // [n_seq + 1] or nullptr: every sequence has uniform_T frames
+  const int64_t* seq_t0 = nullptr;  // nullable [n_seq]: frame g of sequence s is its STFT frame
+                                    // seq_t0[s] + (g - frame_base[s]) (a frame range of a file)
   int64_t uniform_len;
   int uniform_T;
   int n_seq;

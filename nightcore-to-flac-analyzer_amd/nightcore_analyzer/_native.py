@@ -61,6 +61,11 @@ SIGNATURES = {
     "nc_ibi_onset": (I32, [P, P, P, P, I32, I64, I32, P, P, P, SZ, P]),
     "nc_ibi_tempogram_workspace_bytes": (SZ, [P, I32, I64, I32, I32]),
     "nc_ibi_tempogram": (I32, [P, P, P, I32, I64, I32, I32, P, P, SZ, P]),
+    "nc_ibi_range_workspace_bytes": (SZ, [P, I32, I64]),
+    "nc_ibi_mel_range": (I32, [P, P, P, P, I32, P, P, I32, I64, P, P, SZ, P]),
+    "nc_ibi_onset_range": (I32, [P, I32, P, I32, I64, P, P, P, I64, P]),
+    "nc_ibi_tempogram_tiles": (I32, [P, P, P, I32, I64, I32, I32, P, P, P, P, SZ, P]),
+    "nc_ibi_tempogram_reduce": (I32, [P, P, P, I32, I32, I32, P, P]),
     "nc_xcorr_search": (I32, [P, P, P, P, I32, I32, P, P, P, P, P, P, P, P, P, P, I32, P, P, P]),
     "nc_align_workspace_bytes": (SZ, [P, I32, I32, I64, I64, I32]),
     "nc_align_offsets": (I32, [P, P, P, P, P, P, I32, P, I32, I32, I64, I64, P, P, P, P, SZ, P]),

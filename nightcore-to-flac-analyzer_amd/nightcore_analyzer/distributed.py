@@ -89,7 +89,7 @@ def _run_windows(pairs, group, world, rank, split_offset, log=None, **kw) -> lis
     outs, err = None, None
     try:
         lengths = [decoded_length(x) for nc, src in pairs for x in (nc, src)]
-        touched = shard_plan(lengths, p, world, split_offset).touched(rank)
+        touched = shard_plan(lengths, p, world, split_offset).needed(rank, p.compute_ibi and world > 1)
         arrays = [a for b in touched for a in (_load(pairs[b][0], quiet, "nightcore"),
                                                 _load(pairs[b][1], quiet, "source"))]
         eng = get_engine()

@@ -60,8 +60,9 @@ import torch
 import torch.distributed as dist
 
 from . import consensus as C
-from .engine import (CHUNK_SEC, HOP_LENGTH, MIN_BEATS, MIN_CHUNKS, REF_HZ, SR, DeviceSignals, Engine, PairOutcome,
-                     Params, _Upload, assemble_pair, plan_batch)
+from .distributed import shard_range
+from .engine import (CHUNK_SEC, HOP_LENGTH, IBI_HOP, MIN_BEATS, MIN_CHUNKS, REF_HZ, SR, DeviceSignals, Engine,
+                     PairOutcome, Params, _Upload, assemble_pair, plan_batch)
 
 # exchanged window record: exists, energy_db, bpm, nbeats, tempo lag, decision margin
 R_EXISTS, R_ENERGY, R_BPM, R_NBEATS, R_LAG, R_MARGIN = range(6)
@@ -70,6 +71,8 @@ W_FIELDS = 6
 # tuning decision margins (src, nc)
 CP_FIELDS = 1 + 3 + 24 + 1 + 2
 CP_COST = 8          # a chunk pair's weight in the item line, in windows
+IBI_TILE = 2048      # frames per tempogram tile (csrc/ibi.hip TG_TB): the IBI frame split's unit
+IBI_PAD = 1 + 1024 // IBI_HOP   # onset_strength's lag + n_fft // (2 hop) left pad at hop 64
 
 
 class ShardError(RuntimeError):
@@ -103,6 +106,11 @@ class ShardPlan:
 
     def touched(self, r: int) -> List[int]:
         return [b for b in range(self.B) if self.owner[b] == r or self.on_rank(b, r)]
+
+    def needed(self, r: int, ibi: bool) -> List[int]:
+        """Pairs rank r must hold: the ones it touches, and with the hop-64 IBI pass every
+        split pair (the pass of a split pair's files is split over all ranks, C2-C4)."""
+        return [b for b in range(self.B) if self.owner[b] == r or self.on_rank(b, r) or (ibi and self.split[b])]
 
     def owned(self, r: int) -> List[int]:
         return [b for b in range(self.B) if self.owner[b] == r]
@@ -224,6 +232,28 @@ class Exchange:
         if bad:
             raise ShardError(f"window-sharded analysis failed on rank(s) {bad}")
         return np.concatenate([allr[r, :counts[r]] for r in range(self.world)], axis=0) if S else np.zeros((0, k))
+
+    def allreduce_max(self, vals: np.ndarray, failed: Optional[BaseException]) -> np.ndarray:
+        """Element-wise maximum over the ranks (C2: power_to_db's top_db reference of a file
+        whose frames are split); the error flag rides along as one more element."""
+        if not self.on or self.world == 1:
+            if failed is not None:
+                raise failed
+            return np.asarray(vals, np.float64)
+        buf = np.concatenate([np.asarray(vals, np.float64), [1.0 if failed is not None else 0.0]])
+        t = torch.from_numpy(buf).to(self.dev)
+        if self.dev.type == "cuda" and self.stream is not None:
+            with torch.cuda.stream(self.stream):
+                dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group)
+                out = t.cpu().numpy()
+        else:
+            dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group)
+            out = t.cpu().numpy()
+        if failed is not None:
+            raise failed
+        if out[-1] != 0.0:
+            raise ShardError("window-sharded analysis failed on another rank")
+        return out[:-1]
 
     def check(self, failed: Optional[BaseException]) -> None:
         """Fail together: one flag gather."""
@@ -406,6 +436,120 @@ class DeviceStages:
             return ibis, nibi, core["nbeats"].cpu().numpy(), core["lag"].cpu().numpy()
 
 
+    # ---- the hop-64 IBI pass of split pairs, split over the ranks (C2-C4; csrc/ibi.hip part D)
+    def ibi_mel(self, f_off, f_len, t0, t1) -> np.ndarray:
+        """Mel dB rows for this rank's onset frames [t0, t1) of each file -> per-file max."""
+        eng, n = self.eng, len(f_off)
+        T = 1 + np.asarray(f_len, np.int64) // IBI_HOP
+        t0, t1 = np.asarray(t0, np.int64), np.asarray(t1, np.int64)
+        rows = int(np.maximum(0, np.minimum(T, t1 - IBI_PAD + 1) - np.maximum(0, t0 - IBI_PAD)).sum())
+        with torch.cuda.stream(self.stream):
+            up = _Upload()
+            up.add("off", f_off, np.int64)
+            up.add("len", f_len, np.int64)
+            up.add("t0", t0, np.int64)
+            up.add("t1", t1, np.int64)
+            d = up.commit(eng.dev)
+            ws = eng.workspace("sp_ibi_rng", eng.ctx.lib.nc_ibi_range_workspace_bytes(eng.ctx.h, n, rows))
+            mx = torch.empty(n, dtype=torch.float32, device=eng.dev)
+            eng.call("nc_ibi_mel_range", self.sig.buf.data_ptr(), d["off"].data_ptr(), d["len"].data_ptr(), n,
+                     d["t0"].data_ptr(), d["t1"].data_ptr(), IBI_HOP, rows, mx.data_ptr(), ws.data_ptr(), ws.numel(),
+                     eng.stream())
+            self._ibi = dict(d=d, ws=ws, rows=rows, n=n, total=int(np.maximum(0, t1 - t0).sum()))
+            return mx.cpu().numpy()
+
+    def ibi_onset(self, gmax: np.ndarray) -> np.ndarray:
+        """This rank's onset frames [t0, t1) of every file (concatenated) against the global maxima."""
+        eng, st = self.eng, self._ibi
+        if st["total"] == 0:
+            return np.zeros(0, np.float32)
+        with torch.cuda.stream(self.stream):
+            g = torch.from_numpy(np.asarray(gmax, np.float32)).to(eng.dev)
+            out = torch.empty(st["total"], dtype=torch.float32, device=eng.dev)
+            eng.call("nc_ibi_onset_range", st["n"], st["d"]["t0"].data_ptr(), IBI_HOP, st["total"], g.data_ptr(),
+                     out.data_ptr(), st["ws"].data_ptr(), st["rows"], eng.stream())
+            return out.cpu().numpy()
+
+    def ibi_tiles(self, onsets: List[np.ndarray], b0, b1) -> np.ndarray:
+        """Tempogram partial rows of this rank's 2048-frame tiles [b0, b1) of each file, from the
+        full onsets -> [tiles, N] in (file, tile) order."""
+        eng = self.eng
+        T = np.array([len(o) for o in onsets], np.int64)
+        n, total, mxf = len(T), int(T.sum()), int(T.max())
+        N = int(int(8.0 * SR) // IBI_HOP)
+        ntb = -(-mxf // IBI_TILE)
+        sel = [f * ntb + b for f in range(n) for b in range(int(b0[f]), int(b1[f]))]
+        if not sel:
+            return np.zeros((0, N))
+        with torch.cuda.stream(self.stream):
+            up = _Upload()
+            up.add("onset", np.concatenate(onsets), np.float32)
+            up.add("fb", np.concatenate([[0], np.cumsum(T)]), np.int64)
+            up.add("b0", b0, np.int64)
+            up.add("b1", b1, np.int64)
+            up.add("sel", sel, np.int64)
+            d = up.commit(eng.dev)
+            slab = torch.zeros(n * ntb * N, dtype=torch.float64, device=eng.dev)
+            ws = eng.workspace("sp_ibi_tg", eng.ctx.lib.nc_ibi_tempogram_workspace_bytes(eng.ctx.h, n, total, mxf,
+                                                                                        IBI_HOP))
+            eng.call("nc_ibi_tempogram_tiles", d["onset"].data_ptr(), d["fb"].data_ptr(), n, total, mxf, IBI_HOP,
+                     d["b0"].data_ptr(), d["b1"].data_ptr(), slab.data_ptr(), ws.data_ptr(), ws.numel(), eng.stream())
+            return slab.view(n * ntb, N)[d["sel"]].cpu().numpy()
+
+    def ibi_reduce(self, tiles: List[List[np.ndarray]], T: np.ndarray) -> np.ndarray:
+        """Fixed-order sum of every tile's row / T_f (nc_ibi_tempogram_reduce) -> [files, N]."""
+        eng = self.eng
+        n, N = len(tiles), len(tiles[0][0])
+        ntb = max(len(t) for t in tiles)
+        full = np.zeros((n, ntb, N), np.float64)
+        for f, rows in enumerate(tiles):
+            full[f, :len(rows)] = np.stack(rows)
+        with torch.cuda.stream(self.stream):
+            up = _Upload()
+            up.add("slab", full, np.float64)
+            up.add("fb", np.concatenate([[0], np.cumsum(T)]), np.int64)
+            d = up.commit(eng.dev)
+            tg = torch.empty(n * N, dtype=torch.float64, device=eng.dev)
+            eng.call("nc_ibi_tempogram_reduce", d["slab"].data_ptr(), d["fb"].data_ptr(), n, int(np.max(T)), IBI_HOP,
+                     tg.data_ptr(), eng.stream())
+            return tg.cpu().numpy().reshape(n, N)
+
+    def ibi_beats(self, onsets: List[np.ndarray], tgs: np.ndarray, start_bpm) -> tuple:
+        """beat_track on the full onsets with their tempogram means, then the IBIs
+        (tempo.py:158-172) -> (ibis (array, or None under 4), IBI counts, beat counts, tempo lags)."""
+        eng = self.eng
+        T = np.array([len(o) for o in onsets], np.int64)
+        n, total = len(T), int(T.sum())
+        N = tgs.shape[1]
+        with torch.cuda.stream(self.stream):
+            up = _Upload()
+            up.add("onset", np.concatenate(onsets), np.float32)
+            up.add("fb", np.concatenate([[0], np.cumsum(T)]), np.int64)
+            up.add("len", T, np.int32)
+            up.add("tg", tgs, np.float64)
+            up.add("start", start_bpm, np.float64)
+            up.add("pidx", np.arange(n), np.int32)
+            d = up.commit(eng.dev)
+            bpm = torch.zeros(n, dtype=torch.float64, device=eng.dev)
+            lag = torch.zeros(n, dtype=torch.int32, device=eng.dev)
+            nb = torch.zeros(n, dtype=torch.int32, device=eng.dev)
+            mg = torch.zeros(n, dtype=torch.float64, device=eng.dev)
+            beats = torch.empty(max(1, total), dtype=torch.int32, device=eng.dev)
+            ws = eng.workspace("sp_ibi_beats", eng.ctx.lib.nc_tempo_beats_workspace_bytes(total))
+            eng.call("nc_tempo_beats", d["onset"].data_ptr(), d["fb"].data_ptr(), d["len"].data_ptr(), n, int(T.max()),
+                     d["tg"].data_ptr(), N, d["start"].data_ptr(), d["pidx"].data_ptr(), None, IBI_HOP, 1,
+                     bpm.data_ptr(), lag.data_ptr(), nb.data_ptr(), mg.data_ptr(), beats.data_ptr(), total,
+                     ws.data_ptr(), ws.numel(), eng.stream())
+            ibis = torch.empty(max(1, total), dtype=torch.float64, device=eng.dev)
+            nibi = torch.zeros(n, dtype=torch.int32, device=eng.dev)
+            eng.call("nc_ibi_from_beats", beats.data_ptr(), d["fb"].data_ptr(), nb.data_ptr(), n, IBI_HOP, 4,
+                     ibis.data_ptr(), nibi.data_ptr(), eng.stream())
+            vals, ni = ibis.cpu().numpy(), nibi.cpu().numpy()
+            fb = np.concatenate([[0], np.cumsum(T)])
+            out = [vals[fb[i]:fb[i] + ni[i]].copy() if ni[i] >= 4 else None for i in range(n)]
+            return out, ni, nb.cpu().numpy(), lag.cpu().numpy()
+
+
 # ------------------------------------------------------------------------------ orchestration
 def _gate(energy: np.ndarray, w0, w1, threshold_db: float) -> np.ndarray:
     """io.energy_gate (io.py:115-126) for every file: keep energy >= file max + threshold."""
@@ -462,14 +606,16 @@ def analyze_sharded(stages, p: Optional[Params] = None, group=None, *, lengths: 
     sp = shard_plan(L, p, world, split_offset)
     local_pairs = list(range(sp.B)) if local_pairs is None else list(local_pairs)
     pos = {b: j for j, b in enumerate(local_pairs)}
+    ibi_split = p.compute_ibi and world > 1 and bool(sp.split.any())   # C2-C4 for the split pairs
     touched = sp.touched(r)
-    missing = [b for b in touched if b not in pos]
+    needed = sp.needed(r, ibi_split)
+    missing = [b for b in needed if b not in pos]
     if missing:
-        raise ValueError(f"rank {r} touches pairs {missing} that its stages do not hold")
+        raise ValueError(f"rank {r} needs pairs {missing} that its stages do not hold")
     ex.stream = getattr(stages, "stream", None)
     interior = [b for b in touched if not sp.split[b]]
     fast = hasattr(stages, "pipeline") and bool(interior)
-    stage_pairs = [b for b in touched if sp.split[b]] if fast else touched
+    stage_pairs = [b for b in needed if sp.split[b]] if fast else needed
     pump = _Pump(stages.pipeline(_files([pos[b] for b in interior]), p, steps) if fast else None)
     pump(3)                                     # Engine.GROUPS_IN_FLIGHT groups queued before any wait
     split_st = stages.restrict(_files([pos[b] for b in stage_pairs]))
@@ -642,12 +788,78 @@ def _split_stages(stages, p: Params, ex: Exchange, sp: ShardPlan, r: int, pairs:
                         raise ShardError(f"chunk-pair record of pair {b} missing from the exchange")
                     cps[c0 + k] = row[1:]
     owned = [j for j, b in enumerate(pairs) if sp.owner[b] == r]
-    res = _consensus(stages, p, pl, st["align"], st["active"], st["energy"], full, st["prior"], cps, owned)
+    ibi_pre = None
+    if p.compute_ibi and exchange:
+        # the hop-64 pass of every split pair, its frames split over all ranks (C2-C4); every
+        # rank holds every split pair (ShardPlan.needed); the owners get the results
+        ibi_pre = _sharded_ibi(stages, ex, sp, pl, pairs, st["prior"], r, pump)
+    res = _consensus(stages, p, pl, st["align"], st["active"], st["energy"], full, st["prior"], cps, owned, ibi_pre)
     return [(pairs[j], o) for j, o in zip(owned, res)]
 
 
-def _consensus(stages, p: Params, pl, align, active, energy, full, prior, cps, owned: List[int]) -> list:
-    """Bootstraps, IBI pass and host assembly of the held pairs ``owned`` (plan indices)."""
+def _ibi_share(T: int, world: int, r: int) -> Tuple[int, int, int, int]:
+    """Rank r's share of a T-frame file in the split hop-64 pass: tempogram tiles [b0, b1)
+    (contiguous blocks of 2048-frame tiles) and the onset frames [t0, t1) those tiles cover."""
+    b0, b1 = shard_range(-(-T // IBI_TILE), world, r)
+    return b0, b1, min(T, b0 * IBI_TILE), min(T, b1 * IBI_TILE)
+
+
+def _sharded_ibi(stages, ex: Exchange, sp: ShardPlan, pl, pairs: List[int], prior: np.ndarray, r: int, pump) -> dict:
+    """estimate_ibis_global (tempo.py:120-173) of every split pair's two files with the frames
+    split over the ranks:
+      rank r: mel dB of its frames' rows -> C2 all-reduce MAX of each file's dB maximum (the
+      power_to_db top_db reference) -> onsets of its frames -> C4 all-gather of the onset
+      segments (every rank: the full onsets) -> tempogram partial rows of its tiles -> C3
+      all-gather of the tile rows, summed in tile order (the one-GPU bits) -> the owner runs
+      the beat tracker on the full onset and the IBI extraction.
+    Returns {plan pair index: (ibis (nc, src), IBI counts, beat counts, tempo lags)} for the
+    split pairs this rank owns."""
+    W = ex.world
+    js = [j for j, b in enumerate(pairs) if sp.split[b]]
+    files = [f for j in js for f in (2 * j, 2 * j + 1)]
+    f_off, f_len = pl.f_off[files], pl.f_len[files]
+    T = 1 + np.asarray(f_len, np.int64) // IBI_HOP
+    share = [[_ibi_share(int(t), W, q) for t in T] for q in range(W)]
+    b0, b1, t0, t1 = (np.array([m[i] for m in share[r]], np.int64) for i in range(4))
+    mx, err = _try(stages.ibi_mel, f_off, f_len, t0, t1)
+    gmax = ex.allreduce_max(mx if err is None else np.full(len(files), -np.inf), err)             # C2
+    pump()
+    seg, err = _try(stages.ibi_onset, gmax)
+    cnt = [sum(m[3] - m[2] for m in share[q]) for q in range(W)]
+    rows = ex.gather_blocks(np.asarray(seg if err is None else np.zeros(0), np.float64)[:, None], cnt, err)  # C4
+    onsets = [np.zeros(int(t), np.float32) for t in T]
+    pos = 0
+    for q in range(W):
+        for f, m in enumerate(share[q]):
+            onsets[f][m[2]:m[3]] = rows[pos:pos + m[3] - m[2], 0]
+            pos += m[3] - m[2]
+    pump()
+    slab, err = _try(stages.ibi_tiles, onsets, b0, b1)
+    N = int(int(8.0 * SR) // IBI_HOP)
+    cnt = [sum(m[1] - m[0] for m in share[q]) for q in range(W)]
+    rows = ex.gather_blocks(slab if err is None else np.zeros((0, N)), cnt, err)                    # C3
+    tiles = [[None] * int(-(-t // IBI_TILE)) for t in T]
+    pos = 0
+    for q in range(W):
+        for f, m in enumerate(share[q]):
+            for b in range(m[0], m[1]):
+                tiles[f][b] = rows[pos]
+                pos += 1
+    tg = stages.ibi_reduce(tiles, T)
+    pump()
+    out = {}
+    for i, j in enumerate(js):
+        if sp.owner[pairs[j]] == r:
+            ibis, nibi, nb, lg = stages.ibi_beats([onsets[2 * i], onsets[2 * i + 1]], tg[2 * i:2 * i + 2],
+                                                  [prior[j], 120.0])
+            out[j] = (ibis, nibi, nb, lg)
+    return out
+
+
+def _consensus(stages, p: Params, pl, align, active, energy, full, prior, cps, owned: List[int],
+               ibi_pre: Optional[dict] = None) -> list:
+    """Bootstraps, IBI pass and host assembly of the held pairs ``owned`` (plan indices);
+    ``ibi_pre`` holds the split pairs' IBI results of the sharded pass."""
     B, n_cp = pl.B, pl.n_cp
     w0, w1 = pl.w0, pl.w1
     lags = [int(v) for v in cps[:, 0]] if n_cp else []
@@ -683,9 +895,27 @@ def _consensus(stages, p: Params, pl, align, active, energy, full, prior, cps, o
     ibi = None
     if p.compute_ibi:
         # hop-64 pass of the owned pairs' files (nc with the pair prior, src with 120)
-        files = [f for b in owned for f in (2 * b, 2 * b + 1)]
+        ibi_pre = ibi_pre or {}
+        rest = [b for b in owned if b not in ibi_pre]
+        files = [f for b in rest for f in (2 * b, 2 * b + 1)]
         sb = np.array([prior[f // 2] if f % 2 == 0 else 120.0 for f in files])
-        ibis, nibi, nb, lg = stages.ibi(pl.f_off[files], pl.f_len[files], sb)
+        r_ibis, r_nibi, r_nb, r_lg = stages.ibi(pl.f_off[files], pl.f_len[files], sb)
+        ibis, nibi, nb, lg = [], [], [], []
+        k = 0
+        for b in owned:                 # the owned pairs' (nc, src) results, in owned order
+            if b in ibi_pre:
+                pi, pn, pb, pg = ibi_pre[b]
+                ibis += list(pi)
+                nibi += list(pn)
+                nb += list(pb)
+                lg += list(pg)
+            else:
+                ibis += list(r_ibis[2 * k:2 * k + 2])
+                nibi += list(r_nibi[2 * k:2 * k + 2])
+                nb += list(r_nb[2 * k:2 * k + 2])
+                lg += list(r_lg[2 * k:2 * k + 2])
+                k += 1
+        files = [f for b in owned for f in (2 * b, 2 * b + 1)]
         nF = 2 * B
         ibi = dict(nibi=np.zeros(nF, np.int64), nbeats=np.zeros(nF, np.int64), lag=np.zeros(nF, np.int64),
                    out=np.full(3 * B, np.nan))
@@ -724,7 +954,7 @@ def run_window_sharded(pairs: Sequence[Tuple[np.ndarray, np.ndarray]], p: Option
     world = dist.get_world_size(group) if dist.is_available() and dist.is_initialized() else 1
     rank = dist.get_rank(group) if dist.is_available() and dist.is_initialized() else 0
     lengths = [len(a) for nc, src in pairs for a in (nc, src)]
-    touched = shard_plan(lengths, p, world, split_offset).touched(rank)
+    touched = shard_plan(lengths, p, world, split_offset).needed(rank, p.compute_ibi and world > 1)
     flat = [np.asarray(a, np.float32) for b in touched for a in pairs[b]]
     sig = eng.upload_signals(flat) if flat else DeviceSignals(torch.zeros(64, device=eng.dev),
                                                              np.zeros(0, np.int64), np.zeros(0, np.int64))

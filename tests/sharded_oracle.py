@@ -95,6 +95,60 @@ class OracleStages:
             res.append((point, (float(np.percentile(boot, 2.5)), float(np.percentile(boot, 97.5)))))
         return res
 
+    # ---- the split hop-64 pass (sharded._sharded_ibi): the same onset and tempogram sums
+    def ibi_mel(self, f_off, f_len, t0, t1):
+        self._check("ibi")
+        self._ibi_S, self._ibi_r = [], []
+        mx = []
+        for o, n, a, b in zip(f_off, f_len, t0, t1):
+            S = ncref.mel_db(self.buf[o:o + n], 22050, 2048, 64)
+            T = S.shape[1]
+            r0, r1 = max(0, a - 17), min(T, b - 17 + 1)
+            self._ibi_S.append(S)
+            self._ibi_r.append((a, b))
+            mx.append(float(S[:, r0:r1].max()) if r1 > r0 else -np.inf)
+        return np.array(mx)
+
+    def ibi_onset(self, gmax):
+        out = []
+        for S, (a, b), g in zip(self._ibi_S, self._ibi_r, gmax):
+            Sc = np.maximum(S, np.float32(g) - np.float32(80.0))
+            d = np.maximum(np.float32(0.0), Sc[:, 1:] - Sc[:, :-1])
+            od = np.concatenate([np.zeros(17, np.float32), np.mean(d, axis=0, dtype=np.float32)])[:S.shape[1]]
+            out.append(od[a:b])
+        return np.concatenate(out) if out else np.zeros(0, np.float32)
+
+    def ibi_tiles(self, onsets, b0, b1):
+        rows = []
+        for on, a, b in zip(onsets, b0, b1):
+            for k in range(a, b):
+                rows.append(ncref.tempogram_sum(on, 2756, k * 2048, min(len(on), (k + 1) * 2048)))
+        return np.array(rows).reshape(-1, 2756)
+
+    def ibi_reduce(self, tiles, T):
+        out = []
+        for rows, t in zip(tiles, T):
+            acc = np.zeros(2756)
+            for row in rows:
+                acc = acc + row
+            out.append(acc / t)
+        return np.array(out)
+
+    def ibi_beats(self, onsets, tgs, start_bpm):
+        ibis, nibi = [], []
+        for on, tg, sb in zip(onsets, tgs, start_bpm):
+            _, beats = ncref.beat_track(on, 22050, 64, float(sb), tg_mean=tg)
+            v = None
+            if len(beats) >= 5:
+                t = ncref.frames_to_time(beats, 22050, 64)
+                d = np.diff(t)
+                d = d[d > 0.05]
+                v = d if len(d) >= 4 else None
+            ibis.append(v)
+            nibi.append(0 if v is None else len(v))
+        z = np.zeros(len(onsets), np.int64)
+        return ibis, np.array(nibi, np.int64), z, z
+
     def ibi(self, f_off, f_len, start_bpm):
         ibis, nibi = [], []
         for o, n, sb in zip(f_off, f_len, start_bpm):

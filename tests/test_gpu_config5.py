@@ -77,3 +77,62 @@ def test_config5_waveform_xcorr(case):
     ratio, quality = xcorr.estimate_speed_xcorr_arrays(src_t, nc_t)
     assert abs(ratio - g["xcorr"]["ratio"]) < 1e-9
     assert abs(quality - g["xcorr"]["quality"]) < 1e-5
+
+
+def _shard_worker(rank, world, port, path, q):
+    import os
+    import torch.distributed as dist
+    from nightcore_analyzer.sharded import run_window_sharded, shard_plan
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        d = np.load(path)
+        nc, src = d["nc"], d["src"]
+        sp = shard_plan([len(nc), len(src)], E.Params(), world)
+        outs = run_window_sharded([(nc, src)], E.Params(), device=0)
+        o = outs[0]
+        q.put((rank, bool(sp.split[0]), None if o.error is None else repr(o.error),
+               None if o.result is None else (o.result.src_tempos_raw, o.result.nc_tempos_raw, o.result.tempo_ratio,
+                                              list(o.result.tempo_ci), o.result.pitch_ratio, o.result.ibi_ratio,
+                                              list(o.result.ibi_ci)),
+               {k: o.detail.get(k) for k in ("chunk_lags", "ibi_lag", "ibi_n", "nc_start_bpm")}))
+    except Exception as exc:          # noqa: BLE001
+        q.put((rank, None, repr(exc), None, None))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_config5_window_sharded_two_ranks(case, tmp_path):
+    """The 60-min pair split over two ranks (gloo on the one GPU): its windows and chunk
+    pairs by the item plan, its hop-64 IBI pass by frames (C2 all-reduce MAX of the dB
+    reference, C4 gather of the onset segments, C3 gather of the tempogram tile rows, beat
+    tracking on the owner); every rank's result equals the fixtures, IBI ratio and CI exactly
+    (the same IBIs as one GPU: every tile row is the one-GPU row, summed in the same order)."""
+    import socket
+    import torch.multiprocessing as mp
+    g, nc, src = case
+    path = tmp_path / "pair.npz"
+    np.savez(path, nc=nc, src=src)
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_shard_worker, args=(r, 2, port, str(path), q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=140) for _ in range(2)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, split, err, r, d in res:
+        assert err is None, (rank, err)
+        assert split, "the single pair must be split over the ranks"
+        src_t, nc_t, tr, tci, pr, ir, ici = r
+        assert src_t == g["src_tempos"] and nc_t == g["nc_tempos"]
+        assert tr == g["tempo_ratio"] and tci == g["tempo_ci"] and pr == g["pitch_ratio"]
+        assert d["chunk_lags"] == g["chunk_lags"] and d["nc_start_bpm"] == g["nc_start_bpm"]
+        assert d["ibi_lag"] == (g["ibi"]["nc"]["lag"], g["ibi"]["src"]["lag"])
+        assert d["ibi_n"] == (g["ibi"]["nc"]["n_ibis"], g["ibi"]["src"]["n_ibis"])
+        assert ir == g["ibi"]["ratio"] and ici == g["ibi"]["ci"]
