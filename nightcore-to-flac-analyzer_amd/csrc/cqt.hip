@@ -186,16 +186,20 @@ __global__ __launch_bounds__(256) void decimate3_kernel(const float* sig, const 
   __shared__ __attribute__((aligned(16))) float e1[D3_N1 / 2], o1[D3_N1 / 2];
   __shared__ float wmax[4];
   const int c = blockIdx.y;
-  const int64_t* len = oct_len + c * 7 + base;
   const int64_t m0 = (int64_t)blockIdx.x * D3_T;
-  if (m0 >= len[3]) return;
+  // every descriptor read up front, unconditionally: one round trip of scalar loads instead of
+  // a chain (the early exit below would otherwise order the offset loads after the length's)
+  const int64_t* len = oct_len + c * 7 + base;
+  const int64_t L0 = len[0], L1 = len[1], L2 = len[2], L3 = len[3];
+  const int64_t coff = chunk_off[c], oin = oct_off[c * 7 + base];
+  const int64_t oo1 = oct_off[c * 7 + base + 1], oo2 = oct_off[c * 7 + base + 2], oo3 = oct_off[c * 7 + base + 3];
+  if (m0 >= L3) return;
   const float (&h)[2 * kHalfbandK + 1] = taps.h;
-  const float* in = base == 0 ? sig + chunk_off[c] : ws_oct + oct_off[c * 7 + base];
-  const int64_t L0 = len[0];
+  const float* in = base == 0 ? sig + coff : ws_oct + oin;
   const bool vec = ((reinterpret_cast<uintptr_t>(in) & 15) == 0);
-  float* out1 = ws_oct + oct_off[c * 7 + base + 1];
-  float* out2 = ws_oct + oct_off[c * 7 + base + 2];
-  float* out3 = ws_oct + oct_off[c * 7 + base + 3];
+  float* out1 = ws_oct + oo1;
+  float* out2 = ws_oct + oo2;
+  float* out3 = ws_oct + oo3;
   // level base of tile m0: values [8 m0 - 168, 8 m0 - 168 + 2 D3_P0), 4 values (2 pairs) per float4
   auto load_tile = [&](int64_t m0, float4 (&pf)[D3_LD]) {
     const int64_t v0 = 8 * m0 - 168;
@@ -238,15 +242,15 @@ __global__ __launch_bounds__(256) void decimate3_kernel(const float* sig, const 
     // one maximum per workgroup, no atomics: slot c + oct_off[c][3] / 256 + blockIdx.x (distinct
     // per chunk; read back by cqt_mfma_kernel)
     if (base == 0 && xmax && threadIdx.x == 0)
-      xmax[c + oct_off[c * 7 + 3] / 256 + blockIdx.x] = fmaxf(fmaxf(wmax[0], wmax[1]), fmaxf(wmax[2], wmax[3]));
+      xmax[c + (base == 0 ? oo3 : oct_off[c * 7 + 3]) / 256 + blockIdx.x] = fmaxf(fmaxf(wmax[0], wmax[1]), fmaxf(wmax[2], wmax[3]));
     // level base+1: [4 m0 - 72, +D3_N1), owned [4 m0, 4 m0 + 4 T); phases -> e1/o1
-    d3_level(e0, o0, D3_N1, 4 * m0 - 72, len[1], h, e1, o1, out1, 72, 4 * D3_T);
+    d3_level(e0, o0, D3_N1, 4 * m0 - 72, L1, h, e1, o1, out1, 72, 4 * D3_T);
     __syncthreads();
     // level base+2: [2 m0 - 24, +D3_N2), owned [2 m0, 2 m0 + 2 T); phases -> e0/o0 (reused)
-    d3_level(e1, o1, D3_N2, 2 * m0 - 24, len[2], h, e0, o0, out2, 24, 2 * D3_T);
+    d3_level(e1, o1, D3_N2, 2 * m0 - 24, L2, h, e0, o0, out2, 24, 2 * D3_T);
     __syncthreads();
     // level base+3: [m0, m0 + T), all owned
-    d3_level(e0, o0, D3_T, m0, len[3], h, nullptr, nullptr, out3, 0, D3_T);
+    d3_level(e0, o0, D3_T, m0, L3, h, nullptr, nullptr, out3, 0, D3_T);
   }
 }
 
@@ -290,39 +294,60 @@ __global__ __launch_bounds__(TP_WAVES * 64) void tuning_peaks_kernel(PeakArgs a)
   __syncthreads();
   const int64_t n_groups = (a.total_tframes + TP_WAVES - 1) / TP_WAVES;
   const int64_t gb = n_groups * blockIdx.x / gridDim.x, ge = n_groups * (blockIdx.x + 1) / gridDim.x;
+  // The wave's work-list frames gf rise by TP_WAVES: their chunk is tracked forward, its
+  // bounds and descriptors reloaded only when gf crosses into a later chunk (no binary search
+  // and dependent loads per frame)
+  int c = -1, nt = 0, skip = 0;
+  int64_t cb = 0, ce = -1, coff = 0, clen = 0, ctf = 0;
   for (int64_t grp = gb; grp < ge; ++grp) {
     const int64_t gf = grp * TP_WAVES + wave;
     if (gf >= a.total_tframes) break;
-    int lo = 0, hi = a.n_chunks - 1;
-    while (lo < hi) {
-      const int mid = (lo + hi + 1) >> 1;
-      if (a.tp_base[mid] <= gf) lo = mid;
-      else hi = mid - 1;
+    if (gf >= ce) {
+      if (c < 0) {
+        int lo = 0, hi = a.n_chunks - 1;
+        while (lo < hi) {
+          const int mid = (lo + hi + 1) >> 1;
+          if (a.tp_base[mid] <= gf) lo = mid;
+          else hi = mid - 1;
+        }
+        c = lo;
+      } else {
+        do ++c;
+        while (c + 1 < a.n_chunks && a.tp_base[c + 1] <= gf);
+      }
+      c = uniform32(c);
+      cb = uniform64(a.tp_base[c]);
+      ce = uniform64(c + 1 < a.n_chunks ? a.tp_base[c + 1] : INT64_MAX);
+      // frames [0, tf_skip[c]) of the chunk were done by the window stage: the work list is
+      // the remaining frames only, so the persistent workgroups stay balanced
+      skip = uniform32(a.tf_skip ? a.tf_skip[c] : 0);
+      nt = uniform32(a.n_tframes[c]);
+      coff = uniform64(a.chunk_off[c]);
+      clen = uniform64(a.chunk_len[c]);
+      ctf = uniform64(a.tf_base[c]);
     }
-    const int c = lo;
-    // frames [0, tf_skip[c]) of the chunk were done by the window stage: the work list is
-    // the remaining frames only, so the persistent workgroups stay balanced
-    const int t = (int)(gf - a.tp_base[c]) + (a.tf_skip ? a.tf_skip[c] : 0);
-    if (t >= a.n_tframes[c]) continue;
+    const int t = (int)(gf - cb) + skip;
+    if (t >= nt) continue;
     int lane = lane0;
     asm volatile("" : "+v"(lane));
-    const int64_t off = a.chunk_off[c];
+    const int jin = fft_in_lane(lane);  // this lane's stage-1 butterfly: samples x[2 (jin + 64 r)]
+    const int64_t off = coff;
     const float* x = a.sig + off;
-    const int64_t L = a.chunk_len[c];
+    const int64_t L = clen;
     const int64_t s0 = (int64_t)t * 512 - 1024;
     FftIn<1024> in;
     if (s0 >= 0 && s0 + 2048 <= L && ((off & 1) == 0)) {
       const float2* x2 = reinterpret_cast<const float2*>(x + s0);
       float2 xv[16], hw[16];
 #pragma unroll
-      for (int r = 0; r < 16; ++r) xv[r] = x2[lane + 64 * r];  // issued first: the LDS batch hides under them
-      lds_read16_strided<0, 64 * 8>(hw, lds_addr(sh_hann + lane));
+      for (int r = 0; r < 16; ++r) xv[r] = x2[jin + 64 * r];  // issued first: the LDS batch hides under them
+      lds_read16_strided<0, 64 * 8>(hw, lds_addr(sh_hann + jin));
 #pragma unroll
       for (int r = 0; r < 16; ++r) in[0][r] = make_float2(xv[r].x * hw[r].x, xv[r].y * hw[r].y);
     } else {
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const int n = lane + 64 * r;
+        const int n = jin + 64 * r;
         const int64_t i0 = s0 + 2 * n;
         const float x0 = (i0 >= 0 && i0 < L) ? x[i0] : 0.0f;
         const float x1 = (i0 + 1 >= 0 && i0 + 1 < L) ? x[i0 + 1] : 0.0f;
@@ -331,7 +356,7 @@ __global__ __launch_bounds__(TP_WAVES * 64) void tuning_peaks_kernel(PeakArgs a)
     }
     // stages 1-2 through LDS, the last stage on mirror-paired butterflies, then the real split
     // and |X| straight from registers (stft_mel structure)
-    stockham_stage_regs<1024, 16, 1, 64, false, 0, 0>(in, fftbuf, sh_tw, lane);
+    stockham_stage_regs<1024, 16, 1, 64, false, 0, 0>(in, fftbuf, sh_tw, jin);
     stockham_stage<1024, 16, 16, 64, false, 0, 0>(fftbuf, sh_tw, lane);
     float2 v[4][4];
     fft1024_last_mirror<TpTw::s3>(fftbuf, sh_tw, lane, v);
@@ -353,8 +378,8 @@ __global__ __launch_bounds__(TP_WAVES * 64) void tuning_peaks_kernel(PeakArgs a)
       const int k = kPipLo - 1 + 64 * q + lane;
       if (k <= kPipHi + 1) S[k] = __fsqrt_rn(S[k]);
     }
-    piptrack_append([&](int k) { return S[k]; }, mx, lane, &a.chunk_npk[c],
-                    a.peak_pitch + a.tf_base[c] * kPeakSlots, a.peak_mag + a.tf_base[c] * kPeakSlots);
+    piptrack_append([&](int k) { return S[k]; }, mx, lane, &a.chunk_npk[c], a.peak_pitch + ctf * kPeakSlots,
+                    a.peak_mag + ctf * kPeakSlots);
   }
 }
 
@@ -396,12 +421,42 @@ __device__ __forceinline__ int wave_incl_scan_i(int v) {
 // the chunk's compact peak list, plus one pass for the upper middle of an even count),
 // then the 100-bin residual histogram and its first argmax (librosa estimate_tuning /
 // pitch_tuning, oracle/ncref.py).
+// The CQT kernels' per-(chunk, octave) f16 split exponent: 2^ex scales the octave's samples so
+// their largest (bounded by the chunk's max |level 0| times the octave's gain) sits below 2^13
+struct OctScale {
+  const float* xmax;      // decimate3 workgroup maxima of |level 0| (slot c + oct_off[c][3] / 256 + tile)
+  const int64_t* oct_off;
+  const int64_t* oct_len;
+  int d3_span;            // level-3 outputs per decimate3 workgroup
+  float gpow[7];
+  int* oct_ex;            // [n][7]
+};
+
 template <int NT>
 __global__ __launch_bounds__(NT) void tuning_select_kernel(const float* peak_pitch, const float* peak_mag,
                                                            const int* chunk_npk, const int64_t* tf_base,
                                                            int* tuning_idx, float* tuning_val, int* tuning_margin,
-                                                           unsigned long long* span) {
+                                                           OctScale os, unsigned long long* span) {
   const Span span_(span);
+  if (threadIdx.x < 64) {  // wave 0: the chunk's octave exponents (the CQT kernels read them)
+    const int c = blockIdx.x, lane = threadIdx.x;
+    const int64_t l3 = os.oct_len[c * 7 + 3];
+    const int ntl = (int)((l3 + os.d3_span - 1) / os.d3_span);
+    const float* xm = os.xmax + c + os.oct_off[c * 7 + 3] / 256;
+    float m0 = 0.0f;
+    for (int i = lane; i < ntl; i += 64) m0 = fmaxf(m0, xm[i]);
+    const float m = wave_max_u(m0);
+    if (lane < 7) {
+      const float mx = m * os.gpow[lane];
+      int ex = 0;
+      if (mx > 0.0f) {
+        int e;
+        frexpf(mx, &e);  // mx < 2^e
+        ex = min(13 - e, 100);
+      }
+      os.oct_ex[c * 7 + lane] = ex;
+    }
+  }
   __shared__ BlockScratch<NT> bs;
   __shared__ int hist[256];
   __shared__ int counts[100];
@@ -574,9 +629,7 @@ struct CqmArgs {
   const uint4* bfrag;    // Tables::cqm_b
   const int* bexp;       // Tables::cqm_bexp
   const float* cqt_isl;
-  const float* xmax;     // decimate3 workgroup maxima of |level 0| (slot c + oct_off[c][3] / 256 + tile)
-  int d3_span;           // level-3 outputs per decimate3 workgroup
-  float gpow[7];
+  const int* oct_ex;     // [n][7] f16 split exponents (tuning_select_kernel, OctScale)
   float* gpart;          // [tf_base[c] + t][7][12] octave chroma partial rows
   unsigned long long* span = nullptr;
 };
@@ -614,14 +667,15 @@ __global__ __launch_bounds__(CM_NTH) void cqt_mfma_kernel(CqmArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   uint4* sB = reinterpret_cast<uint4*>(smem);  // [CM_R][CM_SLICE]
   const int c = blockIdx.y;
-  const int T = a.n_frames[c];
-  const int t0 = blockIdx.x * CM_FR;
-  if (t0 >= T) return;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int nfr = min(CM_FR, T - t0);
   const int oct = CM_LO + wave;
-  const int ti = a.tuning_idx[c];
+  // every descriptor read up front, unconditionally: one round trip of scalar loads
+  const int T = a.n_frames[c], ti = a.tuning_idx[c], ex = a.oct_ex[c * 7 + oct];
+  const int64_t yoff = a.oct_off[c * 7 + oct], Ly = a.oct_len[c * 7 + oct];
+  const int t0 = blockIdx.x * CM_FR;
+  if (t0 >= T) return;
+  const int nfr = min(CM_FR, T - t0);
   const uint4* bsrc = a.bfrag + (size_t)ti * (CM_KS * CM_SLICE);
   // the first filter slice is in flight while the image is built
   auto fetch_slice = [&](int ks) {
@@ -635,23 +689,8 @@ __global__ __launch_bounds__(CM_NTH) void cqt_mfma_kernel(CqmArgs a) {
   fetch_slice(0);
 
   // this wave's octave: rows t0 .. t0 + 63, row t at sample t hop - 512
-  const float* y = a.ws_oct + a.oct_off[c * 7 + oct];
-  const int64_t Ly = a.oct_len[c * 7 + oct];
+  const float* y = a.ws_oct + yoff;
   const int hop = 512 >> oct;
-  int ex = 0;
-  {
-    const int64_t l3 = a.oct_len[c * 7 + 3];
-    const int ntl = (int)((l3 + a.d3_span - 1) / a.d3_span);
-    const float* xm = a.xmax + c + a.oct_off[c * 7 + 3] / 256;
-    float m0 = 0.0f;
-    for (int i = lane; i < ntl; i += 64) m0 = fmaxf(m0, xm[i]);
-    const float mx = wave_max_u(m0) * a.gpow[oct];
-    if (mx > 0.0f) {
-      int e;
-      frexpf(mx, &e);  // mx < 2^e
-      ex = min(13 - e, 100);
-    }
-  }
   const float sx = ldexpf(1.0f, ex);
   const int64_t s0 = (int64_t)t0 * hop - 512;  // first sample of the tile's span
   const int S = (CM_FR - 1) * hop + kCqtNfft;
@@ -818,15 +857,16 @@ __device__ __forceinline__ void cqt_mfma_low(const CqmArgs& a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   uint4* sB = reinterpret_cast<uint4*>(smem);  // [2][CM_SLICE]
   const int c = blockIdx.y;
-  const int T = a.n_frames[c];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int tw = wave >> 1, hw = wave & 1;  // tile of the workgroup, row half of the tile
+  // every descriptor read up front, unconditionally: one round trip of scalar loads
+  const int T = a.n_frames[c], ti = a.tuning_idx[c], ex = a.oct_ex[c * 7 + OCT];
+  const int64_t yoff = OCT == 0 ? a.chunk_off[c] : a.oct_off[c * 7 + OCT], Ly = a.oct_len[c * 7 + OCT];
   if (blockIdx.x * (CL_TPW * CM_FR) >= T) return;
   int t0 = (blockIdx.x * CL_TPW + tw) * CM_FR;
   const bool active = t0 < T;  // an idle tile's waves still share the DMA and the barriers
   if (!active) t0 = 0;
-  const int ti = a.tuning_idx[c];
   const uint4* bsrc = a.bfrag + (size_t)ti * (CM_KS * CM_SLICE);
   float* blk = reinterpret_cast<float*>(smem + CM_BBYTES) + tw * (2 * L::BLK);
   auto kstep = [](int n) { return n / M + G * (n % M); };  // step n -> k-step (group n / M, shift n % M)
@@ -840,22 +880,7 @@ __device__ __forceinline__ void cqt_mfma_low(const CqmArgs& a) {
   };
   fetch_slice(0);
 
-  const float* y = OCT == 0 ? a.sig + a.chunk_off[c] : a.ws_oct + a.oct_off[c * 7 + OCT];
-  const int64_t Ly = a.oct_len[c * 7 + OCT];
-  int ex = 0;
-  {
-    const int64_t l3 = a.oct_len[c * 7 + 3];
-    const int ntl = (int)((l3 + a.d3_span - 1) / a.d3_span);
-    const float* xm = a.xmax + c + a.oct_off[c * 7 + 3] / 256;
-    float m0 = 0.0f;
-    for (int i = lane; i < ntl; i += 64) m0 = fmaxf(m0, xm[i]);
-    const float mx = wave_max_u(m0) * a.gpow[OCT];
-    if (mx > 0.0f) {
-      int e;
-      frexpf(mx, &e);
-      ex = min(13 - e, 100);
-    }
-  }
+  const float* y = (OCT == 0 ? a.sig : a.ws_oct) + yoff;
   const float sx = ldexpf(1.0f, ex);
   const int64_t s0 = (int64_t)t0 * H - 512;
   // tile-uniform: both waves of a tile take the same path (their vmcnt bookkeeping agrees)
@@ -1069,6 +1094,7 @@ struct ChromaWs {
   int* tuning_idx;
   float* xmax;  // decimate3 workgroup maxima of |level 0|
   float* gpart; // [tuning frame][7][12] octave chroma partial rows (hybrid CQT)
+  int* oct_ex;  // [n][7] f16 split exponents of the CQT operands
 };
 
 static inline size_t al256(size_t n) { return (n + 255) & ~(size_t)255; }
@@ -1086,6 +1112,7 @@ size_t chroma_ws_bytes(int n, int64_t total_len) {
   b += al256(sizeof(int64_t) * (n + 1));
   b += al256(sizeof(float) * (size_t)(n + (total_len + 64 * 7 * (int64_t)n) / 256 + 2));
   b += al256(sizeof(float) * (size_t)tfr * 84);
+  b += al256(sizeof(int) * 7 * n);
   return b + 4096;
 }
 
@@ -1131,6 +1158,7 @@ int launch_chroma_mean(Context& ctx, const float* sig, const int64_t* chunk_off,
   int64_t* tp_base = reinterpret_cast<int64_t*>(take(sizeof(int64_t) * (n + 1)));
   w.xmax = reinterpret_cast<float*>(take(sizeof(float) * (size_t)(n + (total_len + 64 * 7 * (int64_t)n) / 256 + 2)));
   w.gpart = reinterpret_cast<float*>(take(sizeof(float) * (size_t)tfr * 84));
+  w.oct_ex = reinterpret_cast<int*>(take(sizeof(int) * 7 * n));
   if (ext) {  // the caller's lists (zeroed counts): the window stage appends to them too
     w.peak_pitch = ext_pitch;
     w.peak_mag = ext_mag;
@@ -1183,8 +1211,15 @@ int launch_chroma_mean(Context& ctx, const float* sig, const int64_t* chunk_off,
   if (wait_event) NC_HIP(hipStreamWaitEvent(st, static_cast<hipEvent_t>(wait_event), 0));
   {
     KTimer kt_(ctx, "tuning_select", st);
+    OctScale os;
+    os.xmax = w.xmax;
+    os.oct_off = w.oct_off;
+    os.oct_len = w.oct_len;
+    os.d3_span = D3_T;
+    std::copy(ctx.t.cqm_gpow, ctx.t.cqm_gpow + 7, os.gpow);
+    os.oct_ex = w.oct_ex;
     hipLaunchKernelGGL((tuning_select_kernel<TS_NT>), dim3(n), dim3(TS_NT), 0, st, w.peak_pitch, w.peak_mag,
-                       w.chunk_npk, w.tf_base, w.tuning_idx, out_tuning, out_tuning_margin, kt_.span());
+                       w.chunk_npk, w.tf_base, w.tuning_idx, out_tuning, out_tuning_margin, os, kt_.span());
   }
   CqmArgs ma;
   ma.sig = sig;
@@ -1198,9 +1233,7 @@ int launch_chroma_mean(Context& ctx, const float* sig, const int64_t* chunk_off,
   ma.bfrag = ctx.t.cqm_b;
   ma.bexp = ctx.t.cqm_bexp;
   ma.cqt_isl = ctx.t.cqt_inv_sqrt_len;
-  ma.xmax = w.xmax;
-  ma.d3_span = D3_T;
-  std::copy(ctx.t.cqm_gpow, ctx.t.cqm_gpow + 7, ma.gpow);
+  ma.oct_ex = w.oct_ex;
   ma.gpart = w.gpart;
   const int ntile = (int)((1 + max_chunk_len / 512 + CM_FR - 1) / CM_FR);
   {

@@ -216,7 +216,16 @@ __device__ __forceinline__ int64_t uniform64(int64_t v) {
 }
 
 // ------------------------------------------------------------------ Stockham wave FFT
-__device__ __forceinline__ int lpad(int i) { return i + (i >> 4); }
+// Exchange layout of the 1024-point wave FFT: one pad element per 32.  ds_read_b64 services
+// 32 lanes over all 64 banks, so the stage-2 reads (element l + 64 r) need 32 consecutive
+// elements on distinct banks, which a pad every 16 breaks (lanes 0 and 31 collide: 2x on every
+// read).  The stage-1 writes (element 16 j + r, 16-lane groups on 32 banks) stay conflict free
+// when lane l takes j = fft_in_lane(l) (below) instead of j = l.
+__device__ __forceinline__ int lpad(int i) { return i + (i >> 5); }
+// Stage-1 butterfly of lane l: j = 2 (l mod 16) + bit 4 of l, + 32 for the upper half-wave, so
+// the 16 lanes of a ds_write_b64 group write rows j whose pads j / 2 differ.  The input reads
+// x[j + 64 r] stay one contiguous 512-byte span per load.
+__device__ __forceinline__ int fft_in_lane(int l) { return (((l & 15) << 1) | ((l >> 4) & 1)) | (l & 32); }
 
 // f(std::integral_constant<int, i>{}) for i < N_, unrolled by construction: the loop unroller
 // leaves loops around inline asm alone, and a rolled loop over a register array homes the
@@ -302,7 +311,7 @@ __device__ __forceinline__ void lds_read16_strided(float2 (&o)[16], uint32_t a) 
 }
 template <int N>
 struct LdsSize {
-  static constexpr int value = N + N / 16;  // float2 elements
+  static constexpr int value = N + N / 32;  // float2 elements
 };
 
 // Stage with radix R, NS = product of the previous radices, NT threads (lanes of
@@ -317,6 +326,7 @@ __device__ __forceinline__ void stockham_stage_regs(float2 (&v)[N / (R * NT)][R]
                                                     const float2* __restrict__ tw, int tid) {
   constexpr int NB = N / (R * NT);
   static_assert(NB >= 1, "radix too large for the thread count");
+  static_assert(NS == 1 || NS == 16 || NS % 32 == 0, "stride offsets assume the pad-per-32 layout");
 #pragma unroll
   for (int b = 0; b < NB; ++b) {
     const int j = tid + NT * b;
@@ -338,8 +348,8 @@ __device__ __forceinline__ void stockham_stage_regs(float2 (&v)[N / (R * NT)][R]
     DFT<R>::run(v[b]);
   }
   if (SYNC) __syncthreads();  // every thread has loaded this stage's inputs
-  // lpad(i + off) == lpad(i) + off * 17 / 16 whenever off % 16 == 0, so strides that
-  // are multiples of 16 become immediate LDS offsets instead of per-access index math
+  // lpad(base + r NS) == lpad(base) + lpad(r NS) when NS % 32 == 0, or NS == 16 (base % 32 is
+  // then k < 16), so the strides become immediate LDS offsets instead of per-access index math
 #pragma unroll
   for (int b = 0; b < NB; ++b) {
     const int j = tid + NT * b;
@@ -348,7 +358,7 @@ __device__ __forceinline__ void stockham_stage_regs(float2 (&v)[N / (R * NT)][R]
     if constexpr (NS % 16 == 0) {
       float2* p = lds + lpad(base);
 #pragma unroll
-      for (int r = 0; r < R; ++r) p[r * NS * 17 / 16] = v[b][r];
+      for (int r = 0; r < R; ++r) p[lpad(r * NS)] = v[b][r];
     } else {
 #pragma unroll
       for (int r = 0; r < R; ++r) lds[lpad(base + r * NS)] = v[b][r];
@@ -361,15 +371,15 @@ template <int N, int R, int NS, int NT, bool SYNC, int TWN = 8192, int STO = 0>
 __device__ __forceinline__ void stockham_stage(float2* lds, const float2* __restrict__ tw, int tid) {
   constexpr int NB = N / (R * NT);
   float2 v[NB][R];
-  if constexpr (NT % 16 == 0 && (N / R) % 16 == 0) {
+  if constexpr (NT % 32 == 0 && (N / R) % 32 == 0) {
     const float2* p = lds + lpad(tid);
     if constexpr (NB == 1 && R == 16) {
-      lds_read16_strided<0, (N / R) * 17 / 16 * 8>(v[0], lds_addr(p));
+      lds_read16_strided<0, (N / R) * 33 / 32 * 8>(v[0], lds_addr(p));
     } else {
 #pragma unroll
       for (int b = 0; b < NB; ++b)
 #pragma unroll
-        for (int r = 0; r < R; ++r) v[b][r] = p[(NT * b + r * (N / R)) * 17 / 16];
+        for (int r = 0; r < R; ++r) v[b][r] = p[lpad(NT * b + r * (N / R))];
     }
   } else {
 #pragma unroll
@@ -464,40 +474,6 @@ __device__ __forceinline__ void block_fft(FftIn<N, NT>& in, float2* lds, const f
   fft_impl<N, NT, true>(in, lds, tw, tid);
 }
 
-// Real-FFT split: Z = FFT_N(z), z[n] = x[2n] + i x[2n+1] (x real, length 2N).
-// Returns X[k] and X[N-k] for 0 <= k <= N/2.
-// rfft_split for k = lane + 64 m (m compile-time after unrolling) with the padded LDS
-// indices folded: pa = lpad(lane), pb = lpad(N - lane); Z[N-k] sits at pb - 68 m except
-// for k == 0, which wraps to Z[0].  Same arithmetic as rfft_split.
-template <int N, int TWN, int SPLIT>
-__device__ __forceinline__ void rfft_split_m(const float2* lds, const float2* __restrict__ tw, int lane, int m,
-                                             int pa, int pb, float2& Xk, float2& XNk) {
-  const int k = lane + 64 * m;
-  const float2 a = lds[pa + 68 * m];
-  const int ib = (m == 0 && lane == 0) ? 0 : pb - 68 * m;
-  const float2 b = cconj(lds[ib]);
-  const float2 E = cscale(cadd(a, b), 0.5f);
-  const float2 O = cmul_mi(cscale(csub(a, b), 0.5f));  // (a-b)/(2i)
-  const float2 W = TWN > 0 ? tw[(k * (TWN > 0 ? TWN / (2 * N) : 1)) & (TWN - 1)] : tw[SPLIT + k];
-  const float2 WO = cmul(W, O);
-  Xk = cadd(E, WO);
-  XNk = cconj(csub(E, WO));
-}
-
-template <int TWN = 8192, int SPLIT = 0>
-__device__ __forceinline__ void rfft_split(const float2* lds, const float2* __restrict__ tw, int N, int k,
-                                           float2& Xk, float2& XNk) {
-  const float2 a = lds[lpad(k & (N - 1))];
-  const float2 b = cconj(lds[lpad((N - k) & (N - 1))]);
-  const float2 E = cscale(cadd(a, b), 0.5f);
-  const float2 O = cmul_mi(cscale(csub(a, b), 0.5f));  // (a-b)/(2i)
-  const float2 W = TWN > 0 ? tw[(k * (TWN > 0 ? TWN / (2 * N) : 1)) & (TWN - 1)] : tw[SPLIT + k];  // exp(-2 pi i k / 2N)
-  const float2 WO = cmul(W, O);
-  Xk = cadd(E, WO);
-  XNk = cconj(csub(E, WO));
-}
-
-
 // ------------------------------------------------------------------ mirror-paired last stage
 // Last radix-4 stage (NS = 256) of the 1024-point plan 16.16.4 done on the lane's butterfly
 // set J = {l, 128-l, 128+l, 256-l} (lane 0: {0, 64, 192, 128}) instead of j = l + 64 b.  The
@@ -512,9 +488,9 @@ __device__ __forceinline__ int mirror_J(int l, int b) {
 // (spectral_frames) keeps them compiler-scheduled, or the compiler homes v in scratch.
 template <int STW3, bool TWB = false>
 __device__ __forceinline__ void fft1024_last_mirror(const float2* lds, const float2* tw, int l, float2 (&v)[4][4]) {
-  // lpad(J + 256 r) = lpad(J) + 272 r: four bases, immediate offsets
+  // lpad(J + 256 r) = lpad(J) + 264 r: four bases, immediate offsets
   float2 o[16];
-  lds_read16<0, 2176, 4352, 6528, 0, 2176, 4352, 6528, 0, 2176, 4352, 6528, 0, 2176, 4352, 6528>(
+  lds_read16<0, 2112, 4224, 6336, 0, 2112, 4224, 6336, 0, 2112, 4224, 6336, 0, 2112, 4224, 6336>(
       o, lds_addr(lds + lpad(mirror_J(l, 0))), lds_addr(lds + lpad(mirror_J(l, 1))),
       lds_addr(lds + lpad(mirror_J(l, 2))), lds_addr(lds + lpad(mirror_J(l, 3))));
 #pragma unroll
@@ -543,8 +519,8 @@ __device__ __forceinline__ void fft1024_last_mirror(const float2* lds, const flo
 
 // Real-FFT split of a 2048-sample real frame packed as z[n] = x[2n] + i x[2n+1] from the
 // mirror-paired outputs: f(k, X[k], X[1024 - k]) for the lane's 8 pairs (9 on lane 0),
-// k <= 512, together covering X[0..1024] once (X[512] twice on lane 0).  Same arithmetic as
-// rfft_split_m; SPLIT = offset of W_2048^k in tw.
+// k <= 512, together covering X[0..1024] once (X[512] twice on lane 0).  SPLIT = offset of
+// W_2048^k in tw.
 template <int SPLIT, class F>
 __device__ __forceinline__ void rsplit_mirror(const float2 (&v)[4][4], const float2* tw, int l, F&& f) {
   const bool l0 = l == 0;

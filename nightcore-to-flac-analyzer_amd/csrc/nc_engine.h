@@ -34,12 +34,14 @@ struct Tables {
   int* mel_off = nullptr;
   float* mel_w = nullptr;
   int mel_nnz = 0;
-  // the same filterbank as two lane slots (slot 0: band l, slot 1: band 127 - l), each read
-  // from a 16-byte aligned first bin lo4 in float4 steps: weights [mel_j0 + mel_j1][64]
-  // float4 (zero outside the band), lo4 / steps per (slot, lane)
+  // the same filterbank as two lane slots (slot 0: bands 0..63, slot 1: bands 64..127, lane
+  // l of slot s holds band mel_band[64 s + l]), each read from a 16-byte aligned first bin
+  // lo4 in float4 steps: weights [mel_j0 + mel_j1][64] float4 (zero outside the band), lo4 /
+  // steps per (slot, lane)
   float4* mel_w4 = nullptr;
   int* mel_lo4 = nullptr;  // [2][64]
   int* mel_nj4 = nullptr;  // [2][64]
+  int* mel_band = nullptr;  // [2][64]
   int mel_j0 = 0, mel_j1 = 0;
   // CQT: per tuning index, per filter: [lo, len, off] into a complex weight pool
   int* cqt_lo = nullptr;        // [kNTunings][36]

@@ -69,9 +69,15 @@ __device__ __forceinline__ int seq_of_frame(const int64_t* base, int n, int64_t 
 
 __host__ __device__ __forceinline__ int al4(int n) { return (n + 3) & ~3; }
 
+// mel lane-slot descriptors staged in LDS (a global read at the mel step exposes its latency):
+// lo4 | nj4 << 11 | band << 16 per (slot, lane)
+constexpr int SM_MT = 128;
+__host__ __device__ __forceinline__ int mel_pack(int lo4, int nj4, int band) { return lo4 | (nj4 << 11) | (band << 16); }
+
 size_t stft_mel_lds_bytes(int mel_j) {
   return (size_t)al4(SmTw::size) * sizeof(float2) + (size_t)mel_j * 64 * sizeof(float4) +
-         (size_t)SM_HANN2 * sizeof(float2) + (size_t)SM_WAVES * LdsSize<1024>::value * sizeof(float2);
+         (size_t)SM_HANN2 * sizeof(float2) + (size_t)SM_MT * sizeof(int) +
+         (size_t)SM_WAVES * LdsSize<1024>::value * sizeof(float2);
 }
 
 __global__ __launch_bounds__(SM_THREADS) void stft_mel_kernel(StftMelArgs a) {
@@ -81,33 +87,46 @@ __global__ __launch_bounds__(SM_THREADS) void stft_mel_kernel(StftMelArgs a) {
   float4* sh_w4 = reinterpret_cast<float4*>(sh_tw + al4(SmTw::size));  // [mel_j0 + mel_j1][64]
   const int lane0 = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform (SGPR)
   float2* sh_hann = reinterpret_cast<float2*>(sh_w4 + (a.mel_j0 + a.mel_j1) * 64);
-  float2* fftbuf = sh_hann + SM_HANN2 + wave * LdsSize<1024>::value;
+  int* sh_mt = reinterpret_cast<int*>(sh_hann + SM_HANN2);
+  float2* fftbuf = reinterpret_cast<float2*>(sh_mt + SM_MT) + wave * LdsSize<1024>::value;
 
   fill_staged_tw<1024>(sh_tw, a.tw, threadIdx.x, SM_THREADS);
   for (int i = threadIdx.x; i < SM_HANN2; i += SM_THREADS) sh_hann[i] = reinterpret_cast<const float2*>(a.hann2048)[i];
   for (int i = threadIdx.x; i < (a.mel_j0 + a.mel_j1) * 64; i += SM_THREADS) sh_w4[i] = a.mel_w4[i];
+  if (threadIdx.x < SM_MT) sh_mt[threadIdx.x] = mel_pack(a.mel_lo4[threadIdx.x], a.mel_nj4[threadIdx.x], a.mel_band[threadIdx.x]);
   const float4* mw4 = sh_w4;
   __syncthreads();
 
   const int64_t n_groups = (a.total_frames + SM_WAVES - 1) / SM_WAVES;
   const int64_t gb = n_groups * blockIdx.x / gridDim.x, ge = n_groups * (blockIdx.x + 1) / gridDim.x;
+  // The wave's frames g = grp * SM_WAVES + wave rise by SM_WAVES: their sequence is tracked
+  // forward, its bounds, flags, length and offset reloaded only when g crosses into a later
+  // sequence, instead of a 64-bit division or binary search and dependent loads per frame
+  int s = -1;
+  int64_t sb = 0, se = -1, t0 = 0, L = 0, off = 0;
+  bool act = true;
   for (int64_t grp = gb; grp < ge; ++grp) {
     const int64_t g = grp * SM_WAVES + wave;
     if (g >= a.total_frames) break;
-    int s;
-    int64_t t, L;
-    if (a.frame_base) {
-      s = seq_of_frame(a.frame_base, a.n_seq, g);
-      t = g - a.frame_base[s] + (a.seq_t0 ? a.seq_t0[s] : 0);
-    } else {
-      s = (int)(g / a.uniform_T);
-      t = g - (int64_t)s * a.uniform_T;
+    if (g >= se) {
+      if (s < 0) {
+        s = a.frame_base ? seq_of_frame(a.frame_base, a.n_seq, g) : (int)(g / a.uniform_T);
+      } else if (a.frame_base) {
+        do ++s;
+        while (s + 1 < a.n_seq && a.frame_base[s + 1] <= g);
+      } else {
+        s = (int)(g / a.uniform_T);
+      }
+      s = uniform32(s);
+      sb = uniform64(a.frame_base ? a.frame_base[s] : (int64_t)s * a.uniform_T);
+      se = uniform64(a.frame_base ? (s + 1 < a.n_seq ? a.frame_base[s + 1] : INT64_MAX) : sb + a.uniform_T);
+      t0 = uniform64(a.frame_base && a.seq_t0 ? a.seq_t0[s] : 0);
+      act = !a.active || a.active[s];
+      L = uniform64(a.seq_len ? a.seq_len[s] : a.uniform_len);
+      off = uniform64(a.seq_off[s]);
     }
-    s = uniform32(s);
-    t = uniform64(t);
-    if (a.active && !a.active[s]) continue;
-    L = uniform64(a.seq_len ? a.seq_len[s] : a.uniform_len);
-    const int64_t off = uniform64(a.seq_off[s]);
+    if (!act) continue;
+    const int64_t t = g - sb + t0;
     const float* x = a.sig + off;
     const int64_t s0 = t * a.hop - 1024;
 
@@ -115,6 +134,7 @@ __global__ __launch_bounds__(SM_THREADS) void stft_mel_kernel(StftMelArgs a) {
     // frame instead of being hoisted out of the loop (which would cost occupancy).
     int lane = lane0;
     asm volatile("" : "+v"(lane));
+    const int jin = fft_in_lane(lane);  // this lane's stage-1 butterfly: samples x[2 (jin + 64 r)]
     const float2* twl = sh_tw;
     const float* hann = a.hann2048;
     FftIn<1024> in;
@@ -124,11 +144,11 @@ __global__ __launch_bounds__(SM_THREADS) void stft_mel_kernel(StftMelArgs a) {
       const float2* x2 = reinterpret_cast<const float2*>(x + s0);
       float2 xv[16], hw[16];  // samples and window pairs (h[2n], h[2n + 1]), n = lane + 64 r
 #pragma unroll
-      for (int r = 0; r < 16; ++r) xv[r] = x2[lane + 64 * r];  // issued first: the LDS batch hides under them
-      lds_read16_strided<0, 64 * 8>(hw, lds_addr(sh_hann + lane));
+      for (int r = 0; r < 16; ++r) xv[r] = x2[jin + 64 * r];  // issued first: the LDS batch hides under them
+      lds_read16_strided<0, 64 * 8>(hw, lds_addr(sh_hann + jin));
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const int n = lane + 64 * r;
+        const int n = jin + 64 * r;
         const float2 v = xv[r];
         const float2 h = hw[r];
         if (r >= 8 && r < 12) {
@@ -143,7 +163,7 @@ __global__ __launch_bounds__(SM_THREADS) void stft_mel_kernel(StftMelArgs a) {
     } else {
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const int n = lane + 64 * r;
+        const int n = jin + 64 * r;
         const int64_t i0 = s0 + 2 * n;
         const float x0 = (i0 >= 0 && i0 < L) ? x[i0] : 0.0f;
         const float x1 = (i0 + 1 >= 0 && i0 + 1 < L) ? x[i0 + 1] : 0.0f;
@@ -163,7 +183,7 @@ __global__ __launch_bounds__(SM_THREADS) void stft_mel_kernel(StftMelArgs a) {
     }
     // 1024-point complex FFT of the packed frame: stages 1-2 through LDS, the last stage on
     // mirror-paired butterflies, then the real split and |X|^2 straight from registers
-    stockham_stage_regs<1024, 16, 1, 64, false, 0, 0>(in, fftbuf, twl, lane);
+    stockham_stage_regs<1024, 16, 1, 64, false, 0, 0>(in, fftbuf, twl, jin);
     stockham_stage<1024, 16, 16, 64, false, 0, 0>(fftbuf, twl, lane);
     float2 v[4][4];
     fft1024_last_mirror<SmTw::s3, true>(fftbuf, twl, lane, v);
@@ -187,16 +207,18 @@ __global__ __launch_bounds__(SM_THREADS) void stft_mel_kernel(StftMelArgs a) {
                         a.peak_mag + base);
       }
     }
-    // Slaney mel: lane l owns bands l and 127 - l, read as float4 steps from a 16-byte aligned
-    // first bin with zero-padded weights (fmaf chain in bin order, as the CSR form)
+    // Slaney mel: lane l owns one short and one long band (mel_band: spread over the lanes so
+    // the float4 power reads are bank-conflict free), read as float4 steps from a 16-byte
+    // aligned first bin with zero-padded weights (fmaf chain in bin order, as the CSR form)
     float acc0 = 0.0f, acc1 = 0.0f;
-    mel_unrolled<kMelJ0>(pw, mw4, a.mel_lo4[lane], a.mel_nj4[lane], lane, acc0);
-    mel_unrolled<kMelJ1>(pw, mw4 + kMelJ0 * 64, a.mel_lo4[64 + lane], a.mel_nj4[64 + lane], lane, acc1);
+    const int mt0 = sh_mt[lane], mt1 = sh_mt[64 + lane];
+    mel_unrolled<kMelJ0>(pw, mw4, mt0 & 2047, (mt0 >> 11) & 31, lane, acc0);
+    mel_unrolled<kMelJ1>(pw, mw4 + kMelJ0 * 64, mt1 & 2047, (mt1 >> 11) & 31, lane, acc1);
     const float db0 = 10.0f * log10f(fmaxf(1e-10f, acc0));
     const float db1 = 10.0f * log10f(fmaxf(1e-10f, acc1));
     float* row = a.sdb + g * 128;
-    row[lane] = db0;
-    row[127 - lane] = db1;
+    row[mt0 >> 16] = db0;
+    row[mt1 >> 16] = db1;
     const float mx = wave_max_u(fmaxf(db0, db1));
     if (lane == 0) a.frame_max[g] = mx;
   }
@@ -215,6 +237,7 @@ int launch_stft_mel(Context& ctx, const StftMelArgs& args, hipStream_t st) {
   a.mel_w4 = ctx.t.mel_w4;
   a.mel_lo4 = ctx.t.mel_lo4;
   a.mel_nj4 = ctx.t.mel_nj4;
+  a.mel_band = ctx.t.mel_band;
   a.mel_j0 = ctx.t.mel_j0;
   a.mel_j1 = ctx.t.mel_j1;
   if (a.hop <= 0 || a.hop > 512 || (a.hop & 1)) {

@@ -33,6 +33,7 @@ struct StftMelArgs {
   const float4* mel_w4;
   const int* mel_lo4;
   const int* mel_nj4;
+  const int* mel_band;
   int mel_j0, mel_j1;
   // shared tuning frames (nullable win_chunk): frames t < tp_frames of sequence s with
   // win_chunk[s] = c >= 0 are also tuning frames t of chunk c; their piptrack peaks are
