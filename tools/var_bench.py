@@ -78,6 +78,12 @@ class Variant:
         cks = (float(self.onset.double().sum()), float(self.tg.sum()), float(self.chroma.double().sum()))
         print(f"{self.name:18s} min us/run {self.best}  checksum onset {cks[0]:.6f} tg {cks[1]:.9f} "
               f"chroma {cks[2]:.7f}", flush=True)
+        if hasattr(self.lib, "nc_dbg_stamps"):  # a phase-stamped diagnostic build
+            buf = (C.c_ulonglong * 16)()
+            self.lib.nc_dbg_stamps(buf, 0)
+            n = max(1, buf[7])
+            print(f"  stamped kernel, cycles per item over {n} items, by phase: " +
+                  ", ".join(f"{buf[i] / n:.0f}" for i in range(7)), flush=True)
 
 
 def inputs(src):
