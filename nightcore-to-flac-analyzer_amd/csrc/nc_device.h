@@ -133,6 +133,16 @@ struct Span {
   __device__ __forceinline__ ~Span() { span_record(sp, t0); }
 };
 
+// XCD-aware workgroup order (cdna_hip_programming.md T1): the dispatcher deals linear
+// workgroup ids round robin to the 8 XCDs (blockIdx % 8 labels the workgroups that share an
+// L2); this bijective remap gives each of those classes a contiguous 1/8 of the logical ids, so
+// neighbouring logical work (the same chunk, the same tuning's filters) shares one L2.  Speed
+// only: any placement computes the same results.
+__device__ __forceinline__ unsigned xcd_remap(unsigned l, unsigned n) {
+  const unsigned q = n / 8, r = n % 8, x = l % 8;
+  return x * q + min(x, r) + l / 8;
+}
+
 // float <-> order-preserving int (for atomicMax on floats of either sign)
 __device__ __forceinline__ int f2ord(float f) {
   int i = __float_as_int(f);

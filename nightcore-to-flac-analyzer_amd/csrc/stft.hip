@@ -104,6 +104,7 @@ __global__ __launch_bounds__(SM_THREADS) void stft_mel_kernel(StftMelArgs a) {
   // sequence, instead of a 64-bit division or binary search and dependent loads per frame
   int s = -1;
   int64_t sb = 0, se = -1, t0 = 0, L = 0, off = 0;
+  int wc = -1;  // the 20 s chunk the sequence starts (shared tuning frames), or -1
   bool act = true;
   for (int64_t grp = gb; grp < ge; ++grp) {
     const int64_t g = grp * SM_WAVES + wave;
@@ -124,6 +125,7 @@ __global__ __launch_bounds__(SM_THREADS) void stft_mel_kernel(StftMelArgs a) {
       act = !a.active || a.active[s];
       L = uniform64(a.seq_len ? a.seq_len[s] : a.uniform_len);
       off = uniform64(a.seq_off[s]);
+      wc = uniform32(a.win_chunk ? a.win_chunk[s] : -1);
     }
     if (!act) continue;
     const int64_t t = g - sb + t0;
@@ -188,24 +190,33 @@ __global__ __launch_bounds__(SM_THREADS) void stft_mel_kernel(StftMelArgs a) {
     float2 v[4][4];
     fft1024_last_mirror<SmTw::s3, true>(fftbuf, twl, lane, v);
     float* pw = reinterpret_cast<float*>(fftbuf);  // power P[k], k in [0, 1024] (all Z reads precede)
-    rsplit_mirror<SmTw::split>(v, twl, lane, [&](int k, float2 X, float2 XN) {
-      pw[k] = fmaf(X.x, X.x, X.y * X.y);
-      pw[1024 - k] = fmaf(XN.x, XN.x, XN.y * XN.y);
-    });
     // a leading frame of a window that starts a 20 s chunk is also that chunk's tuning frame
     // t (same samples, padding and FFT): estimate_tuning's piptrack runs here, on the same
-    // |X| values tuning_peaks_kernel would compute (nc_piptrack.h)
-    if (a.win_chunk && t < a.tp_frames) {
-      const int c = uniform32(a.win_chunk[s]);
-      if (c >= 0) {
-        float pm = pw[1024];
+    // |X| values tuning_peaks_kernel computes (nc_piptrack.h): the frame max of |X| from the
+    // split's registers, |X| of the stencil bins beside the power (which the mel step needs)
+    if (wc >= 0 && t < a.tp_frames) {
+      float pmax = 0.0f;
+      rsplit_mirror<SmTw::split>(v, twl, lane, [&](int k, float2 X, float2 XN) {
+        const float p1 = fmaf(X.x, X.x, X.y * X.y), p2 = fmaf(XN.x, XN.x, XN.y * XN.y);
+        pw[k] = p1;
+        pw[1024 - k] = p2;
+        pmax = fmaxf(pmax, fmaxf(p1, p2));
+      });
+      const float mx = __fsqrt_rn(wave_max_u(pmax));
+      float* mg = pw + kPipMag;  // |X[k]| at mg[k - (kPipLo - 1)]
 #pragma unroll
-        for (int j = 0; j < 16; ++j) pm = fmaxf(pm, pw[lane + 64 * j]);
-        const float mx = __fsqrt_rn(wave_max_u(pm));
-        const int64_t base = uniform64(a.chunk_tf_base[c]) * kPeakSlots;
-        piptrack_append([&](int k) { return __fsqrt_rn(pw[k]); }, mx, lane, &a.chunk_npk[c], a.peak_pitch + base,
-                        a.peak_mag + base);
+      for (int q = 0; q < (kPipHi - kPipLo + 3 + 63) / 64; ++q) {
+        const int k = kPipLo - 1 + 64 * q + lane;
+        if (k <= kPipHi + 1) mg[k - (kPipLo - 1)] = __fsqrt_rn(pw[k]);
       }
+      const int64_t base = uniform64(a.chunk_tf_base[wc]) * kPeakSlots;
+      piptrack_append([&](int k) { return mg[k - (kPipLo - 1)]; }, mx, lane, &a.chunk_npk[wc], a.peak_pitch + base,
+                      a.peak_mag + base, reinterpret_cast<int*>(pw + kPipKpk));
+    } else {
+      rsplit_mirror<SmTw::split>(v, twl, lane, [&](int k, float2 X, float2 XN) {
+        pw[k] = fmaf(X.x, X.x, X.y * X.y);
+        pw[1024 - k] = fmaf(XN.x, XN.x, XN.y * XN.y);
+      });
     }
     // Slaney mel: lane l owns one short and one long band (mel_band: spread over the lanes so
     // the float4 power reads are bank-conflict free), read as float4 steps from a 16-byte

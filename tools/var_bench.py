@@ -7,6 +7,7 @@ drift over the run hits them alike; each prints its per-kernel minimum over the 
 and a checksum of its outputs so variants can be compared for equality.
     python3 tools/var_bench.py tools/var/<name>/libncgpu.so [...]"""
 import ctypes as C
+import os
 import sys
 from pathlib import Path
 
@@ -50,12 +51,36 @@ class Variant:
         self.cwsb = lib.nc_chroma_workspace_bytes(self.ctx, cn, cn * inp["CL"])
         self.cws = torch.empty(self.cwsb, dtype=torch.uint8, device=dev)
         self.best = {}
+        # VB_TUNING=1: the window STFT also runs the shared tuning frames' piptrack, as in the
+        # engine (nc_window_stage_tuning), for every fourth window (a 20 s chunk start)
+        self.tuning = os.environ.get("VB_TUNING") == "1"
+        if self.tuning:
+            lib.nc_window_stage_tuning.argtypes = [P, P, P, P, I32, I32, I32, P, P, P, P, P, I32, P, P, P, P, P,
+                                                   SZ, P]
+            nch = (n + 3) // 4
+            wc = np.full(n, -1, np.int32)
+            wc[::4] = np.arange(nch, dtype=np.int32)
+            self.win_chunk = torch.from_numpy(wc).to(dev)
+            self.tf_base = torch.arange(nch + 1, dtype=torch.int64, device=dev) * (1 + inp["CL"] // 512)
+            slots = int(self.tf_base[-1]) * 192
+            self.pp = torch.empty(slots, device=dev)
+            self.pm = torch.empty(slots, device=dev)
+            self.npk = torch.zeros(nch, dtype=torch.int32, device=dev)
+            self.tp = (inp["L"] - 1024) // 512 + 1
 
     def run(self):
         i, lib, st = self.inp, self.lib, torch.cuda.current_stream().cuda_stream
-        assert lib.nc_window_stage(self.ctx, i["sig"].data_ptr(), i["off"].data_ptr(), None, i["n"], i["L"], 512,
-                                   self.onset.data_ptr(), self.tg.data_ptr(), self.en.data_ptr(),
-                                   self.ws.data_ptr(), self.wsb, st) == 0
+        if self.tuning:
+            self.npk.zero_()
+            assert lib.nc_window_stage_tuning(self.ctx, i["sig"].data_ptr(), i["off"].data_ptr(), None, i["n"], i["L"],
+                                              512, self.onset.data_ptr(), self.tg.data_ptr(), self.en.data_ptr(),
+                                              self.win_chunk.data_ptr(), self.tf_base.data_ptr(), self.tp,
+                                              self.pp.data_ptr(), self.pm.data_ptr(), self.npk.data_ptr(), None,
+                                              self.ws.data_ptr(), self.wsb, st) == 0
+        else:
+            assert lib.nc_window_stage(self.ctx, i["sig"].data_ptr(), i["off"].data_ptr(), None, i["n"], i["L"], 512,
+                                       self.onset.data_ptr(), self.tg.data_ptr(), self.en.data_ptr(),
+                                       self.ws.data_ptr(), self.wsb, st) == 0
         assert lib.nc_chroma_mean(self.ctx, i["csig"].data_ptr(), i["coff"].data_ptr(), i["clen"].data_ptr(),
                                   i["cn"], i["cn"] * i["CL"], i["CL"], self.chroma.data_ptr(), self.tun.data_ptr(),
                                   None, None, self.cws.data_ptr(), self.cwsb, st) == 0
@@ -76,6 +101,8 @@ class Variant:
 
     def report(self):
         cks = (float(self.onset.double().sum()), float(self.tg.sum()), float(self.chroma.double().sum()))
+        if self.tuning:
+            print(f"  tuning peaks {int(self.npk.sum())}", flush=True)
         print(f"{self.name:18s} min us/run {self.best}  checksum onset {cks[0]:.6f} tg {cks[1]:.9f} "
               f"chroma {cks[2]:.7f}", flush=True)
         if hasattr(self.lib, "nc_dbg_stamps"):  # a phase-stamped diagnostic build
