@@ -646,6 +646,24 @@ __device__ __forceinline__ void cm_dma16(const void* gsrc, const void* lds_dst) 
                : "memory");
 }
 
+// Fragment reads issued by asm with no wait, retired by counted waits (cm_wait) that also tie
+// the fragments' registers, so no MFMA can read one early.  The compiler's scheduler sinks
+// each column tile's compiler-issued B reads next to that tile's MFMAs, with an
+// s_waitcnt lgkmcnt between every two tiles: one exposed LDS latency per column tile.
+// Only these reads are outstanding on lgkmcnt inside the k-loop (the loop top drains it).
+template <int OFF>
+__device__ __forceinline__ void cm_rd(cm_u4& d, uint32_t a) {
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=&v"(d) : "v"(a), "i"(OFF) : "memory");
+}
+template <int N>
+__device__ __forceinline__ void cm_wait(cm_u4& x, cm_u4& y) {
+  asm volatile("s_waitcnt lgkmcnt(%2)" : "+v"(x), "+v"(y) : "i"(N) : "memory");
+}
+template <int N>
+__device__ __forceinline__ void cm_wait(cm_u4& x, cm_u4& y, cm_u4& z, cm_u4& w) {
+  asm volatile("s_waitcnt lgkmcnt(%4)" : "+v"(x), "+v"(y), "+v"(z), "+v"(w) : "i"(N) : "memory");
+}
+
 // 8 samples -> f16 hi (f32 truncated to 11 significant bits: exact in f16) and lo (the
 // exact f32 remainder, rounded toward zero)
 __device__ __forceinline__ void cm_split(const float (&v)[8], float s, cm_half8& hi, cm_half8& lo) {
@@ -662,7 +680,7 @@ __device__ __forceinline__ void cm_split(const float (&v)[8], float s, cm_half8&
   lo = __builtin_bit_cast(cm_half8, l);
 }
 
-__global__ __launch_bounds__(CM_NTH) void cqt_mfma_kernel(CqmArgs a) {
+__global__ __launch_bounds__(CM_NTH, 2) void cqt_mfma_kernel(CqmArgs a) {
   const Span span_(a.span);
   extern __shared__ __attribute__((aligned(16))) char smem[];
   uint4* sB = reinterpret_cast<uint4*>(smem);  // [CM_R][CM_SLICE]
@@ -770,26 +788,56 @@ __global__ __launch_bounds__(CM_NTH) void cqt_mfma_kernel(CqmArgs a) {
     asm volatile("" ::: "memory");
     if (ks + 1 < CM_KS) fetch_slice(ks + 1);
     // A fragments of k-step ks (this wave's own image: written by this wave only, and LDS
-    // operations of one wave complete in order, so no barrier guards them)
-    cm_half8 ah[CM_RT], al[CM_RT];
+    // operations of one wave complete in order, so no barrier guards them), then the B
+    // fragments two column tiles ahead of their MFMAs
     const int kt = 32 * ks + (32 * ks / hop) * pad;
-#pragma unroll
-    for (int rt = 0; rt < CM_RT; ++rt) {
-      ah[rt] = *reinterpret_cast<const cm_half8*>(aimg + abase[rt] + kt);
-      al[rt] = *reinterpret_cast<const cm_half8*>(aimg + img + abase[rt] + kt);
-    }
-    const uint4* sb = sB + (ks % CM_R) * CM_SLICE + lane;
-#pragma unroll
-    for (int nt = 0; nt < CM_NT; ++nt) {
-      const cm_half8 bh = __builtin_bit_cast(cm_half8, sb[(nt * 2) * 64]);
-      const cm_half8 bl = __builtin_bit_cast(cm_half8, sb[(nt * 2 + 1) * 64]);
+    const uint32_t sbl = lds_addr(sB + (ks % CM_R) * CM_SLICE + lane);
+    cm_u4 a0, a1, a2, a3, l0, l1, l2, l3, b[CM_NT][2];
+    static_assert(CM_RT == 4 && CM_NT == 5, "fragment schedule");
+    cm_rd<0>(a0, lds_addr(aimg + abase[0] + kt));
+    cm_rd<0>(a1, lds_addr(aimg + abase[1] + kt));
+    cm_rd<0>(a2, lds_addr(aimg + abase[2] + kt));
+    cm_rd<0>(a3, lds_addr(aimg + abase[3] + kt));
+    cm_rd<0>(l0, lds_addr(aimg + img + abase[0] + kt));
+    cm_rd<0>(l1, lds_addr(aimg + img + abase[1] + kt));
+    cm_rd<0>(l2, lds_addr(aimg + img + abase[2] + kt));
+    cm_rd<0>(l3, lds_addr(aimg + img + abase[3] + kt));
+    cm_rd<0 * 1024>(b[0][0], sbl);
+    cm_rd<1 * 1024>(b[0][1], sbl);
+    cm_rd<2 * 1024>(b[1][0], sbl);
+    cm_rd<3 * 1024>(b[1][1], sbl);
+    cm_rd<4 * 1024>(b[2][0], sbl);
+    cm_rd<5 * 1024>(b[2][1], sbl);
+    cm_wait<4>(a0, a1, a2, a3);  // A + tile 0 landed; tiles 1, 2 in flight
+    cm_wait<4>(l0, l1, l2, l3);
+    const cm_half8 ah[CM_RT] = {__builtin_bit_cast(cm_half8, a0), __builtin_bit_cast(cm_half8, a1),
+                                __builtin_bit_cast(cm_half8, a2), __builtin_bit_cast(cm_half8, a3)};
+    const cm_half8 al[CM_RT] = {__builtin_bit_cast(cm_half8, l0), __builtin_bit_cast(cm_half8, l1),
+                                __builtin_bit_cast(cm_half8, l2), __builtin_bit_cast(cm_half8, l3)};
+    auto tile = [&](int nt) {
+      const cm_half8 bh = __builtin_bit_cast(cm_half8, b[nt][0]);
+      const cm_half8 bl = __builtin_bit_cast(cm_half8, b[nt][1]);
 #pragma unroll
       for (int rt = 0; rt < CM_RT; ++rt) {
         acc[rt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[rt], bh, acc[rt][nt], 0, 0, 0);
         acc[rt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[rt], bl, acc[rt][nt], 0, 0, 0);
         acc[rt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al[rt], bh, acc[rt][nt], 0, 0, 0);
       }
-    }
+    };
+    cm_wait<4>(b[0][0], b[0][1]);
+    tile(0);
+    cm_rd<6 * 1024>(b[3][0], sbl);
+    cm_rd<7 * 1024>(b[3][1], sbl);
+    cm_wait<4>(b[1][0], b[1][1]);
+    tile(1);
+    cm_rd<8 * 1024>(b[4][0], sbl);
+    cm_rd<9 * 1024>(b[4][1], sbl);
+    cm_wait<4>(b[2][0], b[2][1]);
+    tile(2);
+    cm_wait<2>(b[3][0], b[3][1]);
+    tile(3);
+    cm_wait<0>(b[4][0], b[4][1]);
+    tile(4);
   }
   __syncthreads();  // every wave's last ring / image reads done before the rows overlay them
 
@@ -936,28 +984,57 @@ __device__ __forceinline__ void cqt_mfma_low(const CqmArgs& a, int bx, int c) {
     asm volatile("" ::: "memory");
     if (n + 1 < CM_KS) fetch_slice(n + 1);         // into the slot step n - 1 read
     if (q == 0 && g + 1 < G) fetch_block(g + 1);  // into the buffer group g - 1 read
+    // the rows' f32 pieces, then the B fragments two column tiles ahead of their MFMAs
+    // (asm-issued reads, counted waits: cm_rd)
     const float4* b = reinterpret_cast<const float4*>(blk + (g & 1) * L::BLK);
-    cm_half8 ah[CL_RT], al[CL_RT];
+    static_assert(CL_RT == 2 && CM_NT == 5, "fragment schedule");
+    cm_u4 u[CL_RT][2], bq[CM_NT][2];
 #pragma unroll
     for (int rt = 0; rt < CL_RT; ++rt) {
       const int R = 32 * hw + 16 * rt + (lane & 15) + q;
       const int sw = (R >> 1) & 7;
-      const float4 u0 = b[R * 8 + (p0 ^ sw)], u1 = b[R * 8 + ((p0 + 1) ^ sw)];
+      cm_rd<0>(u[rt][0], lds_addr(b + R * 8 + (p0 ^ sw)));
+      cm_rd<0>(u[rt][1], lds_addr(b + R * 8 + ((p0 + 1) ^ sw)));
+    }
+    const uint32_t sbl = lds_addr(sB + (n & 1) * CM_SLICE + lane);
+    cm_rd<0 * 1024>(bq[0][0], sbl);
+    cm_rd<1 * 1024>(bq[0][1], sbl);
+    cm_rd<2 * 1024>(bq[1][0], sbl);
+    cm_rd<3 * 1024>(bq[1][1], sbl);
+    cm_rd<4 * 1024>(bq[2][0], sbl);
+    cm_rd<5 * 1024>(bq[2][1], sbl);
+    cm_wait<6>(u[0][0], u[0][1], u[1][0], u[1][1]);  // the rows landed; tiles 0-2 in flight
+    cm_half8 ah[CL_RT], al[CL_RT];
+#pragma unroll
+    for (int rt = 0; rt < CL_RT; ++rt) {
+      const float4 u0 = __builtin_bit_cast(float4, u[rt][0]), u1 = __builtin_bit_cast(float4, u[rt][1]);
       const float v[8] = {u0.x, u0.y, u0.z, u0.w, u1.x, u1.y, u1.z, u1.w};
       cm_split(v, sx, ah[rt], al[rt]);
     }
-    const uint4* sb = sB + (n & 1) * CM_SLICE + lane;
-#pragma unroll
-    for (int nt = 0; nt < CM_NT; ++nt) {
-      const cm_half8 bh = __builtin_bit_cast(cm_half8, sb[(nt * 2) * 64]);
-      const cm_half8 bl = __builtin_bit_cast(cm_half8, sb[(nt * 2 + 1) * 64]);
+    auto tile = [&](int nt) {
+      const cm_half8 bh = __builtin_bit_cast(cm_half8, bq[nt][0]);
+      const cm_half8 bl = __builtin_bit_cast(cm_half8, bq[nt][1]);
 #pragma unroll
       for (int rt = 0; rt < CL_RT; ++rt) {
         acc[rt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[rt], bh, acc[rt][nt], 0, 0, 0);
         acc[rt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[rt], bl, acc[rt][nt], 0, 0, 0);
         acc[rt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al[rt], bh, acc[rt][nt], 0, 0, 0);
       }
-    }
+    };
+    cm_wait<4>(bq[0][0], bq[0][1]);
+    tile(0);
+    cm_rd<6 * 1024>(bq[3][0], sbl);
+    cm_rd<7 * 1024>(bq[3][1], sbl);
+    cm_wait<4>(bq[1][0], bq[1][1]);
+    tile(1);
+    cm_rd<8 * 1024>(bq[4][0], sbl);
+    cm_rd<9 * 1024>(bq[4][1], sbl);
+    cm_wait<4>(bq[2][0], bq[2][1]);
+    tile(2);
+    cm_wait<2>(bq[3][0], bq[3][1]);
+    tile(3);
+    cm_wait<0>(bq[4][0], bq[4][1]);
+    tile(4);
   }
   __syncthreads();  // the rows overlay the ring and blocks
   if (!active) return;
