@@ -73,6 +73,32 @@ def test_chroma_mean_and_tuning_match_oracle(gpu_ctx, seed):
         np.testing.assert_allclose(got[i], ref_c, rtol=0, atol=2e-5)
 
 
+def dense_peak_chunk(n=441000, seed=7):
+    """32 tones a semitone apart between 600 and 3 900 Hz, all 0.3 of a 36-per-octave bin
+    off the A440 grid, in white noise: 58-91 piptrack peaks per frame (median 80), so the
+    peak compaction of nc_piptrack.h takes more than one 64-peak pass on nearly every frame,
+    while the common detuning keeps the tuning decision far from a tie (oracle margin 166)."""
+    rng = np.random.default_rng(seed)
+    t = np.arange(n) / 22050
+    y = np.zeros(n)
+    for m in range(0, 400, 3):
+        f = 27.5 * 2 ** ((m + 0.3) / 36)
+        if 600 <= f <= 3900:
+            y += 0.03 * np.sin(2 * np.pi * f * t + rng.uniform(0, 6.28))
+    return (y + rng.normal(0, 0.08, n)).astype(np.float32)
+
+
+def test_tuning_with_more_than_64_peaks_per_frame(gpu_ctx):
+    y = dense_peak_chunk()
+    p, _ = ncref.piptrack(y)
+    assert np.median((p > 0).sum(axis=0)) > 64
+    got, tun, _, tidx = _chroma_gpu(gpu_ctx, y, [(0, len(y))])
+    ref_t = _check_tuning(0, y, tidx, _chroma_gpu.margin)
+    assert tun[0] == np.float32(ref_t), (tun[0], ref_t)
+    ref_c = ncref.chroma_cqt(y, 22050, 512, 36, tuning=ref_t).mean(axis=1)
+    np.testing.assert_allclose(got[0], ref_c, rtol=0, atol=2e-5)
+
+
 @pytest.mark.parametrize("scale", [3e-7, 1e-3, 40.0, 3e4])
 def test_chroma_f16_split_scaling_across_amplitudes(gpu_ctx, scale):
     """Octaves 3-6 run on the f16 matrix cores with hi/lo split operands at a per-chunk

@@ -44,6 +44,20 @@ def test_shared_tuning_frames_are_bit_identical(eng):
         assert str(x.result) == str(y.result)
 
 
+def test_shared_tuning_bit_identical_with_dense_peaks(eng):
+    """Frames with more than 64 piptrack peaks (two compaction passes) through the window
+    STFT's piptrack and through tuning_peaks_kernel."""
+    import scipy.signal
+    from test_gpu_chroma import dense_peak_chunk
+    src = dense_peak_chunk(45 * 22050, 11)
+    nc = scipy.signal.resample_poly(src, 4, 5).astype(np.float32)
+    a = _run(eng, [(nc, src)], False)[0]
+    b = _run(eng, [(nc, src)], True)[0]
+    assert repr(a.error) == repr(b.error)
+    assert np.array_equal(a.detail["tuning"], b.detail["tuning"])
+    assert np.array_equal(a.detail["chroma"], b.detail["chroma"])
+
+
 def test_shared_tuning_with_trim_and_offsets(eng):
     """Windows and chunks start at the trimmed file start (silence strip, src_trim_sec)."""
     nc, src = synth.make_pair(70.0, 1002)
