@@ -37,9 +37,10 @@ def report(d: Path) -> None:
                 parts.append(f"valu/disp {v['SQ_INSTS_VALU'] / nd:.3g} lds/disp {v['SQ_INSTS_LDS'] / nd:.3g}")
             if v.get("SQ_VALU_MFMA_BUSY_CYCLES", 0.0) > 0 and v.get("GRBM_GUI_ACTIVE", 0.0) > 0:
                 # MFMA pipe busy cycles summed over the chip's 1024 SIMDs, against the dispatches'
-                # GPU-active cycles (MI355X_MICROARCH.md: 16 per 16x16x32 f16 MFMA)
+                # GPU-active cycles (MI355X_MICROARCH.md: 16 per 16x16x32 f16 MFMA).  GRBM_GUI_ACTIVE
+                # comes summed over the 8 XCDs (3 x 0.49 ms of stft_mel read 2.63e7 cycles), hence / 8
                 nd = n[(k, "SQ_VALU_MFMA_BUSY_CYCLES")]
-                parts.append(f"mfma busy {100 * v['SQ_VALU_MFMA_BUSY_CYCLES'] / (1024 * v['GRBM_GUI_ACTIVE']):4.1f}% "
+                parts.append(f"mfma busy {100 * v['SQ_VALU_MFMA_BUSY_CYCLES'] / (1024 * v['GRBM_GUI_ACTIVE'] / 8):4.1f}% "
                              f"mfma/disp {v.get('SQ_INSTS_MFMA', 0.0) / nd:.4g}")
             for c in ("FETCH_SIZE", "WRITE_SIZE"):
                 if c in v and v[c] > 1e4:

@@ -123,7 +123,9 @@ def inputs(src):
                 sig=torch.from_numpy(wins.reshape(-1)).to(dev),
                 off=torch.arange(n, dtype=torch.int64, device=dev) * L,
                 csig=torch.from_numpy(chunks.reshape(-1)).to(dev),
-                coff=torch.arange(cn, dtype=torch.int64, device=dev) * CL,
+                # VB_SAMECHUNK=1: every chunk at offset 0 (their level-0 reads become L2 / MALL hits;
+                # a probe of the low-octave CQT's exposed block latency)
+                coff=torch.arange(cn, dtype=torch.int64, device=dev) * CL * (os.environ.get("VB_SAMECHUNK") != "1"),
                 clen=torch.full((cn,), CL, dtype=torch.int64, device=dev))
 
 
