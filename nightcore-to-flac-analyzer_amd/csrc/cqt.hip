@@ -365,7 +365,7 @@ __global__ __launch_bounds__(TP_WAVES * 64) void tuning_peaks_kernel(PeakArgs a)
     // 2/3 of the bins need no square root at all
     float* S = reinterpret_cast<float*>(fftbuf);  // (all Z reads precede)
     float pmax = 0.0f;
-    rsplit_mirror<TpTw::split>(v, sh_tw, lane, [&](int k, float2 X, float2 XN) {
+    rsplit_mirror<TpTw::split, false>(v, sh_tw, lane, [&](int k, float2 X, float2 XN) {
       const float p1 = fmaf(X.x, X.x, X.y * X.y), p2 = fmaf(XN.x, XN.x, XN.y * XN.y);
       if (k >= kPipLo - 1 && k <= kPipHi + 1) S[k] = p1;
       if (1024 - k <= kPipHi + 1) S[1024 - k] = p2;

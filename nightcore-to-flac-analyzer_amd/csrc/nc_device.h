@@ -531,14 +531,17 @@ __device__ __forceinline__ void fft1024_last_mirror(const float2* lds, const flo
 // mirror-paired outputs: f(k, X[k], X[1024 - k]) for the lane's 8 pairs (9 on lane 0),
 // k <= 512, together covering X[0..1024] once (X[512] twice on lane 0).  SPLIT = offset of
 // W_2048^k in tw.
-template <int SPLIT, class F>
+// HALF = false: the outputs are 2 X[k] exactly (the two 0.5 scalings left out: a power-of-two
+// scale commutes with every rounding of the split, so |2X|^2 = 4 |X|^2 bit for bit); callers
+// that only compare or project |X|^2 fold the factor into their constants.
+template <int SPLIT, bool HALF = true, class F>
 __device__ __forceinline__ void rsplit_mirror(const float2 (&v)[4][4], const float2* tw, int l, F&& f) {
   const bool l0 = l == 0;
   const int J1 = l0 ? 64 : 128 - l, J2 = l0 ? 192 : 128 + l, J3 = l0 ? 128 : 256 - l;
   auto pair = [&](float2 za, float2 zm, int k) {
     const float2 b = cconj(zm);
-    const float2 E = cscale(cadd(za, b), 0.5f);
-    const float2 O = cmul_mi(cscale(csub(za, b), 0.5f));  // (a-b)/(2i)
+    const float2 E = HALF ? cscale(cadd(za, b), 0.5f) : cadd(za, b);
+    const float2 O = cmul_mi(HALF ? cscale(csub(za, b), 0.5f) : csub(za, b));  // (a-b)/(2i), or 2x
     const float2 WO = cmul(tw[SPLIT + k], O);
     f(k, cadd(E, WO), cconj(csub(E, WO)));
   };

@@ -225,7 +225,7 @@ void build_tables(Context& ctx) {
           const int k = lo4[sl * 64 + l] + j;
           const float wv = (k >= lo[b] && k < lo[b] + len[b]) ? wts[offs[b] + k - lo[b]] : 0.0f;
           float* q = reinterpret_cast<float*>(&w4[(size_t)((sl ? jmax[0] : 0) + j / 4) * 64 + l]);
-          q[j % 4] = wv;
+          q[j % 4] = 0.25f * wv;  // stft_mel's power is |2X|^2 (rsplit_mirror<.., false>): exact
         }
       }
     t.mel_w4 = upload(w4);

@@ -196,7 +196,7 @@ __global__ __launch_bounds__(SM_THREADS) void stft_mel_kernel(StftMelArgs a) {
     // split's registers, |X| of the stencil bins beside the power (which the mel step needs)
     if (wc >= 0 && t < a.tp_frames) {
       float pmax = 0.0f;
-      rsplit_mirror<SmTw::split>(v, twl, lane, [&](int k, float2 X, float2 XN) {
+      rsplit_mirror<SmTw::split, false>(v, twl, lane, [&](int k, float2 X, float2 XN) {
         const float p1 = fmaf(X.x, X.x, X.y * X.y), p2 = fmaf(XN.x, XN.x, XN.y * XN.y);
         pw[k] = p1;
         pw[1024 - k] = p2;
@@ -213,7 +213,7 @@ __global__ __launch_bounds__(SM_THREADS) void stft_mel_kernel(StftMelArgs a) {
       piptrack_append([&](int k) { return mg[k - (kPipLo - 1)]; }, mx, lane, &a.chunk_npk[wc], a.peak_pitch + base,
                       a.peak_mag + base, reinterpret_cast<int*>(pw + kPipKpk));
     } else {
-      rsplit_mirror<SmTw::split>(v, twl, lane, [&](int k, float2 X, float2 XN) {
+      rsplit_mirror<SmTw::split, false>(v, twl, lane, [&](int k, float2 X, float2 XN) {
         pw[k] = fmaf(X.x, X.x, X.y * X.y);
         pw[1024 - k] = fmaf(XN.x, XN.x, XN.y * XN.y);
       });
