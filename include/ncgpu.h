@@ -156,7 +156,8 @@ int nc_chroma_mean(nc_ctx* ctx, const float* sig, const int64_t* chunk_off, cons
  * (pitch.py:58 -> librosa.estimate_tuning) on those frames: win_chunk[w] = the chunk
  * window w starts (or -1), chunk_tf_base[c] = sum_{q<c} (1 + chunk_len[q] / 512) (the
  * chunk's slot base in the peak lists, in units of 192 slots), peak_pitch / peak_mag =
- * chunk_tf_base[n] * 192 floats each, chunk_npk[n] zeroed by the caller.  If
+ * chunk_tf_base[n] * 192 floats each (peak_mag holds 2x piptrack's magnitude, exactly:
+ * only its median and comparisons are consumed), chunk_npk[n] zeroed by the caller.  If
  * stft_done_event (a hipEvent_t) is given it is recorded once the peaks are written.
  * nc_chroma_mean_shared = nc_chroma_mean on the same peak lists: tuning frames
  * t < tf_skip[c] are not recomputed (tf_skip_total = sum of tf_skip, host value), the
