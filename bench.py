@@ -182,7 +182,8 @@ def main():
     win_mode = world > 1 and args.shard != "pairs"
     P = args.pairs
     own_ids = list(range(rank * P, (rank + 1) * P))
-    ids = sorted(set(own_ids) | ({rank * P - 1, (rank + 1) * P} & set(range(world * P)) if win_mode else set()))
+    # (both modes: the side variants timed beside the headline include the split-boundary one)
+    ids = sorted(set(own_ids) | ({rank * P - 1, (rank + 1) * P} & set(range(world * P)) if world > 1 else set()))
     pairs = dict(zip(ids, make_pairs_ids(ids, args.seconds, 1000, max(1, args.workers // max(1, world)))))
     # NC_BENCH_REHEARSE=1: rehearse the N > 1 path on fewer GPUs than ranks (ranks share devices
     # round-robin; gloo instead of RCCL, which refuses two ranks on one device).  Never used for

@@ -51,6 +51,7 @@ consensus placement are tested without a GPU.  Every result equals the single-ra
 """
 from __future__ import annotations
 
+import gc
 import math
 from dataclasses import dataclass
 from typing import List, Optional, Sequence, Tuple
@@ -598,7 +599,19 @@ def analyze_sharded(stages, p: Optional[Params] = None, group=None, *, lengths: 
     ``gather`` every rank returns all outcomes in pair order; without, this rank's owned
     pairs as [(pair index, outcome)].  ``steps`` > 1 analyses the batch that many times
     back to back, the interior groups pipelined across steps as Engine.analyze_batches
-    does (the benchmark's timed region), and returns one such list per step."""
+    does (the benchmark's timed region), and returns one such list per step.  Python's cyclic
+    collector is paused for the call, as in Engine.analyze (a generation-2 pass, ~10 ms, would
+    otherwise stall the host loop that keeps the device queues full)."""
+    gc_was_enabled = gc.isenabled()
+    gc.disable()
+    try:
+        return _analyze_sharded(stages, p, group, lengths, local_pairs, split_offset, gather, steps)
+    finally:
+        if gc_was_enabled:
+            gc.enable()
+
+
+def _analyze_sharded(stages, p, group, lengths, local_pairs, split_offset, gather, steps):
     p = p or Params()
     ex = Exchange(group)
     r, world = ex.rank, ex.world
