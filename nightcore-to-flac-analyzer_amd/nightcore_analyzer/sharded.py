@@ -105,16 +105,21 @@ class ShardPlan:
     def on_rank(self, b: int, r: int) -> bool:
         return bool(np.any(self.rng[b, :, r, 1] > self.rng[b, :, r, 0]))
 
+    def _present(self) -> np.ndarray:
+        """[B, world] bool: pair b has items on rank r."""
+        return np.any(self.rng[:, :, :, 1] > self.rng[:, :, :, 0], axis=1)
+
     def touched(self, r: int) -> List[int]:
-        return [b for b in range(self.B) if self.owner[b] == r or self.on_rank(b, r)]
+        return np.flatnonzero((self.owner == r) | self._present()[:, r]).tolist()
 
     def needed(self, r: int, ibi: bool) -> List[int]:
         """Pairs rank r must hold: the ones it touches, and with the hop-64 IBI pass every
         split pair (the pass of a split pair's files is split over all ranks, C2-C4)."""
-        return [b for b in range(self.B) if self.owner[b] == r or self.on_rank(b, r) or (ibi and self.split[b])]
+        m = (self.owner == r) | self._present()[:, r]
+        return np.flatnonzero(m | (self.split if ibi else False)).tolist()
 
     def owned(self, r: int) -> List[int]:
-        return [b for b in range(self.B) if self.owner[b] == r]
+        return np.flatnonzero(self.owner == r).tolist()
 
     def window_row(self, b: int, side: int, k: int) -> int:
         return int(self.wrow[b] + (k if side == 0 else self.slots[b, 0] + k))
@@ -145,11 +150,14 @@ def shard_plan(lengths: Sequence[int], p: Params, world: int, split_offset: floa
     B = len(L) // 2
     win_n, hop_n = int(p.window_sec * SR), int(p.hop_sec * SR)
     cn = int(CHUNK_SEC * SR)
-    slots = np.zeros((B, 3), np.int64)
-    for b in range(B):
-        ln, ls = int(L[2 * b]), int(L[2 * b + 1])
-        slots[b] = (n_window_slots(ls, win_n, hop_n), n_window_slots(ln, win_n, hop_n),
-                    max(1, min(ls // cn, ln // cn)) if p.compute_pitch else 0)
+    ln, ls = L[0::2], L[1::2]
+
+    def n_slots(x):  # n_window_slots, vectorised
+        return np.where((x >= win_n) & (hop_n > 0), (x - win_n) // max(hop_n, 1) + 1, 0)
+
+    slots = np.stack([n_slots(ls), n_slots(ln),
+                      np.maximum(1, np.minimum(ls // cn, ln // cn)) if p.compute_pitch else np.zeros(B, np.int64)],
+                     axis=1).astype(np.int64).reshape(B, 3)
     cost = slots[:, 0] + slots[:, 1] + CP_COST * slots[:, 2]
     base = np.concatenate([[0], np.cumsum(cost)]).astype(np.int64)
     T = int(base[-1])
@@ -160,30 +168,25 @@ def shard_plan(lengths: Sequence[int], p: Params, world: int, split_offset: floa
     bounds = np.maximum.accumulate(bounds)
     bounds[world] = np.iinfo(np.int64).max // 4          # every unit < T lies in some block
 
-    def rank_of(u: int) -> int:
-        return int(min(world - 1, max(0, np.searchsorted(bounds, u, side="right") - 1)))
-
-    rng = np.zeros((B, 3, world, 2), np.int64)
-    for b in range(B):
-        u0 = (base[b], base[b] + slots[b, 0], base[b] + slots[b, 0] + slots[b, 1])
-        for s, stride in ((0, 1), (1, 1), (2, CP_COST)):
-            n = int(slots[b, s])
-            for r in range(world):
-                lo = -(-(int(bounds[r]) - int(u0[s])) // stride)
-                hi = -(-(int(bounds[r + 1]) - int(u0[s])) // stride)
-                rng[b, s, r] = (min(n, max(0, lo)), min(n, max(0, hi)))
-    owner = np.array([rank_of(min(int(base[b]), max(T - 1, 0))) for b in range(B)], np.int64)
-    split = np.zeros(B, bool)
-    for b in range(B):
-        split[b] = any(rng[b, s, r, 1] > rng[b, s, r, 0] for s in range(3) for r in range(world) if r != owner[b])
+    # segment s of pair b starts at unit u0[b, s] and spends `stride` units per slot; rank r
+    # holds the slots whose first unit lies in [bounds[r], bounds[r + 1])
+    u0 = np.stack([base[:-1], base[:-1] + slots[:, 0], base[:-1] + slots[:, 0] + slots[:, 1]], axis=1)
+    stride = np.array([1, 1, CP_COST], np.int64)
+    edge = -(-(bounds[None, None, :] - u0[:, :, None]) // stride[None, :, None])    # [B, 3, world + 1]
+    edge = np.minimum(slots[:, :, None], np.maximum(0, edge))
+    rng = np.stack([edge[:, :, :-1], edge[:, :, 1:]], axis=3)                         # [B, 3, world, 2]
+    first = np.minimum(base[:-1], max(T - 1, 0))
+    owner = np.clip(np.searchsorted(bounds, first, side="right") - 1, 0, world - 1).astype(np.int64)
+    present = rng[:, :, :, 1] > rng[:, :, :, 0]                                       # [B, 3, world]
+    others = np.ones((B, world), bool)
+    others[np.arange(B), owner] = False
+    split = np.any(present & others[:, None, :], axis=(1, 2))
     wrow = np.full(B, -1, np.int64)
     crow = np.full(B, -1, np.int64)
-    nw = nc_ = 0
-    for b in np.flatnonzero(split):
-        wrow[b], crow[b] = nw, nc_
-        nw += int(slots[b, 0] + slots[b, 1])
-        nc_ += int(slots[b, 2])
-    return ShardPlan(world, B, slots, rng, owner, split, wrow, crow, nw, nc_)
+    sw = slots[split, 0] + slots[split, 1]
+    wrow[split] = np.concatenate([[0], np.cumsum(sw)[:-1]]) if sw.size else sw
+    crow[split] = np.concatenate([[0], np.cumsum(slots[split, 2])[:-1]]) if sw.size else sw
+    return ShardPlan(world, B, slots, rng, owner, split, wrow, crow, int(sw.sum()), int(slots[split, 2].sum()))
 
 
 # ------------------------------------------------------------------------------ exchange
