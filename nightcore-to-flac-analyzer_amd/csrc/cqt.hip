@@ -360,9 +360,10 @@ __global__ __launch_bounds__(TP_WAVES * 64) void tuning_peaks_kernel(PeakArgs a)
     stockham_stage<1024, 16, 16, 64, false, 0, 0>(fftbuf, sh_tw, lane);
     float2 v[4][4];
     fft1024_last_mirror<TpTw::s3>(fftbuf, sh_tw, lane, v);
-    // |X|^2 into LDS only where the peak stencil reads it (bins kPipLo-1 .. kPipHi+1); the frame
-    // max of |X| is sqrt(max |X|^2) (the correctly rounded sqrt is monotonic), so the other
-    // 2/3 of the bins need no square root at all
+    // |2X|^2 (the split without its 0.5 scalings: piptrack's decisions are scale-free, and its
+    // magnitudes come out as exactly 2|X|, as in stft_mel's shared frames) into LDS only where
+    // the peak stencil reads it (bins kPipLo-1 .. kPipHi+1); the frame max is sqrt(max |2X|^2)
+    // (the correctly rounded sqrt is monotonic), so the other 2/3 of the bins need no square root
     float* S = reinterpret_cast<float*>(fftbuf);  // (all Z reads precede)
     float pmax = 0.0f;
     rsplit_mirror<TpTw::split, false>(v, sh_tw, lane, [&](int k, float2 X, float2 XN) {

@@ -189,11 +189,14 @@ __global__ __launch_bounds__(SM_THREADS) void stft_mel_kernel(StftMelArgs a) {
     stockham_stage<1024, 16, 16, 64, false, 0, 0>(fftbuf, twl, lane);
     float2 v[4][4];
     fft1024_last_mirror<SmTw::s3, true>(fftbuf, twl, lane, v);
-    float* pw = reinterpret_cast<float*>(fftbuf);  // power P[k], k in [0, 1024] (all Z reads precede)
+    // power |2 X[k]|^2 = 4 P[k], k in [0, 1024] (the split without its 0.5 scalings, exact; the mel
+    // weights carry the 0.25), over the FFT slot (all Z reads precede)
+    float* pw = reinterpret_cast<float*>(fftbuf);
     // a leading frame of a window that starts a 20 s chunk is also that chunk's tuning frame
     // t (same samples, padding and FFT): estimate_tuning's piptrack runs here, on the same
-    // |X| values tuning_peaks_kernel computes (nc_piptrack.h): the frame max of |X| from the
-    // split's registers, |X| of the stencil bins beside the power (which the mel step needs)
+    // 2|X| values tuning_peaks_kernel computes (nc_piptrack.h; its decisions are scale-free): the
+    // frame max from the split's registers, the stencil bins' 2|X| beside the power (which the
+    // mel step needs)
     if (wc >= 0 && t < a.tp_frames) {
       float pmax = 0.0f;
       rsplit_mirror<SmTw::split, false>(v, twl, lane, [&](int k, float2 X, float2 XN) {
