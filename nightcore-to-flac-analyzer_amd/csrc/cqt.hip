@@ -368,8 +368,9 @@ __global__ __launch_bounds__(TP_WAVES * 64) void tuning_peaks_kernel(PeakArgs a)
     float pmax = 0.0f;
     rsplit_mirror<TpTw::split, false>(v, sh_tw, lane, [&](int k, float2 X, float2 XN) {
       const float p1 = fmaf(X.x, X.x, X.y * X.y), p2 = fmaf(XN.x, XN.x, XN.y * XN.y);
-      if (k >= kPipLo - 1 && k <= kPipHi + 1) S[k] = p1;
-      if (1024 - k <= kPipHi + 1) S[1024 - k] = p2;
+      // k <= 512 covers the stencil's bins (<= kPipHi + 1) and 1024 - k >= 512 never does:
+      // the low half is stored unconditionally (no exec-masked branch per pair)
+      S[k] = p1;
       pmax = fmaxf(pmax, fmaxf(p1, p2));
     });
     const float mx = __fsqrt_rn(wave_max_u(pmax));

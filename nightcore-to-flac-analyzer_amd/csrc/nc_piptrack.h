@@ -17,6 +17,7 @@ constexpr int kPipRounds = (kPipHi - kPipLo + 64) / 64;
 constexpr int kPipMag = 1088, kPipKpk = 1472;
 static_assert(kPipMag >= 1025 && kPipMag + (kPipHi - kPipLo + 3) <= kPipKpk, "piptrack slot layout");
 static_assert(kPipKpk + (kPipHi - kPipLo + 1) <= 2112, "piptrack slot layout");
+static_assert(kPipHi + 1 < 512, "tuning_peaks stores only the split's low half (bins <= 512)");
 
 // One wave, one frame.  mag(k) = |X[k]| (k in [kPipLo - 1, kPipHi + 1]), mx = max_k |X[k]|
 // over all 1025 bins.  Peaks are appended to the chunk's list at an atomically reserved
