@@ -378,7 +378,7 @@ __global__ __launch_bounds__(TP_WAVES * 64) void tuning_peaks_kernel(PeakArgs a)
 #pragma unroll
     for (int q = 0; q < (kPipHi - kPipLo + 3 + 63) / 64; ++q) {
       const int k = kPipLo - 1 + 64 * q + lane;
-      if (k <= kPipHi + 1) S[k] = __fsqrt_rn(S[k]);
+      if (64 * (q + 1) <= kPipHi - kPipLo + 3 || k <= kPipHi + 1) S[k] = __fsqrt_rn(S[k]);  // test the last round only
     }
     piptrack_append([&](int k) { return S[k]; }, mx, lane, &a.chunk_npk[c], a.peak_pitch + ctf * kPeakSlots,
                     a.peak_mag + ctf * kPeakSlots, reinterpret_cast<int*>(S + kPipKpk));

@@ -37,7 +37,7 @@ __device__ __forceinline__ void piptrack_append(Mag&& mag, float mx, int lane, i
   for (int q = 0; q < kPipRounds; ++q) {
     const int k = kPipLo + 64 * q + lane;
     bool pk = false;
-    if (k <= kPipHi) {
+    if (64 * (q + 1) <= kPipHi - kPipLo + 1 || k <= kPipHi) {  // only the last round is partial
       const float sm = mag(k - 1), s = mag(k), sp = mag(k + 1);
       const float zm = sm > ref ? sm : 0.0f, z = s > ref ? s : 0.0f, zp = sp > ref ? sp : 0.0f;
       pk = (z > zm) && (z >= zp);

@@ -217,7 +217,8 @@ __global__ __launch_bounds__(SM_THREADS) void stft_mel_kernel(StftMelArgs a) {
 #pragma unroll
       for (int q = 0; q < (kPipHi - kPipLo + 3 + 63) / 64; ++q) {
         const int k = kPipLo - 1 + 64 * q + lane;
-        if (k <= kPipHi + 1) mg[k - (kPipLo - 1)] = __fsqrt_rn(pw[k]);
+        if (64 * (q + 1) <= kPipHi - kPipLo + 3 || k <= kPipHi + 1)  // test the last round only
+          mg[k - (kPipLo - 1)] = __fsqrt_rn(pw[k]);
       }
       const int64_t base = uniform64(a.chunk_tf_base[wc]) * kPeakSlots;
       piptrack_append([&](int k) { return mg[k - (kPipLo - 1)]; }, mx, lane, &a.chunk_npk[wc], a.peak_pitch + base,
