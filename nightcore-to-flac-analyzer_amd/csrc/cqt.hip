@@ -211,6 +211,8 @@ __global__ __launch_bounds__(256) void decimate3_kernel(const float* sig, const 
       if (u < D3_P0 / 2) {
         if (vec && i >= 0 && i + 3 < L0) {
           v = *reinterpret_cast<const float4*>(in + i);
+        } else if (i >= 0 && i + 3 < L0) {  // in bounds, not 16-byte aligned: four dwords, no tests
+          v = make_float4(in[i], in[i + 1], in[i + 2], in[i + 3]);
         } else {
           v.x = (i >= 0 && i < L0) ? in[i] : 0.f;
           v.y = (i + 1 >= 0 && i + 1 < L0) ? in[i + 1] : 0.f;
@@ -336,11 +338,18 @@ __global__ __launch_bounds__(TP_WAVES * 64) void tuning_peaks_kernel(PeakArgs a)
     const int64_t L = clen;
     const int64_t s0 = (int64_t)t * 512 - 1024;
     FftIn<1024> in;
-    if (s0 >= 0 && s0 + 2048 <= L && ((off & 1) == 0)) {
-      const float2* x2 = reinterpret_cast<const float2*>(x + s0);
+    if (s0 >= 0 && s0 + 2048 <= L) {
       float2 xv[16], hw[16];
+      if ((off & 1) == 0) {
+        const float2* x2 = reinterpret_cast<const float2*>(x + s0);
 #pragma unroll
-      for (int r = 0; r < 16; ++r) xv[r] = x2[jin + 64 * r];  // issued first: the LDS batch hides under them
+        for (int r = 0; r < 16; ++r) xv[r] = x2[jin + 64 * r];  // issued first: the LDS batch hides under them
+      } else {
+        // a chunk at an odd sample: two dword loads per pair, no bounds tests (stft_mel)
+        const float* xs = x + s0;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) xv[r] = make_float2(xs[2 * (jin + 64 * r)], xs[2 * (jin + 64 * r) + 1]);
+      }
       lds_read16_strided<0, 64 * 8>(hw, lds_addr(sh_hann + jin));
 #pragma unroll
       for (int r = 0; r < 16; ++r) in[0][r] = make_float2(xv[r].x * hw[r].x, xv[r].y * hw[r].y);
@@ -911,7 +920,10 @@ constexpr int CL_GQ = (CM_NT * 2 + CL_NW - 1) / CL_NW;  // filter DMA pieces per
 __device__ __forceinline__ int cl_sw(int R) { return ((R >> 2) & 1) | (((R >> 1) & 1) << 2); }
 size_t cql_lds_bytes() { return CM_BBYTES + CL_TPW * 2 * CmLow<2>::BLK * 4; }  // octave 2 has the largest block
 
-template <int OCT>
+// VEC: the tile takes the DMA path (in bounds and 16-byte aligned).  The kernel calls both
+// instances; each wave runs the one that matches its tile (both issue the same barriers), so
+// the aligned path keeps its own register allocation and schedule.
+template <int OCT, bool VEC>
 __device__ __forceinline__ void cqt_mfma_low(const CqmArgs& a, int bx, int c) {
   using L = CmLow<OCT>;
   constexpr int H = L::H, G = L::G, M = L::M, NI = L::NI, QB = L::QB;
@@ -940,7 +952,6 @@ __device__ __forceinline__ void cqt_mfma_low(const CqmArgs& a, int bx, int c) {
       cm_dma16(bsrc + kstep(n) * CM_SLICE + i * 64 + lane, sB + (n & 1) * CM_SLICE + i * 64);
     }
   };
-  fetch_slice(0);
 
   const float* y = (OCT == 0 ? a.sig : a.ws_oct) + yoff;
   const float sx = ldexpf(1.0f, ex);
@@ -948,10 +959,20 @@ __device__ __forceinline__ void cqt_mfma_low(const CqmArgs& a, int bx, int c) {
   // tile-uniform: both waves of a tile take the same path (their vmcnt bookkeeping agrees)
   const bool vec = s0 >= 0 && s0 + (int64_t)(CM_FR - 1) * H + kCqtNfft <= Ly &&
                    (reinterpret_cast<uintptr_t>(y) & 15) == 0;
+  if (vec != VEC) return;
+  fetch_slice(0);
   // block g: row R (< NR) holds samples s0 + R H + 32 g + [0, 32), piece p at slot p ^ cl_sw(R);
   // the tile's two waves each move half of the NI 8-row DMA groups (QB each, one repeated if odd)
   const int dr = lane >> 3;
-  auto fetch_block = [&](int g) {
+  // Without the DMA (a chunk at a sample that is not 16-byte aligned -- a trimmed file starts
+  // anywhere -- or a tile at the signal's edge) a block's pieces are loaded into registers at
+  // its group's first step and stored to LDS at the second, so the load latency hides under a
+  // k-step as the DMA's does (round 3: the load-then-store form stalled every group, +33 % on
+  // unaligned chunks); inside the signal the loads need no bounds tests.
+  const bool inner = s0 >= 0 && s0 + (int64_t)(CM_FR - 1) * H + kCqtNfft <= Ly;
+  static_assert(L::M >= 2, "a staged block is stored at its group's second step");
+  float4 stg[QB];
+  auto fetch_block = [&](int g) {  // VEC: DMA straight into the buffer; otherwise into stg
     float* b = blk + (g & 1) * L::BLK;
 #pragma unroll
     for (int k = 0; k < QB; ++k) {
@@ -959,9 +980,12 @@ __device__ __forceinline__ void cqt_mfma_low(const CqmArgs& a, int bx, int c) {
       if (i >= NI) i = hw;
       const int R = 8 * i + dr;
       const int p = (lane & 7) ^ cl_sw(R);
-      if (vec) {
-        const int Rc = min(R, L::NR - 1);  // rows past NR: a valid address, never read
+      const int Rc = min(R, L::NR - 1);  // rows past NR: a valid address, never read
+      if (VEC) {
         cm_dma16(y + s0 + (int64_t)Rc * H + 32 * g + 4 * p, b + i * 256);
+      } else if (inner) {
+        const float* q = y + s0 + (int64_t)Rc * H + 32 * g + 4 * p;
+        stg[k] = make_float4(q[0], q[1], q[2], q[3]);
       } else {
         const int64_t q = s0 + (int64_t)R * H + 32 * g + 4 * p;
         float4 v;
@@ -969,11 +993,21 @@ __device__ __forceinline__ void cqt_mfma_low(const CqmArgs& a, int bx, int c) {
         v.y = (q + 1 >= 0 && q + 1 < Ly) ? y[q + 1] : 0.0f;
         v.z = (q + 2 >= 0 && q + 2 < Ly) ? y[q + 2] : 0.0f;
         v.w = (q + 3 >= 0 && q + 3 < Ly) ? y[q + 3] : 0.0f;
-        reinterpret_cast<float4*>(b)[i * 64 + lane] = v;
+        stg[k] = v;
       }
     }
   };
+  auto store_block = [&](int g) {  // the staged pieces of block g into its buffer
+    float4* b = reinterpret_cast<float4*>(blk + (g & 1) * L::BLK);
+#pragma unroll
+    for (int k = 0; k < QB; ++k) {
+      int i = hw + 2 * k;
+      if (i >= NI) i = hw;
+      b[i * 64 + lane] = stg[k];
+    }
+  };
   fetch_block(0);
+  if (!VEC) store_block(0);
 
   cm_f4 acc[CL_RT][CM_NT];
 #pragma unroll
@@ -994,7 +1028,8 @@ __device__ __forceinline__ void cqt_mfma_low(const CqmArgs& a, int bx, int c) {
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
     if (n + 1 < CM_KS) fetch_slice(n + 1);         // into the slot step n - 1 read
-    if (q == 0 && g + 1 < G) fetch_block(g + 1);  // into the buffer group g - 1 read
+    if (q == 0 && g + 1 < G) fetch_block(g + 1);  // into the buffer group g - 1 read (or stg)
+    if (!VEC && q == 1 && g + 1 < G) store_block(g + 1);  // staged at q == 0, landed at this step's top
     // the rows' f32 pieces, then the B fragments two column tiles ahead of their MFMAs
     // (asm-issued reads, counted waits: cm_rd)
     const float4* b = reinterpret_cast<const float4*>(blk + (g & 1) * L::BLK);
@@ -1086,9 +1121,16 @@ __device__ __forceinline__ void cqt_mfma_low(const CqmArgs& a, int bx, int c) {
 // The XCD-contiguous order of cqt_mfma_kernel measured slower here (429 against 398 us per 224
 // chunks, FETCH_SIZE 348 against 361 MiB per 112 chunks, round 3): grid order stays.
 __global__ __launch_bounds__(CL_NW * 64) void cqt_mfma_low_kernel(CqmArgs a) {
-  if (blockIdx.z == 0) cqt_mfma_low<0>(a, blockIdx.x, blockIdx.y);
-  else if (blockIdx.z == 1) cqt_mfma_low<1>(a, blockIdx.x, blockIdx.y);
-  else cqt_mfma_low<2>(a, blockIdx.x, blockIdx.y);
+  if (blockIdx.z == 0) {
+    cqt_mfma_low<0, true>(a, blockIdx.x, blockIdx.y);
+    cqt_mfma_low<0, false>(a, blockIdx.x, blockIdx.y);
+  } else if (blockIdx.z == 1) {
+    cqt_mfma_low<1, true>(a, blockIdx.x, blockIdx.y);
+    cqt_mfma_low<1, false>(a, blockIdx.x, blockIdx.y);
+  } else {
+    cqt_mfma_low<2, true>(a, blockIdx.x, blockIdx.y);
+    cqt_mfma_low<2, false>(a, blockIdx.x, blockIdx.y);
+  }
 }
 
 // Per (chunk, 64-frame tile): chroma = the 7 octave partial rows summed (ascending bins),

@@ -148,12 +148,21 @@ __global__ __launch_bounds__(SM_THREADS) void stft_mel_kernel(StftMelArgs a) {
     const float* hann = a.hann2048;
     FftIn<1024> in;
     double e = 0.0;
-    const bool interior = s0 >= 0 && s0 + 2048 <= L && ((off & 1) == 0);
+    const bool interior = s0 >= 0 && s0 + 2048 <= L;
     if (interior) {
-      const float2* x2 = reinterpret_cast<const float2*>(x + s0);
       float2 xv[16], hw[16];  // samples and window pairs (h[2n], h[2n + 1]), n = lane + 64 r
+      if ((off & 1) == 0) {
+        const float2* x2 = reinterpret_cast<const float2*>(x + s0);
 #pragma unroll
-      for (int r = 0; r < 16; ++r) xv[r] = x2[jin + 64 * r];  // issued first: the LDS batch hides under them
+        for (int r = 0; r < 16; ++r) xv[r] = x2[jin + 64 * r];  // issued first: the LDS batch hides under them
+      } else {
+        // a sequence at an odd sample (a trimmed file starts anywhere): the pairs are not 8-byte
+        // aligned, so two dword loads each, still without bounds tests (round 3: the per-sample
+        // edge path used to take these frames, +45 % on stft_mel)
+        const float* xs = x + s0;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) xv[r] = make_float2(xs[2 * (jin + 64 * r)], xs[2 * (jin + 64 * r) + 1]);
+      }
       lds_read16_strided<0, 64 * 8>(hw, lds_addr(sh_hann + jin));
 #pragma unroll
       for (int r = 0; r < 16; ++r) {

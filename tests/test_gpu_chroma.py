@@ -99,6 +99,23 @@ def test_tuning_with_more_than_64_peaks_per_frame(gpu_ctx):
     np.testing.assert_allclose(got[0], ref_c, rtol=0, atol=2e-5)
 
 
+@pytest.mark.parametrize("shift", [1, 2, 3])
+def test_chroma_independent_of_chunk_alignment(gpu_ctx, shift):
+    """Chunks at any sample offset (a trimmed file starts anywhere): the tuning frames load
+    odd-offset pairs as two dwords, the low-octave CQT stages unaligned blocks through
+    registers instead of the 16-byte LDS-DMA.  Same samples, same arithmetic: tuning and
+    chroma bit-identical to the aligned chunks."""
+    nc, src = synth.make_pair(45.0, 1001)
+    cn = 441000
+    sig = np.concatenate([src, nc]).astype(np.float32)
+    chunks = [(0, cn), (len(src), cn), (len(src) + 3, cn - 7)]
+    ref, rtun, _, ridx = _chroma_gpu(gpu_ctx, sig, chunks)
+    sig2 = np.concatenate([np.zeros(shift, np.float32), sig])
+    got, tun, _, tidx = _chroma_gpu(gpu_ctx, sig2, [(o + shift, L) for o, L in chunks])
+    assert np.array_equal(tidx, ridx) and np.array_equal(tun, rtun)
+    assert np.array_equal(got, ref)
+
+
 @pytest.mark.parametrize("scale", [3e-7, 1e-3, 40.0, 3e4])
 def test_chroma_f16_split_scaling_across_amplitudes(gpu_ctx, scale):
     """Octaves 3-6 run on the f16 matrix cores with hi/lo split operands at a per-chunk

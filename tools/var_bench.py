@@ -120,12 +120,19 @@ def inputs(src):
     cn, CL = 224, 441000
     chunks = np.stack([src[(i % 9) * CL:(i % 9) * CL + CL] for i in range(cn)]).astype(np.float32)
     return dict(n=n, L=L, T=T, acw=acw, cn=cn, CL=CL,
-                sig=torch.from_numpy(wins.reshape(-1)).to(dev),
-                off=torch.arange(n, dtype=torch.int64, device=dev) * L,
-                csig=torch.from_numpy(chunks.reshape(-1)).to(dev),
+                # VB_WINSHIFT=k: every window k samples later in the buffer (a trimmed file's windows
+                # start at any sample; odd starts miss stft_mel's float2 fast path)
+                sig=torch.from_numpy(np.concatenate([np.zeros(int(os.environ.get("VB_WINSHIFT", "0")), np.float32),
+                                                     wins.reshape(-1)])).to(dev),
+                off=torch.arange(n, dtype=torch.int64, device=dev) * L + int(os.environ.get("VB_WINSHIFT", "0")),
+                # VB_CHUNKSHIFT=k: every chunk k samples past a 16-byte boundary (a trimmed file's
+                # chunks start anywhere; the low-octave CQT's DMA path needs 16-byte alignment)
+                csig=torch.from_numpy(np.concatenate([np.zeros(int(os.environ.get("VB_CHUNKSHIFT", "0")), np.float32),
+                                                      chunks.reshape(-1)])).to(dev),
                 # VB_SAMECHUNK=1: every chunk at offset 0 (their level-0 reads become L2 / MALL hits;
                 # a probe of the low-octave CQT's exposed block latency)
-                coff=torch.arange(cn, dtype=torch.int64, device=dev) * CL * (os.environ.get("VB_SAMECHUNK") != "1"),
+                coff=torch.arange(cn, dtype=torch.int64, device=dev) * CL * (os.environ.get("VB_SAMECHUNK") != "1")
+                + int(os.environ.get("VB_CHUNKSHIFT", "0")),
                 clen=torch.full((cn,), CL, dtype=torch.int64, device=dev))
 
 
