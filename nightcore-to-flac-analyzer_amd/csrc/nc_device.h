@@ -534,7 +534,7 @@ __device__ __forceinline__ void fft1024_last_mirror(const float2* lds, const flo
 // HALF = false: the outputs are 2 X[k] exactly (the two 0.5 scalings left out: a power-of-two
 // scale commutes with every rounding of the split, so |2X|^2 = 4 |X|^2 bit for bit); callers
 // that only compare or project |X|^2 fold the factor into their constants.
-template <int SPLIT, bool HALF = true, class F>
+template <int SPLIT, bool HALF = true, bool OPAQUE0 = false, class F>
 __device__ __forceinline__ void rsplit_mirror(const float2 (&v)[4][4], const float2* tw, int l, F&& f) {
   const bool l0 = l == 0;
   const int J1 = l0 ? 64 : 128 - l, J2 = l0 ? 192 : 128 + l, J3 = l0 ? 128 : 256 - l;
@@ -545,10 +545,18 @@ __device__ __forceinline__ void rsplit_mirror(const float2 (&v)[4][4], const flo
     const float2 WO = cmul(tw[SPLIT + k], O);
     f(k, cadd(E, WO), cconj(csub(E, WO)));
   };
-  pair(v[0][0], l0 ? v[0][0] : v[3][3], l);
-  pair(v[0][1], l0 ? v[0][3] : v[3][2], l + 256);
-  pair(l0 ? v[0][2] : v[3][1], v[0][2], l0 ? 512 : J3 + 256);
-  pair(v[3][0], l0 ? v[3][3] : v[0][3], J3);
+  // OPAQUE0: lane 0's operands as opaque values. A select between two elements of v can be
+  // folded into a load through a selected address, which puts v in scratch (spectral_frames:
+  // 10 scratch accesses per frame); where it is not (stft_mel, tuning_peaks) the barrier only
+  // costs moves
+  auto sel = [&](float2 a, float2 b) {
+    if constexpr (OPAQUE0) asm("" : "+v"(a.x), "+v"(a.y));
+    return make_float2(l0 ? a.x : b.x, l0 ? a.y : b.y);
+  };
+  pair(v[0][0], sel(v[0][0], v[3][3]), l);
+  pair(v[0][1], sel(v[0][3], v[3][2]), l + 256);
+  pair(sel(v[0][2], v[3][1]), v[0][2], l0 ? 512 : J3 + 256);
+  pair(v[3][0], sel(v[3][3], v[0][3]), J3);
   pair(v[1][0], v[2][3], J1);
   pair(v[1][1], v[2][2], J1 + 256);
   pair(v[2][1], v[1][2], J2 + 256);
