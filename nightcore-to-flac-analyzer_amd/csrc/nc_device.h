@@ -63,6 +63,14 @@ template <int CTRL, int ROWMASK = 0xf>
 __device__ __forceinline__ int dpp_i(int v, int old) {
   return __builtin_amdgcn_update_dpp(old, v, CTRL, ROWMASK, 0xf, false);
 }
+// v + v of the DPP source lane CTRL (every lane of every row; a partner outside the row pattern
+// is not used by the controls passed here: quad perms and row mirrors)
+template <int CTRL>
+__device__ __forceinline__ double dpp_add_f64(double v) {
+  const long long b = __double_as_longlong(v);
+  const int lo = dpp_i<CTRL, 0xf>((int)(unsigned)b, 0), hi = dpp_i<CTRL, 0xf>((int)(unsigned)(b >> 32), 0);
+  return v + __longlong_as_double((long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo));
+}
 template <class Op>
 __device__ __forceinline__ float wave_reduce_u(float v, float id, Op op) {
   auto step = [&](auto ctrl, auto rmask) {
