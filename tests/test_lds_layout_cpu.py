@@ -83,3 +83,24 @@ def test_low_octave_block_reads_conflict_free():
 def test_low_octave_swizzle_is_a_permutation_of_each_row():
     for R in range(64):
         assert sorted(p ^ cl_sw(R) for p in range(8)) == list(range(8))
+
+
+SF_RS = 72  # spectral.hip spectral_frames_kernel: row stride (f64) of the frame-sum reduction
+
+
+def test_spectral_frame_sum_reduction_conflict_free():
+    """Writes red[v][lane] (ds_write_b64: 4 x 16 contiguous lanes, banks (a/4) mod 32) and reads
+    red[lane >> 3][(lane & 7) + 8 i] (ds_read_b64: lanes 0-31 and 32-63, banks (a/4) mod 64)
+    of spectral_frames_kernel each take one LDS cycle per lane group."""
+    for v in range(8):
+        for g in range(4):
+            dw = [2 * (SF_RS * v + l) for l in range(16 * g, 16 * g + 16)]
+            banks = [(d + k) % 32 for d in dw for k in range(2)]
+            assert len(set(banks)) == 32, (v, g)
+    for i in range(8):
+        for half in range(2):
+            dw = [2 * (SF_RS * (l >> 3) + (l & 7) + 8 * i) for l in range(32 * half, 32 * half + 32)]
+            banks = [(d + k) % 64 for d in dw for k in range(2)]
+            assert len(set(banks)) == 64, (i, half)
+    # the eight rows fit the wave's FFT slot (LdsSize<1024> = 1056 float2)
+    assert 8 * SF_RS * 8 <= 1056 * 8
