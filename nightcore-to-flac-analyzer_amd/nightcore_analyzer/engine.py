@@ -658,15 +658,20 @@ class Engine:
         T = 1 + length // 512                                              # centred frames
         base = np.zeros(n + 1, np.int64)
         base[1:] = np.cumsum(T)
-        bands = np.zeros((n, len(self.SPECTRAL_BANDS), 2), np.int32)
-        hz = np.zeros(n, np.float64)
-        for f, sr in enumerate(srs):
+        # bin spacing and band bins once per distinct rate (a per-file loop of rfftfreq and band
+        # masks cost ~4 ms per 128 files, as much as the device work)
+        rates, inv = np.unique(np.asarray(srs, np.float64), return_inverse=True)
+        rb = np.zeros((len(rates), len(self.SPECTRAL_BANDS), 2), np.int32)
+        rhz = np.zeros(len(rates), np.float64)
+        for u, sr in enumerate(rates):
             freqs = np.fft.rfftfreq(2048, 1.0 / sr)                        # librosa.fft_frequencies
-            hz[f] = freqs[1]
+            rhz[u] = freqs[1]
             for b, (lo, hi) in enumerate(self.SPECTRAL_BANDS):
                 idx = np.flatnonzero((freqs >= lo) & (freqs < hi))
                 if idx.size:
-                    bands[f, b] = (idx[0], idx[-1] + 1)
+                    rb[u, b] = (idx[0], idx[-1] + 1)
+        bands = np.ascontiguousarray(rb[inv])
+        hz = np.ascontiguousarray(rhz[inv])
         up = _Upload()
         up.add("off", off, np.int64)
         up.add("len", length, np.int64)
