@@ -180,10 +180,14 @@ __global__ void tg_reduce_kernel(const double* slab, const int64_t* frame_base, 
 __global__ __launch_bounds__(256) void ibi_range_plan_kernel(const int64_t* file_len, const int64_t* t0,
                                                              const int64_t* t1, int n_files, int hop, int pad,
                                                              int64_t* row0, int64_t* row_base, int64_t* obase) {
-  // rows [row0, row1) of file f: its STFT frames [t0 - pad, t1 - pad + 1) within [0, T_f)
+  // rows [row0, row1) of file f: its STFT frames [t0 - pad, t1 - pad + 1) within [0, T_f);
+  // the share that ends the file takes every row up to T_f: rows T_f - pad + 1 .. T_f - 1
+  // feed no onset but do feed the file's dB maximum (the top_db reference all-reduced by C2),
+  // as over the whole file on one GPU (sharded._ibi_mel_rows: the same bounds)
   auto rows = [&](int f) -> int64_t {
     const int64_t T = 1 + file_len[f] / hop;
-    const int64_t r0 = max((int64_t)0, t0[f] - pad), r1 = min(T, t1[f] - pad + 1);
+    const int64_t r0 = max((int64_t)0, t0[f] - pad);
+    const int64_t r1 = (t1[f] >= T && t1[f] > t0[f]) ? T : min(T, t1[f] - pad + 1);
     return r1 > r0 ? r1 - r0 : 0;
   };
   block_prefix_table<256>(n_files, row_base, rows);

@@ -81,7 +81,7 @@ def _run_windows(pairs, group, world, rank, split_offset, log=None, **kw) -> lis
     upload only the pairs this rank touches (sharded.run over DeviceStages)."""
     from .engine import Params, get_engine
     from .io import decoded_length
-    from .pipeline import _load
+    from .pipeline import _load, _melodia_hook
     from .sharded import DeviceStages, Exchange, ShardError, analyze_sharded, shard_plan
     p = Params(**kw)
     quiet = (lambda m: None)
@@ -92,6 +92,10 @@ def _run_windows(pairs, group, world, rank, split_offset, log=None, **kw) -> lis
         touched = shard_plan(lengths, p, world, split_offset).needed(rank, p.compute_ibi and world > 1)
         arrays = [a for b in touched for a in (_load(pairs[b][0], quiet, "nightcore"),
                                                 _load(pairs[b][1], quiet, "source"))]
+        if p.compute_pitch:
+            # MELODIA where essentia is installed, as run_batch does; the hook is called with
+            # global pair indices (sharded.analyze_sharded maps the engine's local ones)
+            p.melodia = _melodia_hook({b: (arrays[2 * i], arrays[2 * i + 1]) for i, b in enumerate(touched)})
         eng = get_engine()
         sig = eng.upload_signals(arrays) if arrays else None
     except Exception as exc:           # noqa: BLE001 - carried to every rank below

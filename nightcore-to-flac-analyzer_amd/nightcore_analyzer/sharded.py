@@ -35,13 +35,20 @@ xGMI before consensus".  SURVEY.md §8(e) lays the split out and this module fol
 * The results of every pair are gathered to every rank (``gather=True``, the API
   default; the benchmark leaves it off, as its pair mode does).
 
-The records are fixed-size f64 rows (``all_gather_into_tensor`` of device tensors over
-RCCL with the "nccl" backend — no host hop before the collective — or of CPU tensors with
-gloo); blocks of unequal size are padded to the largest, and every gathered block carries
-its rank's error flag, so a failure on one rank raises on every rank (``ShardError`` on
-the others) instead of leaving them blocked in a collective.  When no pair is split
-(equal pairs, B divisible by the world size: BASELINE config 4) the plan has no exchange
-on the data path.
+The records are fixed-size f64 rows.  They are assembled on the host from the stage
+results (a few hundred bytes per window), copied to the exchange device on the split-pair
+stream and gathered with ``all_gather_into_tensor`` (device tensors over RCCL with the
+"nccl" backend, CPU tensors with gloo), then read back.  Blocks of unequal size are padded
+to the largest.  When no pair is split (equal pairs, B divisible by the world size:
+BASELINE config 4) the plan has no exchange on the data path.
+
+**Fail together.**  Every rank runs the same sequence of collectives, fixed by the plan
+alone.  A local exception is never raised where it happens: it is held and carried, as
+the rank's error flag, into the next collective, and every collective either returns on
+every rank or raises on every rank (the failing rank's own exception there, ``ShardError``
+on the others).  With ``steps`` > 1 an error after a step's last collective rides into the
+next step's first gather; the interior pipeline's errors are held by the pump and raised
+after the last split-pair collective, before the final flag check.
 
 The split-pair stages run over a small stage interface: ``DeviceStages`` (libncgpu on
 this rank's GPU) or, in the multi-process CPU tests, the oracle
@@ -51,6 +58,7 @@ consensus placement are tested without a GPU.  Every result equals the single-ra
 """
 from __future__ import annotations
 
+import dataclasses
 import gc
 import math
 from dataclasses import dataclass
@@ -191,16 +199,21 @@ def shard_plan(lengths: Sequence[int], p: Params, world: int, split_offset: floa
 
 # ------------------------------------------------------------------------------ exchange
 class Exchange:
-    """Fixed-size f64 record gathers over the default (or given) process group."""
+    """Fixed-size f64 record gathers over the default (or given) process group.
 
-    def __init__(self, group=None):
+    ``device``: where the exchanged tensors live.  Default: this rank's GPU under RCCL
+    ("nccl"), the CPU under gloo.  A test may pass a CUDA device with gloo to run the
+    device-tensor code (upload and gather on the split-pair stream, read-back) on one GPU."""
+
+    def __init__(self, group=None, device: Optional[torch.device] = None):
         self.group = group
         self.on = dist.is_available() and dist.is_initialized()
         self.world = dist.get_world_size(group) if self.on else 1
         self.rank = dist.get_rank(group) if self.on else 0
         backend = dist.get_backend(group) if self.on else "gloo"
-        # RCCL gathers device tensors (no host hop before the collective); gloo CPU tensors
-        self.dev = torch.device("cuda", torch.cuda.current_device()) if backend == "nccl" else torch.device("cpu")
+        if device is None:
+            device = torch.device("cuda", torch.cuda.current_device()) if backend == "nccl" else torch.device("cpu")
+        self.dev = torch.device(device)
 
     stream: Optional[torch.cuda.Stream] = None    # RCCL: the stream the exchanged records live on
 
@@ -245,12 +258,16 @@ class Exchange:
                 raise failed
             return np.asarray(vals, np.float64)
         buf = np.concatenate([np.asarray(vals, np.float64), [1.0 if failed is not None else 0.0]])
-        t = torch.from_numpy(buf).to(self.dev)
         if self.dev.type == "cuda" and self.stream is not None:
+            # the upload, the collective and the read-back all on the split-pair stream: the
+            # host waits for this exchange only, not for the interior groups queued on the
+            # launch stream
             with torch.cuda.stream(self.stream):
+                t = torch.from_numpy(buf).to(self.dev, non_blocking=True)
                 dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group)
                 out = t.cpu().numpy()
         else:
+            t = torch.from_numpy(buf).to(self.dev)
             dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group)
             out = t.cpu().numpy()
         if failed is not None:
@@ -272,6 +289,18 @@ class Exchange:
         for part in buf:
             out.extend(part)
         return out
+
+
+# Fault-injection points of the fail-together tests (tests/test_sharded_cpu.py): host-only
+# steps ("records", "consensus") mapped to the call (1-based) that raises.  Empty in use.
+FAULTS: dict = {}
+
+
+def _fault(point: str) -> None:
+    if point in FAULTS:
+        FAULTS[point] -= 1
+        if FAULTS[point] == 0:
+            raise RuntimeError(f"injected failure in {point}")
 
 
 def _try(fn, *args):
@@ -446,7 +475,8 @@ class DeviceStages:
         eng, n = self.eng, len(f_off)
         T = 1 + np.asarray(f_len, np.int64) // IBI_HOP
         t0, t1 = np.asarray(t0, np.int64), np.asarray(t1, np.int64)
-        rows = int(np.maximum(0, np.minimum(T, t1 - IBI_PAD + 1) - np.maximum(0, t0 - IBI_PAD)).sum())
+        rr = _ibi_mel_rows(T, t0, t1)
+        rows = int((rr[:, 1] - rr[:, 0]).sum())
         with torch.cuda.stream(self.stream):
             up = _Upload()
             up.add("off", f_off, np.int64)
@@ -570,10 +600,15 @@ def _files(pairs: Sequence[int]) -> List[int]:
 
 
 class _Pump:
-    """Advances the engine's interior group pipeline one group at a time (no-op without one)."""
+    """Advances the engine's interior group pipeline one group at a time (no-op without one).
+
+    It never raises: the pump runs between the collectives of the split-pair stages, where
+    an exception on one rank would leave the others in a collective.  An exception from the
+    pipeline ends it and is kept in ``error``; ``drain`` raises it after the last split-pair
+    collective, before the final flag check that every rank meets."""
 
     def __init__(self, gen):
-        self.gen, self.value = gen, None
+        self.gen, self.value, self.error = gen, None, None
 
     def __call__(self, n: int = 1) -> None:
         for _ in range(n):
@@ -583,16 +618,20 @@ class _Pump:
                 next(self.gen)
             except StopIteration as stop:
                 self.value, self.gen = stop.value, None
+            except BaseException as exc:       # noqa: BLE001 - raised by drain()
+                self.error, self.gen = exc, None
 
     def drain(self):
         while self.gen is not None:
             self()
+        if self.error is not None:
+            raise self.error
         return self.value
 
 
 def analyze_sharded(stages, p: Optional[Params] = None, group=None, *, lengths: Optional[Sequence[int]] = None,
                     local_pairs: Optional[Sequence[int]] = None, split_offset: float = 0.0, gather: bool = True,
-                    steps: int = 1):
+                    steps: int = 1, exchange_device: Optional[torch.device] = None):
     """pipeline.run's analysis of a batch with its windows and chunk pairs split over the
     ranks of ``group`` (module docstring).
 
@@ -602,21 +641,31 @@ def analyze_sharded(stages, p: Optional[Params] = None, group=None, *, lengths: 
     ``gather`` every rank returns all outcomes in pair order; without, this rank's owned
     pairs as [(pair index, outcome)].  ``steps`` > 1 analyses the batch that many times
     back to back, the interior groups pipelined across steps as Engine.analyze_batches
-    does (the benchmark's timed region), and returns one such list per step.  Python's cyclic
+    does (the benchmark's timed region), and returns one such list per step.
+    ``exchange_device`` overrides where the exchanged records live (``Exchange``).  A
+    ``Params.melodia`` hook is called with global pair indices.  Python's cyclic
     collector is paused for the call, as in Engine.analyze (a generation-2 pass, ~10 ms, would
     otherwise stall the host loop that keeps the device queues full)."""
     gc_was_enabled = gc.isenabled()
     gc.disable()
     try:
-        return _analyze_sharded(stages, p, group, lengths, local_pairs, split_offset, gather, steps)
+        return _analyze_sharded(stages, p, group, lengths, local_pairs, split_offset, gather, steps, exchange_device)
     finally:
         if gc_was_enabled:
             gc.enable()
 
 
-def _analyze_sharded(stages, p, group, lengths, local_pairs, split_offset, gather, steps):
+def _local_melodia(p: Params, index: Sequence[int]) -> Params:
+    """Params whose melodia hook maps the engine's local pair index to the global one."""
+    if p.melodia is None:
+        return p
+    hook, index = p.melodia, list(index)
+    return dataclasses.replace(p, melodia=lambda b, st, log, span: hook(index[b], st, log, span))
+
+
+def _analyze_sharded(stages, p, group, lengths, local_pairs, split_offset, gather, steps, exchange_device=None):
     p = p or Params()
-    ex = Exchange(group)
+    ex = Exchange(group, exchange_device)
     r, world = ex.rank, ex.world
     L = np.asarray(stages.length if lengths is None else lengths, np.int64)
     sp = shard_plan(L, p, world, split_offset)
@@ -626,21 +675,30 @@ def _analyze_sharded(stages, p, group, lengths, local_pairs, split_offset, gathe
     touched = sp.touched(r)
     needed = sp.needed(r, ibi_split)
     missing = [b for b in needed if b not in pos]
-    if missing:
-        raise ValueError(f"rank {r} needs pairs {missing} that its stages do not hold")
+    # held, not raised: the other ranks are about to enter the step's collectives
+    err: Optional[BaseException] = \
+        ValueError(f"rank {r} needs pairs {missing} that its stages do not hold") if missing else None
     ex.stream = getattr(stages, "stream", None)
-    interior = [b for b in touched if not sp.split[b]]
-    fast = hasattr(stages, "pipeline") and bool(interior)
-    stage_pairs = [b for b in needed if sp.split[b]] if fast else needed
-    pump = _Pump(stages.pipeline(_files([pos[b] for b in interior]), p, steps) if fast else None)
+    exchange = sp.n_wrows > 0 or sp.n_crows > 0          # identical on every rank
+    interior = [b for b in touched if not sp.split[b]] if err is None else []
+    fast = getattr(stages, "pipeline", None) is not None and bool(interior)
+    stage_pairs = ([b for b in needed if sp.split[b]] if fast else needed) if err is None else []
+    pump = _Pump(stages.pipeline(_files([pos[b] for b in interior]), _local_melodia(p, interior), steps)
+                 if fast else None)
     pump(3)                                     # Engine.GROUPS_IN_FLIGHT groups queued before any wait
     split_st = stages.restrict(_files([pos[b] for b in stage_pairs]))
-    per_step, err = [], None
+    per_step = []
     for _ in range(steps):
-        outs, err = _try(_split_stages, split_st, p, ex, sp, r, stage_pairs, pump)
-        if err is not None:
+        res, exc = _try(_split_stages, split_st, p, ex, sp, r, stage_pairs, pump, err)
+        if exc is not None:                     # a collective raised: it did so on every rank
+            err = exc
             break
-        per_step.append(outs)
+        outs, err = res
+        if err is None:
+            per_step.append(outs)
+        elif not exchange:                      # no collective before the final check
+            break
+        # else: the next step's first gather carries the error (or the final check does)
     if err is None and fast:
         res, err = _try(pump.drain)
         if err is None:
@@ -662,11 +720,13 @@ def _analyze_sharded(stages, p, group, lengths, local_pairs, split_offset, gathe
     return result[0] if steps == 1 else result
 
 
-def _split_stages(stages, p: Params, ex: Exchange, sp: ShardPlan, r: int, pairs: List[int], pump) -> list:
+def _split_stages(stages, p: Params, ex: Exchange, sp: ShardPlan, r: int, pairs: List[int], pump,
+                  err: Optional[BaseException] = None):
     """Stages 1-3 of the module docstring for ``pairs`` (global indices) held by ``stages``
-    (files nc, src per pair, in that order); returns [(pair, outcome)] of the owned ones.
-    Every exception between two exchanges is carried into the next one, so all ranks meet
-    every collective and a failure raises everywhere."""
+    (files nc, src per pair, in that order) -> ([(pair, outcome)] of the owned ones, held
+    error).  ``err`` is an error held from before the step; while one is held no stage runs
+    and the error rides into the next collective.  Only the collectives raise, and they raise
+    on every rank; a local error after the step's last collective is returned, not raised."""
     nP = len(pairs)
     exchange = sp.n_wrows > 0 or sp.n_crows > 0          # identical on every rank
     cw_cnt = [len(sp.contrib_w(q)) for q in range(sp.world)] if exchange else []
@@ -678,10 +738,9 @@ def _split_stages(stages, p: Params, ex: Exchange, sp: ShardPlan, r: int, pairs:
 
     def gather(table_rows, local_rows, local_vals, cnt, all_rows, n_rows, width, failed):
         """Exchange-table rows of the split pairs: this rank's `local_rows` (values
-        `local_vals`) in, the whole table out (None without an exchange)."""
+        `local_vals`) in, the whole table out (None without an exchange, where a held error
+        simply stays held)."""
         if not exchange:
-            if failed is not None:
-                raise failed
             return None
         mine = np.zeros((len(table_rows), width), np.float64)   # slots past a trimmed count stay empty
         if failed is None:
@@ -727,7 +786,8 @@ def _split_stages(stages, p: Params, ex: Exchange, sp: ShardPlan, r: int, pairs:
         pump()
         st.update(pl=pl, align=align, wl=wl, wl_src=wl_src, wl_row=wl_row, cpl=cpl, cpl_row=cpl_row, rec=rec)
 
-    _, err = _try(phase0)
+    if err is None:
+        _, err = _try(phase0)
     gtab = gather(cw, st.get("wl_row", []), st.get("rec"), cw_cnt, cw_all, sp.n_wrows, W_FIELDS, err)       # C1a
 
     def fill(full, have, table):
@@ -779,38 +839,54 @@ def _split_stages(stages, p: Params, ex: Exchange, sp: ShardPlan, r: int, pairs:
         pump()
         st.update(full=full, have=have, energy=energy, active=active, prior=prior, crec=crec)
 
-    _, err = _try(phase1) if err is None else (None, err)
+    if err is None:
+        _, err = _try(phase1)
     gtab = gather(cw, st.get("wl_row", []), st.get("rec"), cw_cnt, cw_all, sp.n_wrows, W_FIELDS, err)       # C1b
     ctab = gather(cc, st.get("cpl_row", []), st.get("crec"), cc_cnt, cc_all, sp.n_crows, CP_FIELDS, None)
     pump()
 
     # ---- phase 2: every record in plan order, then consensus on the owner of each pair
-    pl, full, have = st["pl"], st["full"], st["have"]
-    full[st["wl"]] = st["rec"]
-    if gtab is not None:
-        fill(full, have, gtab)
-    cps = np.zeros((pl.n_cp, CP_FIELDS - 1), np.float64)
-    got = np.zeros(pl.n_cp, bool)
-    if len(st["cpl"]):
-        cps[st["cpl"]] = st["crec"][:, 1:]
-        got[st["cpl"]] = True
-    for j, b in enumerate(pairs):
-        if sp.split[b] and p.compute_pitch:
-            c0, c1 = pl.pair_chunks[j]
-            for k in range(c1 - c0):
-                if not got[c0 + k]:
-                    row = ctab[sp.crow[b] + k]
-                    if row[0] != 1.0:
-                        raise ShardError(f"chunk-pair record of pair {b} missing from the exchange")
-                    cps[c0 + k] = row[1:]
-    owned = [j for j, b in enumerate(pairs) if sp.owner[b] == r]
+    def records():
+        _fault("records")
+        pl, full, have = st["pl"], st["full"], st["have"]
+        full[st["wl"]] = st["rec"]
+        if gtab is not None:
+            fill(full, have, gtab)
+        cps = np.zeros((pl.n_cp, CP_FIELDS - 1), np.float64)
+        got = np.zeros(pl.n_cp, bool)
+        if len(st["cpl"]):
+            cps[st["cpl"]] = st["crec"][:, 1:]
+            got[st["cpl"]] = True
+        for j, b in enumerate(pairs):
+            if sp.split[b] and p.compute_pitch:
+                c0, c1 = pl.pair_chunks[j]
+                for k in range(c1 - c0):
+                    if not got[c0 + k]:
+                        row = ctab[sp.crow[b] + k]
+                        if row[0] != 1.0:
+                            raise ShardError(f"chunk-pair record of pair {b} missing from the exchange")
+                        cps[c0 + k] = row[1:]
+        st["cps"] = cps
+
+    if err is None:
+        _, err = _try(records)
     ibi_pre = None
     if p.compute_ibi and exchange:
         # the hop-64 pass of every split pair, its frames split over all ranks (C2-C4); every
-        # rank holds every split pair (ShardPlan.needed); the owners get the results
-        ibi_pre = _sharded_ibi(stages, ex, sp, pl, pairs, st["prior"], r, pump)
-    res = _consensus(stages, p, pl, st["align"], st["active"], st["energy"], full, st["prior"], cps, owned, ibi_pre)
-    return [(pairs[j], o) for j, o in zip(owned, res)]
+        # rank holds every split pair (ShardPlan.needed); the owners get the results.  Every
+        # rank enters it, a held error included, so the collectives stay matched.
+        ibi_pre, err = _sharded_ibi(stages, ex, sp, st.get("pl"), pairs, st.get("prior"), r, pump, err)
+    if err is not None:
+        return [], err
+
+    def consensus():
+        _fault("consensus")
+        owned = [j for j, b in enumerate(pairs) if sp.owner[b] == r]
+        res = _consensus(stages, p, st["pl"], st["align"], st["active"], st["energy"], st["full"], st["prior"],
+                         st["cps"], owned, ibi_pre, index=pairs)
+        return [(pairs[j], o) for j, o in zip(owned, res)]
+
+    return _try(consensus)
 
 
 def _ibi_share(T: int, world: int, r: int) -> Tuple[int, int, int, int]:
@@ -820,7 +896,20 @@ def _ibi_share(T: int, world: int, r: int) -> Tuple[int, int, int, int]:
     return b0, b1, min(T, b0 * IBI_TILE), min(T, b1 * IBI_TILE)
 
 
-def _sharded_ibi(stages, ex: Exchange, sp: ShardPlan, pl, pairs: List[int], prior: np.ndarray, r: int, pump) -> dict:
+def _ibi_mel_rows(T: np.ndarray, t0: np.ndarray, t1: np.ndarray) -> np.ndarray:
+    """Mel dB rows [r0, r1) a rank computes for its onset frames [t0, t1) of each T-frame
+    file: the rows its onsets read, [t0 - pad, t1 - pad + 1), and, for the share that ends
+    the file, every row up to T — rows T - pad + 1 .. T - 1 feed no onset but do feed
+    power_to_db's maximum (the C2 reference), exactly as over the whole file on one GPU.
+    csrc/ibi.hip ibi_range_plan_kernel computes the same bounds."""
+    T, t0, t1 = (np.asarray(x, np.int64) for x in (T, t0, t1))
+    r0 = np.maximum(0, t0 - IBI_PAD)
+    r1 = np.where((t1 >= T) & (t1 > t0), T, np.minimum(T, t1 - IBI_PAD + 1))
+    return np.stack([r0, np.maximum(r0, r1)], axis=1)
+
+
+def _sharded_ibi(stages, ex: Exchange, sp: ShardPlan, pl, pairs: List[int], prior, r: int, pump,
+                 err: Optional[BaseException] = None):
     """estimate_ibis_global (tempo.py:120-173) of every split pair's two files with the frames
     split over the ranks:
       rank r: mel dB of its frames' rows -> C2 all-reduce MAX of each file's dB maximum (the
@@ -828,54 +917,71 @@ def _sharded_ibi(stages, ex: Exchange, sp: ShardPlan, pl, pairs: List[int], prio
       segments (every rank: the full onsets) -> tempogram partial rows of its tiles -> C3
       all-gather of the tile rows, summed in tile order (the one-GPU bits) -> the owner runs
       the beat tracker on the full onset and the IBI extraction.
-    Returns {plan pair index: (ibis (nc, src), IBI counts, beat counts, tempo lags)} for the
-    split pairs this rank owns."""
+    Returns ({plan pair index: (ibis (nc, src), IBI counts, beat counts, tempo lags)} for the
+    split pairs this rank owns, held error).  A held ``err`` rides into C2; every collective
+    raises on every rank; an error after C3 is returned."""
     W = ex.world
     js = [j for j, b in enumerate(pairs) if sp.split[b]]
-    files = [f for j in js for f in (2 * j, 2 * j + 1)]
-    f_off, f_len = pl.f_off[files], pl.f_len[files]
-    T = 1 + np.asarray(f_len, np.int64) // IBI_HOP
-    share = [[_ibi_share(int(t), W, q) for t in T] for q in range(W)]
-    b0, b1, t0, t1 = (np.array([m[i] for m in share[r]], np.int64) for i in range(4))
-    mx, err = _try(stages.ibi_mel, f_off, f_len, t0, t1)
-    gmax = ex.allreduce_max(mx if err is None else np.full(len(files), -np.inf), err)             # C2
+    nF = 2 * len(js)
+    g = {}
+
+    def prep():
+        files = [f for j in js for f in (2 * j, 2 * j + 1)]
+        g["f_off"], g["f_len"] = pl.f_off[files], pl.f_len[files]
+        g["T"] = T = 1 + np.asarray(g["f_len"], np.int64) // IBI_HOP
+        g["share"] = share = [[_ibi_share(int(t), W, q) for t in T] for q in range(W)]
+        g["b0"], g["b1"], g["t0"], g["t1"] = (np.array([m[i] for m in share[r]], np.int64) for i in range(4))
+        return stages.ibi_mel(g["f_off"], g["f_len"], g["t0"], g["t1"])
+
+    mx, err = _try(prep) if err is None else (None, err)
+    gmax = ex.allreduce_max(mx if err is None else np.full(nF, -np.inf), err)                       # C2
     pump()
+    T, share = g["T"], g["share"]
     seg, err = _try(stages.ibi_onset, gmax)
     cnt = [sum(m[3] - m[2] for m in share[q]) for q in range(W)]
     rows = ex.gather_blocks(np.asarray(seg if err is None else np.zeros(0), np.float64)[:, None], cnt, err)  # C4
-    onsets = [np.zeros(int(t), np.float32) for t in T]
-    pos = 0
-    for q in range(W):
-        for f, m in enumerate(share[q]):
-            onsets[f][m[2]:m[3]] = rows[pos:pos + m[3] - m[2], 0]
-            pos += m[3] - m[2]
-    pump()
-    slab, err = _try(stages.ibi_tiles, onsets, b0, b1)
+
+    def onsets_of(rows):
+        onsets = [np.zeros(int(t), np.float32) for t in T]
+        pos = 0
+        for q in range(W):
+            for f, m in enumerate(share[q]):
+                onsets[f][m[2]:m[3]] = rows[pos:pos + m[3] - m[2], 0]
+                pos += m[3] - m[2]
+        g["onsets"] = onsets
+        pump()
+        return stages.ibi_tiles(onsets, g["b0"], g["b1"])
+
     N = int(int(8.0 * SR) // IBI_HOP)
+    slab, err = _try(onsets_of, rows)
     cnt = [sum(m[1] - m[0] for m in share[q]) for q in range(W)]
     rows = ex.gather_blocks(slab if err is None else np.zeros((0, N)), cnt, err)                    # C3
-    tiles = [[None] * int(-(-t // IBI_TILE)) for t in T]
-    pos = 0
-    for q in range(W):
-        for f, m in enumerate(share[q]):
-            for b in range(m[0], m[1]):
-                tiles[f][b] = rows[pos]
-                pos += 1
-    tg = stages.ibi_reduce(tiles, T)
-    pump()
-    out = {}
-    for i, j in enumerate(js):
-        if sp.owner[pairs[j]] == r:
-            ibis, nibi, nb, lg = stages.ibi_beats([onsets[2 * i], onsets[2 * i + 1]], tg[2 * i:2 * i + 2],
-                                                  [prior[j], 120.0])
-            out[j] = (ibis, nibi, nb, lg)
-    return out
+
+    def tail():
+        onsets = g["onsets"]
+        tiles = [[None] * int(-(-t // IBI_TILE)) for t in T]
+        pos = 0
+        for q in range(W):
+            for f, m in enumerate(share[q]):
+                for b in range(m[0], m[1]):
+                    tiles[f][b] = rows[pos]
+                    pos += 1
+        tg = stages.ibi_reduce(tiles, T)
+        pump()
+        out = {}
+        for i, j in enumerate(js):
+            if sp.owner[pairs[j]] == r:
+                out[j] = stages.ibi_beats([onsets[2 * i], onsets[2 * i + 1]], tg[2 * i:2 * i + 2], [prior[j], 120.0])
+        return out
+
+    return _try(tail)
 
 
 def _consensus(stages, p: Params, pl, align, active, energy, full, prior, cps, owned: List[int],
-               ibi_pre: Optional[dict] = None) -> list:
+               ibi_pre: Optional[dict] = None, index: Optional[Sequence[int]] = None) -> list:
     """Bootstraps, IBI pass and host assembly of the held pairs ``owned`` (plan indices);
-    ``ibi_pre`` holds the split pairs' IBI results of the sharded pass."""
+    ``ibi_pre`` holds the split pairs' IBI results of the sharded pass; ``index`` maps plan
+    indices to the global pair indices a ``Params.melodia`` hook is called with."""
     B, n_cp = pl.B, pl.n_cp
     w0, w1 = pl.w0, pl.w1
     lags = [int(v) for v in cps[:, 0]] if n_cp else []
@@ -954,8 +1060,17 @@ def _consensus(stages, p: Params, pl, align, active, energy, full, prior, cps, o
          "margin": full[:, R_MARGIN]}
     starts_l = [s.tolist() for s in pl.starts]
     w0l, w1l = [int(v) for v in w0], [int(v) for v in w1]
+    def span(b):
+        """(global pair index, trimmed (src, nc) spans relative to the files) for the hook."""
+        if p.melodia is None:
+            return None
+        fs, fn = 2 * b + 1, 2 * b
+        rel = lambda f: (int(pl.f_off[f] - stages.off[f]), int(pl.f_len[f]))
+        return (index[b] if index is not None else b, (rel(fs), rel(fn)))
+
     return [assemble_pair(b, p, h, ibi, starts_l, w0l, w1l, pl.f_len, pl.strip_len, pl.lead, pl.trail,
-                          pl.intro[b], pl.win_n, pl.pair_chunks, n_cp, nj, n_pj, align[b] if align else None)
+                          pl.intro[b], pl.win_n, pl.pair_chunks, n_cp, nj, n_pj, align[b] if align else None,
+                          span=span(b))
             for b in owned]
 
 

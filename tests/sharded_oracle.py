@@ -103,7 +103,9 @@ class OracleStages:
         for o, n, a, b in zip(f_off, f_len, t0, t1):
             S = ncref.mel_db(self.buf[o:o + n], 22050, 2048, 64)
             T = S.shape[1]
-            r0, r1 = max(0, a - 17), min(T, b - 17 + 1)
+            # the rows its onsets read; the share ending the file also takes the last rows,
+            # which feed only the maximum (power_to_db's top_db reference over every frame)
+            r0, r1 = max(0, a - 17), (T if b >= T and b > a else min(T, b - 17 + 1))
             self._ibi_S.append(S)
             self._ibi_r.append((a, b))
             mx.append(float(S[:, r0:r1].max()) if r1 > r0 else -np.inf)
@@ -157,3 +159,96 @@ class OracleStages:
             nibi.append(0 if v is None else len(v))
         z = np.zeros(len(f_off), np.int64)
         return ibis, np.array(nibi, np.int64), z, z
+
+
+class FakeStages:
+    """Stage outputs of the right shapes with no DSP at all, for the fail-together tests: the
+    orchestration's collectives are what is under test, so every stage is cheap.  ``fail_in``
+    names the stage that raises on its ``fail_call``-th call (1-based); "pipeline" makes the
+    interior pipeline generator raise after its first group."""
+
+    N = 2756                                     # hop-64 tempogram lags (8 s)
+
+    def __init__(self, lengths, fail_in=None, fail_call=1):
+        self.length = np.asarray(lengths, np.int64)
+        self.off = np.concatenate([[0], np.cumsum(self.length)[:-1]]).astype(np.int64)
+        self.fail_in, self._left = fail_in, fail_call
+        self._n = 0
+
+    def restrict(self, files):
+        f = np.asarray(files, np.int64)
+        o = FakeStages.__new__(FakeStages)
+        o.length, o.off, o.fail_in, o._left, o._n = self.length[f], self.off[f], self.fail_in, self._left, 0
+        o._root = getattr(self, "_root", self)
+        return o
+
+    def _check(self, name):
+        root = getattr(self, "_root", self)
+        if root.fail_in == name:
+            root._left -= 1
+            if root._left == 0:
+                raise RuntimeError(f"injected failure in {name}")
+
+    def pipeline(self, files, p, steps=1):
+        n = len(files) // 2
+        fail = self.fail_in == "pipeline"
+
+        def gen():
+            from nightcore_analyzer.engine import PairOutcome
+            for _ in range(2 * steps):
+                yield
+                if fail:
+                    raise RuntimeError("injected failure in pipeline")
+            return [[PairOutcome() for _ in range(n)] for _ in range(steps)]
+        return gen()
+
+    def trim(self, p):
+        self._check("trim")
+        return np.zeros(len(self.length), np.int64), self.length.copy()
+
+    def windows(self, win_abs, win_n):
+        self._check("windows")
+        self._n = len(win_abs)
+        return np.zeros(len(win_abs))
+
+    def tempo(self, sel, start_bpm):
+        self._check("tempo")
+        out = np.zeros((len(sel), 4))
+        out[:, 0], out[:, 1] = 120.0, 8
+        return out
+
+    def chunks(self, chunk_off, chunk_len):
+        self._check("chunks")
+        return np.zeros((len(chunk_off) // 2, 30))
+
+    def bootstrap(self, jobs, seed):
+        self._check("bootstrap")
+        return [(1.0, (1.0, 1.0)) for _ in jobs]
+
+    def ibi_mel(self, f_off, f_len, t0, t1):
+        self._check("ibi_mel")
+        self._t = (np.asarray(t0), np.asarray(t1))
+        return np.zeros(len(f_off))
+
+    def ibi_onset(self, gmax):
+        self._check("ibi_onset")
+        t0, t1 = self._t
+        return np.zeros(int(np.maximum(0, t1 - t0).sum()), np.float32)
+
+    def ibi_tiles(self, onsets, b0, b1):
+        self._check("ibi_tiles")
+        return np.zeros((int(np.maximum(0, np.asarray(b1) - np.asarray(b0)).sum()), self.N))
+
+    def ibi_reduce(self, tiles, T):
+        self._check("ibi_reduce")
+        return np.zeros((len(tiles), self.N))
+
+    def ibi_beats(self, onsets, tgs, start_bpm):
+        self._check("ibi_beats")
+        z = np.zeros(len(onsets), np.int64)
+        return [np.full(8, 0.5)] * len(onsets), z + 8, z + 9, z
+
+    def ibi(self, f_off, f_len, start_bpm):
+        self._check("ibi")
+        z = np.zeros(len(f_off), np.int64)
+        return [np.full(8, 0.5)] * len(f_off), z + 8, z + 9, z

@@ -151,3 +151,34 @@ def test_sharded_four_ranks_seventeen_pairs_equal_engine(eng):
         assert len(res[r]) == len(ref)
         for i, (a, b) in enumerate(zip(res[r], ref)):
             assert _norm(list(a)) == _norm(list(b)), (r, i)
+
+
+def test_split_ibi_onsets_with_loud_tail_equal_one_gpu(eng):
+    """the share that ends a file computes mel rows T - 16 .. T - 1 too
+    (csrc/ibi.hip ibi_range_plan_kernel), so the all-reduced dB maximum (C2) and the onsets
+    split over 1..4 ranks equal the one-GPU onsets bit for bit on a file whose loudest frame
+    is in its last 14 ms."""
+    from nightcore_analyzer.engine import _Upload
+    from nightcore_analyzer.sharded import DeviceStages, _ibi_share
+    from test_sharded_cpu import _loud_tail_signal
+    y = _loud_tail_signal()
+    n = len(y)
+    T = 1 + n // 64
+    sig = eng.upload_signals([y])
+    up = _Upload()
+    up.add("off", sig.off, np.int64)
+    up.add("len", sig.length, np.int64)
+    up.add("start", [120.0], np.float64)
+    d = up.commit(eng.dev)
+    core = eng.ibi_core(sig.buf, d["off"], d["len"], np.array([n], np.int64), d["start"],
+                        torch.zeros(1, dtype=torch.int32, device=eng.dev))
+    full = core["onset"][:T].cpu().numpy()
+    st = DeviceStages(eng, sig)
+    for world in (1, 2, 3, 4):
+        shares = [_ibi_share(T, world, q) for q in range(world)]
+        mx = max(float(st.ibi_mel(sig.off, sig.length, [s[2]], [s[3]])[0]) for s in shares)
+        seg = []
+        for s in shares:
+            st.ibi_mel(sig.off, sig.length, [s[2]], [s[3]])
+            seg.append(st.ibi_onset(np.array([mx], np.float32)))
+        np.testing.assert_array_equal(np.concatenate(seg), full, err_msg=f"world {world}")

@@ -145,3 +145,180 @@ def test_window_sharded_split_pairs_match_reference_goldens(golden_pipeline):
         kind, outs = res[r]
         assert kind == "ok", (r, outs)
         _check_golden(outs, names, golden_pipeline)
+
+
+# ---- fail together: a failure at any point of a window-sharded
+# step raises on every rank (the failing rank's own exception, ShardError on the others) and
+# leaves no rank inside a collective.  All cases run one after another in ONE process group:
+# a rank left behind in a collective would mismatch (or hang) the next case's collectives.
+FAULT_LENGTHS = [882000, 1102500] * 5          # 5 pairs of 40 s / 50 s; world 3, split_offset 0.37:
+FAULT_OFFSET = 0.37                            # pairs 2 and 3 split, IBI exchange on (C2-C4)
+# (point, failing rank, steps, failing call): rank 2 runs interior pair 4 through the pipeline;
+# ranks 0 and 1 own the split pairs (ibi_beats); rank 1 holds split chunk pairs
+FAULT_CASES = [("missing", 1, 1, 1), ("missing", 1, 2, 1),
+               ("windows", 2, 1, 1), ("tempo", 1, 2, 2), ("chunks", 1, 1, 1), ("chunks", 1, 2, 1),
+               ("records", 2, 1, 1), ("records", 0, 2, 1),
+               ("ibi_mel", 2, 1, 1), ("ibi_onset", 0, 2, 1), ("ibi_tiles", 1, 1, 1), ("ibi_tiles", 1, 2, 2),
+               ("ibi_reduce", 2, 1, 1), ("ibi_reduce", 2, 2, 1), ("ibi_beats", 0, 1, 1), ("ibi_beats", 0, 2, 1),
+               ("bootstrap", 1, 2, 1), ("consensus", 2, 1, 1), ("consensus", 2, 2, 1), ("consensus", 0, 2, 2),
+               ("pipeline", 2, 1, 1), ("pipeline", 2, 2, 1), ("none", -1, 2, 1)]
+
+
+def _fault_worker(rank, world, port, q):
+    import torch.distributed as dist
+    from nightcore_analyzer import sharded
+    from nightcore_analyzer.engine import Params
+    from sharded_oracle import FakeStages
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    p = Params(compute_ibi=True)
+    out = []
+    try:
+        for point, fr, steps, call in FAULT_CASES:
+            mine = rank == fr
+            sharded.FAULTS.clear()
+            if mine and point in ("records", "consensus"):
+                sharded.FAULTS[point] = call
+            st = FakeStages(FAULT_LENGTHS, fail_in=point if mine else None, fail_call=call)
+            local = None
+            if mine and point == "missing":
+                sp = sharded.shard_plan(FAULT_LENGTHS, p, world, FAULT_OFFSET)
+                need = sp.needed(rank, True)
+                local = [b for b in range(sp.B) if b != need[0]]
+                st = st.restrict([f for b in local for f in (2 * b, 2 * b + 1)])
+            try:
+                res = sharded.analyze_sharded(st, p, lengths=FAULT_LENGTHS, local_pairs=local,
+                                              split_offset=FAULT_OFFSET, steps=steps)
+                out.append(("ok", len(res)))
+            except Exception as exc:        # noqa: BLE001
+                out.append(("raised", type(exc).__name__, str(exc)))
+        q.put((rank, out))
+    except BaseException as exc:            # noqa: BLE001
+        q.put((rank, repr(exc)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_window_sharded_fails_together_at_every_point():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    world = 3
+    procs = [ctx.Process(target=_fault_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=240) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for r in range(world):
+        assert isinstance(res[r], list), (r, res[r])
+        assert len(res[r]) == len(FAULT_CASES)
+        for (point, fr, steps, call), got in zip(FAULT_CASES, res[r]):
+            case = (point, fr, steps, call, r)
+            if point == "none":
+                assert got == ("ok", steps), case
+            elif r != fr:
+                assert got[:2] == ("raised", "ShardError"), (case, got)
+            elif point == "missing":
+                assert got[:2] == ("raised", "ValueError") and "needs pairs" in got[2], (case, got)
+            else:
+                assert got == ("raised", "RuntimeError", f"injected failure in {point}"), (case, got)
+
+
+def _loud_tail_signal(seconds=12.0, seed=7):
+    """A quiet body (noise + tone at -60 dB) with a loud 3 kHz burst in the file's last 14 ms:
+    the loudest mel bin lies in rows no onset reads (T - 16 .. T - 1 at hop 64)."""
+    rng = np.random.default_rng(seed)
+    n = int(seconds * 22050)
+    t = np.arange(n) / 22050
+    y = 1e-3 * (rng.standard_normal(n) + np.sin(2 * np.pi * 440 * t))
+    y[-300:] += np.sin(2 * np.pi * 3000 * t[-300:])
+    return y.astype(np.float32)
+
+
+def test_split_ibi_share_bounds_cover_the_maximum():
+    """in the split hop-64 pass the share that ends a file also computes
+    mel rows T - 16 .. T - 1, which feed only power_to_db's maximum.  Over world 1..4 the
+    all-reduced maximum of the shares equals the maximum over every row, as on one GPU, and
+    the split onsets equal the oracle's whole-file onsets."""
+    from nightcore_analyzer.sharded import IBI_PAD, _ibi_mel_rows, _ibi_share
+    from oracle import ncref
+    from sharded_oracle import OracleStages
+    y = _loud_tail_signal()
+    S = ncref.mel_db(y, 22050, 2048, 64)
+    T = S.shape[1]
+    assert T == 1 + len(y) // 64
+    # the case is sensitive: the rows the onsets read miss the maximum by a wide margin
+    assert S.max() > S[:, :T - IBI_PAD + 1].max() + 3.0
+    full = ncref.onset_strength(y, 22050, 64)
+    st = OracleStages([(y, y)])
+    for world in (1, 2, 3, 4):
+        shares = [_ibi_share(T, world, q) for q in range(world)]
+        rows = _ibi_mel_rows([T] * world, [s[2] for s in shares], [s[3] for s in shares])
+        assert max(r[1] for r in rows) == T and rows[0][0] == 0
+        mx = max(float(st.ibi_mel([0], [len(y)], [s[2]], [s[3]])[0]) for s in shares)
+        assert mx == float(S.max())
+        seg = []
+        for s in shares:
+            st.ibi_mel([0], [len(y)], [s[2]], [s[3]])
+            seg.append(st.ibi_onset(np.array([mx])))
+        np.testing.assert_array_equal(np.concatenate(seg), full)
+
+
+def _melodia_worker(rank, world, port, q):
+    import torch.distributed as dist
+    from nightcore_analyzer import sharded
+    from nightcore_analyzer.engine import Params
+    from sharded_oracle import FakeStages
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        calls = []
+
+        def hook(b, chroma_st, log, span):
+            calls.append((b, span))
+            log("    melodia hook")
+            return None
+        st = FakeStages(FAULT_LENGTHS)
+        st.pipeline = None                    # every pair through the stage path
+        sp = sharded.shard_plan(FAULT_LENGTHS, Params(), world, FAULT_OFFSET)
+        local = sp.needed(rank, True)
+        st = st.restrict([f for b in local for f in (2 * b, 2 * b + 1)])
+        st.pipeline = None
+        outs = sharded.analyze_sharded(st, Params(compute_ibi=True, melodia=hook), lengths=FAULT_LENGTHS,
+                                       local_pairs=local, split_offset=FAULT_OFFSET, gather=False)
+        q.put((rank, (calls, [b for b, _ in outs], sp.owned(rank))))
+    except BaseException as exc:            # noqa: BLE001
+        q.put((rank, repr(exc)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_window_sharded_melodia_hook_gets_global_pairs():
+    """in window mode the MELODIA hook is called for every owned pair with
+    the pair's GLOBAL index and its trimmed (src, nc) spans relative to the files, as
+    pipeline.run_batch calls it (essentia itself is absent: the hook here records its calls)."""
+    from nightcore_analyzer.engine import Params
+    from nightcore_analyzer.sharded import _local_melodia
+    seen = []
+    p = _local_melodia(Params(melodia=lambda b, st, log, span: seen.append(b)), [5, 9, 11])
+    p.melodia(1, 0.0, None, None)
+    assert seen == [9]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_melodia_worker, args=(r, 3, port, q)) for r in range(3)]
+    for pr in procs:
+        pr.start()
+    res = dict(q.get(timeout=240) for _ in range(3))
+    for pr in procs:
+        pr.join(timeout=60)
+        assert pr.exitcode == 0
+    for r in range(3):
+        assert isinstance(res[r], tuple), res[r]
+        calls, got, owned = res[r]
+        assert got == owned
+        assert [b for b, _ in calls] == owned
+        for b, span in calls:
+            assert span == ((0, FAULT_LENGTHS[2 * b + 1]), (0, FAULT_LENGTHS[2 * b])), (b, span)
