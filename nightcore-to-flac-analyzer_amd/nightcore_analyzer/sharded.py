@@ -1076,7 +1076,7 @@ def _consensus(stages, p: Params, pl, align, active, energy, full, prior, cps, o
 
 def run_window_sharded(pairs: Sequence[Tuple[np.ndarray, np.ndarray]], p: Optional[Params] = None,
                        group=None, device: Optional[int] = None, split_offset: float = 0.0,
-                       gather: bool = True):
+                       gather: bool = True, exchange_device: Optional[torch.device] = None):
     """Upload the (nc, src) pairs this rank touches to its GPU and run ``analyze_sharded``
     (``pairs`` may hold every pair of the batch; only the touched ones are uploaded)."""
     from .engine import get_engine
@@ -1090,4 +1090,4 @@ def run_window_sharded(pairs: Sequence[Tuple[np.ndarray, np.ndarray]], p: Option
     sig = eng.upload_signals(flat) if flat else DeviceSignals(torch.zeros(64, device=eng.dev),
                                                              np.zeros(0, np.int64), np.zeros(0, np.int64))
     return analyze_sharded(DeviceStages(eng, sig), p, group, lengths=lengths, local_pairs=touched,
-                           split_offset=split_offset, gather=gather)
+                           split_offset=split_offset, gather=gather, exchange_device=exchange_device)

@@ -9,8 +9,9 @@ the piptrack peak lists through a ring of GROUPS_IN_FLIGHT + 1 workspaces
 these tests check, on batches that take it:
 
 * every pair of the config-3 batch equals its own B = 1 run (results, report
-  text, logs, chunk lags, tempo margins), and the first and last pairs equal the
-  CPU oracle (oracle/refglue.run_arrays: the port of pipeline.py:23-216);
+  text, logs, chunk lags, tempo margins), and all 64 pairs equal the CPU oracle
+  (oracle/refglue.run_arrays: the port of pipeline.py:23-216), run in a process
+  pool that starts with the module so it overlaps the GPU tests;
 * every PIPELINE_CASES golden (the reference's own pipeline.run outputs) inside a
   17-pair batch, with the default schedule and with group_pairs=3 (6 groups, more
   than the peak ring's 4 slots), equals the fixture field for field, including
@@ -19,6 +20,7 @@ these tests check, on batches that take it:
 import dataclasses
 import math
 import multiprocessing as mp
+import os
 
 import numpy as np
 import pytest
@@ -47,8 +49,59 @@ def eng():
     return E.get_engine(0)
 
 
+def _oracle(seed):
+    from oracle import refglue
+    nc, src = _gen(seed)
+    return refglue.run_arrays(nc, src, compute_ibi=False)
+
+
+def oracle_pool(seeds, reserve: int = 2):
+    """(pool, AsyncResult) of refglue.run_arrays(compute_ibi=False) over the synthetic
+    3-min pairs of `seeds`: one single-threaded process per host core of this process
+    (os.sched_getaffinity: the box's CPU share), `reserve` cores left to the test process.
+    spawn: the children never touch the GPU and start from a clean interpreter."""
+    n = max(1, min(len(seeds), len(os.sched_getaffinity(0)) - reserve))
+    keys = ("OMP_NUM_THREADS", "OPENBLAS_NUM_THREADS", "MKL_NUM_THREADS")
+    saved = {k: os.environ.get(k) for k in keys}
+    os.environ.update({k: "1" for k in keys})          # inherited by the children at spawn
+    try:
+        pool = mp.get_context("spawn").Pool(n)
+    finally:
+        for k, v in saved.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+    return pool, pool.map_async(_oracle, list(seeds), chunksize=1)
+
+
+def check_against_oracle(o: E.PairOutcome, pair, ref: dict, tag=""):
+    """One outcome of Params(compute_ibi=False) against refglue.run_arrays of the same pair:
+    tempo lists, chunk lags, nc prior, ratios, CIs, classification, counts, exact duration ratio."""
+    assert o.error is None, (tag, o.error)
+    r, d = o.result, o.detail
+    assert r.src_tempos_raw == ref["src_tempos"] and r.nc_tempos_raw == ref["nc_tempos"], tag
+    assert d["chunk_lags"] == ref["chunk_lags"], tag
+    assert d["nc_start_bpm"] == ref["nc_start_bpm"], tag
+    for k in ("tempo_ratio", "pitch_ratio", "classification", "n_source_tempo_windows", "n_nc_tempo_windows",
+              "nc_median_bpm", "src_median_bpm"):
+        assert getattr(r, k) == ref[k], (tag, k)
+    assert tuple(r.tempo_ci) == tuple(ref["tempo_ci"]) and tuple(r.pitch_ci) == tuple(ref["pitch_ci"]), tag
+    nc, src = pair
+    assert r.src_duration / r.nc_duration == len(src) / len(nc)          # exact sample-count ratio
+
+
 @pytest.fixture(scope="module")
-def bench_pairs():
+def oracle_results():
+    """The oracle on all 64 config-3 pairs, started with the module's first test."""
+    pool, res = oracle_pool([1000 + i for i in range(N_PAIRS)])
+    yield res
+    pool.terminate()
+    pool.join()
+
+
+@pytest.fixture(scope="module")
+def bench_pairs(oracle_results):
     # spawn: the children never touch the GPU and start from a clean interpreter
     with mp.get_context("spawn").Pool(8) as pool:
         return pool.map(_gen, [1000 + i for i in range(N_PAIRS)])
@@ -90,23 +143,6 @@ def test_config3_batch_equals_single_pair_runs(eng, bench_pairs):
     # the same batch again (workspaces, peak ring and pinned buffers reused): identical
     again = eng.analyze(bench_pairs, p)
     assert [_key(o) for o in again] == [_key(o) for o in outs]
-
-
-@pytest.mark.parametrize("i", [0, N_PAIRS - 1])
-def test_config3_batch_matches_oracle(eng, bench_pairs, i):
-    from oracle import refglue
-    outs = eng.analyze(bench_pairs, E.Params(compute_ibi=False))
-    r, d = outs[i].result, outs[i].detail
-    nc, src = bench_pairs[i]
-    ref = refglue.run_arrays(nc, src, compute_ibi=False)
-    assert r.src_tempos_raw == ref["src_tempos"] and r.nc_tempos_raw == ref["nc_tempos"]
-    assert d["chunk_lags"] == ref["chunk_lags"]
-    assert d["nc_start_bpm"] == ref["nc_start_bpm"]
-    for k in ("tempo_ratio", "pitch_ratio", "classification", "n_source_tempo_windows", "n_nc_tempo_windows",
-              "nc_median_bpm", "src_median_bpm"):
-        assert getattr(r, k) == ref[k], k
-    assert tuple(r.tempo_ci) == tuple(ref["tempo_ci"]) and tuple(r.pitch_ci) == tuple(ref["pitch_ci"])
-    assert r.src_duration / r.nc_duration == 1.25          # exact sample-count ratio
 
 
 def _kw_classes():
@@ -199,3 +235,15 @@ def test_pipelined_batches_equal_separate_calls(eng, bench_pairs):
     got3 = eng.analyze_batches([a, c], p, group_pairs=3)
     assert [_key(o) for o in got3[0]] == [_key(o) for o in eng.analyze(signals=a, params=p)]
     assert [_key(o) for o in got3[1]] == [_key(o) for o in eng.analyze(signals=c, params=p)]
+
+
+@pytest.mark.timeout(600)
+def test_config3_batch_matches_oracle(eng, bench_pairs, oracle_results):
+    """every one of the 64 config-3 pairs against the CPU oracle, not 2
+    (last in the module: the pool has been running beside the tests above)."""
+    outs = eng.analyze(bench_pairs, E.Params(compute_ibi=False))
+    refs = oracle_results.get(timeout=600)
+    assert len(refs) == len(outs) == N_PAIRS
+    for i, (o, pair, ref) in enumerate(zip(outs, bench_pairs, refs)):
+        check_against_oracle(o, pair, ref, tag=f"pair {i}")
+        assert o.result.src_duration / o.result.nc_duration == 1.25

@@ -12,7 +12,7 @@
   for field, on every rank.
 
 The 8-GPU RCCL run is the driver's; here the exchange is the same all_gather_into_tensor
-call on CPU tensors.
+call, on CPU tensors and (exchange_device) on device tensors through gloo.
 """
 import dataclasses
 import math
@@ -79,14 +79,15 @@ def _free_port():
     return port
 
 
-def _worker(rank, world, port, names, q, split_offset=0.0, full=False):
+def _worker(rank, world, port, names, q, split_offset=0.0, full=False, exchange_device=None):
     import torch.distributed as dist
     from nightcore_analyzer.sharded import run_window_sharded
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         pairs = _batch(names)
-        outs = run_window_sharded(pairs, E.Params(), device=0, split_offset=split_offset)
+        outs = run_window_sharded(pairs, E.Params(), device=0, split_offset=split_offset,
+                                  exchange_device=exchange_device)
         if full:
             q.put((rank, [_key(o) for o in outs]))
         else:
@@ -104,11 +105,12 @@ def _batch(names):
     return [synth.make_pair(n[1], n[2]) if isinstance(n, tuple) else make_case(synth, n)[:2] for n in names]
 
 
-def _spawn(world, names, split_offset=0.0, full=False, timeout=240):
+def _spawn(world, names, split_offset=0.0, full=False, timeout=240, exchange_device=None):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, names, q, split_offset, full)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, names, q, split_offset, full, exchange_device))
+             for r in range(world)]
     for p in procs:
         p.start()
     res = dict(q.get(timeout=timeout) for _ in range(world))
@@ -118,9 +120,14 @@ def _spawn(world, names, split_offset=0.0, full=False, timeout=240):
     return res
 
 
-def test_sharded_two_ranks_one_pair_matches_reference(eng, golden_pipeline):
+@pytest.mark.parametrize("exchange_device", [None, "cuda:0"])
+def test_sharded_two_ranks_one_pair_matches_reference(eng, golden_pipeline, exchange_device):
+    """One pair split over two ranks.  With exchange_device "cuda:0" the records take the
+    device-tensor path of sharded.Exchange that RCCL runs (upload on the split-pair stream,
+    all_gather_into_tensor / all_reduce of device tensors, read-back), here through gloo's
+    CUDA-tensor collectives, C1a, C1b and the split IBI pass's C2-C4 included."""
     names = ["chords80"]
-    res = _spawn(2, names)
+    res = _spawn(2, names, exchange_device=exchange_device)
     g = golden_pipeline["chords80"]
     for r in (0, 1):
         assert isinstance(res[r], list), res[r]
