@@ -43,6 +43,7 @@ struct Tables {
   int* mel_nj4 = nullptr;  // [2][64]
   int* mel_band = nullptr;  // [2][64]
   int mel_j0 = 0, mel_j1 = 0;
+  int mel_reach = 0;  // 1 + the largest power index the unrolled mel steps read (lo4 + 4 J)
   // CQT: per tuning index, per filter: [lo, len, off] into a complex weight pool
   int* cqt_lo = nullptr;        // [kNTunings][36]
   int* cqt_len = nullptr;

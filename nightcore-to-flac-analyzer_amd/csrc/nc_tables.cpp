@@ -217,6 +217,8 @@ void build_tables(Context& ctx) {
     }
     t.mel_j0 = jmax[0];
     t.mel_j1 = jmax[1];
+    for (int sl = 0; sl < 2; ++sl)
+      for (int l = 0; l < 64; ++l) t.mel_reach = std::max(t.mel_reach, lo4[sl * 64 + l] + 4 * jmax[sl]);
     std::vector<float4> w4((size_t)(jmax[0] + jmax[1]) * 64, make_float4(0.f, 0.f, 0.f, 0.f));
     for (int sl = 0; sl < 2; ++sl)
       for (int l = 0; l < 64; ++l) {
