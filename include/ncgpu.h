@@ -35,7 +35,7 @@ extern "C" {
 
 typedef struct nc_ctx nc_ctx;
 
-#define NCGPU_ABI_VERSION 3  /* 3: tuning decision margin outputs (nc_chroma_mean*), nc_xcorr_peak */
+#define NCGPU_ABI_VERSION 4  /* 4: nc_melodia_salience; 3: tuning decision margins, nc_xcorr_peak */
 
 int nc_abi_version(void);
 const char* nc_last_error(void);
@@ -363,6 +363,30 @@ int nc_spectral_stats(nc_ctx* ctx, const float* sig, const int64_t* file_off, co
 int nc_resample_poly(nc_ctx* ctx, const float* x, const int64_t* in_off, const int64_t* in_len, int n_files,
                      float* y, const int64_t* out_off, const int64_t* out_len, int64_t max_out,
                      const double* h, int h_len, int up, int down, int64_t pre_remove, void* stream);
+
+/* -------------------------------------------------------------------------
+ * MELODIA front end (opt-in; replaces the frame-level part of essentia's
+ * PredominantPitchMelodia that pitch.estimate_pitch_melodia calls,
+ * pitch.py:210-215: frameSize 2048, hopSize 128).  PARITY UNPINNED: essentia is
+ * not installed here; the CPU restatement is oracle/melodia_ref.py.
+ *
+ * nc_melodia_salience: for every frame t < n_frames[f] of every file f (frame g
+ * = frame_base[f] + t; n_frames = ceil((len + 1024) / hop), frames centred at
+ * t hop): the 2048-sample frame times win (2048 floats, device: essentia's
+ * normalised symmetric Hann), zero-padded to 8192 -> |X| -> the 100 largest
+ * spectral peaks (parabolic interpolation) -> the 600-bin, 10-cent pitch
+ * salience from 55 Hz (20 harmonics, weight 0.8^h, cos^2 over +-1 semitone,
+ * peaks within 40 dB of the frame's largest) -> its local maxima in bins
+ * [sal_min_bin, 599], the NC_MELODIA_SALPK largest:
+ *   pk_count[g], pk_bin[g * NC_MELODIA_SALPK + i] (int), pk_sal[...] (float),
+ *   i < pk_count[g], ordered by salience (descending), ties by bin.
+ * frame_base: device int64 [n_files + 1].  No workspace.
+ * ------------------------------------------------------------------------- */
+#define NC_MELODIA_SALPK 128
+int nc_melodia_salience(nc_ctx* ctx, const float* sig, const int64_t* file_off, const int64_t* file_len,
+                        const int64_t* frame_base, int n_files, int64_t total_frames, int hop, float sample_rate,
+                        const float* win, int sal_min_bin, int* pk_count, int* pk_bin, float* pk_sal,
+                        void* stream);
 
 #ifdef __cplusplus
 }

@@ -13,6 +13,10 @@ thread_local std::string g_err;
 void set_error(const std::string& msg) { g_err = msg; }
 
 // kernels (defined in the .hip translation units)
+int launch_melodia_salience(Context& ctx, const float* sig, const int64_t* file_off, const int64_t* file_len,
+                            const int64_t* frame_base, int n_files, int64_t total_frames, int hop, float sr,
+                            const float* win, int sal_min_bin, int* pk_count, int* pk_bin, float* pk_sal,
+                            hipStream_t st);
 struct BeatArgs;
 size_t window_stage_ws_bytes(const Context& ctx, int n_win, int T);
 int launch_window_stage(Context& ctx, const float* sig, const int64_t* win_off, const uint8_t* active,
@@ -501,6 +505,16 @@ int nc_resample_poly(nc_ctx* ctx, const float* x, const int64_t* in_off, const i
   SET_DEVICE(ctx);
   return nc::launch_resample_poly(x, in_off, in_len, n_files, y, out_off, out_len, max_out, h, h_len, up, down,
                                   pre_remove, (hipStream_t)stream);
+}
+
+int nc_melodia_salience(nc_ctx* ctx, const float* sig, const int64_t* file_off, const int64_t* file_len,
+                        const int64_t* frame_base, int n_files, int64_t total_frames, int hop, float sample_rate,
+                        const float* win, int sal_min_bin, int* pk_count, int* pk_bin, float* pk_sal,
+                        void* stream) {
+  CHECK_CTX(ctx);
+  SET_DEVICE(ctx);
+  return nc::launch_melodia_salience(ctx->c, sig, file_off, file_len, frame_base, n_files, total_frames, hop,
+                                     sample_rate, win, sal_min_bin, pk_count, pk_bin, pk_sal, (hipStream_t)stream);
 }
 
 }  // extern "C"

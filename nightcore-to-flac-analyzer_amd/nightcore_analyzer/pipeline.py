@@ -67,11 +67,12 @@ analyze = run
 
 
 def _melodia_hook(pairs):
-    """Params.melodia for pairs of host arrays (nc, src) when essentia is installed (None
-    otherwise, the case in this image): MELODIA on the pair's trimmed signals, then
+    """Params.melodia for pairs of host arrays (nc, src) when MELODIA runs (essentia installed,
+    or the opt-in device restatement asked for with NC_MELODIA=device; None otherwise, the
+    default in this image): MELODIA on the pair's trimmed signals, then
     estimate_pitch_combined's acceptance rule (pitch.py:246-291)."""
     from . import pitch
-    if pitch._try_import_essentia() is None:
+    if pitch.melodia_backend() is None:
         return None
 
     def hook(b, chroma_st, log, span):         # b: pair index in `pairs`; span: trimmed (src, nc)

@@ -6,11 +6,14 @@ Faithful to the reference including its 1/3 quirk:
 the 12-lag cyclic cross-correlation finds whole-semitone lags and
 ``_chroma_shift_for_chunk`` divides by 3.0 — reported shifts are one third of
 the true semitone shift.  MELODIA refinement needs essentia, which is not
-installed; as in the reference (pitch.py:178-201) it is then skipped.
+installed; as in the reference (pitch.py:178-201) it is then skipped, unless the
+opt-in device restatement is asked for (``backend="device"`` or NC_MELODIA=device:
+nightcore_analyzer/melodia.py, parity unpinned).
 """
 from __future__ import annotations
 
 import math
+import os
 from typing import Callable, List, Optional, Tuple
 
 import numpy as np
@@ -102,24 +105,45 @@ def _try_import_essentia():
         return None
 
 
-def estimate_pitch_melodia(src_audio, nc_audio, sr, log=None):
-    """pitch.py:187-241: essentia's PredominantPitchMelodia (frame 2048, hop 128) on both
-    signals -> voiced F0 lists (Hz), each thinned to at most MAX_MELODIA_FRAMES by a fixed
-    stride; None when essentia is absent (the case in this image), when extraction fails or
-    when a side has no voiced frame.  MELODIA is not rebuilt on the device: like the
-    reference, this step is essentia's own CPU algorithm and runs only where essentia is
-    installed."""
-    es = _try_import_essentia()
-    if es is None:
+def melodia_backend(backend: Optional[str] = None) -> Optional[str]:
+    """Which MELODIA runs: "essentia" (the reference's), "device" (opt-in restatement on the
+    MI355X, parity unpinned) or None (skipped, the reference's behaviour without essentia).
+    ``backend`` (or NC_MELODIA when None) = "device" opts in; anything else keeps the default."""
+    choice = backend if backend is not None else os.environ.get("NC_MELODIA", "")
+    if choice == "device":
+        return "device"
+    return "essentia" if _try_import_essentia() is not None else None
+
+
+def estimate_pitch_melodia(src_audio, nc_audio, sr, log=None, backend: Optional[str] = None):
+    """pitch.py:187-241: PredominantPitchMelodia (frame 2048, hop 128) on both signals -> voiced
+    F0 lists (Hz), each thinned to at most MAX_MELODIA_FRAMES by a fixed stride; None when the
+    step is skipped, when extraction fails or when a side has no voiced frame.  By default this
+    is essentia's own CPU algorithm where essentia is installed, and skipped otherwise (the
+    reference's behaviour; essentia is not in this image).  ``backend="device"`` (or
+    NC_MELODIA=device) runs the opt-in restatement instead: the frame front end on the MI355X,
+    contours and melody selection on the host (melodia.py; parity unpinned: no essentia output
+    exists here to check it against)."""
+    which = melodia_backend(backend)
+    if which is None:
         if log:
             log("    essentia not available — skipping MELODIA refinement")
         return None
+    es = _try_import_essentia() if which == "essentia" else None
+
+    def extract(audio):
+        if which == "device":
+            from .melodia import predominant_pitch_melodia
+            from .tempo import require_rate
+            require_rate(sr, "estimate_pitch_melodia")
+            return predominant_pitch_melodia([audio], sr)[0]
+        f0, _ = es.PredominantPitchMelodia(frameSize=2048, hopSize=128, sampleRate=float(sr))(
+            np.asarray(audio, dtype=np.float32))
+        return f0
 
     def voiced_f0(audio):
         try:
-            f0, _ = es.PredominantPitchMelodia(frameSize=2048, hopSize=128, sampleRate=float(sr))(
-                np.asarray(audio, dtype=np.float32))
-            f0 = np.asarray(f0)
+            f0 = np.asarray(extract(audio))
             v = f0[f0 > 0.0]
             if v.size == 0:
                 return None
@@ -127,6 +151,9 @@ def estimate_pitch_melodia(src_audio, nc_audio, sr, log=None):
                 v = v[::v.size // MAX_MELODIA_FRAMES]
             return v
         except Exception as exc:           # noqa: BLE001 - reported, never raised (pitch.py:223-226)
+            from ._native import NativeUnavailable
+            if isinstance(exc, NativeUnavailable):
+                raise                      # the device backend without its library fails loudly
             if log:
                 log(f"    MELODIA extraction failed: {exc}")
             return None
@@ -160,10 +187,10 @@ def melodia_choice(mel, chroma_st: float, log: Optional[Callable[[str], None]] =
 
 
 def estimate_pitch_combined(src_audio: np.ndarray, nc_audio: np.ndarray, sr: int,
-                            log: Optional[Callable[[str], None]] = None
+                            log: Optional[Callable[[str], None]] = None, backend: Optional[str] = None
                             ) -> Tuple[List[Optional[float]], List[Optional[float]], str]:
     src_hz, nc_hz, chroma_st, _, _ = estimate_pitch_chroma(src_audio, nc_audio, sr, log=log)
-    pick = melodia_choice(estimate_pitch_melodia(src_audio, nc_audio, sr, log=log), chroma_st, log)
+    pick = melodia_choice(estimate_pitch_melodia(src_audio, nc_audio, sr, log=log, backend=backend), chroma_st, log)
     if pick is not None:
         return pick[0], pick[1], "chroma+melodia"
     return src_hz, nc_hz, "chroma_xcorr"

@@ -86,6 +86,26 @@ def make_pair(seconds: float = 180.0, seed: int = 1000, kind: str = "chords",
     return nc, src
 
 
+def make_melody_pair(seconds: float = 6.0, seed: int = 7, up: int = 4, down: int = 5):
+    """(nightcore, source) with one clear melody line (MELODIA cases): 0.5 s notes drawn from
+    MIDI 57-71, 6 harmonics at 0.5^h, 20 ms ramps, amplitude 0.3, over white noise at 0.02;
+    nc = resample_poly(src, up, down)."""
+    rng = np.random.default_rng(seed)
+    n = int(round(seconds * SR))
+    y = np.zeros(n)
+    t = np.arange(int(0.5 * SR)) / SR
+    env = np.minimum(1.0, np.minimum(t, t[-1] - t) / 0.02)
+    for s in range(0, n, len(t)):
+        f0 = 440.0 * 2 ** ((int(rng.integers(57, 72)) - 69) / 12)
+        note = sum((0.5 ** h) * np.sin(2 * np.pi * f0 * (h + 1) * t) for h in range(6)) * env
+        e = min(n, s + len(t))
+        y[s:e] += 0.3 * note[:e - s]
+    y += 0.02 * rng.standard_normal(n)
+    src = y.astype(np.float32)
+    nc = scipy.signal.resample_poly(src.astype(np.float64), up, down).astype(np.float32)
+    return nc, src
+
+
 def pair_lengths(seconds: float = 180.0, up: int = 4, down: int = 5):
     """(nightcore, source) lengths of make_pair(seconds, ...) without making the pair."""
     n = int(round(seconds * SR))
