@@ -252,11 +252,20 @@ def main():
         for off in (0.0, 0.5):
             run_windows(max(1, args.warmup), off)
 
-    # timed region: K steps with the kernels' own execution spans recorded (nc_profile mode 2:
-    # two fire-and-forget atomics per wave, no host work per launch), so the per-kernel
-    # durations below come from exactly the launches the headline number times
-    eng.kernel_profile(2)
+    # timed region: K steps with every launch bracketed by a HIP event pair on the stream it runs
+    # on, and the kernels' own execution spans recorded beside them (nc_profile mode 1), so the
+    # per-kernel durations below come from exactly the launches the headline number times.  The
+    # roofline divides by the event durations (dispatch to completion on the kernel's stream,
+    # what rocprofv3 --kernel-trace reports, waiting for CUs the other stream holds included);
+    # the execution span (first workgroup start to last workgroup end) is reported beside it
+    eng.kernel_profile(1)
     barrier()
+    torch.cuda.synchronize()
+    # a marker launch (torch.cumsum: no engine kernel is a scan) on each side of the timed region,
+    # so a rocprofv3 --kernel-trace of this command can be cut to exactly the timed launches
+    # (tools/rocprof_timed.py: their average durations against this line's)
+    marker = torch.arange(8, dtype=torch.float64, device=eng.dev)
+    torch.cumsum(marker, 0)
     torch.cuda.synchronize()
     # pair mode: the K steps are K complete analyses of the batch, issued as one pipelined
     # Engine.analyze_batches call (batch k + 1's trims and first groups are queued while batch
@@ -275,6 +284,8 @@ def main():
     torch.cuda.synchronize()
     barrier()
     el = time.perf_counter() - t0
+    torch.cumsum(marker, 0)
+    torch.cuda.synchronize()
     if win_mode:
         mine = [o for _, o in res[0]]
         if any(o.error is not None for o in mine) or any(len(r) != len(res[0]) for r in res):
@@ -287,6 +298,7 @@ def main():
             raise RuntimeError("analyze_batches returned an incomplete result")
         if any(r[0].result.tempo_ratio != tr or r[0].result.pitch_ratio != pr for r in res):
             raise RuntimeError("a pipelined batch differs from the single-call result")
+    evt = eng.kernel_times()
     spans = eng.kernel_spans()
     eng.kernel_profile(False)
     el = max_over_ranks(el)
@@ -321,7 +333,8 @@ def main():
                                       how="every inner block boundary moved half a pair (split_offset 0.5): the "
                                           "cut pairs' window and chunk-pair records all-gathered (C1a, C1b)")
     # {kernel: (average launch ms, launches per step)} from the spans of the timed region
-    kper = {k: (ms / n, n / args.steps) for k, (ms, n) in spans.items()}
+    kper = {k: (ms / n, n / args.steps) for k, (ms, n) in evt.items()}
+    kspan = {k: ms / n for k, (ms, n) in spans.items()}
 
     # the same steps as separate analyze calls (each with its own start-up), for comparison
     single_ms = None
@@ -348,7 +361,7 @@ def main():
     # compute roof per kernel: f32 VALU for the FFT kernels, f64 VALU for the tempogram
     compute_roof = {"window_tg": ("valu_f64", F64_PEAK_TFS), "cqt_chroma": ("mfma_f16", MFMA_F16_PEAK_TFS)}
 
-    def roof(tag, times, table=None):
+    def roof(tag, times, table=None, span=None):
         table = table or units
         if tag not in times or tag not in table:
             return None
@@ -362,7 +375,8 @@ def main():
         out = {"bound": "hbm", "kernel": tag, "achieved": a, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                "frac": a / HBM_PEAK_GBS, "traffic": tr["bytes_per_launch"] if tr else None,
                "traffic_source": tr["source"] if tr else None, "alg_bytes_per_launch": alg, "avg_launch_ms": avg_ms,
-               "launches_per_step": launches,
+               "launches_per_step": launches, "timing": "HIP events around each launch on its stream",
+               "exec_span_ms": span.get(tag) if span else None,
                # the roof that actually binds: VALU / f64 VALU / matrix cores
                "compute": {"bound": cb, "achieved": c, "peak": cp, "unit": "TFLOP/s",
                            "frac": c / cp, "alg_flop_per_launch": flop}}
@@ -379,19 +393,20 @@ def main():
     # §8d unit (what rocprofv3 --stats ranks first); cqt_chroma (north_star's named target) is
     # always reported beside it
     dom = max(units, key=lambda k: kper.get(k, (0, 0))[0] * kper.get(k, (0, 0))[1])
-    roofline = roof(dom, kper)
+    roofline = roof(dom, kper, span=kspan)
     if dom != "cqt_chroma" and "cqt_chroma" in kper:
-        roofline["cqt_chroma"] = roof("cqt_chroma", kper)
+        roofline["cqt_chroma"] = roof("cqt_chroma", kper, span=kspan)
     # the per-window tempogram kernel against its f64 roof (its bytes are the S_db scratch)
     wtg_units = {"window_tg": (win_per_step, WTG_BYTES, WTG_FLOP)}
     if "window_tg" in kper:
-        roofline["window_tg"] = roof("window_tg", kper, wtg_units)
+        roofline["window_tg"] = roof("window_tg", kper, wtg_units, span=kspan)
     # the same kernels launched alone (streams serialized for one more untimed step): their own
     # speed, where the timed launches share the chip with the other streams' chains
     eng.set_serial(True)
-    eng.kernel_profile(2)
+    eng.kernel_profile(1)
     step()
-    iso = eng.kernel_spans()
+    iso = eng.kernel_times()
+    eng.kernel_spans()
     eng.kernel_profile(False)
     eng.set_serial(False)
     iso_t = {k: (ms / n, n) for k, (ms, n) in iso.items()}
@@ -617,9 +632,11 @@ def main():
                        "pairs_per_gpu": args.pairs, "windows_per_gpu_step": win_per_step,
                        "cqt_chunks_per_gpu_step": chunks_per_step, "parallelism": f"dp{world} (" + ("windows sharded, split-pair record all-gathers)" if win_mode else
                                                     "pairs sharded)")},
-            # avg_launch_ms: the kernel's execution spans over the timed steps (rocprofv3's
-            # kernel duration, sharing the chip with the concurrent chain); isolated: the same
-            # kernels with the other streams idle
+            # avg_launch_ms: HIP events around each launch of the timed steps on its stream
+            # (rocprofv3's kernel duration, sharing the chip with the concurrent chain;
+            # tools/rocprof_timed.py checks them against a trace of this command); exec_span_ms:
+            # the kernel's own first-start .. last-end span; isolated: the same kernels with the
+            # other streams idle
             "roofline": roofline,
             "kernels_ms_per_step": {k: round(v[0] * v[1], 4) for k, v in kper.items()},
             "entry_points_ms_per_step": {k: round(v[0] * v[1], 4) for k, v in per.items()},
