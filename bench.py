@@ -248,6 +248,10 @@ def main():
     pr = outs[0].result.pitch_ratio
     for _ in range(max(0, args.warmup - 1)):
         step()
+    if not win_mode and not args.no_pipeline and args.warmup > 0:
+        # the pipelined call's own first-use paths (trims queued ahead on the trim stream, their
+        # workspaces and pinned read-back buffers) are warmed too, not only analyze's
+        eng.analyze_batches([own] * 2, params)
     if win_mode:
         for off in (0.0, 0.5):
             run_windows(max(1, args.warmup), off)

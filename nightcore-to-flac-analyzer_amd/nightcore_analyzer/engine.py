@@ -424,6 +424,7 @@ class Engine:
         self.num_cu = self.ctx.lib.nc_num_cu(self.ctx.h)
         self.timers: Optional[Dict[str, list]] = None
         self.host_stats: Optional[Dict[str, float]] = None  # {phase: seconds} when enabled
+        self.host_trace: Optional[list] = None   # [(perf_counter, label)] of the pipelined loop when enabled
         # the chroma chain runs on its own stream, concurrently with the window/tempo chain
         # (NC_SERIAL_STREAMS=1 queues it on the launch stream instead: isolated per-kernel timings)
         # NC_STREAM_PRIO="chroma,tail" sets the two side streams' priorities (torch: lower = more
@@ -833,9 +834,16 @@ class Engine:
                                      ev_sig)
             return dict(groups=groups, split=True, first=first, rest=rest, f1=f1)
 
+        trace = self.host_trace
+
+        def mark(label):
+            if trace is not None:
+                trace.append((time.perf_counter(), label))
+
         nxt = None
         for bi, signals in enumerate(batches):
             t0 = time.perf_counter()
+            mark(f"b{bi} trim")
             tr = nxt if nxt is not None else trim_begin(bi, False)
             nxt = None
             groups = tr["groups"]
@@ -859,20 +867,26 @@ class Engine:
                 sl = slice(2 * g0, 2 * g1)
                 sub = DeviceSignals(signals.buf, signals.off[sl], signals.length[sl])
                 t0 = time.perf_counter()
+                mark(f"b{bi} g{gi} launch")
                 g = self._launch_group(sub, p, start[sl].copy(), end[sl].copy(),
                                        align[g0:g1] if align is not None else None, log is not None)
                 g["g0"], g["bi"] = g0, bi
                 pending.append(g)
                 if gi == len(groups) - 1 and bi + 1 < len(batches):
+                    mark(f"b{bi + 1} trim_begin")
                     nxt = trim_begin(bi + 1, True)
                 if hs is not None:
                     hs["launch"] = hs.get("launch", 0.0) + time.perf_counter() - t0
                 if len(pending) > self.GROUPS_IN_FLIGHT:
                     g = pending.pop(0)
+                    mark(f"finish b{g['bi']} g{g['g0']}")
                     results[g["bi"]] += self._finish_group(g, log)
+                mark("yield")
                 yield
         for g in pending:
+            mark(f"finish b{g['bi']} g{g['g0']}")
             results[g["bi"]] += self._finish_group(g, log)
+        mark("end")
         return results
 
     def _trim_launch(self, signals: DeviceSignals, f0: int, f1: int, p: Params, stream, ws_name: str,
@@ -1234,6 +1248,8 @@ class Engine:
         if log is None:
             g["event"].synchronize()
         t1 = time.perf_counter()
+        if self.host_trace is not None:
+            self.host_trace.append((t1, "synced"))
         h = _HostViews(g["host"])
         g["starts_l"] = [x.tolist() for x in g["starts"]]
         g["w0"], g["w1"] = g["w0"].tolist(), g["w1"].tolist()
