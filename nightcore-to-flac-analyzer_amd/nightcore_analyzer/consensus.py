@@ -121,6 +121,13 @@ def _valid(values: List[Optional[float]]) -> np.ndarray:
                     dtype=np.float64)
 
 
+def _valid_list(values) -> list:
+    """``_valid`` as a list (same elements, same order): what ``assemble`` needs (counts and
+    medians) without building four small arrays per pair on the host's assembly path."""
+    isf = math.isfinite
+    return [v for v in values if v is not None and isf(v) and v > 0]
+
+
 def _classify(tempo_ratio: float, pitch_ratio: float, tempo_ci: Tuple[float, float],
               pitch_ci: Tuple[float, float], tol: float = PURE_NC_TOLERANCE) -> str:
     diff = pitch_ratio - tempo_ratio
@@ -254,8 +261,8 @@ def assemble(src_pitches, nc_pitches, src_tempos, nc_tempos, *, nc_duration, src
              tempo_boot: Tuple[float, Tuple[float, float]]) -> AnalysisResult:
     """build_result (consensus.py:519-608) after the bootstraps: gates, half-time
     flip, medians, classification, Rubber Band parameters, warnings."""
-    src_p, nc_p, src_t, nc_t = (_valid(src_pitches), _valid(nc_pitches), _valid(src_tempos),
-                                _valid(nc_tempos))
+    src_p, nc_p, src_t, nc_t = (_valid_list(src_pitches), _valid_list(nc_pitches), _valid_list(src_tempos),
+                                _valid_list(nc_tempos))
     if len(src_t) < MIN_VALID or len(nc_t) < MIN_VALID:
         raise insufficient_tempo_error(len(src_t), len(nc_t))
     if len(src_p) >= MIN_VALID and len(nc_p) >= MIN_VALID:
@@ -270,8 +277,8 @@ def assemble(src_pitches, nc_pitches, src_tempos, nc_tempos, *, nc_duration, src
         tempo_ratio = 1.0 / tempo_ratio
         tempo_ci = (1.0 / tempo_ci[1], 1.0 / tempo_ci[0])
         corrected = True
-    nc_med = _median(nc_t.tolist()) if len(nc_t) > 0 else None
-    src_med = _median(src_t.tolist()) if len(src_t) > 0 else None
+    nc_med = _median(nc_t) if len(nc_t) > 0 else None
+    src_med = _median(src_t) if len(src_t) > 0 else None
     return AnalysisResult(
         tempo_ratio=tempo_ratio, pitch_ratio=pitch_ratio, tempo_ci=tempo_ci, pitch_ci=pitch_ci,
         classification=_classify(tempo_ratio, pitch_ratio, tempo_ci, pitch_ci),

@@ -83,8 +83,47 @@ TUNING_NEAR_TIE = 1  # tuning decisions whose histogram argmax leads by at most 
 _logger = logging.getLogger("nightcore_analyzer")
 
 
+class _DevSpan:
+    """A typed span of a device byte buffer as the native entry points take it: an address
+    and a length.  Carving the pipeline's ~50 plan and result arrays as torch views costs a
+    few microseconds of host time each (one group's launch spent ~0.25 ms there); a span is
+    a plain address, sliced like a 1-D tensor, and becomes a tensor only on request (``t``)."""
+    __slots__ = ("base", "addr", "n", "dtype", "isz")
+
+    def __init__(self, base: torch.Tensor, addr: int, n: int, dtype: torch.dtype, isz: int):
+        self.base, self.addr, self.n, self.dtype, self.isz = base, addr, n, dtype, isz
+
+    def data_ptr(self) -> int:
+        return self.addr
+
+    def numel(self) -> int:
+        return self.n
+
+    def __len__(self) -> int:
+        return self.n
+
+    def __getitem__(self, sl: slice) -> "_DevSpan":
+        a, b, step = sl.indices(self.n)
+        if step != 1:
+            raise ValueError("a device span slices contiguously")
+        return _DevSpan(self.base, self.addr + a * self.isz, max(0, b - a), self.dtype, self.isz)
+
+    @property
+    def t(self) -> torch.Tensor:
+        o = self.addr - self.base.data_ptr()
+        return self.base[o:o + self.n * self.isz].view(self.dtype)
+
+    def fill_(self, v) -> None:
+        self.t.fill_(v)
+
+
+def _tensor(x):
+    return x.t if isinstance(x, _DevSpan) else x
+
+
 class _Upload:
-    """Packs many small host arrays into one H2D copy; returns device views."""
+    """Packs many small host arrays into one H2D copy; returns device views (torch views,
+    or ``_DevSpan`` address spans with ``spans=True``)."""
 
     def __init__(self):
         self.parts: List[Tuple[str, np.ndarray]] = []
@@ -93,7 +132,7 @@ class _Upload:
         a = np.ascontiguousarray(np.asarray(arr, dtype=dtype).reshape(-1))
         self.parts.append((name, a))
 
-    def commit(self, dev: torch.device) -> Dict[str, torch.Tensor]:
+    def commit(self, dev: torch.device, spans: bool = False) -> Dict[str, torch.Tensor]:
         offs, total = [], 0
         for _, a in self.parts:
             total = (total + 15) & ~15
@@ -104,6 +143,10 @@ class _Upload:
             host[o:o + a.nbytes] = a.view(np.uint8)
         # pinned staging + async copy: never waits for work already queued on the stream
         d = torch.from_numpy(host).pin_memory().to(dev, non_blocking=True)
+        if spans:
+            p0 = d.data_ptr()
+            return {name: _DevSpan(d, p0 + o, max(1, a.size), _TORCH_DTYPE[a.dtype.str], a.itemsize)
+                    for (name, a), o in zip(self.parts, offs)}
         out = {}
         for (name, a), o in zip(self.parts, offs):
             t = d[o:o + max(a.nbytes, a.itemsize)].view(_TORCH_DTYPE[a.dtype.str])
@@ -127,7 +170,7 @@ class _Arena:
     def add(self, name: str, n: int, dtype) -> None:
         self.parts.append((name, np.dtype(dtype), max(1, int(n))))
 
-    def commit(self, dev: torch.device) -> Dict[str, torch.Tensor]:
+    def commit(self, dev: torch.device, spans: bool = False) -> Dict[str, torch.Tensor]:
         self.offs, total = [], 0
         for _, dt, n in self.parts:
             total = (total + 15) & ~15
@@ -135,6 +178,10 @@ class _Arena:
             total += n * dt.itemsize
         self.nbytes = max(16, total)
         self.buf = torch.zeros(self.nbytes, dtype=torch.uint8, device=dev)
+        if spans:
+            p0 = self.buf.data_ptr()
+            return {name: _DevSpan(self.buf, p0 + o, n, _TORCH_DTYPE[dt.str], dt.itemsize)
+                    for (name, dt, n), o in zip(self.parts, self.offs)}
         return {name: self.buf[o:o + n * dt.itemsize].view(_TORCH_DTYPE[dt.str])
                 for (name, dt, n), o in zip(self.parts, self.offs)}
 
@@ -374,6 +421,35 @@ def plan_batch(off: np.ndarray, length: np.ndarray, start: np.ndarray, end: np.n
                      n_src_w, chunk_off, chunk_len, pair_chunks, n_chunks, n_cp)
 
 
+def shared_tuning_map(pl: BatchPlan, tp: int, win_chunk: np.ndarray, tf_skip: np.ndarray) -> None:
+    """Chunks whose first ``tp`` tuning frames are a window's leading STFT frames: a standard
+    20 s chunk (chunk i of file f starts at i * CHUNK) that starts where a window of the same
+    file starts.  Sets win_chunk[window] = chunk and tf_skip[chunk] = tp for each such pair
+    (vectorised over the batch's chunks; a per-chunk loop cost ~0.5 ms of host time per
+    26-pair group)."""
+    n_chunks, hop_n = pl.n_chunks, pl.hop_n
+    if n_chunks == 0 or hop_n <= 0:
+        return
+    cn = int(CHUNK_SEC * SR)
+    cl = np.asarray(pl.chunk_len, np.int64)
+    per = np.array([c1 - c0 for c0, c1 in pl.pair_chunks], np.int64)
+    first = np.array([c0 for c0, _ in pl.pair_chunks], np.int64)
+    pc = np.arange(n_chunks) >> 1                      # chunk pair of chunk c (src, nc interleaved)
+    side = np.arange(n_chunks) & 1                     # 0: source (file 2b + 1), 1: nightcore (2b)
+    b = np.repeat(np.arange(len(per)), per)[pc]
+    i = pc - np.repeat(first, per)[pc]                 # chunk index within its pair
+    f = 2 * b + 1 - side
+    pos = i * cn                                       # the chunk's start inside its file
+    k = pos // hop_n                                   # the window that would start there
+    w0, w1 = np.asarray(pl.w0, np.int64), np.asarray(pl.w1, np.int64)
+    ok = (cl == cn) & (pos % hop_n == 0) & (k < w1[f] - w0[f])
+    c = np.flatnonzero(ok)
+    wk = w0[f[c]] + k[c]
+    hit = np.asarray(pl.win_abs, np.int64)[wk] - np.asarray(pl.f_off, np.int64)[f[c]] == pos[c]
+    win_chunk[wk[hit]] = c[hit]
+    tf_skip[c[hit]] = tp
+
+
 class _HostViews(dict):
     """A group's host result views, plus python-list forms ("bpm_l", ...) made on first
     access for the scalar lookups of the assembly loops (dropped by ``refresh`` when a
@@ -424,6 +500,7 @@ class Engine:
         self.num_cu = self.ctx.lib.nc_num_cu(self.ctx.h)
         self.timers: Optional[Dict[str, list]] = None
         self.host_stats: Optional[Dict[str, float]] = None  # {phase: seconds} when enabled
+        self._jb_memo: Dict[Tuple[int, int], int] = {}
         self.host_trace: Optional[list] = None   # [(perf_counter, label)] of the pipelined loop when enabled
         # the chroma chain runs on its own stream, concurrently with the window/tempo chain
         # (NC_SERIAL_STREAMS=1 queues it on the launch stream instead: isolated per-kernel timings)
@@ -469,6 +546,14 @@ class Engine:
             self._streams = None
 
     # -------------------------------------------------------------- plumbing
+    def _job_bytes(self, cap: int, n_boot: int) -> int:
+        """nc_bootstrap_job_bytes, memoised (a group asks for ~80 jobs' sizes, most of them equal)."""
+        key = (cap, n_boot)
+        v = self._jb_memo.get(key)
+        if v is None:
+            v = self._jb_memo[key] = int(self.ctx.lib.nc_bootstrap_job_bytes(cap, n_boot))
+        return v
+
     def stream(self) -> int:
         return torch.cuda.current_stream(self.dev).cuda_stream
 
@@ -908,7 +993,7 @@ class Engine:
             up = _Upload()
             up.add("off", off, np.int64)
             up.add("len", lens, np.int64)
-            d0 = up.commit(dev)
+            d0 = up.commit(dev, spans=True)
             wsb = self.ctx.lib.nc_trim_workspace_bytes(lens.ctypes.data, n)
             ws = self.workspace(ws_name, wsb)
             ws.record_stream(stream)
@@ -973,18 +1058,7 @@ class Engine:
         win_chunk = np.full(max(1, n_win), -1, np.int32)
         tf_skip = np.zeros(max(1, n_chunks), np.int32)
         if share:
-            cn = int(CHUNK_SEC * SR)
-            for b, (c0, c1) in enumerate(pair_chunks):
-                for f, side in ((2 * b + 1, 0), (2 * b, 1)):
-                    st_f = starts[f]
-                    for i in range(c1 - c0):
-                        c = 2 * (c0 + i) + side
-                        if chunk_len[c] != cn or (i * cn) % hop_n:
-                            continue
-                        k = i * cn // hop_n
-                        if k < len(st_f) and st_f[k] == i * cn:
-                            win_chunk[w0[f] + k] = c
-                            tf_skip[c] = tp
+            shared_tuning_map(pl, tp, win_chunk, tf_skip)
             share = bool(tf_skip.any())
         chunk_tf_base = np.zeros(max(1, n_chunks) + 1, np.int64)
         if n_chunks:
@@ -999,7 +1073,7 @@ class Engine:
         caps = [max(1, (w1[2 * b] - w0[2 * b]) + (w1[2 * b + 1] - w0[2 * b + 1])) for b in range(B)] + \
                [2 * (c1 - c0) for c0, c1 in pair_chunks]
         p_n = [c1 - c0 for c0, c1 in pair_chunks]
-        jb = self.ctx.lib.nc_bootstrap_job_bytes
+        jb = self._job_bytes
         wsoff, tot = [], 0
         for c in caps:
             wsoff.append(tot)
@@ -1049,7 +1123,7 @@ class Engine:
         up.add("win_chunk", win_chunk, np.int32)
         up.add("tf_skip", tf_skip, np.int32)
         up.add("tf_base", chunk_tf_base, np.int64)
-        d = up.commit(dev)
+        d = up.commit(dev, spans=True)
 
         # one zero-filled output arena, copied back in one D2H
         ar = _Arena()
@@ -1061,7 +1135,7 @@ class Engine:
                             ("bout", 3 * nj, np.float64), ("sout", 3 * max(1, n_pitch_jobs), np.float64),
                             ("npk", n_chunks, np.int32)):
             ar.add(name, n, dt)
-        o = ar.commit(dev)
+        o = ar.commit(dev, spans=True)
         tvals, pvals = o["vals"][:TV], o["vals"][TV:]
 
         # ---------------------------------------------------------------- 3. plan ready -> stream 2
@@ -1251,6 +1325,12 @@ class Engine:
         if self.host_trace is not None:
             self.host_trace.append((t1, "synced"))
         h = _HostViews(g["host"])
+        if log is None:
+            # group-wide screens (every result is on the host): a pair's own near-tie and beat
+            # capacity checks run only when some pair of the group can trip them
+            h["any_nb_neg"] = bool((h["nbeats"] < 0).any())
+            h["any_cm_tie"] = bool((h["cmargin"] < NEAR_TIE).any())
+            h["any_tm_tie"] = bool((h["tmargin"] <= TUNING_NEAR_TIE).any())
         g["starts_l"] = [x.tolist() for x in g["starts"]]
         g["w0"], g["w1"] = g["w0"].tolist(), g["w1"].tolist()
         ibi = {k[4:]: v for k, v in g["host"].items() if k.startswith("ibi_")} if g["has_ibi"] else None
@@ -1317,7 +1397,7 @@ class Engine:
     def _ibi_pass(self, signals, d_off, d_len, f_len, prior, B, keep_beats=False):
         dev, st = self.dev, self.stream()
         nF = 2 * B
-        starts = torch.cat([prior[:B], torch.full((1,), 120.0, dtype=torch.float64, device=dev)])
+        starts = torch.cat([_tensor(prior)[:B], torch.full((1,), 120.0, dtype=torch.float64, device=dev)])
         pidx = h2d([f // 2 if f % 2 == 0 else B for f in range(nF)], np.int32, dev)
         core = self.ibi_core(signals.buf, d_off, d_len, f_len, starts, pidx)
         frames, fb_h, ibis, nibi = core["frames"], core["fbase_h"], core["ibis"], core["nibi"]
@@ -1403,11 +1483,10 @@ def assemble_pair(b, p: Params, h, ibi, starts, w0, w1, f_len, strip_len, lead, 
         n = c1 - c0
         wait("pitch")
         lags = h["clag_l"][c0:c1]
-        shifts = h["pvals"][c0:c1]
         pv = h["pvals_l"]
         src_p = pv[2 * n_cp + c0:2 * n_cp + c1]
         nc_p = pv[n_cp + c0:n_cp + c1]
-        point_st = C._median(shifts.tolist())
+        point_st = C._median(pv[c0:c1])          # the shifts, as python floats
         if n >= MIN_CHUNKS:
             j = b
             lo_st, hi_st = h["sout_l"][n_pitch_jobs + j], h["sout_l"][2 * n_pitch_jobs + j]
@@ -1433,11 +1512,11 @@ def assemble_pair(b, p: Params, h, ibi, starts, w0, w1, f_len, strip_len, lead, 
         tmargins = h["tmargin"][2 * c0:2 * c1].copy() if "tmargin" in h else None
         out.detail.update(chunk_lags=lags, chunk_lag_margin=margins, tuning=h["tuning"][2 * c0:2 * c1].copy(),
                           chroma=h["chroma"][24 * c0:24 * c1].reshape(-1, 12).copy(), tuning_margin=tmargins)
-        if len(margins) and margins.min() < NEAR_TIE:
+        if h.get("any_cm_tie", True) and len(margins) and margins.min() < NEAR_TIE:
             # not in the reference's log stream (kept identical); Python logging only
             _logger.info("chroma lag near-tie in pair %d: chunk(s) %s, relative margin %s", b,
                          np.flatnonzero(margins < NEAR_TIE).tolist(), np.round(margins[margins < NEAR_TIE], 6).tolist())
-        if tmargins is not None and len(tmargins) and tmargins.min() <= TUNING_NEAR_TIE:
+        if h.get("any_tm_tie", True) and tmargins is not None and len(tmargins) and tmargins.min() <= TUNING_NEAR_TIE:
             # a tuning histogram whose best bin leads by <= 1 residual: one peak decides the
             # CQT's fmin shift, so an f32 / f64 difference in a single peak could flip it
             _logger.info("tuning near-tie in pair %d: chunk(s) %s (src, nc interleaved), count margin %s", b,
@@ -1462,7 +1541,7 @@ def assemble_pair(b, p: Params, h, ibi, starts, w0, w1, f_len, strip_len, lead, 
             for i, w in enumerate(ws_)])
         wait(side)
         bpm_l, nb_l = h["bpm_l"], h["nbeats_l"]
-        if any(nb_l[w] < 0 for w in ws_):
+        if h.get("any_nb_neg", True) and any(nb_l[w] < 0 for w in ws_):
             # the device beat list overflowed its capacity: an engine limit, not "no tempo"
             out.error = _native.NativeError(f"beat tracker capacity exceeded in a {side} window of pair {b}")
             return out
