@@ -33,8 +33,12 @@ def main():
         torch.cuda.synchronize()
         return (time.perf_counter() - t0) / K * 1e3
 
+    gif0 = eng.GROUPS_IN_FLIGHT
     for s in scheds:
-        gp = None if s == "default" else ([int(v) for v in s.split(",")] if "," in s else int(s))
+        # "SCHEDULE@G": that schedule with G pair groups in flight
+        sched, _, gif = s.partition("@")
+        eng.GROUPS_IN_FLIGHT = int(gif) if gif else gif0
+        gp = None if sched == "default" else ([int(v) for v in sched.split(",")] if "," in sched else int(sched))
         for _ in range(2):
             run(gp)
         off = min(run(gp) for _ in range(3))
@@ -47,8 +51,8 @@ def main():
         eng.host_stats = None
         print(f"{s:>12s}: {off:7.3f} ms/step (timers off)  {on:7.3f} (timers on)  host {hs}", flush=True)
 
-    gp = None if scheds[0] == "default" else ([int(v) for v in scheds[0].split(",")] if "," in scheds[0]
-                                              else int(scheds[0]))
+    eng.GROUPS_IN_FLIGHT = gif0
+    gp = None
     eng.host_trace = []
     ms = run(gp)
     tr, eng.host_trace = eng.host_trace, None
