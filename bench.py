@@ -394,12 +394,13 @@ def main():
         return out
 
     # the dominant kernel = the largest total execution time per step among the kernels with a
-    # §8d unit (what rocprofv3 --stats ranks first); cqt_chroma (north_star's named target) is
-    # always reported beside it
+    # §8d unit (what rocprofv3 --stats ranks first); the other one (stft_mel / cqt_chroma,
+    # north_star's named target) is always reported beside it
     dom = max(units, key=lambda k: kper.get(k, (0, 0))[0] * kper.get(k, (0, 0))[1])
     roofline = roof(dom, kper, span=kspan)
-    if dom != "cqt_chroma" and "cqt_chroma" in kper:
-        roofline["cqt_chroma"] = roof("cqt_chroma", kper, span=kspan)
+    for other in units:
+        if other != dom and other in kper:
+            roofline[other] = roof(other, kper, span=kspan)
     # the per-window tempogram kernel against its f64 roof (its bytes are the S_db scratch)
     wtg_units = {"window_tg": (win_per_step, WTG_BYTES, WTG_FLOP)}
     if "window_tg" in kper:
