@@ -97,7 +97,10 @@ __global__ __launch_bounds__(256) void chroma_plan_kernel(const int64_t* chunk_l
 // 0.77 ms per bench step (isolated); 512-output tiles (26 KB LDS) were as fast alone but
 // co-resided worse with stft_mel on the other stream (step 14.5 -> 15.5 ms); 256 (14 KB)
 // gave 14.1 ms.
-constexpr int D3_T = 256;               // level-(base + 3) outputs per decimate3 workgroup
+#ifndef D3_TILE
+#define D3_TILE 256
+#endif
+constexpr int D3_T = D3_TILE;           // level-(base + 3) outputs per decimate3 workgroup
 constexpr int D3_N1 = 4 * D3_T + 144;  // level base+1 values computed (from 4 m0 - 72)
 constexpr int D3_N2 = 2 * D3_T + 48;   // level base+2 values computed (from 2 m0 - 24)
 constexpr int D3_P0 = 4 * D3_T + 168;  // level base pairs staged (values from 8 m0 - 168)
