@@ -30,6 +30,10 @@ struct KernelTimers {
     std::vector<int> spans;     // span slots of this tag's launches since the last read
   };
   std::map<std::string, Slot> slots;
+  // event pairs created when timing is enabled, handed to the first launches of each tag: a
+  // timed region then records events without creating them (hipEventCreate is host work in
+  // the region the events measure)
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> pool;
   bool events = true;
   unsigned long long* span_buf = nullptr;   // [kSpanCap][kSpanLines][kSpanStride]: (start, end, pad)
   int span_used = 0;
@@ -40,6 +44,10 @@ struct KernelTimers {
         (void)hipEventDestroy(p.first);
         (void)hipEventDestroy(p.second);
       }
+    for (auto& p : pool) {
+      (void)hipEventDestroy(p.first);
+      (void)hipEventDestroy(p.second);
+    }
     if (span_buf) (void)hipFree(span_buf);
   }
 };
@@ -63,9 +71,14 @@ KTimer::KTimer(Context& ctx, const char* tag, hipStream_t st) : ctx_(ctx), tag_(
   }
   if (!t.events) return;
   if (slot.used == slot.ev.size()) {
-    hipEvent_t a = nullptr, b = nullptr;
-    if (hipEventCreate(&a) != hipSuccess || hipEventCreate(&b) != hipSuccess) return;
-    slot.ev.emplace_back(a, b);
+    if (!t.pool.empty()) {
+      slot.ev.push_back(t.pool.back());
+      t.pool.pop_back();
+    } else {
+      hipEvent_t a = nullptr, b = nullptr;
+      if (hipEventCreate(&a) != hipSuccess || hipEventCreate(&b) != hipSuccess) return;
+      slot.ev.emplace_back(a, b);
+    }
   }
   auto& p = slot.ev[slot.used++];
   (void)hipEventRecord(p.first, st_);
@@ -91,6 +104,19 @@ void profile_enable(Context& ctx, int mode) {
   if (!mode) return;
   auto* t = new KernelTimers();
   t->events = mode == 1;
+  if (t->events) {
+    constexpr int kPoolPairs = 1024;   // a 10-step bench region launches ~500 timed kernels
+    t->pool.reserve(kPoolPairs);
+    for (int i = 0; i < kPoolPairs; ++i) {
+      hipEvent_t a = nullptr, b = nullptr;
+      if (hipEventCreate(&a) != hipSuccess) break;
+      if (hipEventCreate(&b) != hipSuccess) {
+        (void)hipEventDestroy(a);
+        break;
+      }
+      t->pool.emplace_back(a, b);
+    }
+  }
   if (hipMalloc(&t->span_buf, sizeof(unsigned long long) * kSpanCap * kSpanLaunchU64) != hipSuccess)
     t->span_buf = nullptr;
   int khz = 0;

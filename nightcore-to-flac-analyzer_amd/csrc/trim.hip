@@ -17,6 +17,9 @@ namespace nc {
 // sample read once; block b of file f at blk[frame_base[f] + b].  One workgroup per tile of
 // TR_BPG blocks of one file (tile_base[f] = first tile of file f: one search per workgroup,
 // not per wave); each wave sums TR_BPW consecutive blocks with all their 16-byte loads in flight.
+#ifndef TR_BSEARCH
+#define TR_BSEARCH 0
+#endif
 constexpr int TR_BPW = 4;                  // blocks per wave
 constexpr int TR_BPG = 4 * TR_BPW;         // blocks per workgroup (4 waves)
 
@@ -27,6 +30,11 @@ __global__ __launch_bounds__(256) void trim_blocks_kernel(const float* sig, cons
   const Span span_(span);
   const int lane = threadIdx.x & 63;
   const int64_t tile = blockIdx.x;
+  // the tile's file = the last f with tile_base[f] <= tile (tile_base is non-decreasing): the
+  // wave counts the entries <= tile, 64 independent loads per round, instead of a binary
+  // search's chain of dependent scalar loads (7 round trips for 116 files) ahead of every
+  // workgroup's sample loads.  Entry n_files (the tile total) counts too: past it, no tile.
+#if TR_BSEARCH  // the round-3 binary search (A/B builds only)
   if (tile >= tile_base[n_files]) return;
   int lo = 0, hi = n_files - 1;
   while (lo < hi) {
@@ -35,6 +43,15 @@ __global__ __launch_bounds__(256) void trim_blocks_kernel(const float* sig, cons
     else hi = mid - 1;
   }
   const int f = __builtin_amdgcn_readfirstlane(lo);
+#else
+  int cnt = 0;
+  for (int i0 = 0; i0 <= n_files; i0 += 64) {
+    const int i = i0 + lane;
+    cnt += __popcll(__ballot(i <= n_files && tile_base[i] <= tile));
+  }
+  if (cnt > n_files) return;
+  const int f = __builtin_amdgcn_readfirstlane(cnt - 1);
+#endif
   const int64_t N = file_len[f];
   const int64_t nblk = (N + 511) / 512;
   const int64_t b0 = (tile - tile_base[f]) * TR_BPG + (threadIdx.x >> 6) * TR_BPW;
