@@ -94,11 +94,18 @@ __global__ __launch_bounds__(256) void chroma_plan_kernel(const int64_t* chunk_l
 // level is staged as its even and odd phases with origin qa - 12 (qa = first output the
 // next level computes), so a thread's four consecutive outputs read their 27 odd-phase
 // values as 7 aligned float4 LDS loads and the centre values as one.  Measured: 1.19 ->
-// 0.77 ms per bench step (isolated); 512-output tiles (26 KB LDS) were as fast alone but
-// co-resided worse with stft_mel on the other stream (step 14.5 -> 15.5 ms); 256 (14 KB)
-// gave 14.1 ms.
+// 0.77 ms per bench step (isolated); in round 2, 512-output tiles (26 KB LDS) were as fast
+// alone but co-resided worse with stft_mel on the other stream (step 14.5 -> 15.5 ms; 256
+// (14 KB) gave 14.1 ms) -- see D3_TILE for round 4.
+// Round 4, with stft_mel's LDS reserve keeping this kernel off the STFT's CUs: 128 / 256 / 512 /
+// 768 / 1024 outputs per workgroup (256 threads) ran 1.40 / 0.98 / 0.82 / 0.94 / 1.01 ms per step
+// isolated (six, four and three workgroups per CU past 512 by LDS), the pipelined step the same
+// within its spread (profiles/r4_decimate_tile_ab.txt)
 #ifndef D3_TILE
-#define D3_TILE 256
+#define D3_TILE 512
+#endif
+#ifndef D3_NT
+#define D3_NT 256  // threads per decimate3 workgroup
 #endif
 constexpr int D3_T = D3_TILE;           // level-(base + 3) outputs per decimate3 workgroup
 constexpr int D3_N1 = 4 * D3_T + 144;  // level base+1 values computed (from 4 m0 - 72)
@@ -143,7 +150,7 @@ __device__ __forceinline__ void d3_quad(const float* __restrict__ E, const float
 __device__ __forceinline__ void d3_level(const float* E, const float* O, int cnt, int64_t qa, int64_t L,
                                          const float (&h)[2 * kHalfbandK + 1], float* E2, float* O2, float* dst,
                                          int own0, int own_n) {
-  for (int i = threadIdx.x; i < cnt / 4; i += 256) {
+  for (int i = threadIdx.x; i < cnt / 4; i += D3_NT) {
     float r[4];
     d3_quad(E, O, i, h, r);
     const int64_t q0 = qa + 4 * i;
@@ -171,7 +178,7 @@ __device__ __forceinline__ void d3_level(const float* E, const float* O, int cnt
 // per 224 chunks).  Walking several tiles per workgroup with the next tile's loads in
 // flight during the levels measured slower (round 2: 355 against 228 us; the tile loop moves
 // the taps out of SGPRs and the kernel to 105 VGPRs, four waves per SIMD instead of eight).
-constexpr int D3_LD = (D3_P0 / 2 + 255) / 256;  // float4 input loads per thread per tile
+constexpr int D3_LD = (D3_P0 / 2 + D3_NT - 1) / D3_NT;  // float4 input loads per thread per tile
 
 // the f32 taps by value: kernel arguments are scalar loads, so the taps stay in SGPRs
 // (v_fmac takes one SGPR operand) instead of holding ~37 VGPRs for the whole kernel
@@ -179,7 +186,7 @@ struct D3Taps {
   float h[2 * kHalfbandK + 1];
 };
 
-__global__ __launch_bounds__(256) void decimate3_kernel(const float* sig, const int64_t* chunk_off,
+__global__ __launch_bounds__(D3_NT) void decimate3_kernel(const float* sig, const int64_t* chunk_off,
                                                         const int64_t* oct_off, const int64_t* oct_len,
                                                         float* ws_oct, int base, D3Taps taps, float* xmax,
                                                         unsigned long long* span) {
@@ -187,7 +194,7 @@ __global__ __launch_bounds__(256) void decimate3_kernel(const float* sig, const 
   static_assert(kHalfbandK == 23, "phase windows assume 23");
   __shared__ __attribute__((aligned(16))) float e0[D3_P0], o0[D3_P0];
   __shared__ __attribute__((aligned(16))) float e1[D3_N1 / 2], o1[D3_N1 / 2];
-  __shared__ float wmax[4];
+  __shared__ float wmax[D3_NT / 64];
   const int c = blockIdx.y;
   const int64_t m0 = (int64_t)blockIdx.x * D3_T;
   // every descriptor read up front, unconditionally: one round trip of scalar loads instead of
@@ -208,7 +215,7 @@ __global__ __launch_bounds__(256) void decimate3_kernel(const float* sig, const 
     const int64_t v0 = 8 * m0 - 168;
 #pragma unroll
     for (int k = 0; k < D3_LD; ++k) {
-      const int u = threadIdx.x + 256 * k;
+      const int u = threadIdx.x + D3_NT * k;
       const int64_t i = v0 + 4 * u;
       float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
       if (u < D3_P0 / 2) {
@@ -232,7 +239,7 @@ __global__ __launch_bounds__(256) void decimate3_kernel(const float* sig, const 
     float m = 0.0f;  // max |level 0| over the tile's input (the MFMA CQT's f16 scale)
 #pragma unroll
     for (int k = 0; k < D3_LD; ++k) {
-      const int u = threadIdx.x + 256 * k;
+      const int u = threadIdx.x + D3_NT * k;
       if (u < D3_P0 / 2) {
         *reinterpret_cast<float2*>(e0 + 2 * u) = make_float2(pf[k].x, pf[k].z);
         *reinterpret_cast<float2*>(o0 + 2 * u) = make_float2(pf[k].y, pf[k].w);
@@ -247,7 +254,12 @@ __global__ __launch_bounds__(256) void decimate3_kernel(const float* sig, const 
     // one maximum per workgroup, no atomics: slot c + oct_off[c][3] / 256 + blockIdx.x (distinct
     // per chunk; read back by cqt_mfma_kernel)
     if (base == 0 && xmax && threadIdx.x == 0)
-      xmax[c + (base == 0 ? oo3 : oct_off[c * 7 + 3]) / 256 + blockIdx.x] = fmaxf(fmaxf(wmax[0], wmax[1]), fmaxf(wmax[2], wmax[3]));
+    {
+      float m = wmax[0];
+#pragma unroll
+      for (int w = 1; w < D3_NT / 64; ++w) m = fmaxf(m, wmax[w]);
+      xmax[c + (base == 0 ? oo3 : oct_off[c * 7 + 3]) / 256 + blockIdx.x] = m;
+    }
     // level base+1: [4 m0 - 72, +D3_N1), owned [4 m0, 4 m0 + 4 T); phases -> e1/o1
     d3_level(e0, o0, D3_N1, 4 * m0 - 72, L1, h, e1, o1, out1, 72, 4 * D3_T);
     __syncthreads();
@@ -1316,7 +1328,7 @@ int launch_chroma_mean(Context& ctx, const float* sig, const int64_t* chunk_off,
       KTimer kt_(ctx, "decimate", st);
       D3Taps taps;
       std::copy(ctx.t.halfband_f32, ctx.t.halfband_f32 + 2 * kHalfbandK + 1, taps.h);
-      hipLaunchKernelGGL(decimate3_kernel, grid, dim3(256), 0, st, sig, chunk_off, w.oct_off, w.oct_len, w.ws_oct,
+      hipLaunchKernelGGL(decimate3_kernel, grid, dim3(D3_NT), 0, st, sig, chunk_off, w.oct_off, w.oct_len, w.ws_oct,
                          base, taps, w.xmax, kt_.span());
     }
   }
