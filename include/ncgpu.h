@@ -51,7 +51,10 @@ int nc_num_cu(const nc_ctx* ctx);
 /* Opt-in per-kernel timing (no reference equivalent; measurement only).
  * on = 1: the dominant kernels are bracketed by HIP events on their stream AND record
  *         their own execution span; on = 2: spans only (no host work per launch, cheap
- *         enough for a timed region); on = 0: off.
+ *         enough for a timed region); on = 3: events only around the roofline kernels
+ *         ("stft_mel", "cqt_low", "cqt_high", "window_tg"), spans for every kernel (the
+ *         other kernels' event records are host and queue work a timed region need not
+ *         carry); on = 0: off.
  * nc_profile_read(tag) waits for the recorded launches, returns their summed event
  * duration and count, and resets the tag's events.  nc_profile_read_span(tag) returns
  * the summed execution spans (first wave start .. last wave end on the device wall

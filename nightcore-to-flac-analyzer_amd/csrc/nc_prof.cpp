@@ -13,6 +13,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstring>
 #include <map>
 #include <string>
 #include <utility>
@@ -35,6 +36,7 @@ struct KernelTimers {
   // the region the events measure)
   std::vector<std::pair<hipEvent_t, hipEvent_t>> pool;
   bool events = true;
+  bool roof_only = false;   // mode 3: events only around the roofline kernels
   unsigned long long* span_buf = nullptr;   // [kSpanCap][kSpanLines][kSpanStride]: (start, end, pad)
   int span_used = 0;
   double clock_khz = 100000.0;
@@ -70,6 +72,9 @@ KTimer::KTimer(Context& ctx, const char* tag, hipStream_t st) : ctx_(ctx), tag_(
     span_ = t.span_buf + (size_t)t.span_used++ * kSpanLaunchU64;
   }
   if (!t.events) return;
+  if (t.roof_only && std::strcmp(tag_, "stft_mel") && std::strcmp(tag_, "cqt_low") && std::strcmp(tag_, "cqt_high") &&
+      std::strcmp(tag_, "window_tg"))
+    return;
   if (slot.used == slot.ev.size()) {
     if (!t.pool.empty()) {
       slot.ev.push_back(t.pool.back());
@@ -98,12 +103,13 @@ void free_timers(Context& ctx) {
 
 namespace nc {
 
-// mode 0: off; 1: events + spans; 2: spans only
+// mode 0: off; 1: events + spans; 2: spans only; 3: events around the roofline kernels + spans
 void profile_enable(Context& ctx, int mode) {
   free_timers(ctx);
   if (!mode) return;
   auto* t = new KernelTimers();
-  t->events = mode == 1;
+  t->events = mode == 1 || mode == 3;
+  t->roof_only = mode == 3;
   if (t->events) {
     constexpr int kPoolPairs = 1024;   // a 10-step bench region launches ~500 timed kernels
     t->pool.reserve(kPoolPairs);

@@ -41,15 +41,21 @@ def main():
         gp = None if sched == "default" else ([int(v) for v in sched.split(",")] if "," in sched else int(sched))
         for _ in range(2):
             run(gp)
-        off = min(run(gp) for _ in range(3))
-        eng.kernel_profile(1)
-        on = min(run(gp) for _ in range(3))
-        eng.kernel_profile(False)
+        off, on, on3 = [], [], []
+        for _ in range(3):                       # interleaved: off, events on all, events on roofline kernels
+            off.append(run(gp))
+            eng.kernel_profile(1)
+            on.append(run(gp))
+            eng.kernel_profile(3)
+            on3.append(run(gp))
+            eng.kernel_profile(False)
+        off, on, on3 = min(off), min(on), min(on3)
         eng.host_stats = {}
         run(gp)
         hs = {k: round(v / K * 1e3, 3) for k, v in eng.host_stats.items()}
         eng.host_stats = None
-        print(f"{s:>12s}: {off:7.3f} ms/step (timers off)  {on:7.3f} (timers on)  host {hs}", flush=True)
+        print(f"{s:>12s}: {off:7.3f} ms/step (timers off)  {on:7.3f} (events on all)  {on3:7.3f} (events on the "
+              f"roofline kernels)  host {hs}", flush=True)
 
     eng.GROUPS_IN_FLIGHT = gif0
     gp = None
