@@ -147,7 +147,7 @@ def cpu_baseline(seconds, base_seed, workers):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--steps", type=int, default=30)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--pairs", type=int, default=64, help="pairs per GPU (config 3: 64)")
     ap.add_argument("--seconds", type=float, default=180.0)
@@ -257,14 +257,14 @@ def main():
             run_windows(max(1, args.warmup), off)
 
     # timed region: K steps with every launch of the roofline kernels (stft_mel, cqt_low,
-    # cqt_high, window_tg) bracketed by a HIP event pair on the stream it runs on, and every
-    # kernel's own execution span recorded (nc_profile mode 3), so the per-kernel durations below
-    # come from exactly the launches the headline number times.  The roofline divides by the
-    # event durations (dispatch to completion on the kernel's stream, what rocprofv3
-    # --kernel-trace reports, waiting for CUs the other stream holds included); the execution
-    # span (first workgroup start to last workgroup end) is reported beside it.  The other
-    # kernels carry spans only: their event records would be host and queue work in the region
-    eng.kernel_profile(3)
+    # cqt_high, window_tg) bracketed by a HIP event pair on the stream it runs on (nc_profile
+    # mode 4), so the per-kernel durations below come from exactly the launches the headline
+    # number times.  The roofline divides by the event durations (dispatch to completion on the
+    # kernel's stream, what rocprofv3 --kernel-trace reports, waiting for CUs the other stream
+    # holds included).  No other kernel is timed in the region: events around every launch cost
+    # the step ~5 %, the kernels' own execution spans ~3 % (profiles/r4_timer_modes_probe.txt);
+    # every kernel's time alone is in roofline.isolated
+    eng.kernel_profile(4)
     barrier()
     torch.cuda.synchronize()
     # a marker launch (torch.cumsum: no engine kernel is a scan) on each side of the timed region,
@@ -649,8 +649,7 @@ def main():
             # other streams idle
             "roofline": roofline,
             "kernels_ms_per_step": {k: round(v, 4) for k, v in kstep.items()},
-            "kernels_ms_per_step_timing": "HIP events: stft_mel, cqt_low, cqt_high, cqt_chroma, window_tg; "
-                                          "execution spans: the others",
+            "kernels_ms_per_step_timing": "HIP events around the roofline kernels' launches in the timed steps",
             "entry_points_ms_per_step": {k: round(v[0] * v[1], 4) for k, v in per.items()},
             "check": {"tempo_ratio_pair0": tr, "pitch_ratio_pair0": pr},
         }

@@ -54,7 +54,8 @@ int nc_num_cu(const nc_ctx* ctx);
  *         enough for a timed region); on = 3: events only around the roofline kernels
  *         ("stft_mel", "cqt_low", "cqt_high", "window_tg"), spans for every kernel (the
  *         other kernels' event records are host and queue work a timed region need not
- *         carry); on = 0: off.
+ *         carry); on = 4: the events of on = 3 without spans (the spans' per-workgroup clock
+ *         reads and atomics cost the step ~3 %); on = 0: off.
  * nc_profile_read(tag) waits for the recorded launches, returns their summed event
  * duration and count, and resets the tag's events.  nc_profile_read_span(tag) returns
  * the summed execution spans (first wave start .. last wave end on the device wall

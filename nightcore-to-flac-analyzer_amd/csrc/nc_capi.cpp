@@ -174,9 +174,9 @@ int nc_num_cu(const nc_ctx* ctx) { return ctx ? ctx->c.num_cu : -1; }
 int nc_profile_enable(nc_ctx* ctx, int on) {
   CHECK_CTX(ctx);
   SET_DEVICE(ctx);
-  if (on < 0 || on > 3) {
-    nc::set_error("nc_profile_enable: mode must be 0 (off), 1 (events + spans), 2 (spans only) or 3 "
-                  "(events around the roofline kernels + spans)");
+  if (on < 0 || on > 4) {
+    nc::set_error("nc_profile_enable: mode must be 0 (off), 1 (events + spans), 2 (spans only), 3 "
+                  "(events around the roofline kernels + spans) or 4 (events around the roofline kernels)");
     return -1;
   }
   nc::profile_enable(ctx->c, on);

@@ -103,13 +103,14 @@ void free_timers(Context& ctx) {
 
 namespace nc {
 
-// mode 0: off; 1: events + spans; 2: spans only; 3: events around the roofline kernels + spans
+// mode 0: off; 1: events + spans; 2: spans only; 3: events around the roofline kernels + spans;
+// 4: events around the roofline kernels, no spans
 void profile_enable(Context& ctx, int mode) {
   free_timers(ctx);
   if (!mode) return;
   auto* t = new KernelTimers();
-  t->events = mode == 1 || mode == 3;
-  t->roof_only = mode == 3;
+  t->events = mode == 1 || mode == 3 || mode == 4;
+  t->roof_only = mode == 3 || mode == 4;
   if (t->events) {
     constexpr int kPoolPairs = 1024;   // a 10-step bench region launches ~500 timed kernels
     t->pool.reserve(kPoolPairs);
@@ -123,7 +124,8 @@ void profile_enable(Context& ctx, int mode) {
       t->pool.emplace_back(a, b);
     }
   }
-  if (hipMalloc(&t->span_buf, sizeof(unsigned long long) * kSpanCap * kSpanLaunchU64) != hipSuccess)
+  // mode 4 records no spans: every workgroup's clock read and span atomics cost the step ~3 %
+  if (mode != 4 && hipMalloc(&t->span_buf, sizeof(unsigned long long) * kSpanCap * kSpanLaunchU64) != hipSuccess)
     t->span_buf = nullptr;
   int khz = 0;
   if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, ctx.device) == hipSuccess && khz > 0)

@@ -594,7 +594,8 @@ class Engine:
     def kernel_profile(self, on) -> None:
         """The library's per-kernel timers (nc_profile_enable): False/0 off, True/1 HIP events
         around each launch plus the kernels' own execution spans, 2 spans only (cheap enough
-        to leave on in a timed region), 3 events around the roofline kernels only plus spans."""
+        to leave on in a timed region), 3 events around the roofline kernels only plus spans,
+        4 those events alone."""
         self.ctx.call("nc_profile_enable", int(on))
 
     def _profile_read(self, fn: str) -> Dict[str, Tuple[float, int]]:

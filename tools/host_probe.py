@@ -41,21 +41,25 @@ def main():
         gp = None if sched == "default" else ([int(v) for v in sched.split(",")] if "," in sched else int(sched))
         for _ in range(2):
             run(gp)
-        off, on, on3 = [], [], []
-        for _ in range(3):                       # interleaved: off, events on all, events on roofline kernels
+        off, on, on3, on2, on4 = [], [], [], [], []
+        for _ in range(3):                       # interleaved: off, events on all, on roofline kernels, spans only
             off.append(run(gp))
             eng.kernel_profile(1)
             on.append(run(gp))
             eng.kernel_profile(3)
             on3.append(run(gp))
+            eng.kernel_profile(2)
+            on2.append(run(gp))
+            eng.kernel_profile(4)
+            on4.append(run(gp))
             eng.kernel_profile(False)
-        off, on, on3 = min(off), min(on), min(on3)
+        off, on, on3, on2, on4 = min(off), min(on), min(on3), min(on2), min(on4)
         eng.host_stats = {}
         run(gp)
         hs = {k: round(v / K * 1e3, 3) for k, v in eng.host_stats.items()}
         eng.host_stats = None
         print(f"{s:>12s}: {off:7.3f} ms/step (timers off)  {on:7.3f} (events on all)  {on3:7.3f} (events on the "
-              f"roofline kernels)  host {hs}", flush=True)
+              f"roofline kernels)  {on2:7.3f} (spans only)  {on4:7.3f} (events on the roofline kernels, no spans)  host {hs}", flush=True)
 
     eng.GROUPS_IN_FLIGHT = gif0
     gp = None
