@@ -249,9 +249,11 @@ def main():
     for _ in range(max(0, args.warmup - 1)):
         step()
     if not win_mode and not args.no_pipeline and args.warmup > 0:
-        # the pipelined call's own first-use paths (trims queued ahead on the trim stream, their
-        # workspaces and pinned read-back buffers) are warmed too, not only analyze's
-        eng.analyze_batches([own] * 2, params)
+        # the pipelined call itself is warmed at the timed size: its first-use paths (trims queued
+        # ahead on the trim stream, their workspaces and pinned read-back buffers) and the host
+        # memory its K batches of results take.  A first K-batch call in the process ran
+        # 10.2-10.3 ms per step where the next ones ran 9.5-9.7 (profiles/r4_bench_timing_variants.txt)
+        eng.analyze_batches([own] * max(2, args.steps), params)
     if win_mode:
         for off in (0.0, 0.5):
             run_windows(max(1, args.warmup), off)
