@@ -254,9 +254,9 @@ def main():
         # memory its K batches of results take.  A first K-batch call in the process ran
         # 10.2-10.3 ms per step where the next ones ran 9.5-9.7 (profiles/r4_bench_timing_variants.txt)
         eng.analyze_batches([own] * max(2, args.steps), params)
-    if win_mode:
+    if win_mode:   # warmed at the timed size, as the pipelined call above
         for off in (0.0, 0.5):
-            run_windows(max(1, args.warmup), off)
+            run_windows(max(1, args.warmup, args.steps), off)
 
     # timed region: K steps with every launch of the roofline kernels (stft_mel, cqt_low,
     # cqt_high, window_tg) bracketed by a HIP event pair on the stream it runs on (nc_profile
