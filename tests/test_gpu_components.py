@@ -144,3 +144,31 @@ def test_long_windows_match_oracle(eng, window_sec, hop_sec):
     assert out.result.tempo_ratio == ref["tempo_ratio"]
     with pytest.raises(ValueError):
         eng.analyze([(nc, src)], E.Params(window_sec=240.0, hop_sec=60.0))
+
+
+def test_profile_modes_time_what_they_say(eng):
+    """nc_profile_enable: 1 events + spans on every kernel, 2 spans only, 3 events on the
+    roofline kernels + spans, 4 events on the roofline kernels only (the bench's timed region);
+    results identical whichever mode is on (timing never changes the arithmetic)."""
+    nc, src = synth.make_pair(40.0, 1011)
+    p = E.Params(compute_ibi=False)
+    roof = {"stft_mel", "cqt_low", "cqt_high", "window_tg"}
+    ref = eng.analyze([(nc, src)], p)[0].result
+    for mode in (1, 2, 3, 4):
+        eng.kernel_profile(mode)
+        out = eng.analyze([(nc, src)], p)[0].result
+        ev, sp = eng.kernel_times(), eng.kernel_spans()
+        eng.kernel_profile(0)
+        assert (out.tempo_ratio, out.pitch_ratio, out.tempo_ci, out.pitch_ci) == \
+               (ref.tempo_ratio, ref.pitch_ratio, ref.tempo_ci, ref.pitch_ci)
+        ev_k = set(ev) - {"cqt_chroma"}
+        sp_k = set(sp) - {"cqt_chroma"}
+        if mode == 1:
+            assert roof <= ev_k and roof <= sp_k and "decimate" in ev_k and "decimate" in sp_k
+        elif mode == 2:
+            assert not ev_k and roof <= sp_k
+        elif mode == 3:
+            assert ev_k == roof and roof <= sp_k and "decimate" in sp_k
+        else:
+            assert ev_k == roof and not sp_k
+        assert all(ms > 0 and n > 0 for ms, n in ev.values())
