@@ -28,7 +28,9 @@
 
 namespace nc {
 
-constexpr int SF_WAVES = 14;
+// 16 waves (four per SIMD at 110 VGPRs; 147 KB of LDS with full exchange slots): 3.95 -> 3.58 ms
+// per 128 3-min files against 14 (round 4, profiles/r4_spectral_waves_ab.txt), outputs unchanged
+constexpr int SF_WAVES = 16;
 constexpr int SF_THREADS = SF_WAVES * 64;
 constexpr int SF_BINS = 1025;
 constexpr int SF_ROW = 1028;  // dB row stride (floats): 16-byte aligned rows
