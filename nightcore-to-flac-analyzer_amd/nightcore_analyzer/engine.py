@@ -83,6 +83,20 @@ TUNING_NEAR_TIE = 1  # tuning decisions whose histogram argmax leads by at most 
 _logger = logging.getLogger("nightcore_analyzer")
 
 
+class _GcPaused:
+    """Python's cyclic collector paused for a host-heavy call (restored on exit): a generation-2
+    pass over a long-lived process's objects costs milliseconds and lands at random inside it;
+    the calls that use this create no reference cycles."""
+
+    def __enter__(self):
+        self.was = gc.isenabled()
+        gc.disable()
+
+    def __exit__(self, *exc):
+        if self.was:
+            gc.enable()
+
+
 class _DevSpan:
     """A typed span of a device byte buffer as the native entry points take it: an address
     and a length.  Carving the pipeline's ~50 plan and result arrays as torch views costs a
@@ -739,6 +753,10 @@ class Engine:
         its own rate srs[f]).  Queues the launch and the D2H copy of the per-file sums (and,
         with frame_rms, of the frame RMS); returns (event, host views, keep-alive).
         ``spectral_finish`` turns the views into per-file statistics."""
+        with _GcPaused():
+            return self._spectral_frames(buf, off, length, srs, roll_percent, frame_rms)
+
+    def _spectral_frames(self, buf, off, length, srs, roll_percent, frame_rms):
         off = np.asarray(off, np.int64)
         length = np.asarray(length, np.int64)
         n = len(off)
@@ -765,11 +783,11 @@ class Engine:
         up.add("base", base, np.int64)
         up.add("hz", hz, np.float64)
         up.add("bands", bands, np.int32)
-        d = up.commit(self.dev)
+        d = up.commit(self.dev, spans=True)
         ar = _Arena()
         ar.add("stats", 12 * n, np.float64)
         ar.add("bins", 1025 * n, np.float64)
-        o = ar.commit(self.dev)
+        o = ar.commit(self.dev, spans=True)
         rms = torch.empty(int(base[-1]), dtype=torch.float32, device=self.dev)
         tot, mx = int(base[-1]), int(T.max())
         ws = self.workspace("spectral", self.ctx.lib.nc_spectral_workspace_bytes(tot, n, mx))
@@ -791,6 +809,11 @@ class Engine:
     def spectral_finish(h) -> List[dict]:
         """Per-file SpectralStats fields from the device sums (spectral.py:54-94): means over
         the T_f frames and band bins, the effective bandwidth from the per-bin dB means."""
+        with _GcPaused():
+            return Engine._spectral_finish(h)
+
+    @staticmethod
+    def _spectral_finish(h) -> List[dict]:
         n = len(h["srs"])
         st = h["stats"].reshape(n, 12)
         T = h["T"].astype(np.float64)
