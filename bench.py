@@ -306,6 +306,9 @@ def main():
             raise RuntimeError("analyze_batches returned an incomplete result")
         if any(r[0].result.tempo_ratio != tr or r[0].result.pitch_ratio != pr for r in res):
             raise RuntimeError("a pipelined batch differs from the single-call result")
+        # the checked outcomes (K x 64 pairs) are not kept: holding them slowed the side legs
+        # measured after (spectral.analyze 5.0 -> 9.9 ms per call; profiles/r4_bench_timing_variants.txt)
+        del res
     evt = eng.kernel_times()
     spans = eng.kernel_spans()
     eng.kernel_profile(False)
