@@ -301,6 +301,7 @@ def main():
         win_total = sum_over_ranks(sum(o.detail["energy_src"].size + o.detail["energy_nc"].size for o in mine))
         if rank == 0 and (mine[0].result.tempo_ratio != tr or mine[0].result.pitch_ratio != pr):
             raise RuntimeError("the window-sharded result of pair 0 differs from the single-GPU engine's")
+        del res, mine                           # not kept (see below)
     elif pipelined:
         if len(res) != args.steps or any(len(r) != len(outs) for r in res):
             raise RuntimeError("analyze_batches returned an incomplete result")
