@@ -81,10 +81,35 @@ def synth_lengths(seconds):
     return synth.pair_lengths(seconds)
 
 
-def _pmc_traffic(kernel_tag):
+def build_provenance():
+    """What build a measurement comes from: the sha256 of the kernel sources (csrc/*, include/,
+    prefix 16), of the loaded libncgpu.so, and the git commit (git, or .build_commit written by
+    tools/stamp_commit.sh before a GPU call: the snapshot sent to the box has no .git)."""
+    import hashlib
+    import subprocess
+    h = hashlib.sha256()
+    src = sorted((REPO / "nightcore-to-flac-analyzer_amd" / "csrc").glob("*")) + sorted((REPO / "include").glob("*.h"))
+    for f in src:
+        h.update(f.name.encode())
+        h.update(f.read_bytes())
+    lib = Path(os.environ.get("NCGPU_LIB") or REPO / "nightcore-to-flac-analyzer_amd" / "nightcore_analyzer" / "_lib"
+               / "libncgpu.so")
+    lib_sha = hashlib.sha256(lib.read_bytes()).hexdigest()[:16] if lib.exists() else None
+    try:
+        commit = subprocess.run(["git", "rev-parse", "--short", "HEAD"], cwd=REPO, capture_output=True,
+                                text=True, timeout=10).stdout.strip()
+    except (OSError, subprocess.SubprocessError):
+        commit = ""
+    if not commit and (REPO / ".build_commit").exists():
+        commit = (REPO / ".build_commit").read_text().strip()
+    return {"src_sha": h.hexdigest()[:16], "lib_sha": lib_sha, "commit": commit or "unknown"}
+
+
+def _pmc_traffic(kernel_tag, prov=None):
     """HBM bytes per launch of a kernel from the newest committed rocprofv3 PMC pass
     (profiles/r*_traffic.json, FETCH_SIZE x 2 + WRITE_SIZE per MI355X_MICROARCH.md), if one
-    exists for this workload; counters cannot be read from inside a timed run."""
+    exists for this workload; counters cannot be read from inside a timed run.  `stale`: the
+    file's kernel-source hash differs from this build's (or it records none)."""
     best = None
     for f in sorted((REPO / "profiles").glob("r*_traffic.json")):
         try:
@@ -93,7 +118,9 @@ def _pmc_traffic(kernel_tag):
             continue
         k = d.get("kernels", {}).get(kernel_tag)
         if k and d.get("workload") == "config3-64pairs":
-            best = {"bytes_per_launch": k["hbm_bytes_per_launch"], "source": f"profiles/{f.name}"}
+            best = {"bytes_per_launch": k["hbm_bytes_per_launch"], "source": f"profiles/{f.name}",
+                    "commit": d.get("commit"), "src_sha": d.get("src_sha"),
+                    "stale": prov is None or d.get("src_sha") != prov["src_sha"]}
     return best
 
 
@@ -231,12 +258,15 @@ def main():
 
     lengths = [n for _ in range(world * P) for n in synth_lengths(args.seconds)]
 
-    def run_windows(k, split_offset=0.0):
-        """k steps of the window-sharded analysis (interior groups pipelined across steps)."""
+    def run_windows(k, split_offset=0.0, gather=True):
+        """k steps of the window-sharded analysis (interior groups pipelined across steps).
+        gather=True is analyze_sharded's default: every step's outcomes of all pairs end on
+        every rank (an all-gather after the step's last record exchange)."""
         from nightcore_analyzer.sharded import DeviceStages, analyze_sharded
         res = analyze_sharded(DeviceStages(eng, signals), params, lengths=lengths, local_pairs=ids,
-                              split_offset=split_offset, gather=False, steps=k)
-        return [res] if k == 1 else res
+                              split_offset=split_offset, gather=gather, steps=k)
+        res = [res] if k == 1 else res
+        return [[(None, o) for o in r] for r in res] if gather else res
 
     outs = step()
     bad = [i for i, o in enumerate(outs) if o.error is not None]
@@ -295,10 +325,10 @@ def main():
     torch.cumsum(marker, 0)
     torch.cuda.synchronize()
     if win_mode:
-        mine = [o for _, o in res[0]]
-        if any(o.error is not None for o in mine) or any(len(r) != len(res[0]) for r in res):
+        mine = [o for _, o in res[0]]           # gather=True: every pair's outcome on every rank
+        if any(o.error is not None for o in mine) or any(len(r) != world * P for r in res):
             raise RuntimeError("a window-sharded step failed or returned an incomplete result")
-        win_total = sum_over_ranks(sum(o.detail["energy_src"].size + o.detail["energy_nc"].size for o in mine))
+        win_total = sum(o.detail["energy_src"].size + o.detail["energy_nc"].size for o in mine)
         if rank == 0 and (mine[0].result.tempo_ratio != tr or mine[0].result.pitch_ratio != pr):
             raise RuntimeError("the window-sharded result of pair 0 differs from the single-GPU engine's")
         del res, mine                           # not kept (see below)
@@ -313,6 +343,29 @@ def main():
     evt = eng.kernel_times()
     spans = eng.kernel_spans()
     eng.kernel_profile(False)
+
+    # device idle, untraced: extra steps of the same call with every kernel recording its own
+    # execution span (profile mode 2, ~3 % slower than the timed steps), then 1 - the union of the
+    # spans over their extent (nc_profile_read_busy).  The extent starts at the call's first
+    # kernel, so the call's start-up (first trim read-back, first group plan) is in it
+    n_idle = max(2, min(args.steps, 10))
+    eng.kernel_profile(2)
+    barrier()
+    torch.cuda.synchronize()
+    if win_mode:
+        run_windows(n_idle)
+    elif pipelined:
+        eng.analyze_batches([own] * n_idle, params)
+    else:
+        for _ in range(n_idle):
+            step()
+    busy_ms, extent_ms, idle_launches = eng.device_busy()
+    eng.kernel_profile(False)
+    idle_frac = max_over_ranks(1.0 - busy_ms / extent_ms) if extent_ms > 0 else None
+    device_idle = {"frac": idle_frac, "busy_ms": busy_ms, "extent_ms": extent_ms, "steps": n_idle,
+                   "launches": idle_launches,
+                   "how": "untimed steps of the headline call, every engine kernel's execution span recorded "
+                          "(nc_profile_read_busy): 1 - union of spans / first start..last end; max over ranks"}
     el = max_over_ranks(el)
     step_ms = el / args.steps * 1e3
     value = (win_total if win_mode else world * win_per_step) * args.steps / el
@@ -321,9 +374,11 @@ def main():
     modes = None
     if world > 1:
         modes = {}
-        variants = [("pairs", None), ("windows_split", 0.5)] if win_mode else [("windows", 0.0),
-                                                                                ("windows_split", 0.5)]
-        for name, off in variants:
+        # windows_nogather: the headline's steps without the final outcome all-gather (each rank
+        # keeps the outcomes of the pairs it owns)
+        variants = [("windows_nogather", 0.0, False), ("pairs", None, False), ("windows_split", 0.5, True)] \
+            if win_mode else [("windows", 0.0, True), ("windows_split", 0.5, True)]
+        for name, off, gat in variants:
             barrier()
             torch.cuda.synchronize()
             t1 = time.perf_counter()
@@ -331,9 +386,10 @@ def main():
                 eng.analyze_batches([own] * args.steps, params)
                 n_win = world * win_per_step
             else:
-                r_ = run_windows(args.steps, off)
-                n_win = sum_over_ranks(sum(o.detail["energy_src"].size + o.detail["energy_nc"].size
-                                           for _, o in r_[0]))
+                r_ = run_windows(args.steps, off, gat)
+                n_win = (sum(o.detail["energy_src"].size + o.detail["energy_nc"].size for _, o in r_[0]) if gat else
+                         sum_over_ranks(sum(o.detail["energy_src"].size + o.detail["energy_nc"].size
+                                            for _, o in r_[0])))
             torch.cuda.synchronize()
             barrier()
             e1 = max_over_ranks(time.perf_counter() - t1)
@@ -376,6 +432,8 @@ def main():
     # compute roof per kernel: f32 VALU for the FFT kernels, f64 VALU for the tempogram
     compute_roof = {"window_tg": ("valu_f64", F64_PEAK_TFS), "cqt_chroma": ("mfma_f16", MFMA_F16_PEAK_TFS)}
 
+    prov = build_provenance()
+
     def roof(tag, times, table=None, span=None):
         table = table or units
         if tag not in times or tag not in table:
@@ -386,10 +444,13 @@ def main():
         a = alg / (avg_ms * 1e-3) / 1e9
         c = flop / (avg_ms * 1e-3) / 1e12
         cb, cp = compute_roof.get(tag, ("valu_f32", VALU_PEAK_TFS))
-        tr = _pmc_traffic(tag)
+        tr = _pmc_traffic(tag, prov)
         out = {"bound": "hbm", "kernel": tag, "achieved": a, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                "frac": a / HBM_PEAK_GBS, "traffic": tr["bytes_per_launch"] if tr else None,
-               "traffic_source": tr["source"] if tr else None, "alg_bytes_per_launch": alg, "avg_launch_ms": avg_ms,
+               "traffic_source": tr["source"] if tr else None,
+               "traffic_commit": tr["commit"] if tr else None,
+               "traffic_stale": tr["stale"] if tr else None,
+               "alg_bytes_per_launch": alg, "avg_launch_ms": avg_ms,
                "launches_per_step": launches, "timing": "HIP events around each launch on its stream",
                "exec_span_ms": span.get(tag) if span else None,
                # the roof that actually binds: VALU / f64 VALU / matrix cores
@@ -639,7 +700,9 @@ def main():
                     + (f"; REHEARSAL: {world} ranks on {torch.cuda.device_count()} GPU(s), gloo" if rehearse else ""),
             "config": {"workload": ("config 3: per GPU a batch of 64 x 3-min 22.05 kHz mono pairs" if world == 1 else
                                     f"config 4 shape: a batch of {world} x 64 x 3-min 22.05 kHz mono pairs, its windows "
-                                    "and chunk pairs split over the ranks (sharded.shard_plan)" if win_mode else
+                                    "and chunk pairs split over the ranks (sharded.shard_plan), every step's outcomes "
+                                    "all-gathered to every rank (analyze_sharded's default gather=True; without it: "
+                                    "modes.windows_nogather)" if win_mode else
                                     f"{world} x 64 x 3-min pairs, whole pairs per rank")
                                    + "; step = pipeline.run analysis of the batch without the hop-64 IBI pass"
                                    + ("; the K steps issued as one pipelined call (batch k+1's trim and first "
@@ -654,10 +717,19 @@ def main():
             # the kernel's own first-start .. last-end span; isolated: the same kernels with the
             # other streams idle
             "roofline": roofline,
-            "kernels_ms_per_step": {k: round(v, 4) for k, v in kstep.items()},
-            "kernels_ms_per_step_timing": "HIP events around the roofline kernels' launches in the timed steps",
+            "device_idle_frac": idle_frac,
+            "device_idle": device_idle,
+            "kernels_ms_per_step": {**{k: round(v[0], 4) for k, v in iso.items()},
+                                    **{k: round(v, 4) for k, v in kstep.items()}},
+            "kernels_ms_per_step_timing": {
+                "timed_region": sorted(kstep),
+                "isolated_step": sorted(set(iso) - set(kstep)),
+                "how": "the roofline kernels: HIP events around their launches in the timed steps (sharing the "
+                       "chip with the other streams); every other kernel: HIP events in one more step with the "
+                       "streams serialized (roofline.isolated)"},
             "entry_points_ms_per_step": {k: round(v[0] * v[1], 4) for k, v in per.items()},
             "check": {"tempo_ratio_pair0": tr, "pitch_ratio_pair0": pr},
+            "build": prov,
         }
         if modes is not None:
             line["modes"] = modes

@@ -63,10 +63,14 @@ int nc_num_cu(const nc_ctx* ctx);
  * queues behind other streams' work) and resets the tag's spans.  Tags: "stft_mel",
  * "window_tg", "tuning_peaks", "decimate", "cqt_chroma", "trim_blocks", "tempo_beat",
  * "tg_slide", "spectral_frames", "spectral_bins".  Enabling (or disabling) discards
- * pending records. */
+ * pending records.  nc_profile_read_busy (modes 1-3) returns the union of every span
+ * recorded since the last read, all tags together (device busy time), the extent from the
+ * first start to the last end, and the number of spanned launches, and clears the spans:
+ * 1 - busy / extent is the device's idle fraction over those launches. */
 int nc_profile_enable(nc_ctx* ctx, int on);
 int nc_profile_read(nc_ctx* ctx, const char* tag, double* total_ms, int* launches);
 int nc_profile_read_span(nc_ctx* ctx, const char* tag, double* total_ms, int* launches);
+int nc_profile_read_busy(nc_ctx* ctx, double* busy_ms, double* extent_ms, int* launches);
 
 /* ---------------------------------------------------------------------------
  * K1a  silence trim — replaces io.strip_silence (io.py:58-79) ->

@@ -1148,6 +1148,354 @@ __global__ __launch_bounds__(CL_NW * 64) void cqt_mfma_low_kernel(CqmArgs a) {
   }
 }
 
+// ---- Octaves 0-2, round 5: one 64-frame tile per wave.
+// The round-2 kernel above split every A fragment from f32 at each of the M k-steps that read
+// its block row (4.8 VALU per MFMA: the issue port, not the matrix core, was full) and ran
+// 30 MFMAs per k-step per wave against a barrier and a vmcnt(0) drain per step.  Here:
+//  * a wave owns a whole tile (4 row tiles x 5 column tiles x 3 products = 60 MFMAs per k-step),
+//    four tiles of one (chunk, octave) per workgroup share the filter slices;
+//  * the block of group g + 1 (NR rows x 32 samples) is loaded into registers at group g's
+//    first step and split ONCE into this wave's f16 hi / lo image at the group's last step
+//    (cm_split: the same values the per-fragment split produced), so a k-step's A fragments
+//    are plain ds_read_b128s at immediate offsets (1 VALU per MFMA on octave 0, less above);
+//  * filter slices go through a 4-slot ring, issued three steps ahead and retired with counted
+//    vmcnt waits: every wave issues the same vector-memory sequence (3 slice pieces per step,
+//    10 block loads at a group's first step), so the count of younger operations is static per
+//    k-step position (c2_wait_slice).  Block loads are dword-aligned dwordx4 (gfx950 serves
+//    unaligned global loads), so an unaligned chunk issues the same instructions; an edge tile
+//    loads clamped pieces and zeroes the samples outside the signal when it splits.
+// Accumulation order per accumulator is the round-2 kernel's (k-steps group by group, hh, hl, lh
+// per step): chroma is bit-identical.  LDS: 40 KB ring + 4 x 9 KB images = 76 KB, two workgroups
+// per CU.
+#ifndef C2_BLOCK_WAIT0
+#define C2_BLOCK_WAIT0 1
+#endif
+#ifndef C2_NW_
+#define C2_NW_ 4
+#endif
+#ifndef C2_R_
+#define C2_R_ 4
+#endif
+#ifndef C2_WPS
+#define C2_WPS 2
+#endif
+constexpr int C2_NW = C2_NW_;                             // tiles (waves) per workgroup
+constexpr int C2_R = C2_R_;                               // filter ring slots
+constexpr int C2_D = C2_R - 1;                            // slices requested ahead of the step that reads them
+constexpr int C2_PS = (CM_NT * 2 + C2_NW - 1) / C2_NW;    // slice DMA pieces per wave per step
+constexpr int C2_NRP = 72;                                // image rows per wave (>= 64 + M - 1)
+constexpr int C2_IMG = C2_NRP * 64;                       // bytes of one hi (or lo) image
+constexpr int C2_RING = C2_R * CM_SLICE * 16;
+constexpr int C2_NU = (C2_NRP * 4 + 63) / 64;             // staging rounds (8-sample units per lane)
+constexpr int C2_NL = 2 * C2_NU;                          // block loads per wave per group
+static_assert(C2_NW * 2 * C2_IMG >= C2_NW * CM_FR * kCqtFilt * 4, "epilogue rows fit the images");
+size_t cql2_lds_bytes() { return C2_RING + C2_NW * 2 * C2_IMG; }
+
+// image row R keeps its 16-byte piece p (8 halves) at slot p ^ c2_sw(R): every ds_read_b128 lane
+// group of an A fragment (rows r..r+15 at pieces 0..3, any r) and every ds_write_b128 group of the
+// split (two rows x four pieces) hits distinct banks (checked in tests/test_lds_layout_cpu.py)
+__host__ __device__ constexpr int c2_sw(int R) { return ((R >> 2) & 1) << 1; }
+
+__device__ __forceinline__ void c2_ld16(cm_u4& d, const float* p) {
+  asm volatile("global_load_dwordx4 %0, %1, off" : "=&v"(d) : "v"(p) : "memory");
+}
+template <int N>
+__device__ __forceinline__ void c2_vmwait() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"i"(N) : "memory");
+}
+template <int N>
+__device__ __forceinline__ void c2_vmwait_st(cm_u4 (&st)[C2_NL]) {
+  static_assert(C2_NL == 10, "staging registers");
+  asm volatile("s_waitcnt vmcnt(%10)"
+               : "+v"(st[0]), "+v"(st[1]), "+v"(st[2]), "+v"(st[3]), "+v"(st[4]), "+v"(st[5]), "+v"(st[6]),
+                 "+v"(st[7]), "+v"(st[8]), "+v"(st[9])
+               : "i"(N)
+               : "memory");
+}
+
+template <int OCT>
+struct C2 {
+  static constexpr int H = 512 >> OCT, G = H / 32, M = 1024 / H, NR = CM_FR + M - 1;
+  // the block loads of a group are issued at its first step (after that step's slice pieces),
+  // and the groups before the last stage the next block
+  __host__ __device__ static constexpr bool stage_at(int q, bool last) { return q == 0 && !last; }
+  // did step n - j (j >= 1) issue block loads, n at group position q (`last`: the final group)?
+  // In the same group: only at position 0 of a group that is not the last; in an earlier group
+  // (q < j): at position (q - j) mod M == 0 (an earlier group is never the last)
+  __host__ __device__ static constexpr bool staged(int q, int j, bool last) {
+    return q >= j ? (q == j && !last) : ((q - j) % M + M) % M == 0;
+  }
+  // did step n - j issue slice n - j + D (only the last group's final steps do not)?
+  __host__ __device__ static constexpr bool sliced(int q, int j, bool last) { return !last || q - j + C2_D < M; }
+  // vector-memory operations this wave issued after its pieces of slice n (issued at step n - D)
+  // when step n starts: the block loads of steps n - D .. n - 1 and slices n + 1 .. n + D - 1.
+  // Steps 0 .. D - 1 over-count (slices 0 .. D - 1 and block 0 were drained in the prologue).
+  __host__ __device__ static constexpr int younger(int q, bool last) {
+    int y = 0;
+    for (int j = 1; j <= C2_D; ++j) y += staged(q, j, last) ? C2_NL : 0;
+    for (int j = 1; j < C2_D; ++j) y += sliced(q, j, last) ? C2_PS : 0;
+    return y;
+  }
+};
+
+// vmcnt(younger(q, last)): retires this wave's pieces of slice n (this step's slot)
+template <int OCT, int Q>
+__device__ __forceinline__ void c2_wait_slice(bool last) {
+#if C2_SLICE_WAIT0
+  c2_vmwait<0>();
+#else
+  if (last) c2_vmwait<C2<OCT>::younger(Q, true)>();
+  else c2_vmwait<C2<OCT>::younger(Q, false)>();
+#endif
+}
+
+// Block g of this wave's tile into registers: 8-sample unit u = 64 k + lane is row min(u / 4,
+// NR - 1), piece u % 4, samples s0 + R H + 32 g + 8 p + [0, 8).  Edge tiles load from clamped
+// positions (every load stays inside the signal); c2_split puts the true samples in place.
+template <int OCT>
+__device__ __forceinline__ void c2_stage(cm_u4 (&st)[C2_NL], const float* y, int64_t s0, int g, int64_t Ly,
+                                         bool edge, int lane) {
+  using L = C2<OCT>;
+#pragma unroll
+  for (int k = 0; k < C2_NU; ++k) {
+    const int u = 64 * k + lane;
+    const int R = min(u >> 2, L::NR - 1), p = u & 3;
+    int64_t q = s0 + (int64_t)R * L::H + 32 * g + 8 * p;
+    int64_t q1 = q + 4;
+    if (edge) {
+      q = max((int64_t)0, min(q, Ly - 4));
+      q1 = max((int64_t)0, min(q1, Ly - 4));
+    }
+    c2_ld16(st[2 * k], y + q);
+    c2_ld16(st[2 * k + 1], y + q1);
+  }
+}
+
+// sample q + e of an edge piece loaded from the clamped position b (zero outside [0, Ly))
+__device__ __forceinline__ float c2_pick(const cm_u4& v, int64_t q, int e, int64_t Ly) {
+  const int64_t b = max((int64_t)0, min(q, Ly - 4));
+  const int64_t d = q + e - b;
+  const float x = d == 0 ? __uint_as_float(v[0]) : d == 1 ? __uint_as_float(v[1]) : d == 2 ? __uint_as_float(v[2])
+                                                                                             : __uint_as_float(v[3]);
+  return (q + e >= 0 && q + e < Ly && d >= 0 && d < 4) ? x : 0.0f;
+}
+
+// the staged block split into this wave's hi / lo images (rows < NR)
+template <int OCT>
+__device__ __forceinline__ void c2_split(const cm_u4 (&st)[C2_NL], char* img, float sx, int64_t s0, int g,
+                                         int64_t Ly, bool edge, int lane) {
+  using L = C2<OCT>;
+#pragma unroll
+  for (int k = 0; k < C2_NU; ++k) {
+    const int u = 64 * k + lane;
+    const int R = u >> 2, p = u & 3;
+    if (64 * k + 63 >= 4 * L::NR && R >= L::NR) continue;
+    float v[8];
+    if (edge) {
+      const int64_t q = s0 + (int64_t)R * L::H + 32 * g + 8 * p;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        v[e] = c2_pick(st[2 * k], q, e, Ly);
+        v[4 + e] = c2_pick(st[2 * k + 1], q + 4, e, Ly);
+      }
+    } else {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        v[e] = __uint_as_float(st[2 * k][e]);
+        v[4 + e] = __uint_as_float(st[2 * k + 1][e]);
+      }
+    }
+    cm_half8 h, l;
+    cm_split(v, sx, h, l);
+    const int off = R * 64 + 16 * (p ^ c2_sw(R));
+    *reinterpret_cast<cm_half8*>(img + off) = h;
+    *reinterpret_cast<cm_half8*>(img + C2_IMG + off) = l;
+  }
+}
+
+template <int OCT, bool EDGE>
+__device__ __forceinline__ void cqt_low2(const CqmArgs& a, int bx, int c) {
+  using L = C2<OCT>;
+  constexpr int H = L::H, G = L::G, M = L::M;
+  static_assert(G * M == CM_KS && M >= 2 && L::NR <= C2_NRP, "k-step groups");
+  const Span span_(a.span);
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  uint4* sB = reinterpret_cast<uint4*>(smem);  // [C2_R][CM_SLICE]
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  // every descriptor read up front, unconditionally: one round trip of scalar loads
+  const int T = a.n_frames[c], ti = a.tuning_idx[c], ex = a.oct_ex[c * 7 + OCT];
+  const int64_t yoff = OCT == 0 ? a.chunk_off[c] : a.oct_off[c * 7 + OCT], Ly = a.oct_len[c * 7 + OCT];
+  if (bx * (C2_NW * CM_FR) >= T) return;
+  int t0 = (bx * C2_NW + wave) * CM_FR;
+  const bool active = t0 < T;  // an idle tile's wave still issues the DMA, the loads and the barriers
+  if (!active) t0 = 0;
+  const float* y = (OCT == 0 ? a.sig : a.ws_oct) + yoff;
+  const int64_t s0 = (int64_t)t0 * H - 512;
+  const bool edge = !(s0 >= 0 && s0 + (int64_t)(CM_FR - 1) * H + kCqtNfft <= Ly);
+  if (edge != EDGE) return;  // wave-uniform; both instances issue the same barriers
+  const uint4* bsrc = a.bfrag + (size_t)ti * (CM_KS * CM_SLICE);
+  char* img = smem + C2_RING + wave * (2 * C2_IMG);
+  const float sx = ldexpf(1.0f, ex);
+  auto kstep = [](int n) { return n / M + G * (n % M); };
+  auto fetch_slice = [&](int n) {
+#pragma unroll
+    for (int j = 0; j < C2_PS; ++j) {
+      int i = wave + C2_NW * j;
+      if (i >= CM_NT * 2) i = wave;  // duplicate of this wave's first piece (same bytes, same place)
+      cm_dma16(bsrc + kstep(n) * CM_SLICE + i * 64 + lane, sB + (n % C2_R) * CM_SLICE + i * 64);
+    }
+  };
+
+  // prologue: slices 0-2 in flight, block 0 split, block 1 requested at step 0
+  for (int d = 0; d < C2_D; ++d) fetch_slice(d);
+  cm_u4 st[C2_NL];
+  c2_stage<OCT>(st, y, s0, 0, Ly, EDGE, lane);
+  c2_vmwait_st<0>(st);
+  if (active) c2_split<OCT>(st, img, sx, s0, 0, Ly, EDGE, lane);
+
+  cm_f4 acc[CM_RT][CM_NT];
+#pragma unroll
+  for (int rt = 0; rt < CM_RT; ++rt)
+#pragma unroll
+    for (int nt = 0; nt < CM_NT; ++nt) acc[rt][nt] = cm_f4{0.f, 0.f, 0.f, 0.f};
+  const int kp = lane >> 4, rl = lane & 15;
+  const uint32_t img_a = lds_addr(img);
+
+  auto step = [&](auto qc, int g, bool last) {
+    constexpr int Q = decltype(qc)::value;
+    const int n = g * M + Q;
+    // retire this wave's pieces of slice n (counted: slices n + 1, n + 2 and the block loads stay
+    // in flight); the barrier makes every wave's pieces visible and ends every read of slot
+    // (n + 3) % R (step n - 1's)
+    c2_wait_slice<OCT, Q>(last);
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's image writes
+#if !C2_PROBE_NOBAR   // timing probe only: races
+    __builtin_amdgcn_s_barrier();
+#endif
+    asm volatile("" ::: "memory");
+    if (n + C2_D < CM_KS) fetch_slice(n + C2_D);
+    if (L::stage_at(Q, last)) c2_stage<OCT>(st, y, s0, g + 1, Ly, EDGE, lane);
+    if (active) {
+      // A fragments: rows 16 rt + rl + Q of the image (this wave's own: no barrier guards it)
+      const int R = rl + Q;
+      const uint32_t aa = img_a + R * 64 + 16 * (kp ^ c2_sw(R));
+      const uint32_t sbl = lds_addr(sB + (n % C2_R) * CM_SLICE + lane);
+      cm_u4 ah4[CM_RT], al4[CM_RT], b[CM_NT][2];
+      cm_rd<0 * 1024>(ah4[0], aa);
+      cm_rd<1 * 1024>(ah4[1], aa);
+      cm_rd<2 * 1024>(ah4[2], aa);
+      cm_rd<3 * 1024>(ah4[3], aa);
+      cm_rd<C2_IMG + 0 * 1024>(al4[0], aa);
+      cm_rd<C2_IMG + 1 * 1024>(al4[1], aa);
+      cm_rd<C2_IMG + 2 * 1024>(al4[2], aa);
+      cm_rd<C2_IMG + 3 * 1024>(al4[3], aa);
+      cm_rd<0 * 1024>(b[0][0], sbl);
+      cm_rd<1 * 1024>(b[0][1], sbl);
+      cm_rd<2 * 1024>(b[1][0], sbl);
+      cm_rd<3 * 1024>(b[1][1], sbl);
+      cm_wait<4>(ah4[0], ah4[1], ah4[2], ah4[3]);  // A + tile 0 landed; tile 1 in flight
+      cm_wait<4>(al4[0], al4[1], al4[2], al4[3]);
+      cm_half8 ah[CM_RT], al[CM_RT];
+#pragma unroll
+      for (int rt = 0; rt < CM_RT; ++rt) {
+        ah[rt] = __builtin_bit_cast(cm_half8, ah4[rt]);
+        al[rt] = __builtin_bit_cast(cm_half8, al4[rt]);
+      }
+      auto tile = [&](int nt) {
+        const cm_half8 bh = __builtin_bit_cast(cm_half8, b[nt][0]);
+        const cm_half8 bl = __builtin_bit_cast(cm_half8, b[nt][1]);
+#if C2_PROBE_NOMFMA   // timing probe only: no matrix work
+        acc[0][nt][0] += (float)bh[0] + (float)bl[1] + (float)ah[0][2] + (float)al[3][3];
+#else
+#pragma unroll
+        for (int rt = 0; rt < CM_RT; ++rt) {
+          acc[rt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[rt], bh, acc[rt][nt], 0, 0, 0);
+          acc[rt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[rt], bl, acc[rt][nt], 0, 0, 0);
+          acc[rt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al[rt], bh, acc[rt][nt], 0, 0, 0);
+        }
+#endif
+      };
+      cm_wait<2>(b[0][0], b[0][1]);
+      cm_rd<4 * 1024>(b[2][0], sbl);
+      cm_rd<5 * 1024>(b[2][1], sbl);
+      tile(0);
+      cm_wait<2>(b[1][0], b[1][1]);
+      cm_rd<6 * 1024>(b[3][0], sbl);
+      cm_rd<7 * 1024>(b[3][1], sbl);
+      tile(1);
+      cm_wait<2>(b[2][0], b[2][1]);
+      cm_rd<8 * 1024>(b[4][0], sbl);
+      cm_rd<9 * 1024>(b[4][1], sbl);
+      tile(2);
+      cm_wait<2>(b[3][0], b[3][1]);
+      tile(3);
+      cm_wait<0>(b[4][0], b[4][1]);
+      tile(4);
+    }
+    if (Q == M - 1 && !last) {
+      // block g + 1 (requested at this group's first step) into the image: every A read of
+      // group g is done (their registers were consumed above); younger than the block loads
+      // are the slice pieces of steps n - M + 2 .. n (none past slice 31)
+      if (C2_BLOCK_WAIT0 || (M == 2 && n + C2_D >= CM_KS)) c2_vmwait_st<0>(st);
+      else c2_vmwait_st<(M - 1) * C2_PS>(st);
+#if !C2_PROBE_NOSPLIT   // timing probe only: the image keeps block 0
+      if (active) c2_split<OCT>(st, img, sx, s0, g + 1, Ly, EDGE, lane);
+#endif
+    }
+  };
+#pragma unroll 1
+  for (int g = 0; g < G; ++g) {
+    const bool last = g == G - 1;
+    static_for<M>([&](auto qc) { step(qc, g, last); });
+  }
+  if (!active) return;
+  const int nrow = min(CM_FR, T - t0);
+  float* mg = reinterpret_cast<float*>(img);  // [64][36] rows over this wave's own images
+  {
+    const float oscale = (float)(1 << (OCT >> 1)) * ((OCT & 1) ? 0x1.6a09e6p+0f : 1.0f);
+    const float* isl = a.cqt_isl + ti * kCqtBins + (kCqtBins - kCqtFilt * (OCT + 1));
+    const int* bxp = a.bexp + ti * kCqtFilt;
+    const int col = lane & 15;
+    const float inv0 = ldexpf(1.0f, -(ex + bxp[col])), inv1 = ldexpf(1.0f, -(ex + bxp[16 + col]));
+    const float inv2 = ldexpf(1.0f, -(ex + bxp[32 + (col & 3)]));
+    const float il0 = isl[col], il1 = isl[16 + col], il2 = isl[32 + (col & 3)];
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // this wave's last A reads are done before the rows overlay them
+#pragma unroll
+    for (int rt = 0; rt < CM_RT; ++rt)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int fr = 16 * rt + 4 * (lane >> 4) + i;
+        float* m = mg + fr * kCqtFilt;
+        m[col] = hypotf(acc[rt][0][i] * inv0 * oscale, acc[rt][1][i] * inv0 * oscale) * il0;
+        m[16 + col] = hypotf(acc[rt][2][i] * inv1 * oscale, acc[rt][3][i] * inv1 * oscale) * il1;
+        const float im = __shfl_down(acc[rt][4][i], 4, 16);
+        if (col < 4) m[32 + col] = hypotf(acc[rt][4][i] * inv2 * oscale, im * inv2 * oscale) * il2;
+      }
+  }
+  __builtin_amdgcn_s_waitcnt(0xc07f);
+  __builtin_amdgcn_wave_barrier();
+  float* gp = a.gpart + (a.tf_base[c] + t0) * (7 * 12) + (6 - OCT) * 12;
+  for (int qq = lane; qq < nrow * 12; qq += 64) {
+    const int fl = qq / 12, cc = qq - 12 * fl;
+    const float* m = mg + fl * kCqtFilt;
+    gp[fl * (7 * 12) + cc] = cc == 0 ? (m[0] + m[1]) + m[35] : (m[3 * cc - 1] + m[3 * cc]) + m[3 * cc + 1];
+  }
+}
+
+__global__ __launch_bounds__(C2_NW * 64, C2_WPS) void cqt_mfma_low2_kernel(CqmArgs a) {
+  if (blockIdx.z == 0) {
+    cqt_low2<0, false>(a, blockIdx.x, blockIdx.y);
+    cqt_low2<0, true>(a, blockIdx.x, blockIdx.y);
+  } else if (blockIdx.z == 1) {
+    cqt_low2<1, false>(a, blockIdx.x, blockIdx.y);
+    cqt_low2<1, true>(a, blockIdx.x, blockIdx.y);
+  } else {
+    cqt_low2<2, false>(a, blockIdx.x, blockIdx.y);
+    cqt_low2<2, true>(a, blockIdx.x, blockIdx.y);
+  }
+}
+
 // Per (chunk, 64-frame tile): chroma = the 7 octave partial rows summed (ascending bins),
 // inf-norm per frame, f64 sum over the tile's frames.
 __global__ __launch_bounds__(256) void cqt_tail_kernel(const float* gpart, const int64_t* tf_base,
@@ -1391,8 +1739,13 @@ int launch_chroma_mean(Context& ctx, const float* sig, const int64_t* chunk_off,
     // bench's cqt_chroma unit (7 octaves of every chunk) is their sum
     KTimer kt_(ctx, "cqt_low", st);
     ma.span = kt_.span();
+#if NC_CQL2
+    const dim3 lg((unsigned)((ntile + C2_NW - 1) / C2_NW), (unsigned)n, 3u);
+    hipLaunchKernelGGL(cqt_mfma_low2_kernel, lg, dim3(C2_NW * 64), cql2_lds_bytes(), st, ma);
+#else
     const dim3 lg((unsigned)((ntile + CL_TPW - 1) / CL_TPW), (unsigned)n, 3u);
     hipLaunchKernelGGL(cqt_mfma_low_kernel, lg, dim3(CL_NW * 64), cql_lds_bytes(), st, ma);
+#endif
   }
   {
     KTimer kt_(ctx, "cqt_high", st);

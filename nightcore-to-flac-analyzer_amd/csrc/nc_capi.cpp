@@ -203,6 +203,16 @@ int nc_profile_read_span(nc_ctx* ctx, const char* tag, double* total_ms, int* la
   return nc::profile_read_span(ctx->c, tag, total_ms, launches);
 }
 
+int nc_profile_read_busy(nc_ctx* ctx, double* busy_ms, double* extent_ms, int* launches) {
+  CHECK_CTX(ctx);
+  if (!busy_ms || !extent_ms || !launches) {
+    nc::set_error("nc_profile_read_busy: null argument");
+    return -1;
+  }
+  SET_DEVICE(ctx);
+  return nc::profile_read_busy(ctx->c, busy_ms, extent_ms, launches);
+}
+
 size_t nc_trim_workspace_bytes(const int64_t* host_file_len, int n_files) {
   return nc::trim_ws_bytes(host_file_len, n_files);
 }

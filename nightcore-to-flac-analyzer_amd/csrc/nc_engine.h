@@ -94,6 +94,7 @@ void free_timers(Context& ctx);
 void profile_enable(Context& ctx, int mode);
 int profile_read(Context& ctx, const char* tag, double* total_ms, int* launches);
 int profile_read_span(Context& ctx, const char* tag, double* total_ms, int* launches);
+int profile_read_busy(Context& ctx, double* busy_ms, double* extent_ms, int* launches);
 
 // bootstrap.hip job description (see nc_bootstrap_ratio in include/ncgpu.h)
 struct BootArgs {

@@ -202,4 +202,59 @@ int profile_read_span(Context& ctx, const char* tag, double* total_ms, int* laun
   return 0;
 }
 
+// Device occupancy over every span recorded since the last reset, all tags together: the
+// union of the launches' execution spans (busy) and first start .. last end (extent).  The
+// engine's kernels are all spanned; torch's small fills and the copies are not, so busy is
+// a lower bound by their few microseconds.  Clears every tag's spans.
+int profile_read_busy(Context& ctx, double* busy_ms, double* extent_ms, int* launches) {
+  *busy_ms = *extent_ms = 0.0;
+  *launches = 0;
+  KernelTimers* t = ctx.timers;
+  if (!t || !t->span_buf) return 0;
+  if (hipDeviceSynchronize() != hipSuccess) {
+    set_error("nc_profile_read_busy: device synchronize failed");
+    return -1;
+  }
+  std::vector<unsigned long long> h((size_t)t->span_used * kSpanLaunchU64);
+  if (t->span_used && hipMemcpy(h.data(), t->span_buf, h.size() * sizeof(unsigned long long),
+                                hipMemcpyDeviceToHost) != hipSuccess) {
+    set_error("nc_profile_read_busy: copy failed");
+    return -1;
+  }
+  std::vector<std::pair<unsigned long long, unsigned long long>> iv;
+  for (int s = 0; s < t->span_used; ++s) {
+    unsigned long long a = ~0ull, b = 0ull;
+    for (int l = 0; l < kSpanLines; ++l) {
+      const unsigned long long* p = h.data() + (size_t)s * kSpanLaunchU64 + (size_t)l * kSpanStride;
+      a = std::min(a, p[0]);
+      b = std::max(b, p[1]);
+    }
+    if (b >= a && a != ~0ull) iv.emplace_back(a, b);
+  }
+  std::sort(iv.begin(), iv.end());
+  unsigned long long busy = 0, cur_a = 0, cur_b = 0;
+  bool open = false;
+  for (auto& p : iv) {
+    if (!open || p.first > cur_b) {
+      if (open) busy += cur_b - cur_a;
+      cur_a = p.first;
+      cur_b = p.second;
+      open = true;
+    } else {
+      cur_b = std::max(cur_b, p.second);
+    }
+  }
+  if (open) busy += cur_b - cur_a;
+  if (!iv.empty()) {
+    unsigned long long last = 0;
+    for (auto& p : iv) last = std::max(last, p.second);
+    *extent_ms = (double)(last - iv.front().first) / t->clock_khz;
+  }
+  *busy_ms = (double)busy / t->clock_khz;
+  *launches = (int)iv.size();
+  for (auto& kv : t->slots) kv.second.spans.clear();
+  span_reset(*t);
+  return 0;
+}
+
 }  // namespace nc

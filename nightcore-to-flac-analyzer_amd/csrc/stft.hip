@@ -219,8 +219,11 @@ __global__ __launch_bounds__(SM_THREADS) void stft_mel_kernel(StftMelArgs a) {
   for (int i = threadIdx.x; i < (a.mel_j0 + a.mel_j1) * 64; i += SM_THREADS) sh_w4[i] = a.mel_w4[i];
   if (threadIdx.x < SM_MT) sh_mt[threadIdx.x] = mel_pack(a.mel_lo4[threadIdx.x], a.mel_nj4[threadIdx.x], a.mel_band[threadIdx.x]);
   const float4* mw4 = sh_w4;
-  // the slot zeroed once: the mel steps past a band's end read slot floats [1025, mel_reach)
-  // (times a zero weight), which no frame writes
+  // the slot zeroed once.  The mel steps past a band's end read slot floats [1025, mel_reach)
+  // times a zero weight: until the first frame they hold these zeros, afterwards the frame's
+  // own exchange-1/2 intermediates (the half-size exchanges write up to float 1055).  fmaf(0,
+  // x, acc) == acc for every finite x, so the dB rows do not depend on them; an intermediate
+  // overflowing to Inf would make a NaN there, but such a frame's power is Inf already
   for (int i = threadIdx.x & 63; i < SM_HALF; i += 64) slot[i] = make_float2(0.f, 0.f);
   __syncthreads();
 
@@ -382,13 +385,23 @@ __global__ __launch_bounds__(SM_THREADS) void stft_mel_kernel(StftMelArgs a) {
     if (pip) {
       // estimate_tuning's piptrack on the same 2|X| values tuning_peaks_kernel computes
       // (nc_piptrack.h): |X| of the stencil bins written over the power in place (bin k at
-      // float k - (kPipLo - 1): round q reads bins >= kPipLo - 1 + 64 q and writes below
-      // kPipLo - 1 + 64 (q + 1), so no bin is overwritten before it is read)
+      // float k - (kPipLo - 1)).  A lane's store of round q + 1 hits bins that other lanes read
+      // in round q, and per-lane alias analysis lets the compiler order them either way, so
+      // every round's power is read into registers first, and the stores follow a compiler
+      // barrier (one wave's LDS operations then complete in program order)
       const float pm = __fsqrt_rn(wave_max_u(pmax));
+      constexpr int kPipQ = (kPipHi - kPipLo + 3 + 63) / 64;
+      float pv[kPipQ];
 #pragma unroll
-      for (int q = 0; q < (kPipHi - kPipLo + 3 + 63) / 64; ++q) {
+      for (int q = 0; q < kPipQ; ++q) {
         const int k = kPipLo - 1 + 64 * q + lane;
-        if (64 * (q + 1) <= kPipHi - kPipLo + 3 || k <= kPipHi + 1) pw[k - (kPipLo - 1)] = __fsqrt_rn(pw[k]);
+        pv[q] = (64 * (q + 1) <= kPipHi - kPipLo + 3 || k <= kPipHi + 1) ? pw[k] : 0.0f;
+      }
+      asm volatile("" ::: "memory");
+#pragma unroll
+      for (int q = 0; q < kPipQ; ++q) {
+        const int k = kPipLo - 1 + 64 * q + lane;
+        if (64 * (q + 1) <= kPipHi - kPipLo + 3 || k <= kPipHi + 1) pw[k - (kPipLo - 1)] = __fsqrt_rn(pv[q]);
       }
       const int64_t base = uniform64(a.chunk_tf_base[wc]) * kPeakSlots;
       piptrack_append([&](int k) { return pw[k - (kPipLo - 1)]; }, pm, lane, &a.chunk_npk[wc], a.peak_pitch + base,

@@ -601,6 +601,8 @@ class Engine:
         return out
 
     GROUPS_IN_FLIGHT = 3    # pair groups queued ahead of the host's oldest wait (analyze)
+    EAGER_FINISH = False    # finish a group only once complete, up to MAX_GROUPS_IN_FLIGHT queued
+    MAX_GROUPS_IN_FLIGHT = 5
 
     KERNEL_TAGS = ("stft_mel", "window_tg", "tuning_peaks", "decimate", "cqt_low", "cqt_high", "trim_blocks", "tempo_beat",
                    "tg_slide", "spectral_frames", "spectral_bins")
@@ -636,6 +638,15 @@ class Engine:
         read (nc_profile_read_span: first wave start .. last wave end, rocprofv3's kernel
         duration); waits for them."""
         return self._profile_read("nc_profile_read_span")
+
+    def device_busy(self) -> Tuple[float, float, int]:
+        """(busy ms, extent ms, launches) over every kernel span recorded since the last read
+        (nc_profile_read_busy: union of the execution spans of all tags; profile modes 1-3);
+        waits for the device and clears the spans."""
+        import ctypes as C
+        b, e, n = C.c_double(0.0), C.c_double(0.0), C.c_int(0)
+        self.ctx.call("nc_profile_read_busy", C.byref(b), C.byref(e), C.byref(n))
+        return b.value, e.value, n.value
 
     def upload_signals(self, arrays: Sequence[np.ndarray]) -> DeviceSignals:
         lens = np.array([len(a) for a in arrays], dtype=np.int64)
@@ -986,7 +997,16 @@ class Engine:
                     nxt = trim_begin(bi + 1, True)
                 if hs is not None:
                     hs["launch"] = hs.get("launch", 0.0) + time.perf_counter() - t0
-                if len(pending) > self.GROUPS_IN_FLIGHT:
+                if self.EAGER_FINISH:
+                    # launch ahead while the oldest group still runs: assemble it only once it
+                    # is complete (or the in-flight cap is reached), so the host's assembly never
+                    # leaves the device with just a small group queued
+                    while pending and (len(pending) > self.MAX_GROUPS_IN_FLIGHT or
+                                       (len(pending) > 1 and pending[0]["event"].query())):
+                        g = pending.pop(0)
+                        mark(f"finish b{g['bi']} g{g['g0']}")
+                        results[g["bi"]] += self._finish_group(g, log)
+                elif len(pending) > self.GROUPS_IN_FLIGHT:
                     g = pending.pop(0)
                     mark(f"finish b{g['bi']} g{g['g0']}")
                     results[g["bi"]] += self._finish_group(g, log)
@@ -1187,7 +1207,8 @@ class Engine:
             # after the host has waited for the group that used it (analyze's in-flight bound),
             # so no large per-group allocation reaches the caching allocator
             n_slots = int(chunk_tf_base[n_chunks]) * PEAK_SLOTS
-            self._peak_ring = (getattr(self, "_peak_ring", -1) + 1) % (self.GROUPS_IN_FLIGHT + 1)
+            ring = max(self.GROUPS_IN_FLIGHT, self.MAX_GROUPS_IN_FLIGHT) + 1
+            self._peak_ring = (getattr(self, "_peak_ring", -1) + 1) % ring
             pk = self.workspace(f"peaks{self._peak_ring}", 8 * n_slots)
             for s_ in (s1, self.chroma_stream):
                 pk.record_stream(s_)

@@ -304,9 +304,12 @@ def _fault(point: str) -> None:
 
 
 def _try(fn, *args):
+    """(result, None), or (None, the exception) for an ``Exception`` (carried into the next
+    collective).  KeyboardInterrupt, SystemExit and GeneratorExit propagate at once: an
+    interrupt is not a stage failure to deliver to the other ranks, and it reaches them too."""
     try:
         return fn(*args), None
-    except BaseException as exc:       # noqa: BLE001 - re-raised after the collective
+    except Exception as exc:           # noqa: BLE001 - re-raised after the collective
         return None, exc
 
 
@@ -602,10 +605,11 @@ def _files(pairs: Sequence[int]) -> List[int]:
 class _Pump:
     """Advances the engine's interior group pipeline one group at a time (no-op without one).
 
-    It never raises: the pump runs between the collectives of the split-pair stages, where
-    an exception on one rank would leave the others in a collective.  An exception from the
-    pipeline ends it and is kept in ``error``; ``drain`` raises it after the last split-pair
-    collective, before the final flag check that every rank meets."""
+    It never raises an ``Exception``: the pump runs between the collectives of the split-pair
+    stages, where an exception on one rank would leave the others in a collective.  An
+    exception from the pipeline ends it and is kept in ``error``; ``drain`` raises it after the
+    last split-pair collective, before the final flag check that every rank meets.
+    KeyboardInterrupt, SystemExit and GeneratorExit are not held: they propagate at once."""
 
     def __init__(self, gen):
         self.gen, self.value, self.error = gen, None, None
@@ -618,7 +622,7 @@ class _Pump:
                 next(self.gen)
             except StopIteration as stop:
                 self.value, self.gen = stop.value, None
-            except BaseException as exc:       # noqa: BLE001 - raised by drain()
+            except Exception as exc:           # noqa: BLE001 - raised by drain(); interrupts propagate
                 self.error, self.gen = exc, None
 
     def drain(self):

@@ -11,13 +11,15 @@ exchanges):
   on block boundaries, so every pair is interior (pipelined engine, no exchange);
 * split_offset 0.5, run()'s defaults (hop-64 IBI on): every inner boundary cuts a pair,
   so 7 pairs exchange their window and chunk-pair records (C1a, C1b) and split their
-  hop-64 IBI pass over the ranks (C2-C4).
+  hop-64 IBI pass over the ranks (C2-C4); the API default gather=True then all-gathers the
+  outcomes, so every rank holds all 512 (the same list on every rank, checked by digest).
 
 Every rank compares each outcome it owns with ``Engine.analyze`` of the same pairs on
 that rank alone, field for field (results, report text, logs, per-window detail), and
 the owners of pairs 0 and 511 compare them with the CPU oracle (refglue.run_arrays).
 """
 import dataclasses
+import hashlib
 import math
 import os
 import socket
@@ -81,14 +83,23 @@ def _worker(rank, world, port, q):
         for off, p, sp in plans:
             local = sp.needed(rank, p.compute_ibi)
             sig = eng.upload_signals([a for b in local for a in arrays[b]])
+            # split_offset 0.5 through the API default gather=True: every rank receives all 512
+            # outcomes (its owned ones are checked below, the whole list's digest across ranks)
+            gat = off != 0.0
             got = analyze_sharded(DeviceStages(eng, sig), p, lengths=L, local_pairs=local, split_offset=off,
-                                  gather=False)
+                                  gather=gat)
             owned = sp.owned(rank)
+            n_all, digest = None, None
+            if gat:
+                n_all = len(got)
+                digest = hashlib.sha256(repr([_key(o) for o in got]).encode()).hexdigest()
+                got = [(b, got[b]) for b in owned]
             ref = eng.analyze([arrays[b] for b in owned], p) if owned else []
             mism = [b for (b, o), r in zip(got, ref) if _key(o) != _key(r)]
             errs = [b for b, o in got if o.error is not None]
             report.append(dict(off=off, owned=[b for b, _ in got], expect=owned, mism=mism, errors=errs,
-                               split=int(sp.split.sum()), split_owned=[b for b in owned if sp.split[b]]))
+                               split=int(sp.split.sum()), split_owned=[b for b in owned if sp.split[b]],
+                               n_all=n_all, digest=digest))
             if off == 0.0:
                 keep = {b: o for b, o in got if b in ORACLE_PAIRS}
             print(f"[config4 rank {rank}] split_offset {off}: {len(got)} owned, {len(mism)} mismatches", flush=True)
@@ -147,5 +158,10 @@ def test_config4_512_pairs_eight_ranks_equal_engine():
             oracle_seen.append(b)
     for off, _ in CASES:
         assert sorted(owned_all[off]) == list(range(N_PAIRS)), off       # every pair owned exactly once
+    # gather=True (split_offset 0.5): every rank holds all 512 outcomes, the same list on every rank
+    # (each pair's outcome checked against Engine.analyze by its owner above)
+    gathered = [c for r in range(WORLD) for c in res[r]["cases"] if c["off"] == 0.5]
+    assert [c["n_all"] for c in gathered] == [N_PAIRS] * WORLD
+    assert len({c["digest"] for c in gathered}) == 1
     assert split_all[0.0] == [] and len(split_all[0.5]) == WORLD - 1       # 0: no exchange; 0.5: 7 cut pairs
     assert sorted(oracle_seen) == list(ORACLE_PAIRS)

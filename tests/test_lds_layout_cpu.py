@@ -104,3 +104,49 @@ def test_spectral_frame_sum_reduction_conflict_free():
             assert len(set(banks)) == 64, (i, half)
     # the eight rows fit the wave's FFT slot (LdsSize<1024> = 1056 float2)
     assert 8 * SF_RS * 8 <= 1056 * 8
+
+
+# ---- cqt_mfma_low2_kernel (round 5): per-wave f16 images, 64-byte rows of four 16-byte pieces
+def c2_sw(R):  # cqt.hip
+    return ((R >> 2) & 1) << 1
+
+
+def c2_off(R, p):
+    return R * 64 + 16 * (p ^ c2_sw(R))
+
+
+@pytest.mark.parametrize("q", range(8))
+@pytest.mark.parametrize("rt", range(4))
+def test_low2_fragment_reads_conflict_free(q, rt):
+    """A fragment of row tile rt at group position q: lane l reads row 16 rt + (l & 15) + q,
+    piece l >> 4 (8 halves)."""
+    addr = [c2_off(16 * rt + (lane & 15) + q, lane >> 4) // 4 for lane in range(64)]
+    assert b128_cycles(addr) == 4
+
+
+def b128_write_cycles(dword_addr):
+    """ds_write_b128: eight groups of 8 consecutive lanes, bank (a / 4) mod 32."""
+    total = 0
+    for g in range(8):
+        banks = {}
+        for lane in range(8 * g, 8 * g + 8):
+            for d in range(4):
+                a = dword_addr[lane] + d
+                banks.setdefault(a % 32, set()).add(a)
+        total += max(len(v) for v in banks.values())
+    return total
+
+
+@pytest.mark.parametrize("k", range(5))
+def test_low2_split_writes_conflict_free(k):
+    """The split of staging round k: lane l writes unit u = 64 k + l (row u / 4, piece u % 4)."""
+    addr = [c2_off((64 * k + lane) >> 2, (64 * k + lane) & 3) // 4 for lane in range(64)]
+    assert b128_write_cycles(addr) == 8
+
+
+def test_low2_images_hold_every_block_row():
+    for o in range(3):
+        H = 512 >> o
+        M = 1024 // H
+        assert 64 + M - 1 <= 72                          # C2_NRP
+        assert 64 * ((72 * 4 + 63) // 64) >= 4 * (64 + M - 1)  # C2_NU staging rounds cover the rows

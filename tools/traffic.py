@@ -12,7 +12,7 @@ import sys
 from pathlib import Path
 
 REPO = Path(__file__).resolve().parents[1]
-TAGS = {"cqt_mfma_kernel": "cqt_high", "cqt_mfma_low_kernel": "cqt_low",
+TAGS = {"cqt_mfma_kernel": "cqt_high", "cqt_mfma_low_kernel": "cqt_low", "cqt_mfma_low2_kernel": "cqt_low",
         "cqt_tail_kernel": "cqt_tail",
         "stft_mel_kernel": "stft_mel", "tuning_peaks_kernel": "tuning_peaks",
         "trim_blocks_kernel": "trim_blocks", "window_tg_kernel": "window_tg", "decimate_kernel": "decimate", "decimate3_kernel": "decimate"}
@@ -47,8 +47,10 @@ def main(out):
     out = Path(out)
     fetch = per_dispatch(out / "FETCH_SIZE", "FETCH_SIZE")
     write = per_dispatch(out / "WRITE_SIZE", "WRITE_SIZE")
-    commit = subprocess.run(["git", "rev-parse", "--short", "HEAD"], cwd=REPO, capture_output=True,
-                            text=True).stdout.strip() or "unknown"
+    sys.path.insert(0, str(REPO))
+    from bench import build_provenance     # kernel-source / library hashes and the commit
+    prov = build_provenance()
+    commit = prov["commit"]
     kern = {}
     # two trim launches per analyze call (engine.Engine.analyze: the first pair group's files,
     # then the rest): the profiled run's call count, hence launches per step of every kernel
@@ -75,7 +77,8 @@ def main(out):
              "launches_per_step": kern["cqt_low"]["launches_per_step"],
              "alg_bytes_per_launch": int(ALG_STEP["cqt_chroma"] * calls / n_calls)}
         kern["cqt_chroma"] = k
-    doc = {"workload": "config3-64pairs", "commit": commit, "analyze_calls": calls,
+    doc = {"workload": "config3-64pairs", "commit": commit, "src_sha": prov["src_sha"], "lib_sha": prov["lib_sha"],
+           "analyze_calls": calls,
            "command": "tools/pmc_traffic.sh: rocprofv3 --pmc FETCH_SIZE, then a separate --pmc WRITE_SIZE pass, "
                       "--output-format csv -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-ibi "
                       "--no-config5 (means over every launch; the engine's default pair-group schedule)",
