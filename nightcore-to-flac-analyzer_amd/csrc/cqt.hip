@@ -904,283 +904,38 @@ __global__ __launch_bounds__(CM_NTH, 2) void cqt_mfma_kernel(CqmArgs a) {
   }
 }
 
-// Octaves 0-2 on the matrix cores.  Their 64-frame spans (9-33 K samples) do not fit LDS as
-// images, but row t + 1 at k-step ks equals row t at k-step ks + G (G = hop / 32): the
-// M = 1024 / hop k-steps {g + G q : q < M} of "group" g read one block of 64 + M - 1 row
-// pieces (32 samples each), row r of step q being block row r + q.  The k-steps run group by
-// group, so each sample is fetched once per tile (M = 2, 4, 8 times fewer bytes than
-// streaming rows per k-step).  Blocks arrive by LDS-DMA (raw f32, 16-byte pieces swizzled so
-// a fragment's 16 rows hit distinct bank groups), double buffered (issued at a group's first
-// step, retired at its second: see the wait below), and are split to f16 hi/lo at each
-// fragment read.  Four waves per workgroup: two 64-frame tiles, two waves per tile (32 rows
-// each) sharing its blocks; all four share the filter ring.  57 KB of LDS, two workgroups per
-// CU.  Per 224 chunks (round 2, one session): 816-856 us with octaves 0-2 here against 866 us
-// on the FFT kernel; 1 / 3 / 4 tiles per workgroup 778 / 782-797 / 989 us against 761 us at
-// 2; the waits below removed (a timing-only build that races, round 3) 922-954 against
-// 733-758 us, so the exposed DMA latency is not what bounds this kernel.
-constexpr int CL_TPW = 2;          // 64-frame tiles per workgroup (two waves each)
-constexpr int CL_NW = 2 * CL_TPW;  // waves per workgroup
-constexpr int CL_RT = 2;   // row tiles per wave
-template <int OCT>
-struct CmLow {
-  static constexpr int H = 512 >> OCT, G = H / 32, M = 1024 / H, NR = CM_FR + M - 1, NI = (NR + 7) / 8;
-  static constexpr int QB = (NI + 1) / 2;  // block DMA pieces per wave (two waves per tile)
-  static constexpr int BLK = NI * 8 * 32;  // floats per block buffer
-};
-constexpr int CL_GQ = (CM_NT * 2 + CL_NW - 1) / CL_NW;  // filter DMA pieces per wave per slice
-// Block row R keeps its 16-byte piece p at slot p ^ cl_sw(R).  A fragment read serves the lane
-// groups of ds_read_b128 (8 rows at piece P, 8 rows at piece P + 2, for any row offset q): this
-// swizzle puts each group's 16 pieces on distinct banks (the round-2 (R >> 1) & 7 left 2-way
-// conflicts on half of the reads)
-__device__ __forceinline__ int cl_sw(int R) { return ((R >> 2) & 1) | (((R >> 1) & 1) << 2); }
-size_t cql_lds_bytes() { return CM_BBYTES + CL_TPW * 2 * CmLow<2>::BLK * 4; }  // octave 2 has the largest block
-
-// VEC: the tile takes the DMA path (in bounds and 16-byte aligned).  The kernel calls both
-// instances; each wave runs the one that matches its tile (both issue the same barriers), so
-// the aligned path keeps its own register allocation and schedule.
-template <int OCT, bool VEC>
-__device__ __forceinline__ void cqt_mfma_low(const CqmArgs& a, int bx, int c) {
-  using L = CmLow<OCT>;
-  constexpr int H = L::H, G = L::G, M = L::M, NI = L::NI, QB = L::QB;
-  static_assert(G * M == CM_KS && CM_R == 2, "k-step groups; two-slot filter ring");
-  const Span span_(a.span);
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  uint4* sB = reinterpret_cast<uint4*>(smem);  // [2][CM_SLICE]
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int tw = wave >> 1, hw = wave & 1;  // tile of the workgroup, row half of the tile
-  // every descriptor read up front, unconditionally: one round trip of scalar loads
-  const int T = a.n_frames[c], ti = a.tuning_idx[c], ex = a.oct_ex[c * 7 + OCT];
-  const int64_t yoff = OCT == 0 ? a.chunk_off[c] : a.oct_off[c * 7 + OCT], Ly = a.oct_len[c * 7 + OCT];
-  if (bx * (CL_TPW * CM_FR) >= T) return;
-  int t0 = (bx * CL_TPW + tw) * CM_FR;
-  const bool active = t0 < T;  // an idle tile's waves still share the DMA and the barriers
-  if (!active) t0 = 0;
-  const uint4* bsrc = a.bfrag + (size_t)ti * (CM_KS * CM_SLICE);
-  float* blk = reinterpret_cast<float*>(smem + CM_BBYTES) + tw * (2 * L::BLK);
-  auto kstep = [](int n) { return n / M + G * (n % M); };  // step n -> k-step (group n / M, shift n % M)
-  auto fetch_slice = [&](int n) {
-#pragma unroll
-    for (int q = 0; q < CL_GQ; ++q) {
-      int i = wave + CL_NW * q;
-      if (i >= CM_NT * 2) i = wave;  // duplicate of this wave's first piece
-      cm_dma16(bsrc + kstep(n) * CM_SLICE + i * 64 + lane, sB + (n & 1) * CM_SLICE + i * 64);
-    }
-  };
-
-  const float* y = (OCT == 0 ? a.sig : a.ws_oct) + yoff;
-  const float sx = ldexpf(1.0f, ex);
-  const int64_t s0 = (int64_t)t0 * H - 512;
-  // tile-uniform: both waves of a tile take the same path (their vmcnt bookkeeping agrees)
-  const bool vec = s0 >= 0 && s0 + (int64_t)(CM_FR - 1) * H + kCqtNfft <= Ly &&
-                   (reinterpret_cast<uintptr_t>(y) & 15) == 0;
-  if (vec != VEC) return;
-  fetch_slice(0);
-  // block g: row R (< NR) holds samples s0 + R H + 32 g + [0, 32), piece p at slot p ^ cl_sw(R);
-  // the tile's two waves each move half of the NI 8-row DMA groups (QB each, one repeated if odd)
-  const int dr = lane >> 3;
-  // Without the DMA (a chunk at a sample that is not 16-byte aligned -- a trimmed file starts
-  // anywhere -- or a tile at the signal's edge) a block's pieces are loaded into registers at
-  // its group's first step and stored to LDS at the second, so the load latency hides under a
-  // k-step as the DMA's does (round 3: the load-then-store form stalled every group, +33 % on
-  // unaligned chunks); inside the signal the loads need no bounds tests.
-  const bool inner = s0 >= 0 && s0 + (int64_t)(CM_FR - 1) * H + kCqtNfft <= Ly;
-  static_assert(L::M >= 2, "a staged block is stored at its group's second step");
-  float4 stg[QB];
-  auto fetch_block = [&](int g) {  // VEC: DMA straight into the buffer; otherwise into stg
-    float* b = blk + (g & 1) * L::BLK;
-#pragma unroll
-    for (int k = 0; k < QB; ++k) {
-      int i = hw + 2 * k;
-      if (i >= NI) i = hw;
-      const int R = 8 * i + dr;
-      const int p = (lane & 7) ^ cl_sw(R);
-      const int Rc = min(R, L::NR - 1);  // rows past NR: a valid address, never read
-      if (VEC) {
-        cm_dma16(y + s0 + (int64_t)Rc * H + 32 * g + 4 * p, b + i * 256);
-      } else if (inner) {
-        const float* q = y + s0 + (int64_t)Rc * H + 32 * g + 4 * p;
-        stg[k] = make_float4(q[0], q[1], q[2], q[3]);
-      } else {
-        const int64_t q = s0 + (int64_t)R * H + 32 * g + 4 * p;
-        float4 v;
-        v.x = (q >= 0 && q < Ly) ? y[q] : 0.0f;
-        v.y = (q + 1 >= 0 && q + 1 < Ly) ? y[q + 1] : 0.0f;
-        v.z = (q + 2 >= 0 && q + 2 < Ly) ? y[q + 2] : 0.0f;
-        v.w = (q + 3 >= 0 && q + 3 < Ly) ? y[q + 3] : 0.0f;
-        stg[k] = v;
-      }
-    }
-  };
-  auto store_block = [&](int g) {  // the staged pieces of block g into its buffer
-    float4* b = reinterpret_cast<float4*>(blk + (g & 1) * L::BLK);
-#pragma unroll
-    for (int k = 0; k < QB; ++k) {
-      int i = hw + 2 * k;
-      if (i >= NI) i = hw;
-      b[i * 64 + lane] = stg[k];
-    }
-  };
-  fetch_block(0);
-  if (!VEC) store_block(0);
-
-  cm_f4 acc[CL_RT][CM_NT];
-#pragma unroll
-  for (int rt = 0; rt < CL_RT; ++rt)
-#pragma unroll
-    for (int nt = 0; nt < CM_NT; ++nt) acc[rt][nt] = cm_f4{0.f, 0.f, 0.f, 0.f};
-  const int p0 = 2 * (lane >> 4);
-#pragma unroll 1
-  for (int n = 0; n < CM_KS; ++n) {
-    const int g = n / M, q = n - M * g;
-    // retire every DMA of this wave (slice n, and block g + 1 when issued at q == 0).  A counted
-    // vmcnt that leaves the block in flight is NOT safe here: LDS-DMA completions of an L2-hit
-    // slice and an HBM block can come back out of order (measured: run-to-run differences up to
-    // 2e-3 with vmcnt(QB) at q == 1, none with vmcnt(0)), so one step of latency is what
-    // either gets.
-    __builtin_amdgcn_s_waitcnt(cm_vmcnt(0));
-    __builtin_amdgcn_s_waitcnt(0xc07f);
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-    if (n + 1 < CM_KS) fetch_slice(n + 1);         // into the slot step n - 1 read
-    if (q == 0 && g + 1 < G) fetch_block(g + 1);  // into the buffer group g - 1 read (or stg)
-    if (!VEC && q == 1 && g + 1 < G) store_block(g + 1);  // staged at q == 0, landed at this step's top
-    // the rows' f32 pieces, then the B fragments two column tiles ahead of their MFMAs
-    // (asm-issued reads, counted waits: cm_rd)
-    const float4* b = reinterpret_cast<const float4*>(blk + (g & 1) * L::BLK);
-    static_assert(CL_RT == 2 && CM_NT == 5, "fragment schedule");
-    cm_u4 u[CL_RT][2], bq[CM_NT][2];
-#pragma unroll
-    for (int rt = 0; rt < CL_RT; ++rt) {
-      const int R = 32 * hw + 16 * rt + (lane & 15) + q;
-      const int sw = cl_sw(R);
-      cm_rd<0>(u[rt][0], lds_addr(b + R * 8 + (p0 ^ sw)));
-      cm_rd<0>(u[rt][1], lds_addr(b + R * 8 + ((p0 + 1) ^ sw)));
-    }
-    const uint32_t sbl = lds_addr(sB + (n & 1) * CM_SLICE + lane);
-    cm_rd<0 * 1024>(bq[0][0], sbl);
-    cm_rd<1 * 1024>(bq[0][1], sbl);
-    cm_rd<2 * 1024>(bq[1][0], sbl);
-    cm_rd<3 * 1024>(bq[1][1], sbl);
-    cm_rd<4 * 1024>(bq[2][0], sbl);
-    cm_rd<5 * 1024>(bq[2][1], sbl);
-    cm_wait<6>(u[0][0], u[0][1], u[1][0], u[1][1]);  // the rows landed; tiles 0-2 in flight
-    cm_half8 ah[CL_RT], al[CL_RT];
-#pragma unroll
-    for (int rt = 0; rt < CL_RT; ++rt) {
-      const float4 u0 = __builtin_bit_cast(float4, u[rt][0]), u1 = __builtin_bit_cast(float4, u[rt][1]);
-      const float v[8] = {u0.x, u0.y, u0.z, u0.w, u1.x, u1.y, u1.z, u1.w};
-      cm_split(v, sx, ah[rt], al[rt]);
-    }
-    auto tile = [&](int nt) {
-      const cm_half8 bh = __builtin_bit_cast(cm_half8, bq[nt][0]);
-      const cm_half8 bl = __builtin_bit_cast(cm_half8, bq[nt][1]);
-#pragma unroll
-      for (int rt = 0; rt < CL_RT; ++rt) {
-        acc[rt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[rt], bh, acc[rt][nt], 0, 0, 0);
-        acc[rt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[rt], bl, acc[rt][nt], 0, 0, 0);
-        acc[rt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al[rt], bh, acc[rt][nt], 0, 0, 0);
-      }
-    };
-    cm_wait<4>(bq[0][0], bq[0][1]);
-    tile(0);
-    cm_rd<6 * 1024>(bq[3][0], sbl);
-    cm_rd<7 * 1024>(bq[3][1], sbl);
-    cm_wait<4>(bq[1][0], bq[1][1]);
-    tile(1);
-    cm_rd<8 * 1024>(bq[4][0], sbl);
-    cm_rd<9 * 1024>(bq[4][1], sbl);
-    cm_wait<4>(bq[2][0], bq[2][1]);
-    tile(2);
-    cm_wait<2>(bq[3][0], bq[3][1]);
-    tile(3);
-    cm_wait<0>(bq[4][0], bq[4][1]);
-    tile(4);
-  }
-  __syncthreads();  // the rows overlay the ring and blocks
-  if (!active) return;
-  const int nrow = min(32, T - t0 - 32 * hw);  // this wave's frames
-  if (nrow <= 0) return;
-  float* mg = reinterpret_cast<float*>(smem) + wave * (32 * kCqtFilt);
-  {
-    const float oscale = (float)(1 << (OCT >> 1)) * ((OCT & 1) ? 0x1.6a09e6p+0f : 1.0f);
-    const float* isl = a.cqt_isl + ti * kCqtBins + (kCqtBins - kCqtFilt * (OCT + 1));
-    const int* bx = a.bexp + ti * kCqtFilt;
-    const int col = lane & 15;
-    const float inv0 = ldexpf(1.0f, -(ex + bx[col])), inv1 = ldexpf(1.0f, -(ex + bx[16 + col]));
-    const float inv2 = ldexpf(1.0f, -(ex + bx[32 + (col & 3)]));
-    const float il0 = isl[col], il1 = isl[16 + col], il2 = isl[32 + (col & 3)];
-#pragma unroll
-    for (int rt = 0; rt < CL_RT; ++rt)
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int fr = 16 * rt + 4 * (lane >> 4) + i;
-        float* m = mg + fr * kCqtFilt;
-        m[col] = hypotf(acc[rt][0][i] * inv0 * oscale, acc[rt][1][i] * inv0 * oscale) * il0;
-        m[16 + col] = hypotf(acc[rt][2][i] * inv1 * oscale, acc[rt][3][i] * inv1 * oscale) * il1;
-        const float im = __shfl_down(acc[rt][4][i], 4, 16);
-        if (col < 4) m[32 + col] = hypotf(acc[rt][4][i] * inv2 * oscale, im * inv2 * oscale) * il2;
-      }
-  }
-  __builtin_amdgcn_s_waitcnt(0xc07f);
-  __builtin_amdgcn_wave_barrier();
-  float* gp = a.gpart + (a.tf_base[c] + t0 + 32 * hw) * (7 * 12) + (6 - OCT) * 12;
-  for (int qq = lane; qq < nrow * 12; qq += 64) {
-    const int fl = qq / 12, cc = qq - 12 * fl;
-    const float* m = mg + fl * kCqtFilt;
-    gp[fl * (7 * 12) + cc] = cc == 0 ? (m[0] + m[1]) + m[35] : (m[3 * cc - 1] + m[3 * cc]) + m[3 * cc + 1];
-  }
-}
-
-// one launch for octaves 0-2 (blockIdx.z = octave), so their workgroups share the machine.
-// The XCD-contiguous order of cqt_mfma_kernel measured slower here (429 against 398 us per 224
-// chunks, FETCH_SIZE 348 against 361 MiB per 112 chunks, round 3): grid order stays.
-__global__ __launch_bounds__(CL_NW * 64) void cqt_mfma_low_kernel(CqmArgs a) {
-  if (blockIdx.z == 0) {
-    cqt_mfma_low<0, true>(a, blockIdx.x, blockIdx.y);
-    cqt_mfma_low<0, false>(a, blockIdx.x, blockIdx.y);
-  } else if (blockIdx.z == 1) {
-    cqt_mfma_low<1, true>(a, blockIdx.x, blockIdx.y);
-    cqt_mfma_low<1, false>(a, blockIdx.x, blockIdx.y);
-  } else {
-    cqt_mfma_low<2, true>(a, blockIdx.x, blockIdx.y);
-    cqt_mfma_low<2, false>(a, blockIdx.x, blockIdx.y);
-  }
-}
-
-// ---- Octaves 0-2, round 5: one 64-frame tile per wave.
-// The round-2 kernel above split every A fragment from f32 at each of the M k-steps that read
-// its block row (4.8 VALU per MFMA: the issue port, not the matrix core, was full) and ran
-// 30 MFMAs per k-step per wave against a barrier and a vmcnt(0) drain per step.  Here:
-//  * a wave owns a whole tile (4 row tiles x 5 column tiles x 3 products = 60 MFMAs per k-step),
-//    four tiles of one (chunk, octave) per workgroup share the filter slices;
-//  * the block of group g + 1 (NR rows x 32 samples) is loaded into registers at group g's
-//    first step and split ONCE into this wave's f16 hi / lo image at the group's last step
-//    (cm_split: the same values the per-fragment split produced), so a k-step's A fragments
-//    are plain ds_read_b128s at immediate offsets (1 VALU per MFMA on octave 0, less above);
-//  * filter slices go through a 4-slot ring, issued three steps ahead and retired with counted
-//    vmcnt waits: every wave issues the same vector-memory sequence (3 slice pieces per step,
-//    10 block loads at a group's first step), so the count of younger operations is static per
-//    k-step position (c2_wait_slice).  Block loads are dword-aligned dwordx4 (gfx950 serves
-//    unaligned global loads), so an unaligned chunk issues the same instructions; an edge tile
-//    loads clamped pieces and zeroes the samples outside the signal when it splits.
+// ---- Octaves 0-2 (hop >= 128): their 64-frame spans (9-33 K samples) do not fit LDS as images,
+// but row t + 1 at k-step ks equals row t at k-step ks + G (G = hop / 32): the M = 1024 / hop
+// k-steps {g + G q : q < M} of "group" g read one block of 64 + M - 1 row pieces (32 samples
+// each), row r of step q being block row r + q.  The k-steps run group by group, so each sample
+// is fetched once per tile.  Round 5 rebuilt the kernel around one 64-frame
+// tile per wave (the round-2 kernel ran two waves of 32 rows per tile and split every A fragment
+// from f32 at each of the M k-steps that read its row: 4.8 VALU per MFMA):
+//  * a wave owns a whole tile (4 row tiles x 5 column tiles x 3 products = 60 MFMAs per k-step);
+//    two tiles of one (chunk, octave) per workgroup share the filter slices;
+//  * the block of group g + 1 is loaded into registers at group g's first step and split ONCE
+//    (cm_split, the same values) into this wave's f16 hi / lo image at the group's last step, so
+//    a k-step's A fragments are plain ds_read_b128s at immediate offsets;
+//  * filter slices go through a two-slot LDS ring by LDS-DMA, slice n + 1 requested at step n
+//    and retired by a counted vmcnt at step n + 1's top (the block loads stay in flight): every
+//    wave issues the same vector-memory sequence (5 slice pieces per step, 10 block loads at a
+//    group's first step), so the count of younger operations is static per position in the
+//    group (C2::younger).  The block itself is waited for with vmcnt(0): a counted wait that
+//    left younger L2-hit slice pieces in flight behind the (HBM) block loads returned before the
+//    loads had landed (NaNs from fresh workspace contents in tools/det_check.py, round 5), so on
+//    gfx950 vmcnt is not retired in issue order across global_load and global_load_lds;
+//  * block loads are dword-aligned dwordx4 (gfx950 serves unaligned global loads), so an
+//    unaligned chunk issues the same instructions; an edge tile loads clamped pieces and zeroes
+//    the samples outside the signal when it splits.
 // Accumulation order per accumulator is the round-2 kernel's (k-steps group by group, hh, hl, lh
-// per step): chroma is bit-identical.  LDS: 40 KB ring + 4 x 9 KB images = 76 KB, two workgroups
-// per CU.
-#ifndef C2_BLOCK_WAIT0
-#define C2_BLOCK_WAIT0 1
-#endif
-#ifndef C2_NW_
-#define C2_NW_ 4
-#endif
-#ifndef C2_R_
-#define C2_R_ 4
-#endif
-#ifndef C2_WPS
-#define C2_WPS 2
-#endif
-constexpr int C2_NW = C2_NW_;                             // tiles (waves) per workgroup
-constexpr int C2_R = C2_R_;                               // filter ring slots
+// per step): chroma is bit-identical to it.  LDS: 20 KB ring + 2 x 9 KB images = 38 KB, four
+// workgroups (eight waves) per CU; 221 VGPRs, two waves per SIMD.  Rotated timer, one session
+// (us per 224 chunks, profiles/r5_cqt_low_variants.txt): round-2 kernel 405.6; this kernel with
+// 4 tiles per workgroup and a 4-slot ring 480.9 (16 tile slots for 13.5 tiles of work), 2 tiles
+// and a 3-slot ring 416.9 (three workgroups per CU), 2 tiles and 2 slots 358.6.  Probes of the
+// last (outputs wrong): no barrier 338.6, no MFMA 259.3, no split 297.5.
+constexpr int C2_NW = 2;                                  // tiles (waves) per workgroup
+constexpr int C2_R = 2;                                   // filter ring slots
 constexpr int C2_D = C2_R - 1;                            // slices requested ahead of the step that reads them
 constexpr int C2_PS = (CM_NT * 2 + C2_NW - 1) / C2_NW;    // slice DMA pieces per wave per step
 constexpr int C2_NRP = 72;                                // image rows per wave (>= 64 + M - 1)
@@ -1189,7 +944,7 @@ constexpr int C2_RING = C2_R * CM_SLICE * 16;
 constexpr int C2_NU = (C2_NRP * 4 + 63) / 64;             // staging rounds (8-sample units per lane)
 constexpr int C2_NL = 2 * C2_NU;                          // block loads per wave per group
 static_assert(C2_NW * 2 * C2_IMG >= C2_NW * CM_FR * kCqtFilt * 4, "epilogue rows fit the images");
-size_t cql2_lds_bytes() { return C2_RING + C2_NW * 2 * C2_IMG; }
+size_t cql_lds_bytes() { return C2_RING + C2_NW * 2 * C2_IMG; }
 
 // image row R keeps its 16-byte piece p (8 halves) at slot p ^ c2_sw(R): every ds_read_b128 lane
 // group of an A fragment (rows r..r+15 at pieces 0..3, any r) and every ds_write_b128 group of the
@@ -1241,12 +996,8 @@ struct C2 {
 // vmcnt(younger(q, last)): retires this wave's pieces of slice n (this step's slot)
 template <int OCT, int Q>
 __device__ __forceinline__ void c2_wait_slice(bool last) {
-#if C2_SLICE_WAIT0
-  c2_vmwait<0>();
-#else
   if (last) c2_vmwait<C2<OCT>::younger(Q, true)>();
   else c2_vmwait<C2<OCT>::younger(Q, false)>();
-#endif
 }
 
 // Block g of this wave's tile into registers: 8-sample unit u = 64 k + lane is row min(u / 4,
@@ -1314,7 +1065,7 @@ __device__ __forceinline__ void c2_split(const cm_u4 (&st)[C2_NL], char* img, fl
 }
 
 template <int OCT, bool EDGE>
-__device__ __forceinline__ void cqt_low2(const CqmArgs& a, int bx, int c) {
+__device__ __forceinline__ void cqt_low_tile(const CqmArgs& a, int bx, int c) {
   using L = C2<OCT>;
   constexpr int H = L::H, G = L::G, M = L::M;
   static_assert(G * M == CM_KS && M >= 2 && L::NR <= C2_NRP, "k-step groups");
@@ -1370,9 +1121,7 @@ __device__ __forceinline__ void cqt_low2(const CqmArgs& a, int bx, int c) {
     // (n + 3) % R (step n - 1's)
     c2_wait_slice<OCT, Q>(last);
     __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's image writes
-#if !C2_PROBE_NOBAR   // timing probe only: races
     __builtin_amdgcn_s_barrier();
-#endif
     asm volatile("" ::: "memory");
     if (n + C2_D < CM_KS) fetch_slice(n + C2_D);
     if (L::stage_at(Q, last)) c2_stage<OCT>(st, y, s0, g + 1, Ly, EDGE, lane);
@@ -1405,16 +1154,12 @@ __device__ __forceinline__ void cqt_low2(const CqmArgs& a, int bx, int c) {
       auto tile = [&](int nt) {
         const cm_half8 bh = __builtin_bit_cast(cm_half8, b[nt][0]);
         const cm_half8 bl = __builtin_bit_cast(cm_half8, b[nt][1]);
-#if C2_PROBE_NOMFMA   // timing probe only: no matrix work
-        acc[0][nt][0] += (float)bh[0] + (float)bl[1] + (float)ah[0][2] + (float)al[3][3];
-#else
 #pragma unroll
         for (int rt = 0; rt < CM_RT; ++rt) {
           acc[rt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[rt], bh, acc[rt][nt], 0, 0, 0);
           acc[rt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[rt], bl, acc[rt][nt], 0, 0, 0);
           acc[rt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al[rt], bh, acc[rt][nt], 0, 0, 0);
         }
-#endif
       };
       cm_wait<2>(b[0][0], b[0][1]);
       cm_rd<4 * 1024>(b[2][0], sbl);
@@ -1435,13 +1180,10 @@ __device__ __forceinline__ void cqt_low2(const CqmArgs& a, int bx, int c) {
     }
     if (Q == M - 1 && !last) {
       // block g + 1 (requested at this group's first step) into the image: every A read of
-      // group g is done (their registers were consumed above); younger than the block loads
-      // are the slice pieces of steps n - M + 2 .. n (none past slice 31)
-      if (C2_BLOCK_WAIT0 || (M == 2 && n + C2_D >= CM_KS)) c2_vmwait_st<0>(st);
-      else c2_vmwait_st<(M - 1) * C2_PS>(st);
-#if !C2_PROBE_NOSPLIT   // timing probe only: the image keeps block 0
+      // group g is done (their registers were consumed above).  vmcnt(0), not a count: younger
+      // slice pieces can retire before the block loads (header)
+      c2_vmwait_st<0>(st);
       if (active) c2_split<OCT>(st, img, sx, s0, g + 1, Ly, EDGE, lane);
-#endif
     }
   };
 #pragma unroll 1
@@ -1483,16 +1225,16 @@ __device__ __forceinline__ void cqt_low2(const CqmArgs& a, int bx, int c) {
   }
 }
 
-__global__ __launch_bounds__(C2_NW * 64, C2_WPS) void cqt_mfma_low2_kernel(CqmArgs a) {
+__global__ __launch_bounds__(C2_NW * 64, 2) void cqt_mfma_low_kernel(CqmArgs a) {
   if (blockIdx.z == 0) {
-    cqt_low2<0, false>(a, blockIdx.x, blockIdx.y);
-    cqt_low2<0, true>(a, blockIdx.x, blockIdx.y);
+    cqt_low_tile<0, false>(a, blockIdx.x, blockIdx.y);
+    cqt_low_tile<0, true>(a, blockIdx.x, blockIdx.y);
   } else if (blockIdx.z == 1) {
-    cqt_low2<1, false>(a, blockIdx.x, blockIdx.y);
-    cqt_low2<1, true>(a, blockIdx.x, blockIdx.y);
+    cqt_low_tile<1, false>(a, blockIdx.x, blockIdx.y);
+    cqt_low_tile<1, true>(a, blockIdx.x, blockIdx.y);
   } else {
-    cqt_low2<2, false>(a, blockIdx.x, blockIdx.y);
-    cqt_low2<2, true>(a, blockIdx.x, blockIdx.y);
+    cqt_low_tile<2, false>(a, blockIdx.x, blockIdx.y);
+    cqt_low_tile<2, true>(a, blockIdx.x, blockIdx.y);
   }
 }
 
@@ -1739,13 +1481,8 @@ int launch_chroma_mean(Context& ctx, const float* sig, const int64_t* chunk_off,
     // bench's cqt_chroma unit (7 octaves of every chunk) is their sum
     KTimer kt_(ctx, "cqt_low", st);
     ma.span = kt_.span();
-#if NC_CQL2
     const dim3 lg((unsigned)((ntile + C2_NW - 1) / C2_NW), (unsigned)n, 3u);
-    hipLaunchKernelGGL(cqt_mfma_low2_kernel, lg, dim3(C2_NW * 64), cql2_lds_bytes(), st, ma);
-#else
-    const dim3 lg((unsigned)((ntile + CL_TPW - 1) / CL_TPW), (unsigned)n, 3u);
-    hipLaunchKernelGGL(cqt_mfma_low_kernel, lg, dim3(CL_NW * 64), cql_lds_bytes(), st, ma);
-#endif
+    hipLaunchKernelGGL(cqt_mfma_low_kernel, lg, dim3(C2_NW * 64), cql_lds_bytes(), st, ma);
   }
   {
     KTimer kt_(ctx, "cqt_high", st);

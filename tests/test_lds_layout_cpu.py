@@ -4,7 +4,7 @@ results), checked against a model of the hardware rules they were designed for:
 * `xcd_remap` (nc_device.h) must be a permutation of the workgroup ids for every grid size,
   or workgroups would be skipped or run twice;
 * the fragment reads of `cqt_mfma_kernel` (image pads `cm_pad`, cqt.hip) and of
-  `cqt_mfma_low_kernel` (block swizzle `cl_sw`) must be free of LDS bank conflicts under the
+  `cqt_mfma_low_kernel` (image swizzle `c2_sw`, round 5) must be free of LDS bank conflicts under the
   `ds_read_b128` lane groups of MI355X_MICROARCH.md (LDS table): one LDS cycle per group.
 
 The C++ rules are restated here; a change to either side has to change both."""
@@ -62,29 +62,6 @@ def test_octave_3_6_image_reads_conflict_free(octave):
             assert b128_cycles([h // 2 for h in halves]) == 4, (octave, rt, ks)
 
 
-def cl_sw(R):  # cqt.hip
-    return ((R >> 2) & 1) | (((R >> 1) & 1) << 2)
-
-
-def test_low_octave_block_reads_conflict_free():
-    """Block row R = 32 hw + 16 rt + (lane & 15) + q (any k-step shift q), 8 pieces of 16 bytes
-    per row, piece p at slot p ^ cl_sw(R); a lane reads pieces 2 (lane >> 4) and + 1."""
-    for hw in (0, 1):
-        for rt in (0, 1):
-            for q in range(8):
-                for piece in (0, 1):
-                    addr = []
-                    for l in range(64):
-                        R = 32 * hw + 16 * rt + (l & 15) + q
-                        addr.append(R * 32 + 4 * ((2 * (l >> 4) + piece) ^ cl_sw(R)))
-                    assert b128_cycles(addr) == 4, (hw, rt, q, piece)
-
-
-def test_low_octave_swizzle_is_a_permutation_of_each_row():
-    for R in range(64):
-        assert sorted(p ^ cl_sw(R) for p in range(8)) == list(range(8))
-
-
 SF_RS = 72  # spectral.hip spectral_frames_kernel: row stride (f64) of the frame-sum reduction
 
 
@@ -106,7 +83,7 @@ def test_spectral_frame_sum_reduction_conflict_free():
     assert 8 * SF_RS * 8 <= 1056 * 8
 
 
-# ---- cqt_mfma_low2_kernel (round 5): per-wave f16 images, 64-byte rows of four 16-byte pieces
+# ---- cqt_mfma_low_kernel (round 5): per-wave f16 images, 64-byte rows of four 16-byte pieces
 def c2_sw(R):  # cqt.hip
     return ((R >> 2) & 1) << 1
 
@@ -117,7 +94,7 @@ def c2_off(R, p):
 
 @pytest.mark.parametrize("q", range(8))
 @pytest.mark.parametrize("rt", range(4))
-def test_low2_fragment_reads_conflict_free(q, rt):
+def test_low_octave_fragment_reads_conflict_free(q, rt):
     """A fragment of row tile rt at group position q: lane l reads row 16 rt + (l & 15) + q,
     piece l >> 4 (8 halves)."""
     addr = [c2_off(16 * rt + (lane & 15) + q, lane >> 4) // 4 for lane in range(64)]
@@ -138,13 +115,13 @@ def b128_write_cycles(dword_addr):
 
 
 @pytest.mark.parametrize("k", range(5))
-def test_low2_split_writes_conflict_free(k):
+def test_low_octave_split_writes_conflict_free(k):
     """The split of staging round k: lane l writes unit u = 64 k + l (row u / 4, piece u % 4)."""
     addr = [c2_off((64 * k + lane) >> 2, (64 * k + lane) & 3) // 4 for lane in range(64)]
     assert b128_write_cycles(addr) == 8
 
 
-def test_low2_images_hold_every_block_row():
+def test_low_octave_images_hold_every_block_row():
     for o in range(3):
         H = 512 >> o
         M = 1024 // H
