@@ -88,22 +88,25 @@ __device__ __forceinline__ int md_pow2(int n) {
 }
 
 // 120 log2(f / 55) + 0.5, floored (essentia's frequency-to-cent-bin of PitchSalienceFunction)
-__device__ __forceinline__ int md_cent_bin(float f) { return (int)floorf(120.0f * log2f(f / 55.0f) + 0.5f); }
+// in f64 (round 5): a harmonic whose position lands near a bin boundary is binned as the f64
+// oracle bins it (f32 log2f moved some across, the main cause of top-bin disagreements)
+__device__ __forceinline__ int md_cent_bin(double f) { return (int)floor(120.0 * log2(f / 55.0) + 0.5); }
 
 __global__ __launch_bounds__(MD_NT) void melodia_salience_kernel(MelodiaArgs a) {
   __shared__ __attribute__((aligned(16))) float2 fft[LdsSize<MD_N>::value];  // 33.8 KB
   __shared__ float mag[MD_BINS + 3];
-  __shared__ float pk_f[MD_MAXPK], pk_a[MD_MAXPK];
-  __shared__ float sal[MD_SAL];
+  __shared__ double pk_f[MD_MAXPK], pk_a[MD_MAXPK];
+  __shared__ double sal[MD_SAL];
   __shared__ int bcount[MD_BUCKETS + 1], bstart[MD_BUCKETS + 1];
   __shared__ int ncand, npk;
   const int tid = threadIdx.x;
   unsigned long long* keys = reinterpret_cast<unsigned long long*>(fft);  // after the spectrum: sort keys
-  // after the spectral peaks: salience entries (key = peak * 20 + h, weight), bucketed by harmonic bin
+  // after the spectral peaks: salience entries (key = peak * 20 + h, f64 weight), bucketed by
+  // harmonic bin
   int* ent_key = reinterpret_cast<int*>(fft);
-  float* ent_w = reinterpret_cast<float*>(fft) + MD_ENT;
-  int* ent_bin = reinterpret_cast<int*>(fft) + 2 * MD_ENT;
+  double* ent_w = reinterpret_cast<double*>(reinterpret_cast<int*>(fft) + MD_ENT);
   int* ent_pos = reinterpret_cast<int*>(fft) + 3 * MD_ENT;  // bucketed order: index into the entries
+  static_assert(4 * MD_ENT * sizeof(int) <= LdsSize<MD_N>::value * sizeof(float2), "entries fit the FFT slot");
 
   for (int64_t g = blockIdx.x; g < a.total_frames; g += gridDim.x) {
     // file of frame g
@@ -148,10 +151,10 @@ __global__ __launch_bounds__(MD_NT) void melodia_salience_kernel(MelodiaArgs a) 
     for (int k = 1 + tid; k < MD_BINS - 1; k += MD_NT) {
       const float l = mag[k - 1], c = mag[k], r = mag[k + 1];
       if (c > l && c >= r && c > 0.0f) {
-        const float pos = (float)k + 0.5f * (l - r) / (l - 2.0f * c + r);
-        const float val = c - 0.25f * (l - r) * (pos - (float)k);
+        const double pos = (double)k + 0.5 * ((double)l - r) / ((double)l - 2.0 * c + r);
+        const double val = c - 0.25 * ((double)l - r) * (pos - (double)k);
         const int q = atomicAdd(&ncand, 1);
-        keys[q] = ((unsigned long long)(~md_ord(val)) << 32) | (unsigned)k;
+        keys[q] = ((unsigned long long)(~md_ord((float)val)) << 32) | (unsigned)k;
       }
     }
     __syncthreads();
@@ -164,18 +167,18 @@ __global__ __launch_bounds__(MD_NT) void melodia_salience_kernel(MelodiaArgs a) 
     if (tid < np) {
       const int k = (int)(unsigned)(keys[tid] & 0xffffffffu);
       const float l = mag[k - 1], c = mag[k], r = mag[k + 1];
-      const float pos = (float)k + 0.5f * (l - r) / (l - 2.0f * c + r);
-      pk_a[tid] = c - 0.25f * (l - r) * (pos - (float)k);
-      pk_f[tid] = pos * a.sr / 8192.0f;
+      const double pos = (double)k + 0.5 * ((double)l - r) / ((double)l - 2.0 * c + r);
+      pk_a[tid] = c - 0.25 * ((double)l - r) * (pos - (double)k);
+      pk_f[tid] = pos * (double)a.sr / 8192.0;
     }
     for (int b = tid; b <= MD_BUCKETS; b += MD_NT) bcount[b] = 0;
     __syncthreads();
     // 4. salience entries of the peaks within 40 dB of the largest (MD_NH harmonics each, stopping
     // at the first below 55 Hz), counted per harmonic bin
-    const float amin = np > 0 ? pk_a[0] * 0.01f : 0.0f;
+    const double amin = np > 0 ? pk_a[0] * 0.01 : 0.0;
     if (tid < np && pk_a[tid] > amin) {
       for (int h = 0; h < MD_NH; ++h) {
-        const int hb = md_cent_bin(pk_f[tid] / (float)(h + 1));
+        const int hb = md_cent_bin(pk_f[tid] / (double)(h + 1));
         if (hb < 0) break;
         if (hb < MD_BUCKETS) atomicAdd(&bcount[hb], 1);
       }
@@ -192,17 +195,14 @@ __global__ __launch_bounds__(MD_NT) void melodia_salience_kernel(MelodiaArgs a) 
     }
     __syncthreads();
     if (tid < np && pk_a[tid] > amin) {
-      float wh = 1.0f;
       for (int h = 0; h < MD_NH; ++h) {
-        const int hb = md_cent_bin(pk_f[tid] / (float)(h + 1));
+        const int hb = md_cent_bin(pk_f[tid] / (double)(h + 1));
         if (hb < 0) break;
         if (hb < MD_BUCKETS) {
           const int e = bstart[hb] + atomicAdd(&bcount[hb], 1);
           ent_key[e] = tid * MD_NH + h;
-          ent_w[e] = pk_a[tid] * wh;
-          ent_bin[e] = hb;
+          ent_w[e] = pk_a[tid] * pow(0.8, (double)h);
         }
-        wh *= 0.8f;
       }
     }
     __syncthreads();
@@ -223,12 +223,12 @@ __global__ __launch_bounds__(MD_NT) void melodia_salience_kernel(MelodiaArgs a) 
     __syncthreads();
     // salience of bin b: the entries of harmonic bins b - 10 .. b + 10, ascending
     for (int b = tid; b < MD_SAL; b += MD_NT) {
-      float s = 0.0f;
+      double s = 0.0;
       for (int hb = max(0, b - MD_SEMI); hb <= b + MD_SEMI; ++hb) {
         const int d = hb > b ? hb - b : b - hb;
-        const float cw = cosf((float)d * (0.5f * 3.14159265358979f / (float)MD_SEMI));
-        const float nbw = cw * cw;
-        for (int i = bstart[hb]; i < bstart[hb + 1]; ++i) s = fmaf(ent_w[ent_pos[i]], nbw, s);
+        const double cw = cos((double)d / MD_SEMI * 3.141592653589793 / 2.0);
+        const double nbw = cw * cw;
+        for (int i = bstart[hb]; i < bstart[hb + 1]; ++i) s += ent_w[ent_pos[i]] * nbw;
       }
       sal[b] = s;
     }
@@ -236,12 +236,12 @@ __global__ __launch_bounds__(MD_NT) void melodia_salience_kernel(MelodiaArgs a) 
     __syncthreads();
     // 5. salience peaks in [sal_min_bin, 599]
     for (int b = max(a.sal_min_bin, 0) + tid; b < MD_SAL; b += MD_NT) {
-      const float c = sal[b];
-      const float l = b > 0 ? sal[b - 1] : -INFINITY;
-      const float r = b + 1 < MD_SAL ? sal[b + 1] : -INFINITY;
-      if (c > l && c >= r && c > 0.0f) {
+      const double c = sal[b];
+      const double l = b > 0 ? sal[b - 1] : -INFINITY;
+      const double r = b + 1 < MD_SAL ? sal[b + 1] : -INFINITY;
+      if (c > l && c >= r && c > 0.0) {
         const int q = atomicAdd(&npk, 1);
-        keys[q] = ((unsigned long long)(~md_ord(c)) << 32) | (unsigned)b;
+        keys[q] = ((unsigned long long)(~md_ord((float)c)) << 32) | (unsigned)b;
       }
     }
     __syncthreads();
@@ -254,7 +254,7 @@ __global__ __launch_bounds__(MD_NT) void melodia_salience_kernel(MelodiaArgs a) 
     if (tid < nout) {
       const int b = (int)(unsigned)(keys[tid] & 0xffffffffu);
       a.pk_bin[g * MD_SALPK + tid] = b;
-      a.pk_sal[g * MD_SALPK + tid] = sal[b];
+      a.pk_sal[g * MD_SALPK + tid] = (float)sal[b];
     }
     if (tid == 0) a.pk_count[g] = nout;
   }

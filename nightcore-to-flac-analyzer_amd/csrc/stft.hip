@@ -36,7 +36,10 @@ constexpr int SM_THREADS = SM_WAVES * 64;
 constexpr int SM_HALF = 528;  // float2 per half-size slot: 512 exchange elements + pads
 // LDS requested per workgroup: 150 KB, so no chroma-chain workgroup shares a CU with the STFT (the
 // kernel needs 105 KB; with the rest free the decimator co-resided and its span per step went
-// 1.2 -> 2.1 ms, the step no faster: tools/ab_bench.sh, profiles/r4_stft_lds_pad_ab.txt)
+// 1.2 -> 2.1 ms, the step no faster: tools/ab_bench.sh, profiles/r4_stft_lds_pad_ab.txt).  Round 5
+// tried letting the octave 0-2 CQT (MFMA-bound, 38 KB, 219 VGPRs) share the STFT's CUs: 12 STFT
+// waves at 96 VGPRs with a 120 KB reserve ran the step at 9.36-10.40 ms against 9.22-9.61 (16 waves,
+// 150 KB) and 16 waves with a 120 KB reserve at 9.31-9.72 (profiles/r5_stft_coresidency_ab.txt)
 constexpr size_t SM_LDS_RESERVE = 150 * 1024;
 using SmTw = StagedTw<1024>;  // per-stage twiddle table in LDS (conflict-free reads)
 

@@ -600,8 +600,11 @@ class Engine:
         self.timers = None
         return out
 
-    GROUPS_IN_FLIGHT = 3    # pair groups queued ahead of the host's oldest wait (analyze)
-    EAGER_FINISH = False    # finish a group only once complete, up to MAX_GROUPS_IN_FLIGHT queued
+    GROUPS_IN_FLIGHT = 3    # pair groups queued ahead of the host's oldest wait (EAGER_FINISH off)
+    # Round 5: the host assembles a group only once its results are on the host (or when
+    # MAX_GROUPS_IN_FLIGHT are queued) and launches the next group meanwhile; untraced device
+    # idle over 10 pipelined steps 4.6-4.9 % -> 4.2-4.7 % (tools/idle_probe.py), the step the same
+    EAGER_FINISH = True
     MAX_GROUPS_IN_FLIGHT = 5
 
     KERNEL_TAGS = ("stft_mel", "window_tg", "tuning_peaks", "decimate", "cqt_low", "cqt_high", "trim_blocks", "tempo_beat",

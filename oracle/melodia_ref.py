@@ -88,3 +88,208 @@ def frame_salience_peaks(y: np.ndarray, t: int, sr: float = 22050.0, hop: int = 
     mag = frame_mag(y, t, hop)
     f, a = spectral_peaks(mag, sr)
     return salience_peaks(salience(f, a), int(cent_bin(80.0)))
+
+
+# ------------------------------------------------------------------------------ contours + melody
+# The host stage of MELODIA, restated for the tests from the published algorithm (Salamon &
+# Gomez 2012, sections II-C and II-D) with essentia 2.1's default PitchContours /
+# PitchContoursMelody parameters.  PARITY UNPINNED like the front end: essentia is absent.  It is
+# written independently of nightcore_analyzer/melodia.py (plain per-frame lists and explicit
+# scans, no vectorised shortcuts) so that an indexing, pool or tie-breaking slip in either one
+# shows up as a difference.  Choices the paper leaves open, taken the same way in both (and
+# named here so a reader can check them against essentia when it is available):
+#   * pitch continuity 27.5625 cents/ms x 1000 x hop / sr / 10 cents = 16 bins at 22 050 Hz, a
+#     peak continues a contour when |bin - last bin| <= 16; the nearest such peak wins, ties to the
+#     earlier peak of the frame (frames list peaks by salience, descending);
+#   * a run of non-salient peaks longer than the time continuity (100 ms) ends the contour before
+#     the peak that would exceed it (that peak stays in the pool); the contour's trailing
+#     non-salient peaks are dropped from it but stay used;
+#   * minimum duration 100 ms: a contour needs at least ceil(100 ms / frame) frames;
+#   * seeds: the largest remaining salient peak, ties to the earlier frame, then the lower bin;
+#   * voicing: contours whose mean salience is below mean - 0.2 std (population std) of the
+#     contours' mean saliences are unvoiced;
+#   * melody pitch mean: per frame the salience-weighted mean bin of the present contours, gaps
+#     interpolated linearly (ends held), a centred 5 s moving average (shortened at the ends);
+#   * octave duplicates: two overlapping contours whose mean bins over the overlap are 1150-1250
+#     cents apart; the one farther (over the overlap) from the melody pitch mean goes;
+#   * pitch outliers: contours whose mean bin is more than 1250 cents from the melody pitch mean
+#     over their frames go; three iterations, the mean recomputed after each removal step;
+#   * output: per frame the present contour with the largest total salience (ties to the earlier
+#     contour in (start, first bin) order), 55 Hz x 2^(bin / 120), 0 outside [80, 20000] Hz.
+PITCH_CONT_CENTS_PER_MS = 27.5625
+TIME_CONT_MS = 100.0
+MIN_DUR_MS = 100.0
+FRAME_THR = 0.9
+DIST_THR = 0.9
+VOICING_TOL = 0.2
+ITERATIONS = 3
+
+
+def contours_ref(frames, sr: float = 22050.0, hop: int = HOP):
+    """frames[t] = (bins, saliences) of frame t (salience descending) -> list of contours
+    (start frame, [bins], [saliences]), sorted by (start, first bin)."""
+    fd = hop / sr
+    cont = PITCH_CONT_CENTS_PER_MS * 1000.0 * fd / 10.0
+    max_gap = TIME_CONT_MS / 1000.0 / fd
+    min_frames = MIN_DUR_MS / 1000.0 / fd
+    T = len(frames)
+    # pool[t] = list of [bin, salience, state]: state 1 salient, 2 non-salient, 0 used
+    pool = []
+    for bins, sals in frames:
+        row = [[float(b), float(s), 1] for b, s in zip(bins, sals)]
+        top = max((r[1] for r in row), default=0.0)
+        for r in row:
+            if r[1] < FRAME_THR * top:
+                r[2] = 2
+        pool.append(row)
+    sal_vals = [r[1] for row in pool for r in row if r[2] == 1]
+    if sal_vals:
+        mu = sum(sal_vals) / len(sal_vals)
+        sd = (sum((v - mu) ** 2 for v in sal_vals) / len(sal_vals)) ** 0.5
+        for row in pool:
+            for r in row:
+                if r[2] == 1 and r[1] < mu - DIST_THR * sd:
+                    r[2] = 2
+
+    def pick(t, last, state):
+        best, bd = None, None
+        for r in pool[t]:
+            if r[2] != state:
+                continue
+            d = abs(r[0] - last)
+            if d <= cont and (bd is None or d < bd):
+                best, bd = r, d
+        return best
+
+    def walk(t0, last, step):
+        out, run = [], 0
+        t = t0 + step
+        while 0 <= t < T:
+            r = pick(t, last, 1)
+            if r is not None:
+                run = 0
+            else:
+                r = pick(t, last, 2)
+                if r is None:
+                    break
+                run += 1
+                if run > max_gap:
+                    break
+            r[2] = 0
+            out.append((t, r, run > 0))
+            last = r[0]
+            t += step
+        while out and out[-1][2]:
+            out.pop()
+        return out
+
+    result = []
+    while True:
+        seed, st = None, None
+        for t in range(T):
+            for r in pool[t]:
+                if r[2] == 1 and (seed is None or r[1] > seed[1] or (r[1] == seed[1] and (t, r[0]) < (st, seed[0]))):
+                    seed, st = r, t
+        if seed is None:
+            break
+        seed[2] = 0
+        fwd = walk(st, seed[0], 1)
+        bwd = walk(st, seed[0], -1)
+        pts = [(t, r) for t, r, _ in reversed(bwd)] + [(st, seed)] + [(t, r) for t, r, _ in fwd]
+        if len(pts) >= min_frames:
+            result.append((pts[0][0], [r[0] for _, r in pts], [r[1] for _, r in pts]))
+    result.sort(key=lambda c: (c[0], c[1][0]))
+    return result
+
+
+def _pitch_mean_ref(contours, T, smooth):
+    num, den = [0.0] * T, [0.0] * T
+    for start, bins, sals in contours:
+        for i, (b, s) in enumerate(zip(bins, sals)):
+            num[start + i] += b * s
+            den[start + i] += s
+    known = [t for t in range(T) if den[t] > 0]
+    if not known:
+        return [0.0] * T
+    m = [0.0] * T
+    for t in known:
+        m[t] = num[t] / den[t]
+    # linear interpolation over the gaps, ends held
+    for t in range(T):
+        if den[t] > 0:
+            continue
+        prev = max((k for k in known if k < t), default=None)
+        nxt = min((k for k in known if k > t), default=None)
+        if prev is None:
+            m[t] = m[nxt]
+        elif nxt is None:
+            m[t] = m[prev]
+        else:
+            m[t] = m[prev] + (m[nxt] - m[prev]) * (t - prev) / (nxt - prev)
+    half = max(1, int(smooth)) // 2
+    out = []
+    for t in range(T):
+        lo, hi = max(0, t - half), min(T, t + half + 1)
+        out.append(sum(m[lo:hi]) / (hi - lo))
+    return out
+
+
+def melody_ref(contours, T, sr: float = 22050.0, hop: int = HOP):
+    """Pitch (Hz) per frame from contours_ref's contours (0 = unvoiced)."""
+    pitch = [0.0] * T
+    if not contours:
+        return np.array(pitch)
+    fd = hop / sr
+    means = [sum(s) / len(s) for _, _, s in contours]
+    mu = sum(means) / len(means)
+    sd = (sum((v - mu) ** 2 for v in means) / len(means)) ** 0.5
+    sel = [c for c, v in zip(contours, means) if v >= mu - VOICING_TOL * sd]
+    smooth = int(round(5.0 / fd))
+    mpm = _pitch_mean_ref(sel, T, smooth)
+
+    def overlap_mean(c, lo, hi):
+        start, bins, _ = c
+        seg = bins[lo - start:hi - start]
+        return sum(seg) / len(seg)
+
+    for _ in range(ITERATIONS):
+        gone = set()
+        for i in range(len(sel)):
+            for j in range(i + 1, len(sel)):
+                if i in gone or j in gone:
+                    continue
+                a, b = sel[i], sel[j]
+                lo, hi = max(a[0], b[0]), min(a[0] + len(a[1]), b[0] + len(b[1]))
+                if hi <= lo:
+                    continue
+                ma, mb = overlap_mean(a, lo, hi), overlap_mean(b, lo, hi)
+                if 115.0 < abs(ma - mb) < 125.0:
+                    ref = sum(mpm[lo:hi]) / (hi - lo)
+                    gone.add(i if abs(ma - ref) > abs(mb - ref) else j)
+        sel = [c for k, c in enumerate(sel) if k not in gone]
+        mpm = _pitch_mean_ref(sel, T, smooth)
+        keep = []
+        for c in sel:
+            start, bins, _ = c
+            ref = sum(mpm[start:start + len(bins)]) / len(bins)
+            if abs(sum(bins) / len(bins) - ref) <= 125.0:
+                keep.append(c)
+        sel = keep
+        mpm = _pitch_mean_ref(sel, T, smooth)
+    best = [None] * T
+    for start, bins, sals in sel:
+        tot = sum(sals)
+        for i, b in enumerate(bins):
+            t = start + i
+            if best[t] is None or tot > best[t]:
+                best[t] = tot
+                hz = 55.0 * 2.0 ** (b * 10.0 / 1200.0)
+                pitch[t] = hz if 80.0 <= hz <= 20000.0 else 0.0
+    return np.array(pitch)
+
+
+def predominant_pitch_ref(y: np.ndarray, sr: float = 22050.0, hop: int = HOP):
+    """The whole oracle: front end of every frame, contours, melody (Hz per frame)."""
+    T = n_frames(len(y), hop)
+    frames = [frame_salience_peaks(y, t, sr, hop) for t in range(T)]
+    return melody_ref(contours_ref(frames, sr, hop), T, sr, hop)

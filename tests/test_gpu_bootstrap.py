@@ -93,3 +93,18 @@ def test_rejections_resolved_by_exact_starts(eng):
     assert flag == 1 and status == 0
     assert nrej_a + nrej_b > 0 and end > 2000 * 5500
     np.testing.assert_array_equal(got, _numpy_boots(a, b, 42))
+
+
+@pytest.mark.parametrize("a,b", [([3.0] * 7, [2.0] * 5),             # every resample equal (no digit pass)
+                                 ([1.0, 2.0] * 4, [1.0] * 3),         # two values, heavy ties at both ranks
+                                 ([-0.5, 0.25, 7.0], None),           # signs and a single array
+                                 ([1e-300, 1e300, 1.0, 2.0, 3.0], [1.0, 1e-300])])
+def test_percentiles_on_tied_and_extreme_boots(eng, a, b):
+    """The order statistics behind the CI (ranks il, il + 1, ih, ih + 1 of the 2000 resample
+    ratios, boot_order_stats) on ties, a constant set, signs and a 600-decade spread."""
+    a = np.array(a)
+    b = None if b is None else np.array(b)
+    got, pt = _device_boots(eng, a, b, 3)
+    ref = _numpy_boots(a, b, 3)
+    np.testing.assert_array_equal(got, ref)
+    assert pt[1] == np.percentile(ref, 2.5) and pt[2] == np.percentile(ref, 97.5)

@@ -131,3 +131,78 @@ def test_oracle_melody_shift_of_a_nightcore_pair():
         assert (hz > 0).sum() > 0.3 * T
         med.append(np.median(hz[hz > 0]))
     assert abs(12 * np.log2(med[1] / med[0]) - 12 * np.log2(1.25)) < 0.15
+
+
+# ---- the host stage against the oracle's independent restatement (oracle/melodia_ref.py)
+def _rows_of(p):
+    return [p.frame(t) for t in range(len(p.counts))]
+
+
+def _ref_contours(p):
+    return R.contours_ref(_rows_of(p))
+
+
+def _same_contours(cs, ref):
+    assert len(cs) == len(ref), (len(cs), len(ref))
+    for c, (start, bins, sals) in zip(cs, ref):
+        assert c.start == start
+        np.testing.assert_array_equal(c.bins, np.array(bins))
+        np.testing.assert_array_equal(c.sal, np.array(sals))
+
+
+def _same_melody(hz, ref):
+    """Same voicing and the same bin per frame (Hz from numpy's vectorised power and Python's
+    scalar one may differ in the last bit)."""
+    np.testing.assert_array_equal(hz > 0, ref > 0)
+    np.testing.assert_allclose(hz, ref, rtol=1e-12, atol=0)
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_contours_and_melody_equal_the_oracle_on_random_peaks(seed):
+    """Random salience peaks with notes, glides, octave copies, gaps and noise peaks: the host's
+    contours and melody equal the restatement's exactly (decisions and values)."""
+    rng = np.random.default_rng(seed)
+    T = 900
+    rows = []
+    note, left = 300, 0
+    for t in range(T):
+        if left == 0:
+            note, left = int(rng.integers(200, 420)), int(rng.integers(20, 120))
+        left -= 1
+        r = []
+        if rng.random() > 0.08:                                    # the melody, with dropouts
+            r.append((note + int(rng.integers(-2, 3)), float(0.8 + 0.2 * rng.random())))
+        if rng.random() < 0.5:                                     # its octave copy, weaker
+            r.append((note + 120, float(0.5 + 0.3 * rng.random())))
+        for _ in range(int(rng.integers(0, 4))):                   # noise peaks
+            r.append((int(rng.integers(65, 600)), float(0.05 + 0.6 * rng.random())))
+        seen = {}
+        for b, s in r:
+            seen[b] = max(s, seen.get(b, 0.0))
+        rows.append(list(seen.items()))
+    p = _peaks(T, rows)
+    cs = M.pitch_contours(p)
+    ref = _ref_contours(p)
+    assert len(cs) > 5
+    _same_contours(cs, ref)
+    _same_melody(M.contours_melody(cs, T), R.melody_ref(ref, T))
+
+
+@pytest.mark.slow
+def test_host_stage_equals_oracle_on_a_melody_pair_front_end():
+    """The oracle's front end of a 1.25x melody pair feeds both host stages: identical contours,
+    identical melody (about 10 s of numpy)."""
+    from nightcore_analyzer import synth
+    nc, src = synth.make_melody_pair(4.0, 7)
+    for y in (src, nc):
+        T = R.n_frames(len(y))
+        rows = []
+        for t in range(T):
+            b, s = R.frame_salience_peaks(y, t)
+            rows.append(list(zip(b.tolist(), s.tolist())))
+        p = _peaks(T, rows)
+        cs = M.pitch_contours(p)
+        _same_contours(cs, _ref_contours(p))
+        hz = M.contours_melody(cs, T)
+        _same_melody(hz, R.melody_ref(_ref_contours(p), T))
+        assert (hz > 0).sum() > 0.3 * T
