@@ -1161,6 +1161,10 @@ __device__ __forceinline__ void cqt_low_tile(const CqmArgs& a, int bx, int c) {
           acc[rt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al[rt], bh, acc[rt][nt], 0, 0, 0);
         }
       };
+      // the MFMA cluster at priority 1: the partner wave on the SIMD (another workgroup's tile)
+      // takes the VALU / LDS slots around it (round 5: 347.7 -> 339.4 us per 224 chunks, the same
+      // pair on cqt_mfma_kernel 328.6 -> 332.1, not kept there; profiles/r5_cqt_sched_variants.txt)
+      __builtin_amdgcn_s_setprio(1);
       cm_wait<2>(b[0][0], b[0][1]);
       cm_rd<4 * 1024>(b[2][0], sbl);
       cm_rd<5 * 1024>(b[2][1], sbl);
@@ -1177,11 +1181,13 @@ __device__ __forceinline__ void cqt_low_tile(const CqmArgs& a, int bx, int c) {
       tile(3);
       cm_wait<0>(b[4][0], b[4][1]);
       tile(4);
+      __builtin_amdgcn_s_setprio(0);
     }
     if (Q == M - 1 && !last) {
       // block g + 1 (requested at this group's first step) into the image: every A read of
       // group g is done (their registers were consumed above).  vmcnt(0), not a count: younger
-      // slice pieces can retire before the block loads (header)
+      // slice pieces can retire before the block loads (header).  Splitting after the first or
+      // third column tile of the step instead: 351.4 / 350.2 against 347.7 us (round 5)
       c2_vmwait_st<0>(st);
       if (active) c2_split<OCT>(st, img, sx, s0, g + 1, Ly, EDGE, lane);
     }
