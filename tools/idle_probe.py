@@ -3,7 +3,7 @@
 batches with every kernel recording its execution span (profile mode 2), then the union of the
 spans (nc_profile_read_busy) against their extent.  Variants are timed in rotation.
 usage: tools/idle_probe.py [K] [variant ...]
-  variant: "default", "SCHEDULE" ("6,26,26,6", "32"), "SCHEDULE@G" (G groups in flight),
+  variant: "default", "SCHEDULE" ("6,26,26,6", "32"), "SCHEDULE@G" (G groups in flight: GROUPS_IN_FLIGHT and, eager, MAX_GROUPS_IN_FLIGHT),
            "...+eager" / "+lazy" (Engine.EAGER_FINISH: assemble a group only once it is complete)"""
 import sys
 import time
@@ -24,12 +24,13 @@ def main():
     eng = E.get_engine(0)
     sig = eng.upload_signals([a for nc, src in pairs for a in (nc, src)])
     params = E.Params(compute_ibi=False)
-    gif0, eager0 = eng.GROUPS_IN_FLIGHT, eng.EAGER_FINISH
+    gif0, eager0, max0 = eng.GROUPS_IN_FLIGHT, eng.EAGER_FINISH, eng.MAX_GROUPS_IN_FLIGHT
 
     def setup(v):
         v, _, flag = v.partition("+")
         sched, _, gif = v.partition("@")
         eng.GROUPS_IN_FLIGHT = int(gif) if gif else gif0
+        eng.MAX_GROUPS_IN_FLIGHT = int(gif) if gif else max0
         eng.EAGER_FINISH = True if flag == "eager" else (False if flag == "lazy" else eager0)
         return None if sched == "default" else ([int(x) for x in sched.split(",")] if "," in sched else int(sched))
 
