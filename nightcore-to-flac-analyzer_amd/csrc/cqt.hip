@@ -309,6 +309,9 @@ __global__ __launch_bounds__(TP_WAVES * 64) void tuning_peaks_kernel(PeakArgs a)
   fill_staged_tw<1024>(sh_tw, a.tw, threadIdx.x, TP_WAVES * 64);
   for (int i = threadIdx.x; i < 1024; i += TP_WAVES * 64) sh_hann[i] = reinterpret_cast<const float2*>(a.hann2048)[i];
   __syncthreads();
+  // this lane's Hann taps held across frames (the stft_mel form, round 5): no LDS reads per frame
+  float2 hw[16];
+  lds_read16_strided<0, 64 * 8>(hw, lds_addr(sh_hann + fft_in_lane(lane0)));
   const int64_t n_groups = (a.total_tframes + TP_WAVES - 1) / TP_WAVES;
   const int64_t gb = n_groups * blockIdx.x / gridDim.x, ge = n_groups * (blockIdx.x + 1) / gridDim.x;
   // The wave's work-list frames gf rise by TP_WAVES: their chunk is tracked forward, its
@@ -354,18 +357,17 @@ __global__ __launch_bounds__(TP_WAVES * 64) void tuning_peaks_kernel(PeakArgs a)
     const int64_t s0 = (int64_t)t * 512 - 1024;
     FftIn<1024> in;
     if (s0 >= 0 && s0 + 2048 <= L) {
-      float2 xv[16], hw[16];
+      float2 xv[16];
       if ((off & 1) == 0) {
         const float2* x2 = reinterpret_cast<const float2*>(x + s0);
 #pragma unroll
-        for (int r = 0; r < 16; ++r) xv[r] = x2[jin + 64 * r];  // issued first: the LDS batch hides under them
+        for (int r = 0; r < 16; ++r) xv[r] = x2[jin + 64 * r];
       } else {
         // a chunk at an odd sample: two dword loads per pair, no bounds tests (stft_mel)
         const float* xs = x + s0;
 #pragma unroll
         for (int r = 0; r < 16; ++r) xv[r] = make_float2(xs[2 * (jin + 64 * r)], xs[2 * (jin + 64 * r) + 1]);
       }
-      lds_read16_strided<0, 64 * 8>(hw, lds_addr(sh_hann + jin));
 #pragma unroll
       for (int r = 0; r < 16; ++r) in[0][r] = make_float2(xv[r].x * hw[r].x, xv[r].y * hw[r].y);
     } else {
@@ -938,7 +940,10 @@ constexpr int C2_NW = 2;                                  // tiles (waves) per w
 constexpr int C2_R = 2;                                   // filter ring slots
 constexpr int C2_D = C2_R - 1;                            // slices requested ahead of the step that reads them
 constexpr int C2_PS = (CM_NT * 2 + C2_NW - 1) / C2_NW;    // slice DMA pieces per wave per step
-constexpr int C2_NRP = 72;                                // image rows per wave (>= 64 + M - 1)
+#ifndef C2_NRP_
+#define C2_NRP_ 72
+#endif
+constexpr int C2_NRP = C2_NRP_;                           // image rows per wave (>= 64 + M - 1)
 constexpr int C2_IMG = C2_NRP * 64;                       // bytes of one hi (or lo) image
 constexpr int C2_RING = C2_R * CM_SLICE * 16;
 constexpr int C2_NU = (C2_NRP * 4 + 63) / 64;             // staging rounds (8-sample units per lane)
@@ -1231,17 +1236,27 @@ __device__ __forceinline__ void cqt_low_tile(const CqmArgs& a, int bx, int c) {
   }
 }
 
+#ifndef CQL_ONLY
+#define CQL_ONLY -1  // timing probe (outputs wrong): >= 0 launches only that octave
+#endif
 __global__ __launch_bounds__(C2_NW * 64, 2) void cqt_mfma_low_kernel(CqmArgs a) {
-  if (blockIdx.z == 0) {
+  const unsigned oz = CQL_ONLY >= 0 ? (unsigned)CQL_ONLY : blockIdx.z;
+  if (oz == 0) {
     cqt_low_tile<0, false>(a, blockIdx.x, blockIdx.y);
     cqt_low_tile<0, true>(a, blockIdx.x, blockIdx.y);
-  } else if (blockIdx.z == 1) {
+  } else if (oz == 1) {
     cqt_low_tile<1, false>(a, blockIdx.x, blockIdx.y);
     cqt_low_tile<1, true>(a, blockIdx.x, blockIdx.y);
-  } else {
+  } else if (CQL_ONLY != 3) {
     cqt_low_tile<2, false>(a, blockIdx.x, blockIdx.y);
     cqt_low_tile<2, true>(a, blockIdx.x, blockIdx.y);
   }
+#if CQL_ONLY == 3
+  else {
+    cqt_low_tile<3, false>(a, blockIdx.x, blockIdx.y);
+    cqt_low_tile<3, true>(a, blockIdx.x, blockIdx.y);
+  }
+#endif
 }
 
 // Per (chunk, 64-frame tile): chroma = the 7 octave partial rows summed (ascending bins),
@@ -1487,7 +1502,7 @@ int launch_chroma_mean(Context& ctx, const float* sig, const int64_t* chunk_off,
     // bench's cqt_chroma unit (7 octaves of every chunk) is their sum
     KTimer kt_(ctx, "cqt_low", st);
     ma.span = kt_.span();
-    const dim3 lg((unsigned)((ntile + C2_NW - 1) / C2_NW), (unsigned)n, 3u);
+    const dim3 lg((unsigned)((ntile + C2_NW - 1) / C2_NW), (unsigned)n, CQL_ONLY >= 0 ? 1u : 3u);
     hipLaunchKernelGGL(cqt_mfma_low_kernel, lg, dim3(C2_NW * 64), cql_lds_bytes(), st, ma);
   }
   {

@@ -207,6 +207,12 @@ __device__ __forceinline__ void sm_exchange2(const float2 (&v)[16], float2 (&o)[
 #undef NC_W_
 #undef NC_R_
 
+// H512: hop 512 (the window path), whose hop slice [1024, 1536) of the frame is exactly stage-1
+// rows r = 8..11 of every lane: the energy needs no per-sample membership test.  With the lane's
+// Hann taps held in registers across frames (124 VGPRs, still four waves per SIMD) instead of 16
+// LDS reads per frame: 483.3 -> 472.6 us per 560 windows, bit-identical (round 5,
+// profiles/r5_stft_variants.txt; either change alone 483.8 / 479.1)
+template <bool H512>
 __global__ __launch_bounds__(SM_THREADS) void stft_mel_kernel(StftMelArgs a) {
   const Span span_(a.span);
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -232,6 +238,8 @@ __global__ __launch_bounds__(SM_THREADS) void stft_mel_kernel(StftMelArgs a) {
 
   const int64_t n_groups = (a.total_frames + SM_WAVES - 1) / SM_WAVES;
   const int64_t gb = n_groups * blockIdx.x / gridDim.x, ge = n_groups * (blockIdx.x + 1) / gridDim.x;
+  float2 hw[16];  // this lane's Hann taps, w[2 (j1 + 64 r)] and w[2 (j1 + 64 r) + 1]
+  lds_read16_strided<0, 64 * 8>(hw, lds_addr(sh_hann + sm_j1(lane0)));
   // the wave's frames g = grp * SM_WAVES + wave rise by SM_WAVES: their sequence is tracked
   // forward, its bounds, flags, length and offset reloaded only when g crosses into a later
   // sequence, instead of a 64-bit division or binary search and dependent loads per frame
@@ -274,7 +282,7 @@ __global__ __launch_bounds__(SM_THREADS) void stft_mel_kernel(StftMelArgs a) {
     double e = 0.0;
     const bool interior = s0 >= 0 && s0 + 2048 <= L;
     if (interior) {
-      float2 xv[16], hw[16];
+      float2 xv[16];
       if ((off & 1) == 0) {
         const float2* x2 = reinterpret_cast<const float2*>(x + s0);
 #pragma unroll
@@ -284,14 +292,13 @@ __global__ __launch_bounds__(SM_THREADS) void stft_mel_kernel(StftMelArgs a) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) xv[r] = make_float2(xs[2 * (jin + 64 * r)], xs[2 * (jin + 64 * r) + 1]);
       }
-      lds_read16_strided<0, 64 * 8>(hw, lds_addr(sh_hann + jin));
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int n = jin + 64 * r;
         const float2 v = xv[r];
         const float2 h = hw[r];
         if (r >= 8 && r < 12) {
-          const bool in_hop = 2 * n - 1024 < a.hop;
+          const bool in_hop = H512 || 2 * n - 1024 < a.hop;
           const double dx = in_hop ? (double)v.x : 0.0, dy = in_hop ? (double)v.y : 0.0;
           e = fma(dx, dx, e);
           e = fma(dy, dy, e);
@@ -451,7 +458,10 @@ int launch_stft_mel(Context& ctx, const StftMelArgs& args, hipStream_t st) {
   {
     KTimer kt_(ctx, "stft_mel", st);
     a.span = kt_.span();
-    hipLaunchKernelGGL(stft_mel_kernel, dim3(grid), dim3(SM_THREADS), lds, st, a);
+    if (a.hop == 512)
+      hipLaunchKernelGGL(stft_mel_kernel<true>, dim3(grid), dim3(SM_THREADS), lds, st, a);
+    else
+      hipLaunchKernelGGL(stft_mel_kernel<false>, dim3(grid), dim3(SM_THREADS), lds, st, a);
   }
   NC_HIP(hipGetLastError());
   return 0;

@@ -292,19 +292,19 @@ def _group_bounds(B: int, group_pairs, ) -> List[Tuple[int, int]]:
             left -= n
             i += 1
     elif group_pairs is None:
-        # default: a 6-pair group to start the device early (its host plan is the only one
-        # exposed), 26-pair groups (fuller launches of the latency-bound per-window kernels),
-        # a 6-pair group at the end to keep the exposed host assembly and the chroma tail
-        # short (tools/group_sweep.py, tools/sched_probe.py: 6,26,26,6 is the fastest
-        # schedule measured for 64 pairs, 2 % ahead of 8,24,24,8)
+        # default: groups of 16 pairs, the last two evened out when 16 does not divide the batch
+        # (no group under 8 pairs once B > 16).  Round 5, with the oldest group assembled as soon
+        # as it completes (Engine.EAGER_FINISH): 4 x 16 ran the 64-pair step 4-5 % faster than the
+        # earlier 6/26/26/6 (8.73-8.84 against 9.18-9.40 ms in five rotated rounds on one box;
+        # 10/18/18/18 8.79-8.97, 12/20/20/12 8.83-9.01, 14/18/18/14 8.79-9.02, 8/14x4 8.96-9.32,
+        # 8x8 10.0; profiles/r5_group_schedule.txt, tools/idle_probe.py)
+        q, r = divmod(B, 16)
         if B <= 16:
             sizes = [B] if B else []
+        elif r == 0 or r >= 8:
+            sizes = [16] * q + ([r] if r else [])
         else:
-            sizes, left = [6], B - 6
-            while left > 32:
-                sizes.append(26)
-                left -= 26
-            sizes += [left - 6, 6] if left > 12 else [left]
+            sizes = [16] * (q - 1) + [(16 + r + 1) // 2, (16 + r) // 2]
     else:
         gp = max(1, int(group_pairs))
         sizes = [gp] * (B // gp) + ([B % gp] if B % gp else [])

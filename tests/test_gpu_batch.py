@@ -1,7 +1,7 @@
 """GPU parity of the engine's batched, multi-group path: the one bench.py times
 (BASELINE config 3: 64 three-minute pairs per GPU).
 
-``Engine.analyze`` splits a batch of more than 16 pairs into pair groups (6/26/26/6
+``Engine.analyze`` splits a batch of more than 16 pairs into pair groups (16/16/16/16
 for 64), runs the silence trim in two launches (the first group's files, then the
 rest on the tail stream), keeps up to GROUPS_IN_FLIGHT groups queued and recycles
 the piptrack peak lists through a ring of GROUPS_IN_FLIGHT + 1 workspaces
@@ -128,7 +128,7 @@ def _key(o: E.PairOutcome):
 
 
 def test_group_schedule_is_multi_group():
-    assert [b - a for a, b in E._group_bounds(N_PAIRS, None)] == [6, 26, 26, 6]
+    assert [b - a for a, b in E._group_bounds(N_PAIRS, None)] == [16, 16, 16, 16]
     assert len(E._group_bounds(17, 3)) == 6 > E.Engine.GROUPS_IN_FLIGHT + 1
 
 

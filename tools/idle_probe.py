@@ -48,7 +48,8 @@ def main():
     for v in variants:          # warm every variant
         run(setup(v), 0)
     res = {v: {"off": [], "span": [], "idle": []} for v in variants}
-    for _ in range(3):
+    import os
+    for _ in range(int(os.environ.get("NC_PROBE_ROUNDS", "3"))):
         for v in variants:
             gp = setup(v)
             res[v]["off"].append(run(gp, 0)[0])
