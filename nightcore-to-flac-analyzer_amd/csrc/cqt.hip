@@ -1236,8 +1236,14 @@ __device__ __forceinline__ void cqt_low_tile(const CqmArgs& a, int bx, int c) {
   }
 }
 
+// CQL_ONLY (timing probe, outputs wrong): >= 0 launches only that octave; 3 (with -DC2_NRP_=80)
+// runs octave 3 through this kernel's structure.  Round 5, rotated timer, us per 224 chunks alone
+// (profiles/r5_cqt_low_octaves.txt): octave 0 175.2, 1 133.0, 2 116.0, 3 107.7, all three 328.0:
+// octave 0 (two k-steps per block, the block loads one k-step ahead of their split) costs most.
+// Interleaving the octaves in dispatch order (each XCD's consecutive workgroups the three octaves
+// of one tile pair) ran 359.6 -> 392.8 (not kept)
 #ifndef CQL_ONLY
-#define CQL_ONLY -1  // timing probe (outputs wrong): >= 0 launches only that octave
+#define CQL_ONLY -1
 #endif
 __global__ __launch_bounds__(C2_NW * 64, 2) void cqt_mfma_low_kernel(CqmArgs a) {
   const unsigned oz = CQL_ONLY >= 0 ? (unsigned)CQL_ONLY : blockIdx.z;
