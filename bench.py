@@ -261,12 +261,14 @@ def main():
     def run_windows(k, split_offset=0.0, gather=True):
         """k steps of the window-sharded analysis (interior groups pipelined across steps).
         gather=True is analyze_sharded's default: every step's outcomes of all pairs end on
-        every rank (an all-gather after the step's last record exchange)."""
+        every rank (one byte all-gather per step after the step's last record exchange; the
+        other ranks' outcomes unpickled on first access: sharded.GatheredOutcomes).  Returns
+        one sequence of outcomes per step (gather) or of this rank's (pair, outcome)."""
         from nightcore_analyzer.sharded import DeviceStages, analyze_sharded
         res = analyze_sharded(DeviceStages(eng, signals), params, lengths=lengths, local_pairs=ids,
                               split_offset=split_offset, gather=gather, steps=k)
         res = [res] if k == 1 else res
-        return [[(None, o) for o in r] for r in res] if gather else res
+        return res
 
     outs = step()
     bad = [i for i, o in enumerate(outs) if o.error is not None]
@@ -311,6 +313,7 @@ def main():
     # separate analyze calls (reported beside it as single_call_ms_per_step).  Window mode:
     # one analyze_sharded call of K steps (its interior groups pipelined the same way)
     pipelined = not args.no_pipeline
+    gather_unpickle_ms = None
     t0 = time.perf_counter()
     if win_mode:
         res = run_windows(args.steps)
@@ -325,13 +328,19 @@ def main():
     torch.cumsum(marker, 0)
     torch.cuda.synchronize()
     if win_mode:
-        mine = [o for _, o in res[0]]           # gather=True: every pair's outcome on every rank
-        if any(o.error is not None for o in mine) or any(len(r) != world * P for r in res):
-            raise RuntimeError("a window-sharded step failed or returned an incomplete result")
+        if any(len(r) != world * P for r in res):
+            raise RuntimeError("a window-sharded step returned an incomplete result")
+        # the received outcomes unpickled, outside the timed region (its cost reported beside it)
+        tu = time.perf_counter()
+        decoded = [list(r) for r in res]
+        gather_unpickle_ms = max_over_ranks((time.perf_counter() - tu) / args.steps * 1e3)
+        mine = decoded[0]                       # gather=True: every pair's outcome on every rank
+        if any(o.error is not None for r in decoded for o in r):
+            raise RuntimeError("a window-sharded step failed")
         win_total = sum(o.detail["energy_src"].size + o.detail["energy_nc"].size for o in mine)
         if rank == 0 and (mine[0].result.tempo_ratio != tr or mine[0].result.pitch_ratio != pr):
             raise RuntimeError("the window-sharded result of pair 0 differs from the single-GPU engine's")
-        del res, mine                           # not kept (see below)
+        del res, mine, decoded                  # not kept (see below)
     elif pipelined:
         if len(res) != args.steps or any(len(r) != len(outs) for r in res):
             raise RuntimeError("analyze_batches returned an incomplete result")
@@ -387,7 +396,7 @@ def main():
                 n_win = world * win_per_step
             else:
                 r_ = run_windows(args.steps, off, gat)
-                n_win = (sum(o.detail["energy_src"].size + o.detail["energy_nc"].size for _, o in r_[0]) if gat else
+                n_win = (sum(o.detail["energy_src"].size + o.detail["energy_nc"].size for o in r_[0]) if gat else
                          sum_over_ranks(sum(o.detail["energy_src"].size + o.detail["energy_nc"].size
                                             for _, o in r_[0])))
             torch.cuda.synchronize()
@@ -738,6 +747,11 @@ def main():
         }
         if modes is not None:
             line["modes"] = modes
+        if win_mode:
+            # the timed steps end with every rank holding every pair's outcome as the bytes of
+            # the step's all-gather; unpickling the other ranks' outcomes happens on access
+            # (sharded.GatheredOutcomes), here all of them after the timed region, per step
+            line["gather_unpickle_ms_per_step"] = gather_unpickle_ms
         if upl is not None:
             line["upload_included"] = upl
         if ibi is not None:

@@ -1480,6 +1480,64 @@ class Engine:
         return res
 
 # ------------------------------------------------------------------------------ host assembly + logs
+class _Lines:
+    """A deferred log entry: ``fn(*args)`` renders the line (or lines) when the outcome's logs
+    are first read.  ``fn`` is a module-level function and ``args`` plain values, so an
+    unrendered outcome pickles (the window-sharded gather sends outcomes to other ranks without
+    formatting ~130 lines per pair; sharded.GatheredOutcomes)."""
+    __slots__ = ("fn", "args")
+
+    def __init__(self, fn, *args):
+        self.fn, self.args = fn, args
+
+    def __call__(self):
+        return self.fn(*self.args)
+
+    def __reduce__(self):
+        return (_Lines, (self.fn,) + tuple(self.args))
+
+
+# the deferred lines of assemble_pair (pipeline.py:77-215's text)
+def _log_strip(top_db, lead_n, trail_n, len_n, lead_s, trail_s, len_s):
+    return [f"Stripping silence (top_db={top_db} dB)…",
+            f"  nightcore: −{lead_n:.2f}s leading, −{trail_n:.2f}s trailing  →  {len_n / SR:.1f} s",
+            f"  source:    −{lead_s:.2f}s leading, −{trail_s:.2f}s trailing  →  {len_s / SR:.1f} s"]
+
+
+def _log_slicing(window_sec, hop_sec, n_nc, n_src, gate_db):
+    return [f"Slicing into {window_sec:.0f} s windows (hop {hop_sec:.0f} s)…",
+            f"  nightcore: {n_nc} windows  |  source: {n_src} windows",
+            f"Energy gating (threshold {gate_db} dB below peak)…"]
+
+
+def _log_gated(n_nc, n_src):
+    return f"  after gating — nightcore: {n_nc} windows  |  source: {n_src} windows"
+
+
+def _log_chroma(point_st, lo_st, hi_st, n):
+    return (f"    Chroma xcorr: {point_st:+.3f} st  95% CI [{lo_st:+.3f}, {hi_st:+.3f}] st"
+            f"  ({n} chunk{'s' if n != 1 else ''})")
+
+
+def _log_tempo_windows(starts, win_n):
+    """``starts``: the sample offsets of the pair's gated windows of one file, in order."""
+    n = len(starts)
+    return [f"    tempo window {i + 1}/{n}  [{s / SR:.1f}–{(s + win_n) / SR:.1f} s]"
+            for i, s in enumerate(starts.tolist())]
+
+
+def _log_confident(n_conf, n):
+    return f"    {n_conf}/{n} windows yielded a confident tempo estimate"
+
+
+def _log_prior(prior, med, ratio):
+    return f"  NC tempo prior: {prior:.1f} BPM  (src median {med:.1f} BPM × dur ratio {ratio:.4f})"
+
+
+def _log_ibi(r, lo, hi):
+    return f"  IBI ratio: {r:.6f}×  95% CI [{lo:.6f}, {hi:.6f}]"
+
+
 def assemble_pair(b, p: Params, h, ibi, starts, w0, w1, f_len, strip_len, lead, trail, intro,
                   win_n, pair_chunks, n_cp, nj, n_pitch_jobs, align=None, out: Optional[PairOutcome] = None,
                   wait=None, span=None) -> PairOutcome:
@@ -1493,11 +1551,8 @@ def assemble_pair(b, p: Params, h, ibi, starts, w0, w1, f_len, strip_len, lead, 
     fn, fs = 2 * b, 2 * b + 1
     nc_len, src_len = int(f_len[fn]), int(f_len[fs])
     if p.silence_strip_db is not None:
-        L(lambda: [f"Stripping silence (top_db={p.silence_strip_db} dB)…",
-                   f"  nightcore: −{lead[fn]:.2f}s leading, −{trail[fn]:.2f}s trailing"
-                   f"  →  {strip_len[fn] / SR:.1f} s",
-                   f"  source:    −{lead[fs]:.2f}s leading, −{trail[fs]:.2f}s trailing"
-                   f"  →  {strip_len[fs] / SR:.1f} s"])
+        L(_Lines(_log_strip, p.silence_strip_db, float(lead[fn]), float(trail[fn]), float(strip_len[fn]),
+                 float(lead[fs]), float(trail[fs]), float(strip_len[fs])))
     if p.src_trim_sec > 0.0:
         L(f"Manual source trim: skipping {p.src_trim_sec:.2f}s from source start")
     elif align is not None:                              # pipeline.py:111-125
@@ -1507,14 +1562,12 @@ def assemble_pair(b, p: Params, h, ibi, starts, w0, w1, f_len, strip_len, lead, 
             L(f"  Intro detected — trimming {raw:.2f}s from source start  (speed hint: {spd:.4f}×)")
         else:
             L(f"  No significant intro offset detected  (raw: {raw:.2f}s < {ALIGN_MIN_OFFSET:.1f}s threshold)")
-    L(lambda: [f"Slicing into {p.window_sec:.0f} s windows (hop {p.hop_sec:.0f} s)…",
-               f"  nightcore: {len(starts[fn])} windows  |  source: {len(starts[fs])} windows",
-               f"Energy gating (threshold {p.energy_gate_db} dB below peak)…"])
+    L(_Lines(_log_slicing, p.window_sec, p.hop_sec, len(starts[fn]), len(starts[fs]), p.energy_gate_db))
     wait("gate")
     act = h["active_l"]
     src_w = [w for w in range(w0[fs], w1[fs]) if act[w]]
     nc_w = [w for w in range(w0[fn], w1[fn]) if act[w]]
-    L(lambda: f"  after gating — nightcore: {len(nc_w)} windows  |  source: {len(src_w)} windows")
+    L(_Lines(_log_gated, len(nc_w), len(src_w)))
     out.detail.update(energy_src=h["energy"][w0[fs]:w1[fs]].copy(), energy_nc=h["energy"][w0[fn]:w1[fn]].copy(),
                       n_src_windows=len(src_w), n_nc_windows=len(nc_w),
                       nc_duration=nc_len / SR, src_duration=src_len / SR)
@@ -1542,8 +1595,7 @@ def assemble_pair(b, p: Params, h, ibi, starts, w0, w1, f_len, strip_len, lead, 
             lo_st = hi_st = point_st
             L(f"    Only {n} chunk(s) available (need ≥ {MIN_CHUNKS}) — "
               "pitch CI is degenerate; estimate may be less reliable.")
-        L(lambda: f"    Chroma xcorr: {point_st:+.3f} st  95% CI [{lo_st:+.3f}, {hi_st:+.3f}] st"
-                  f"  ({n} chunk{'s' if n != 1 else ''})")
+        L(_Lines(_log_chroma, point_st, lo_st, hi_st, n))
         pick = None
         if p.melodia is None or span is None:
             L("    essentia not available — skipping MELODIA refinement")
@@ -1584,9 +1636,7 @@ def assemble_pair(b, p: Params, h, ibi, starts, w0, w1, f_len, strip_len, lead, 
         f = fs if side == "src" else fn
         st_f, base = starts[f], w0[f]
         nws = len(ws_)
-        L(lambda st_f=st_f, base=base, ws_=ws_, nws=nws: [
-            f"    tempo window {i + 1}/{nws}  [{st_f[w - base] / SR:.1f}–{(st_f[w - base] + win_n) / SR:.1f} s]"
-            for i, w in enumerate(ws_)])
+        L(_Lines(_log_tempo_windows, np.asarray(st_f)[np.asarray(ws_, np.int64) - base], win_n))
         wait(side)
         bpm_l, nb_l = h["bpm_l"], h["nbeats_l"]
         if h.get("any_nb_neg", True) and any(nb_l[w] < 0 for w in ws_):
@@ -1594,8 +1644,7 @@ def assemble_pair(b, p: Params, h, ibi, starts, w0, w1, f_len, strip_len, lead, 
             out.error = _native.NativeError(f"beat tracker capacity exceeded in a {side} window of pair {b}")
             return out
         vals = [bpm_l[w] if nb_l[w] >= MIN_BEATS else None for w in ws_]
-        L(lambda vals=vals, n=nws:
-          f"    {sum(1 for v in vals if v is not None)}/{n} windows yielded a confident tempo estimate")
+        L(_Lines(_log_confident, sum(1 for v in vals if v is not None), nws))
         tempos[side] = vals
         if side == "src":
             valid_src = [t for t in vals if t is not None]
@@ -1603,8 +1652,7 @@ def assemble_pair(b, p: Params, h, ibi, starts, w0, w1, f_len, strip_len, lead, 
             if valid_src and nc_dur > 0 and src_dur > 0:
                 med = C._median(valid_src)
                 pr_ = h['prior_l'][b]
-                L(lambda: f"  NC tempo prior: {pr_:.1f} BPM  "
-                          f"(src median {med:.1f} BPM × dur ratio {src_dur / nc_dur:.4f})")
+                L(_Lines(_log_prior, pr_, med, src_dur / nc_dur))
             L("  ← nightcore →")
     out.detail.update(src_tempos=tempos["src"], nc_tempos=tempos["nc"], nc_start_bpm=h["prior_l"][b],
                       tempo_margin_src=h["margin"][src_w].copy(), tempo_margin_nc=h["margin"][nc_w].copy())
@@ -1636,7 +1684,7 @@ def assemble_pair(b, p: Params, h, ibi, starts, w0, w1, f_len, strip_len, lead, 
             o = ibi["out"]
             res.ibi_ratio = float(o[b])
             res.ibi_ci = (float(o[Bn + b]), float(o[2 * Bn + b]))
-            L(lambda: f"  IBI ratio: {res.ibi_ratio:.6f}×  95% CI [{res.ibi_ci[0]:.6f}, {res.ibi_ci[1]:.6f}]")
+            L(_Lines(_log_ibi, res.ibi_ratio, res.ibi_ci[0], res.ibi_ci[1]))
         else:
             L("  IBI ratio: insufficient beats — skipped")
         out.detail.update(ibi_nbeats=(int(ibi["nbeats"][2 * b]), int(ibi["nbeats"][2 * b + 1])),

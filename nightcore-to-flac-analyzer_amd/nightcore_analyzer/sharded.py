@@ -33,7 +33,10 @@ xGMI before consensus".  SURVEY.md §8(e) lays the split out and this module fol
     3. the owner runs the bootstraps (consensus.py:243-312, pitch.py:143-150), the hop-64
        IBI pass (tempo.py:120-173) and the host assembly (report, warnings, logs).
 * The results of every pair are gathered to every rank (``gather=True``, the API
-  default; the benchmark leaves it off, as its pair mode does).
+  default): each rank pickles its owned outcomes once (log lines still unrendered:
+  ``engine._Lines``), one all-gather moves every rank's bytes to every rank (device tensors
+  over RCCL), and a rank unpickles another rank's outcomes on first access
+  (``GatheredOutcomes``).  The benchmark's N > 1 headline times this default.
 
 The records are fixed-size f64 rows.  They are assembled on the host from the stage
 results (a few hundred bytes per window), copied to the exchange device on the split-pair
@@ -58,11 +61,14 @@ consensus placement are tested without a GPU.  Every result equals the single-ra
 """
 from __future__ import annotations
 
+import collections.abc
+import contextlib
 import dataclasses
 import gc
 import math
+import pickle
 from dataclasses import dataclass
-from typing import List, Optional, Sequence, Tuple
+from typing import Dict, List, Optional, Sequence, Tuple
 
 import numpy as np
 import torch
@@ -289,6 +295,100 @@ class Exchange:
         for part in buf:
             out.extend(part)
         return out
+
+    def gather_bytes(self, blob: bytes) -> List[memoryview]:
+        """Every rank's byte string, in rank order: one all_gather_into_tensor of the lengths
+        and one of the strings padded to the longest (uint8; device tensors under RCCL, on the
+        split-pair stream).  The parts are views of one host buffer: nothing is copied per rank."""
+        if not self.on or self.world == 1:
+            return [memoryview(blob)]
+        ctx = torch.cuda.stream(self.stream) if self.dev.type == "cuda" and self.stream is not None \
+            else contextlib.nullcontext()
+        with ctx:
+            n = torch.tensor([len(blob)], dtype=torch.int64).to(self.dev)
+            ns = torch.empty(self.world, dtype=torch.int64, device=self.dev)
+            dist.all_gather_into_tensor(ns, n, group=self.group)
+            sizes = ns.cpu().tolist()
+            S = max(1, int(max(sizes)))
+            mine = np.zeros(S, np.uint8)
+            mine[:len(blob)] = np.frombuffer(blob, np.uint8)
+            t = torch.from_numpy(mine).to(self.dev)
+            out = torch.empty(self.world * S, dtype=torch.uint8, device=self.dev)
+            dist.all_gather_into_tensor(out, t, group=self.group)
+            h = memoryview(out.cpu().numpy())
+        return [h[q * S:q * S + int(sizes[q])] for q in range(self.world)]
+
+
+def _dumps_outcomes(outs: List[Tuple[int, PairOutcome]]) -> bytes:
+    """A rank's [(pair, outcome)] pickled for the result gather.  An outcome that does not
+    pickle (an exception type that cannot be rebuilt) travels with its error as a
+    RuntimeError of the same text and its log lines rendered."""
+    try:
+        return pickle.dumps(outs, protocol=pickle.HIGHEST_PROTOCOL)
+    except Exception:                    # noqa: BLE001
+        safe = []
+        for b, o in outs:
+            try:
+                pickle.dumps(o, protocol=pickle.HIGHEST_PROTOCOL)
+                safe.append((b, o))
+            except Exception:            # noqa: BLE001
+                err = None if o.error is None else RuntimeError(f"{type(o.error).__name__}: {o.error}")
+                safe.append((b, PairOutcome(result=o.result, error=err, _log_ops=list(o.logs))))
+        return pickle.dumps(safe, protocol=pickle.HIGHEST_PROTOCOL)
+
+
+class GatheredOutcomes(collections.abc.Sequence):
+    """Every pair's outcome on every rank, in pair order (``analyze_sharded`` with
+    ``gather=True``).  This rank's own outcomes are the objects it assembled; the other
+    ranks' arrived as the bytes of one all-gather (``Exchange.gather_bytes``) and are
+    unpickled a rank at a time, on the first access to one of its pairs (a config-4 step:
+    64 pairs per rank, about a millisecond each).  Indexing, slicing, iteration, ``len`` and
+    comparison with a list behave as on the list of outcomes."""
+
+    def __init__(self, n: int, owner: np.ndarray, own: Sequence[Tuple[int, PairOutcome]],
+                 parts: Dict[int, memoryview]):
+        self._n = int(n)
+        self._owner = np.asarray(owner)
+        self._items: Dict[int, PairOutcome] = dict(own)
+        self._parts = dict(parts)
+
+    def __len__(self) -> int:
+        return self._n
+
+    def _load(self, q: int) -> None:
+        part = self._parts.pop(q, None)
+        if part is not None:
+            self._items.update(pickle.loads(part))
+
+    def __getitem__(self, i):
+        if isinstance(i, slice):
+            return [self[j] for j in range(*i.indices(self._n))]
+        i = int(i)
+        if i < 0:
+            i += self._n
+        if not 0 <= i < self._n:
+            raise IndexError("pair index out of range")
+        o = self._items.get(i)
+        if o is None:
+            self._load(int(self._owner[i]))
+            o = self._items.get(i)
+            if o is None:
+                raise ShardError(f"pair {i} is missing from rank {int(self._owner[i])}'s gathered outcomes")
+        return o
+
+    def __iter__(self):
+        for i in range(self._n):
+            yield self[i]
+
+    def __eq__(self, other):
+        return isinstance(other, collections.abc.Sequence) and list(self) == list(other)
+
+    def decoded(self) -> int:
+        """How many of the other ranks' parts are still bytes (diagnostics)."""
+        return len(self._parts)
+
+    def __repr__(self) -> str:
+        return f"GatheredOutcomes({self._n} pairs, {len(self._parts)} rank part(s) not yet unpickled)"
 
 
 # Fault-injection points of the fail-together tests (tests/test_sharded_cpu.py): host-only
@@ -717,10 +817,13 @@ def _analyze_sharded(stages, p, group, lengths, local_pairs, split_offset, gathe
         outs.sort(key=lambda t: t[0])
         if not gather:
             result.append(outs)
-            continue
-        for _, o in outs:
-            o.logs                              # render the deferred log lines (plain strings travel)
-        result.append([o for _, o in sorted(ex.gather_objects(outs), key=lambda t: t[0])])
+        elif world == 1:
+            result.append([o for _, o in outs])
+        else:
+            # every rank's owned outcomes to every rank: one byte all-gather per step (the log
+            # lines travel unrendered, engine._Lines); the others' parts unpickled on access
+            parts = ex.gather_bytes(_dumps_outcomes(outs))
+            result.append(GatheredOutcomes(sp.B, sp.owner, outs, {q: parts[q] for q in range(world) if q != r}))
     return result[0] if steps == 1 else result
 
 

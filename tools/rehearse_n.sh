@@ -11,4 +11,5 @@ NC_BENCH_REHEARSE=1 timeout -k 10 900 python -m torch.distributed.run --nnodes=1
   || { echo "rehearsal N=$N failed"; tail -20 $O/n$N.err; exit 1; }
 python3 -c "
 import json; d=json.loads(open('$O/n$N.json').read().strip().splitlines()[-1])
-print('N=$N', round(d['value']), 'windows/s', round(d['ms_per_step'], 2), 'ms/step', d['config']['parallelism'], d['data'][-40:])"
+print('N=$N', round(d['value']), 'windows/s', round(d['ms_per_step'], 2), 'ms/step', d['config']['parallelism'], d['data'][-40:])
+print('  modes', {k: (round(v['value']), round(v['ms_per_step'], 2)) for k, v in (d.get('modes') or {}).items()})"
