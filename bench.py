@@ -373,8 +373,10 @@ def main():
     idle_frac = max_over_ranks(1.0 - busy_ms / extent_ms) if extent_ms > 0 else None
     device_idle = {"frac": idle_frac, "busy_ms": busy_ms, "extent_ms": extent_ms, "steps": n_idle,
                    "launches": idle_launches,
-                   "how": "untimed steps of the headline call, every engine kernel's execution span recorded "
-                          "(nc_profile_read_busy): 1 - union of spans / first start..last end; max over ranks"}
+                   "how": "untimed steps of the headline call, the execution spans of the engine's timed kernels "
+                          "recorded (stft_mel, window_tg, tuning_peaks, decimate, tuning_select, cqt_low, cqt_high, "
+                          "tempo_beat, trim_blocks; the small unspanned kernels count as idle, so this is an upper "
+                          "bound): 1 - union of spans / first start..last end (nc_profile_read_busy); max over ranks"}
     el = max_over_ranks(el)
     step_ms = el / args.steps * 1e3
     value = (win_total if win_mode else world * win_per_step) * args.steps / el

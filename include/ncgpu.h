@@ -71,6 +71,13 @@ int nc_profile_enable(nc_ctx* ctx, int on);
 int nc_profile_read(nc_ctx* ctx, const char* tag, double* total_ms, int* launches);
 int nc_profile_read_span(nc_ctx* ctx, const char* tag, double* total_ms, int* launches);
 int nc_profile_read_busy(nc_ctx* ctx, double* busy_ms, double* extent_ms, int* launches);
+/* nc_profile_dump_spans (modes 1-3): every span recorded since the last read, in launch order:
+ * the launch's tag index into `tags` (the tag names written '\n'-separated, NUL-terminated, at
+ * most tags_cap bytes), its start and end in ms from the earliest start; at most cap spans,
+ * *n = how many.  Clears the spans (as nc_profile_read_busy).  Measurement only: the untraced
+ * timeline of which kernels run together (tools/concurrency.py). */
+int nc_profile_dump_spans(nc_ctx* ctx, char* tags, int tags_cap, int* tag_index, double* start_ms, double* end_ms,
+                          int cap, int* n);
 
 /* ---------------------------------------------------------------------------
  * K1a  silence trim — replaces io.strip_silence (io.py:58-79) ->

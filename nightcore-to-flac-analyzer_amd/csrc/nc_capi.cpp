@@ -213,6 +213,17 @@ int nc_profile_read_busy(nc_ctx* ctx, double* busy_ms, double* extent_ms, int* l
   return nc::profile_read_busy(ctx->c, busy_ms, extent_ms, launches);
 }
 
+int nc_profile_dump_spans(nc_ctx* ctx, char* tags, int tags_cap, int* tag_index, double* start_ms, double* end_ms,
+                          int cap, int* n) {
+  CHECK_CTX(ctx);
+  if (!tags || tags_cap <= 0 || !tag_index || !start_ms || !end_ms || !n || cap < 0) {
+    nc::set_error("nc_profile_dump_spans: null argument");
+    return -1;
+  }
+  SET_DEVICE(ctx);
+  return nc::profile_dump_spans(ctx->c, tags, tags_cap, tag_index, start_ms, end_ms, cap, n);
+}
+
 size_t nc_trim_workspace_bytes(const int64_t* host_file_len, int n_files) {
   return nc::trim_ws_bytes(host_file_len, n_files);
 }

@@ -95,6 +95,8 @@ void profile_enable(Context& ctx, int mode);
 int profile_read(Context& ctx, const char* tag, double* total_ms, int* launches);
 int profile_read_span(Context& ctx, const char* tag, double* total_ms, int* launches);
 int profile_read_busy(Context& ctx, double* busy_ms, double* extent_ms, int* launches);
+int profile_dump_spans(Context& ctx, char* tags, int tags_cap, int* tag_index, double* start_ms, double* end_ms,
+                       int cap, int* n);
 
 // bootstrap.hip job description (see nc_bootstrap_ratio in include/ncgpu.h)
 struct BootArgs {

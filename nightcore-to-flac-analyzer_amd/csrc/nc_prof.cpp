@@ -203,9 +203,10 @@ int profile_read_span(Context& ctx, const char* tag, double* total_ms, int* laun
 }
 
 // Device occupancy over every span recorded since the last reset, all tags together: the
-// union of the launches' execution spans (busy) and first start .. last end (extent).  The
-// engine's kernels are all spanned; torch's small fills and the copies are not, so busy is
-// a lower bound by their few microseconds.  Clears every tag's spans.
+// union of the launches' execution spans (busy) and first start .. last end (extent).  Only
+// the timed (tagged) kernels record spans -- every large one; the small ones (bootstraps,
+// plans, tails, gathers), torch's fills and the copies do not, so busy is a lower bound and
+// 1 - busy / extent an upper bound of the idle fraction.  Clears every tag's spans.
 int profile_read_busy(Context& ctx, double* busy_ms, double* extent_ms, int* launches) {
   *busy_ms = *extent_ms = 0.0;
   *launches = 0;
@@ -252,6 +253,65 @@ int profile_read_busy(Context& ctx, double* busy_ms, double* extent_ms, int* lau
   }
   *busy_ms = (double)busy / t->clock_khz;
   *launches = (int)iv.size();
+  for (auto& kv : t->slots) kv.second.spans.clear();
+  span_reset(*t);
+  return 0;
+}
+
+// Every span since the last reset with its tag, in launch order (start, end relative to the
+// earliest start).  Clears every tag's spans, as profile_read_busy.
+int profile_dump_spans(Context& ctx, char* tags, int tags_cap, int* tag_index, double* start_ms, double* end_ms,
+                       int cap, int* n) {
+  *n = 0;
+  tags[0] = '\0';
+  KernelTimers* t = ctx.timers;
+  if (!t || !t->span_buf) return 0;
+  if (hipDeviceSynchronize() != hipSuccess) {
+    set_error("nc_profile_dump_spans: device synchronize failed");
+    return -1;
+  }
+  std::vector<unsigned long long> h((size_t)t->span_used * kSpanLaunchU64);
+  if (t->span_used && hipMemcpy(h.data(), t->span_buf, h.size() * sizeof(unsigned long long),
+                                hipMemcpyDeviceToHost) != hipSuccess) {
+    set_error("nc_profile_dump_spans: copy failed");
+    return -1;
+  }
+  std::vector<int> owner((size_t)t->span_used, -1);
+  std::string names;
+  int ti = 0;
+  for (auto& kv : t->slots) {
+    for (int sidx : kv.second.spans) owner[(size_t)sidx] = ti;
+    names += kv.first;
+    names += '\n';
+    ++ti;
+  }
+  if ((int)names.size() + 1 > tags_cap) {
+    set_error("nc_profile_dump_spans: tag buffer too small");
+    return -1;
+  }
+  std::memcpy(tags, names.c_str(), names.size() + 1);
+  unsigned long long t0 = ~0ull;
+  std::vector<std::pair<unsigned long long, unsigned long long>> se((size_t)t->span_used, {0ull, 0ull});
+  for (int sidx = 0; sidx < t->span_used; ++sidx) {
+    unsigned long long a = ~0ull, b = 0ull;
+    for (int l = 0; l < kSpanLines; ++l) {
+      const unsigned long long* p = h.data() + (size_t)sidx * kSpanLaunchU64 + (size_t)l * kSpanStride;
+      a = std::min(a, p[0]);
+      b = std::max(b, p[1]);
+    }
+    se[(size_t)sidx] = {a, b};
+    if (b >= a && a != ~0ull) t0 = std::min(t0, a);
+  }
+  int m = 0;
+  for (int sidx = 0; sidx < t->span_used && m < cap; ++sidx) {
+    const auto [a, b] = se[(size_t)sidx];
+    if (!(b >= a && a != ~0ull) || owner[(size_t)sidx] < 0) continue;
+    tag_index[m] = owner[(size_t)sidx];
+    start_ms[m] = (double)(a - t0) / t->clock_khz;
+    end_ms[m] = (double)(b - t0) / t->clock_khz;
+    ++m;
+  }
+  *n = m;
   for (auto& kv : t->slots) kv.second.spans.clear();
   span_reset(*t);
   return 0;

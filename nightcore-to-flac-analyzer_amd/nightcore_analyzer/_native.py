@@ -33,6 +33,7 @@ SIGNATURES = {
     "nc_profile_read": (I32, [P, C.c_char_p, C.POINTER(D), C.POINTER(I32)]),
     "nc_profile_read_span": (I32, [P, C.c_char_p, C.POINTER(D), C.POINTER(I32)]),
     "nc_profile_read_busy": (I32, [P, C.POINTER(D), C.POINTER(D), C.POINTER(I32)]),
+    "nc_profile_dump_spans": (I32, [P, P, I32, P, P, P, I32, C.POINTER(I32)]),
     "nc_destroy": (I32, [P]),
     "nc_num_cu": (I32, [P]),
     "nc_trim_workspace_bytes": (SZ, [P, I32]),

@@ -651,6 +651,19 @@ class Engine:
         self.ctx.call("nc_profile_read_busy", C.byref(b), C.byref(e), C.byref(n))
         return b.value, e.value, n.value
 
+    def device_spans(self, cap: int = 1 << 16) -> List[Tuple[str, float, float]]:
+        """[(tag, start ms, end ms)] of every kernel span recorded since the last read, in launch
+        order (nc_profile_dump_spans; profile modes 1-3); waits for the device, clears the spans."""
+        import ctypes as C
+        tags = C.create_string_buffer(1 << 14)
+        idx = np.zeros(cap, np.int32)
+        st, en = np.zeros(cap), np.zeros(cap)
+        n = C.c_int(0)
+        self.ctx.call("nc_profile_dump_spans", C.addressof(tags), len(tags), idx.ctypes.data, st.ctypes.data,
+                      en.ctypes.data, cap, C.byref(n))
+        names = tags.value.decode().split("\n")
+        return [(names[idx[i]], float(st[i]), float(en[i])) for i in range(n.value)]
+
     def upload_signals(self, arrays: Sequence[np.ndarray]) -> DeviceSignals:
         lens = np.array([len(a) for a in arrays], dtype=np.int64)
         offs = np.zeros(len(arrays), dtype=np.int64)

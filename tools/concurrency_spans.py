@@ -1,0 +1,61 @@
+#!/usr/bin/env python3
+"""Which kernels run together in the pipelined config-3 step, untraced: Engine.analyze_batches
+over K batches with every timed kernel recording its execution span (profile mode 2), the spans
+dumped (nc_profile_dump_spans), and the time spent in each set of concurrently running kernels.
+Only the timed (tagged) kernels record spans; the small ones (bootstraps, plans, gathers,
+tails) count as "nothing", so the "-" row is an upper bound of the device idle.
+    python3 tools/concurrency_spans.py [K]"""
+import sys
+from pathlib import Path
+
+REPO = Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(REPO))
+sys.path.insert(0, str(REPO / "nightcore-to-flac-analyzer_amd"))
+
+CLS = {"stft_mel": "S", "window_tg": "W", "tuning_peaks": "T", "decimate": "D", "cqt_low": "L", "cqt_high": "H",
+       "tempo_beat": "B", "trim_blocks": "R", "tuning_select": "s"}
+
+
+def table(spans, steps):
+    ev = []
+    for tag, a, b in spans:
+        c = CLS.get(tag, "o")
+        ev += [(a, 1, c), (b, -1, c)]
+    ev.sort()
+    active, acc, t_prev = {}, {}, ev[0][0]
+    for t, d, c in ev:
+        key = "".join(sorted(k for k, n in active.items() if n > 0)) or "-"
+        acc[key] = acc.get(key, 0.0) + (t - t_prev)
+        t_prev = t
+        active[c] = active.get(c, 0) + d
+    span = ev[-1][0] - ev[0][0]
+    print(f"extent {span / steps:.3f} ms/step; " + ", ".join(f"{c}={k}" for k, c in CLS.items()))
+    for k, v in sorted(acc.items(), key=lambda x: -x[1])[:20]:
+        print(f"  {k:10s} {v / steps:7.3f} ms/step  {100 * v / span:5.1f} %")
+    def frac(pred):
+        return 100 * sum(v for k, v in acc.items() if pred(set(k))) / span
+    print(f"stft_mel running {frac(lambda s: 'S' in s):.1f} %, a CQT kernel {frac(lambda s: bool(s & set('LH'))):.1f} %, "
+          f"stft_mel with a CQT kernel {frac(lambda s: 'S' in s and bool(s & set('LH'))):.1f} %, "
+          f"no large kernel {frac(lambda s: not (s & set('SWTDLH'))):.1f} %")
+
+
+def main():
+    import torch
+    import bench
+    from nightcore_analyzer import engine as E
+    K = int(sys.argv[1]) if len(sys.argv) > 1 else 10
+    pairs = bench.make_pairs(64, 180.0, 1000, 16)
+    eng = E.get_engine(0)
+    sig = eng.upload_signals([a for nc, src in pairs for a in (nc, src)])
+    p = E.Params(compute_ibi=False)
+    eng.analyze_batches([sig] * K, p)
+    eng.kernel_profile(2)
+    torch.cuda.synchronize()
+    eng.analyze_batches([sig] * K, p)
+    spans = eng.device_spans()
+    eng.kernel_profile(0)
+    table(spans, K)
+
+
+if __name__ == "__main__":
+    main()
