@@ -172,3 +172,32 @@ def test_profile_modes_time_what_they_say(eng):
         else:
             assert ev_k == roof and not sp_k
         assert all(ms > 0 and n > 0 for ms, n in ev.values())
+
+
+def test_profile_span_dump_and_busy_agree(eng):
+    """nc_profile_dump_spans (mode 2): every timed launch of one analysis with its tag, start
+    <= end, inside one extent; the union of the dumped spans equals what nc_profile_read_busy
+    reports for a second, identical call (same kernels, same union semantics)."""
+    nc, src = synth.make_pair(40.0, 1012)
+    p = E.Params(compute_ibi=False)
+    eng.analyze([(nc, src)], p)
+    eng.kernel_profile(2)
+    eng.analyze([(nc, src)], p)
+    spans = eng.device_spans()
+    eng.analyze([(nc, src)], p)
+    busy, extent, n = eng.device_busy()
+    eng.kernel_profile(0)
+    tags = {t for t, _, _ in spans}
+    assert {"stft_mel", "window_tg", "cqt_low", "cqt_high", "decimate", "tuning_peaks"} <= tags
+    assert all(0.0 <= a <= b for _, a, b in spans) and min(a for _, a, _ in spans) == 0.0
+    assert n == len(spans) and extent > 0.0 and 0.0 < busy <= extent * (1 + 1e-9)
+    iv, u, cur = sorted((a, b) for _, a, b in spans), 0.0, None
+    for a, b in iv:
+        if cur is None or a > cur[1]:
+            u += 0.0 if cur is None else cur[1] - cur[0]
+            cur = [a, b]
+        else:
+            cur[1] = max(cur[1], b)
+    u += cur[1] - cur[0]
+    assert 0.5 < u / busy < 2.0          # two runs of the same call: the same order of magnitude
+    assert eng.device_spans() == []      # the dump and the busy read both clear the spans

@@ -39,6 +39,22 @@ def table(spans, steps):
           f"no large kernel {frac(lambda s: not (s & set('SWTDLH'))):.1f} %")
 
 
+def gaps(spans, steps, top=12):
+    """The largest intervals with no timed kernel running, with the kernels that end before and
+    start after each (ms from the first span)."""
+    iv = sorted((a, b, t) for t, a, b in spans)
+    out, end, last = [], iv[0][1], iv[0][2]
+    for a, b, t in iv[1:]:
+        if a > end:
+            out.append((a - end, end, last, t))
+        if b > end:
+            end, last = b, t
+    tot = sum(g for g, *_ in out)
+    print(f"gaps: {len(out)} totalling {tot / steps:.3f} ms/step; largest:")
+    for g, at, before, after in sorted(out, reverse=True)[:top]:
+        print(f"  {1e3 * g:8.1f} us at {at:9.3f} ms  after {before:14s} before {after}")
+
+
 def main():
     import torch
     import bench
@@ -55,6 +71,7 @@ def main():
     spans = eng.device_spans()
     eng.kernel_profile(0)
     table(spans, K)
+    gaps(spans, K)
 
 
 if __name__ == "__main__":
