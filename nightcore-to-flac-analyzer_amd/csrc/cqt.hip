@@ -936,19 +936,38 @@ __global__ __launch_bounds__(CM_NTH, 2) void cqt_mfma_kernel(CqmArgs a) {
 // 4 tiles per workgroup and a 4-slot ring 480.9 (16 tile slots for 13.5 tiles of work), 2 tiles
 // and a 3-slot ring 416.9 (three workgroups per CU), 2 tiles and 2 slots 358.6.  Probes of the
 // last (outputs wrong): no barrier 338.6, no MFMA 259.3, no split 297.5.
-constexpr int C2_NW = 2;                                  // tiles (waves) per workgroup
+// tile geometry knobs (probes; the defaults are the kernel described above).  32-frame tiles, four
+// per workgroup (-DC2_FR_=32 -DC2_NW_=4 -DC2_MINB_=3: three waves per SIMD, 168 VGPRs, spills only
+// in octave 0's edge instance), bit-identical, round 5, us per 224 chunks (profiles/
+// r5_cqt_low_fr32.txt): all three octaves 353.5 against 344.1; octave 0 alone 186.9 against 172.2,
+// octave 1 alone 117.7 against 131.3 (134 VGPRs).  Two waves per SIMD (-DC2_MINB_=2) 396.4.  A
+// mixed launch (octave 0 at 64 frames, 1-2 at 32) needs two kernels and gives up the octaves'
+// overlap inside one launch (all three 328-344 against 424 for the three alone): not built
+#ifndef C2_FR_
+#define C2_FR_ 64
+#endif
+#ifndef C2_NW_
+#define C2_NW_ 2
+#endif
+#ifndef C2_MINB_
+#define C2_MINB_ 2
+#endif
+constexpr int C2_FR = C2_FR_;                             // frames per tile (one wave)
+constexpr int C2_RT = C2_FR / 16;                         // 16-row tiles per wave
+static_assert(C2_RT == 2 || C2_RT == 4, "tile rows");
+constexpr int C2_NW = C2_NW_;                             // tiles (waves) per workgroup
 constexpr int C2_R = 2;                                   // filter ring slots
 constexpr int C2_D = C2_R - 1;                            // slices requested ahead of the step that reads them
 constexpr int C2_PS = (CM_NT * 2 + C2_NW - 1) / C2_NW;    // slice DMA pieces per wave per step
 #ifndef C2_NRP_
-#define C2_NRP_ 72
+#define C2_NRP_ (C2_FR + 8)
 #endif
-constexpr int C2_NRP = C2_NRP_;                           // image rows per wave (>= 64 + M - 1)
+constexpr int C2_NRP = C2_NRP_;                           // image rows per wave (>= C2_FR + M - 1)
 constexpr int C2_IMG = C2_NRP * 64;                       // bytes of one hi (or lo) image
 constexpr int C2_RING = C2_R * CM_SLICE * 16;
 constexpr int C2_NU = (C2_NRP * 4 + 63) / 64;             // staging rounds (8-sample units per lane)
 constexpr int C2_NL = 2 * C2_NU;                          // block loads per wave per group
-static_assert(C2_NW * 2 * C2_IMG >= C2_NW * CM_FR * kCqtFilt * 4, "epilogue rows fit the images");
+static_assert(C2_NW * 2 * C2_IMG >= C2_NW * C2_FR * kCqtFilt * 4, "epilogue rows fit the images");
 size_t cql_lds_bytes() { return C2_RING + C2_NW * 2 * C2_IMG; }
 
 // image row R keeps its 16-byte piece p (8 halves) at slot p ^ c2_sw(R): every ds_read_b128 lane
@@ -965,17 +984,23 @@ __device__ __forceinline__ void c2_vmwait() {
 }
 template <int N>
 __device__ __forceinline__ void c2_vmwait_st(cm_u4 (&st)[C2_NL]) {
-  static_assert(C2_NL == 10, "staging registers");
-  asm volatile("s_waitcnt vmcnt(%10)"
-               : "+v"(st[0]), "+v"(st[1]), "+v"(st[2]), "+v"(st[3]), "+v"(st[4]), "+v"(st[5]), "+v"(st[6]),
-                 "+v"(st[7]), "+v"(st[8]), "+v"(st[9])
-               : "i"(N)
-               : "memory");
+  static_assert(C2_NL == 10 || C2_NL == 6, "staging registers");
+  if constexpr (C2_NL == 10)
+    asm volatile("s_waitcnt vmcnt(%10)"
+                 : "+v"(st[0]), "+v"(st[1]), "+v"(st[2]), "+v"(st[3]), "+v"(st[4]), "+v"(st[5]), "+v"(st[6]),
+                   "+v"(st[7]), "+v"(st[8]), "+v"(st[9])
+                 : "i"(N)
+                 : "memory");
+  else
+    asm volatile("s_waitcnt vmcnt(%6)"
+                 : "+v"(st[0]), "+v"(st[1]), "+v"(st[2]), "+v"(st[3]), "+v"(st[4]), "+v"(st[5])
+                 : "i"(N)
+                 : "memory");
 }
 
 template <int OCT>
 struct C2 {
-  static constexpr int H = 512 >> OCT, G = H / 32, M = 1024 / H, NR = CM_FR + M - 1;
+  static constexpr int H = 512 >> OCT, G = H / 32, M = 1024 / H, NR = C2_FR + M - 1;
   // the block loads of a group are issued at its first step (after that step's slice pieces),
   // and the groups before the last stage the next block
   __host__ __device__ static constexpr bool stage_at(int q, bool last) { return q == 0 && !last; }
@@ -1082,13 +1107,13 @@ __device__ __forceinline__ void cqt_low_tile(const CqmArgs& a, int bx, int c) {
   // every descriptor read up front, unconditionally: one round trip of scalar loads
   const int T = a.n_frames[c], ti = a.tuning_idx[c], ex = a.oct_ex[c * 7 + OCT];
   const int64_t yoff = OCT == 0 ? a.chunk_off[c] : a.oct_off[c * 7 + OCT], Ly = a.oct_len[c * 7 + OCT];
-  if (bx * (C2_NW * CM_FR) >= T) return;
-  int t0 = (bx * C2_NW + wave) * CM_FR;
+  if (bx * (C2_NW * C2_FR) >= T) return;
+  int t0 = (bx * C2_NW + wave) * C2_FR;
   const bool active = t0 < T;  // an idle tile's wave still issues the DMA, the loads and the barriers
   if (!active) t0 = 0;
   const float* y = (OCT == 0 ? a.sig : a.ws_oct) + yoff;
   const int64_t s0 = (int64_t)t0 * H - 512;
-  const bool edge = !(s0 >= 0 && s0 + (int64_t)(CM_FR - 1) * H + kCqtNfft <= Ly);
+  const bool edge = !(s0 >= 0 && s0 + (int64_t)(C2_FR - 1) * H + kCqtNfft <= Ly);
   if (edge != EDGE) return;  // wave-uniform; both instances issue the same barriers
   const uint4* bsrc = a.bfrag + (size_t)ti * (CM_KS * CM_SLICE);
   char* img = smem + C2_RING + wave * (2 * C2_IMG);
@@ -1110,9 +1135,9 @@ __device__ __forceinline__ void cqt_low_tile(const CqmArgs& a, int bx, int c) {
   c2_vmwait_st<0>(st);
   if (active) c2_split<OCT>(st, img, sx, s0, 0, Ly, EDGE, lane);
 
-  cm_f4 acc[CM_RT][CM_NT];
+  cm_f4 acc[C2_RT][CM_NT];
 #pragma unroll
-  for (int rt = 0; rt < CM_RT; ++rt)
+  for (int rt = 0; rt < C2_RT; ++rt)
 #pragma unroll
     for (int nt = 0; nt < CM_NT; ++nt) acc[rt][nt] = cm_f4{0.f, 0.f, 0.f, 0.f};
   const int kp = lane >> 4, rl = lane & 15;
@@ -1135,24 +1160,22 @@ __device__ __forceinline__ void cqt_low_tile(const CqmArgs& a, int bx, int c) {
       const int R = rl + Q;
       const uint32_t aa = img_a + R * 64 + 16 * (kp ^ c2_sw(R));
       const uint32_t sbl = lds_addr(sB + (n % C2_R) * CM_SLICE + lane);
-      cm_u4 ah4[CM_RT], al4[CM_RT], b[CM_NT][2];
-      cm_rd<0 * 1024>(ah4[0], aa);
-      cm_rd<1 * 1024>(ah4[1], aa);
-      cm_rd<2 * 1024>(ah4[2], aa);
-      cm_rd<3 * 1024>(ah4[3], aa);
-      cm_rd<C2_IMG + 0 * 1024>(al4[0], aa);
-      cm_rd<C2_IMG + 1 * 1024>(al4[1], aa);
-      cm_rd<C2_IMG + 2 * 1024>(al4[2], aa);
-      cm_rd<C2_IMG + 3 * 1024>(al4[3], aa);
+      cm_u4 ah4[C2_RT], al4[C2_RT], b[CM_NT][2];
+      static_for<C2_RT>([&](auto rc) { cm_rd<decltype(rc)::value * 1024>(ah4[decltype(rc)::value], aa); });
+      static_for<C2_RT>([&](auto rc) { cm_rd<C2_IMG + decltype(rc)::value * 1024>(al4[decltype(rc)::value], aa); });
       cm_rd<0 * 1024>(b[0][0], sbl);
       cm_rd<1 * 1024>(b[0][1], sbl);
       cm_rd<2 * 1024>(b[1][0], sbl);
       cm_rd<3 * 1024>(b[1][1], sbl);
-      cm_wait<4>(ah4[0], ah4[1], ah4[2], ah4[3]);  // A + tile 0 landed; tile 1 in flight
-      cm_wait<4>(al4[0], al4[1], al4[2], al4[3]);
-      cm_half8 ah[CM_RT], al[CM_RT];
+      if constexpr (C2_RT == 4) {
+        cm_wait<4>(ah4[0], ah4[1], ah4[2], ah4[3]);  // A + tile 0 landed; tile 1 in flight
+        cm_wait<4>(al4[0], al4[1], al4[2], al4[3]);
+      } else {
+        cm_wait<4>(ah4[0], ah4[1], al4[0], al4[1]);
+      }
+      cm_half8 ah[C2_RT], al[C2_RT];
 #pragma unroll
-      for (int rt = 0; rt < CM_RT; ++rt) {
+      for (int rt = 0; rt < C2_RT; ++rt) {
         ah[rt] = __builtin_bit_cast(cm_half8, ah4[rt]);
         al[rt] = __builtin_bit_cast(cm_half8, al4[rt]);
       }
@@ -1160,7 +1183,7 @@ __device__ __forceinline__ void cqt_low_tile(const CqmArgs& a, int bx, int c) {
         const cm_half8 bh = __builtin_bit_cast(cm_half8, b[nt][0]);
         const cm_half8 bl = __builtin_bit_cast(cm_half8, b[nt][1]);
 #pragma unroll
-        for (int rt = 0; rt < CM_RT; ++rt) {
+        for (int rt = 0; rt < C2_RT; ++rt) {
           acc[rt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[rt], bh, acc[rt][nt], 0, 0, 0);
           acc[rt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[rt], bl, acc[rt][nt], 0, 0, 0);
           acc[rt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al[rt], bh, acc[rt][nt], 0, 0, 0);
@@ -1203,8 +1226,8 @@ __device__ __forceinline__ void cqt_low_tile(const CqmArgs& a, int bx, int c) {
     static_for<M>([&](auto qc) { step(qc, g, last); });
   }
   if (!active) return;
-  const int nrow = min(CM_FR, T - t0);
-  float* mg = reinterpret_cast<float*>(img);  // [64][36] rows over this wave's own images
+  const int nrow = min(C2_FR, T - t0);
+  float* mg = reinterpret_cast<float*>(img);  // [C2_FR][36] rows over this wave's own images
   {
     const float oscale = (float)(1 << (OCT >> 1)) * ((OCT & 1) ? 0x1.6a09e6p+0f : 1.0f);
     const float* isl = a.cqt_isl + ti * kCqtBins + (kCqtBins - kCqtFilt * (OCT + 1));
@@ -1215,7 +1238,7 @@ __device__ __forceinline__ void cqt_low_tile(const CqmArgs& a, int bx, int c) {
     const float il0 = isl[col], il1 = isl[16 + col], il2 = isl[32 + (col & 3)];
     __builtin_amdgcn_s_waitcnt(0xc07f);  // this wave's last A reads are done before the rows overlay them
 #pragma unroll
-    for (int rt = 0; rt < CM_RT; ++rt)
+    for (int rt = 0; rt < C2_RT; ++rt)
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int fr = 16 * rt + 4 * (lane >> 4) + i;
@@ -1245,7 +1268,7 @@ __device__ __forceinline__ void cqt_low_tile(const CqmArgs& a, int bx, int c) {
 #ifndef CQL_ONLY
 #define CQL_ONLY -1
 #endif
-__global__ __launch_bounds__(C2_NW * 64, 2) void cqt_mfma_low_kernel(CqmArgs a) {
+__global__ __launch_bounds__(C2_NW * 64, C2_MINB_) void cqt_mfma_low_kernel(CqmArgs a) {
   const unsigned oz = CQL_ONLY >= 0 ? (unsigned)CQL_ONLY : blockIdx.z;
   if (oz == 0) {
     cqt_low_tile<0, false>(a, blockIdx.x, blockIdx.y);
@@ -1508,7 +1531,8 @@ int launch_chroma_mean(Context& ctx, const float* sig, const int64_t* chunk_off,
     // bench's cqt_chroma unit (7 octaves of every chunk) is their sum
     KTimer kt_(ctx, "cqt_low", st);
     ma.span = kt_.span();
-    const dim3 lg((unsigned)((ntile + C2_NW - 1) / C2_NW), (unsigned)n, CQL_ONLY >= 0 ? 1u : 3u);
+    const int ntl = (int)((1 + max_chunk_len / 512 + C2_FR - 1) / C2_FR);
+    const dim3 lg((unsigned)((ntl + C2_NW - 1) / C2_NW), (unsigned)n, CQL_ONLY >= 0 ? 1u : 3u);
     hipLaunchKernelGGL(cqt_mfma_low_kernel, lg, dim3(C2_NW * 64), cql_lds_bytes(), st, ma);
   }
   {
