@@ -222,6 +222,14 @@ class Exchange:
         self.dev = torch.device(device)
 
     stream: Optional[torch.cuda.Stream] = None    # RCCL: the stream the exchanged records live on
+    # run the collectives at world size 1 too (tests: a one-rank RCCL group takes the
+    # device-tensor path on the box's one GPU, tests/test_gpu_rccl.py)
+    collect_at_one: bool = False
+
+    @property
+    def local(self) -> bool:
+        """No collective is issued: no process group, or one rank (unless collect_at_one)."""
+        return not self.on or (self.world == 1 and not self.collect_at_one)
 
     def gather_blocks(self, local: np.ndarray, counts: Sequence[int], failed: Optional[BaseException]) -> np.ndarray:
         """Rank r contributes counts[r] rows of k f64; returns the rows of every rank in rank
@@ -236,7 +244,7 @@ class Exchange:
 
     def _gather_blocks(self, local: np.ndarray, counts: Sequence[int], failed: Optional[BaseException]) -> np.ndarray:
         k = local.shape[1]
-        if not self.on or self.world == 1:
+        if self.local:
             if failed is not None:
                 raise failed
             return np.ascontiguousarray(local, np.float64)
@@ -259,7 +267,7 @@ class Exchange:
     def allreduce_max(self, vals: np.ndarray, failed: Optional[BaseException]) -> np.ndarray:
         """Element-wise maximum over the ranks (C2: power_to_db's top_db reference of a file
         whose frames are split); the error flag rides along as one more element."""
-        if not self.on or self.world == 1:
+        if self.local:
             if failed is not None:
                 raise failed
             return np.asarray(vals, np.float64)
@@ -287,7 +295,7 @@ class Exchange:
         self.gather_blocks(np.zeros((0, 1)), [0] * self.world, failed)
 
     def gather_objects(self, local: list) -> list:
-        if not self.on or self.world == 1:
+        if self.local:
             return list(local)
         buf: List[Optional[list]] = [None] * self.world
         dist.all_gather_object(buf, local, group=self.group)
@@ -300,7 +308,7 @@ class Exchange:
         """Every rank's byte string, in rank order: one all_gather_into_tensor of the lengths
         and one of the strings padded to the longest (uint8; device tensors under RCCL, on the
         split-pair stream).  The parts are views of one host buffer: nothing is copied per rank."""
-        if not self.on or self.world == 1:
+        if self.local:
             return [memoryview(blob)]
         ctx = torch.cuda.stream(self.stream) if self.dev.type == "cuda" and self.stream is not None \
             else contextlib.nullcontext()
@@ -808,7 +816,7 @@ def _analyze_sharded(stages, p, group, lengths, local_pairs, split_offset, gathe
         if err is None:
             for k in range(steps):
                 per_step[k] = per_step[k] + list(zip(interior, res[k]))
-    if world > 1:
+    if not ex.local:
         ex.check(err)                           # fail together before the result gather
     elif err is not None:
         raise err
@@ -817,7 +825,7 @@ def _analyze_sharded(stages, p, group, lengths, local_pairs, split_offset, gathe
         outs.sort(key=lambda t: t[0])
         if not gather:
             result.append(outs)
-        elif world == 1:
+        elif ex.local:
             result.append([o for _, o in outs])
         else:
             # every rank's owned outcomes to every rank: one byte all-gather per step (the log

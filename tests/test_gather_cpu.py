@@ -59,7 +59,7 @@ def _free_port():
     return port
 
 
-def _worker(rank, world, port, q):
+def _worker(rank, world, port, q, at_one=False):
     import torch.distributed as dist
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -68,7 +68,19 @@ def _worker(rank, world, port, q):
         owner = np.array([b * world // B for b in range(B)])
         own = [(b, _outcome(b)) for b in range(B) if owner[b] == rank]
         ex = S.Exchange()
+        ex.collect_at_one = at_one
+        assert ex.local == (world == 1 and not at_one)
+        if at_one:
+            rows = np.arange(6.0).reshape(2, 3)
+            assert np.array_equal(ex.gather_blocks(rows, [2], None), rows)
+            assert np.array_equal(ex.allreduce_max(np.array([1.5, -2.0]), None), [1.5, -2.0])
+            try:
+                ex.check(KeyError("held"))
+                raise AssertionError("the held error did not raise")
+            except KeyError:
+                pass
         parts = ex.gather_bytes(S._dumps_outcomes(own))
+        assert len(parts) == world
         g = S.GatheredOutcomes(B, owner, own, {r: parts[r] for r in range(world) if r != rank})
         q.put((rank, [_key(o) for o in g]))
     except Exception as exc:     # noqa: BLE001
@@ -92,3 +104,18 @@ def test_byte_gather_three_ranks_every_rank_holds_every_outcome():
     ref = [_key(_outcome(b)) for b in range(7)]
     for r in range(world):
         assert res[r] == ref, res[r]
+
+
+def test_one_rank_group_runs_the_collectives_with_collect_at_one():
+    """Exchange.collect_at_one (the one-rank RCCL test on the GPU box, tests/test_gpu_rccl.py):
+    at world size 1 the record gather, the all-reduce, the flag and the byte gather are still
+    issued and return the rank's own data."""
+    assert S.Exchange().local          # no process group: nothing is issued
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_worker, args=(0, 1, _free_port(), q, True))
+    p.start()
+    r, got = q.get(timeout=120)
+    p.join(timeout=60)
+    assert p.exitcode == 0
+    assert got == [_key(_outcome(b)) for b in range(7)], got
