@@ -659,7 +659,8 @@ int launch_tempo_beats(Context& ctx, BeatArgs a, int n_seq, int max_len, hipStre
     {
       KTimer kt_(ctx, "tempo_beat", st);
       a.span = kt_.span();
-      hipLaunchKernelGGL((tempo_beat_kernel<256, true>), dim3(n_seq), dim3(256), small_lds, st, a);
+      for (int rep = 0; rep < NC_PROBE_REPS(0); ++rep)
+        hipLaunchKernelGGL((tempo_beat_kernel<256, true>), dim3(n_seq), dim3(256), small_lds, st, a);
     }
   } else {
     if (!a.ws_ls || !a.ws_cum || !a.ws_back || !a.ws_marks) {

@@ -614,7 +614,8 @@ int launch_bootstrap(const BootArgs& a, int n_jobs, hipStream_t st) {
   hipLaunchKernelGGL(bootstrap_rejscan_kernel, dim3(SCAN_WG, n_jobs), dim3(BT), 0, st, a);
   hipLaunchKernelGGL(bootstrap_walk_kernel, dim3(n_jobs), dim3(BT), 0, st, a);
   hipLaunchKernelGGL(bootstrap_draw_kernel<true>, gd, dim3(BD), 0, st, a);
-  hipLaunchKernelGGL(bootstrap_finish_kernel, dim3(n_jobs), dim3(BT), 0, st, a);
+  for (int rep = 0; rep < NC_PROBE_REPS(1); ++rep)
+    hipLaunchKernelGGL(bootstrap_finish_kernel, dim3(n_jobs), dim3(BT), 0, st, a);
   NC_HIP(hipGetLastError());
   return 0;
 }

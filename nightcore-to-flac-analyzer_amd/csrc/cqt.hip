@@ -100,14 +100,19 @@ __global__ __launch_bounds__(256) void chroma_plan_kernel(const int64_t* chunk_l
 // Round 4, with stft_mel's LDS reserve keeping this kernel off the STFT's CUs: 128 / 256 / 512 /
 // 768 / 1024 outputs per workgroup (256 threads) ran 1.40 / 0.98 / 0.82 / 0.94 / 1.01 ms per step
 // isolated (six, four and three workgroups per CU past 512 by LDS), the pipelined step the same
-// within its spread (profiles/r4_decimate_tile_ab.txt)
+// within its spread (profiles/r4_decimate_tile_ab.txt).  Round 5: 476 outputs, so the level-1
+// pass is exactly two rounds of the 256 threads (4 T + 144 = 2048 values, 512 quads; at 512 it
+// was 548 quads, a third round for 36 threads) and level 2 one (250 quads): 215.0 -> 201.2 us
+// per 224 chunks, bit-identical (profiles/r5_decimate_476.txt).  Launched twice in the pipelined
+// step (NC_PROBE_TWICE), decimate3 adds 0.6-0.75 ms per step: it is on the step's critical path
 #ifndef D3_TILE
-#define D3_TILE 512
+#define D3_TILE 476
 #endif
 #ifndef D3_NT
 #define D3_NT 256  // threads per decimate3 workgroup
 #endif
 constexpr int D3_T = D3_TILE;           // level-(base + 3) outputs per decimate3 workgroup
+static_assert(D3_T % 4 == 0 && D3_T >= 256, "quads per level; xmax slots are spaced 256 apart");
 constexpr int D3_N1 = 4 * D3_T + 144;  // level base+1 values computed (from 4 m0 - 72)
 constexpr int D3_N2 = 2 * D3_T + 48;   // level base+2 values computed (from 2 m0 - 24)
 constexpr int D3_P0 = 4 * D3_T + 168;  // level base pairs staged (values from 8 m0 - 168)
@@ -1468,8 +1473,9 @@ int launch_chroma_mean(Context& ctx, const float* sig, const int64_t* chunk_off,
       KTimer kt_(ctx, "decimate", st);
       D3Taps taps;
       std::copy(ctx.t.halfband_f32, ctx.t.halfband_f32 + 2 * kHalfbandK + 1, taps.h);
-      hipLaunchKernelGGL(decimate3_kernel, grid, dim3(D3_NT), 0, st, sig, chunk_off, w.oct_off, w.oct_len, w.ws_oct,
-                         base, taps, w.xmax, kt_.span());
+      for (int rep = 0; rep < NC_PROBE_REPS(3); ++rep)
+        hipLaunchKernelGGL(decimate3_kernel, grid, dim3(D3_NT), 0, st, sig, chunk_off, w.oct_off, w.oct_len, w.ws_oct,
+                           base, taps, w.xmax, kt_.span());
     }
   }
   PeakArgs pa;
@@ -1533,12 +1539,14 @@ int launch_chroma_mean(Context& ctx, const float* sig, const int64_t* chunk_off,
     ma.span = kt_.span();
     const int ntl = (int)((1 + max_chunk_len / 512 + C2_FR - 1) / C2_FR);
     const dim3 lg((unsigned)((ntl + C2_NW - 1) / C2_NW), (unsigned)n, CQL_ONLY >= 0 ? 1u : 3u);
-    hipLaunchKernelGGL(cqt_mfma_low_kernel, lg, dim3(C2_NW * 64), cql_lds_bytes(), st, ma);
+    for (int rep = 0; rep < NC_PROBE_REPS(4); ++rep)
+      hipLaunchKernelGGL(cqt_mfma_low_kernel, lg, dim3(C2_NW * 64), cql_lds_bytes(), st, ma);
   }
   {
     KTimer kt_(ctx, "cqt_high", st);
     ma.span = kt_.span();
-    hipLaunchKernelGGL(cqt_mfma_kernel, dim3(ntile, n), dim3(CM_NTH), cqm_lds_bytes(), st, ma);
+    for (int rep = 0; rep < NC_PROBE_REPS(5); ++rep)
+      hipLaunchKernelGGL(cqt_mfma_kernel, dim3(ntile, n), dim3(CM_NTH), cqm_lds_bytes(), st, ma);
   }
   hipLaunchKernelGGL(cqt_tail_kernel, dim3(ntile, n), dim3(256), 0, st, w.gpart, w.tf_base, w.n_frames, w.partial);
   hipLaunchKernelGGL(chroma_finalize_kernel, dim3(n), dim3(64), 0, st, w.partial, w.tf_base, w.n_frames, n, CM_FR,

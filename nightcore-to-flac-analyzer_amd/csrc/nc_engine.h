@@ -126,6 +126,14 @@ void set_error(const std::string& msg);
 
 }  // namespace nc
 
+// timing probe (tools/var_build.sh variants only): bit k launches kernel k twice (the kernels
+// listed are idempotent), so the step's growth is that launch's cost inside the pipeline.
+// 1 tempo_beat<256, true>, 2 bootstrap_finish, 4 window_tg, 8 decimate3 (both launches),
+// 16 cqt_mfma_low, 32 cqt_mfma (octaves 3-6); tools/twice_probe.sh, profiles/r5_twice_probe.txt
+#ifndef NC_PROBE_TWICE
+#define NC_PROBE_TWICE 0
+#endif
+#define NC_PROBE_REPS(k) (1 + ((NC_PROBE_TWICE >> (k)) & 1))
 #define NC_HIP(call)                                                                  \
   do {                                                                                \
     hipError_t _e = (call);                                                           \

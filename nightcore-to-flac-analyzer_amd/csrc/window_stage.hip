@@ -384,7 +384,8 @@ int launch_window_stage(Context& ctx, const float* sig, const int64_t* win_off, 
     KTimer kt_(ctx, "window_tg", st);
     a.span = kt_.span();
     if (corr)
-      hipLaunchKernelGGL(window_tg_kernel, dim3(n_win), dim3(WT_THREADS), lds_corr, st, a);
+      for (int rep = 0; rep < NC_PROBE_REPS(2); ++rep)
+        hipLaunchKernelGGL(window_tg_kernel, dim3(n_win), dim3(WT_THREADS), lds_corr, st, a);
     else
       hipLaunchKernelGGL(window_tg_slide_kernel, dim3(n_win), dim3(WS_THREADS), lds_slide, st, a);
   }
