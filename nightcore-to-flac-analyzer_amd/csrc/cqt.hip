@@ -178,6 +178,50 @@ __device__ __forceinline__ void d3_level(const float* E, const float* O, int cnt
   }
 }
 
+// Level base + 1 with its phases written over the level-base phases it reads: every thread
+// computes its quads into registers, the workgroup syncs, then the phases go to E/O [0, N1 / 2).
+// The same values as d3_level (same quads, same arithmetic).  Round 5: without the separate
+// level-1 buffers the workgroup needs 16.6 KB of LDS instead of 24.8, eight waves per SIMD
+// instead of six: 201.9 -> 183.7 us per 224 chunks, bit-identical; 988-output tiles of 512
+// threads in the same form 195.8 (profiles/r5_decimate_476.txt)
+constexpr int D3_R1 = (D3_N1 / 4 + D3_NT - 1) / D3_NT;  // level base + 1 quads per thread
+__device__ __forceinline__ void d3_level1_inplace(float* E, float* O, int64_t qa, int64_t L,
+                                                  const float (&h)[2 * kHalfbandK + 1], float* dst) {
+  float r[D3_R1][4];
+#pragma unroll
+  for (int k = 0; k < D3_R1; ++k) {
+    const int i = threadIdx.x + D3_NT * k;
+    if (i < D3_N1 / 4) {
+      d3_quad(E, O, i, h, r[k]);
+      const int64_t q0 = qa + 4 * i;
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        if (q0 + q < 0 || q0 + q >= L) r[k][q] = 0.f;
+      if (4 * i >= 72 && 4 * i < 72 + 4 * D3_T && q0 < L) {
+        if (q0 + 3 < L) {
+          *reinterpret_cast<float4*>(dst + q0) = make_float4(r[k][0], r[k][1], r[k][2], r[k][3]);
+        } else {
+#pragma unroll
+          for (int q = 0; q < 4; ++q)
+            if (q0 + q < L) dst[q0 + q] = r[k][q];
+        }
+      }
+    }
+  }
+  __syncthreads();  // every read of the level-base phases is done
+#pragma unroll
+  for (int k = 0; k < D3_R1; ++k) {
+    const int i = threadIdx.x + D3_NT * k;
+    if (i < D3_N1 / 4) {
+      *reinterpret_cast<float2*>(E + 2 * i) = make_float2(r[k][0], r[k][2]);
+      *reinterpret_cast<float2*>(O + 2 * i) = make_float2(r[k][1], r[k][3]);
+    }
+  }
+}
+// level base + 2 phases: after level base + 1's, 16-byte aligned
+constexpr int D3_U2 = ((D3_N1 / 2) + 3) & ~3;
+static_assert(D3_U2 + D3_N2 / 2 <= D3_P0 && D3_N1 / 2 <= D3_P0, "phases fit the level-base buffers");
+
 // The level-base input of a tile is requested as D3_LD float4 loads per thread, all issued
 // before any is staged (one global latency per tile instead of one per load; 276 -> 242 us
 // per 224 chunks).  Walking several tiles per workgroup with the next tile's loads in
@@ -198,7 +242,6 @@ __global__ __launch_bounds__(D3_NT) void decimate3_kernel(const float* sig, cons
   const Span span_(span);
   static_assert(kHalfbandK == 23, "phase windows assume 23");
   __shared__ __attribute__((aligned(16))) float e0[D3_P0], o0[D3_P0];
-  __shared__ __attribute__((aligned(16))) float e1[D3_N1 / 2], o1[D3_N1 / 2];
   __shared__ float wmax[D3_NT / 64];
   const int c = blockIdx.y;
   const int64_t m0 = (int64_t)blockIdx.x * D3_T;
@@ -265,14 +308,14 @@ __global__ __launch_bounds__(D3_NT) void decimate3_kernel(const float* sig, cons
       for (int w = 1; w < D3_NT / 64; ++w) m = fmaxf(m, wmax[w]);
       xmax[c + (base == 0 ? oo3 : oct_off[c * 7 + 3]) / 256 + blockIdx.x] = m;
     }
-    // level base+1: [4 m0 - 72, +D3_N1), owned [4 m0, 4 m0 + 4 T); phases -> e1/o1
-    d3_level(e0, o0, D3_N1, 4 * m0 - 72, L1, h, e1, o1, out1, 72, 4 * D3_T);
+    // level base+1: [4 m0 - 72, +D3_N1), owned [4 m0, 4 m0 + 4 T); phases over e0/o0 [0, N1 / 2)
+    d3_level1_inplace(e0, o0, 4 * m0 - 72, L1, h, out1);
     __syncthreads();
-    // level base+2: [2 m0 - 24, +D3_N2), owned [2 m0, 2 m0 + 2 T); phases -> e0/o0 (reused)
-    d3_level(e1, o1, D3_N2, 2 * m0 - 24, L2, h, e0, o0, out2, 24, 2 * D3_T);
+    // level base+2: [2 m0 - 24, +D3_N2), owned [2 m0, 2 m0 + 2 T); phases -> e0/o0 [U2, U2 + N2 / 2)
+    d3_level(e0, o0, D3_N2, 2 * m0 - 24, L2, h, e0 + D3_U2, o0 + D3_U2, out2, 24, 2 * D3_T);
     __syncthreads();
     // level base+3: [m0, m0 + T), all owned
-    d3_level(e0, o0, D3_T, m0, L3, h, nullptr, nullptr, out3, 0, D3_T);
+    d3_level(e0 + D3_U2, o0 + D3_U2, D3_T, m0, L3, h, nullptr, nullptr, out3, 0, D3_T);
   }
 }
 
