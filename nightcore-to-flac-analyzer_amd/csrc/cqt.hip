@@ -639,12 +639,13 @@ __global__ __launch_bounds__(NT) void tuning_select_kernel(const float* peak_pit
 // by 2^ex with max|y_o| * 2^ex < 2^13 (max|y_0| from decimate3, bounded per octave by
 // (sqrt(2) sum|h|)^o) and the filters by 2^e_j; C = acc * 2^-(ex + e_j) exactly.
 //
-// Octaves 3-6 (hop <= 64, cqt_mfma_kernel): one workgroup per (chunk, 64-frame tile), one
-// wave per octave: 4 row tiles x 5 column tiles x 3 products = 60 MFMA 16x16x32 per k-step
-// of 32 taps, 32 k-steps.  The tile's span (63 hop + 1024 samples) is split once into an LDS
+// Octaves 3-6 (hop <= 64, cqt_mfma_kernel): one workgroup per (chunk, 32-frame tile), one
+// wave per octave: 2 row tiles x 5 column tiles x 3 products = 30 MFMA 16x16x32 per k-step
+// of 32 taps, 32 k-steps.  The tile's span (31 hop + 1024 samples) is split once into an LDS
 // image that every k-step's fragments read; the filter slices (one k-step: 10 fragments x
 // 1 KB) stream through a two-slot LDS ring by LDS-DMA, with one raw s_barrier per k-step.
-// 76 KB of LDS: two workgroups per CU, whose k-steps interleave freely.  Octaves 0-2 (hop
+// 52 KB of LDS: three workgroups per CU, whose k-steps interleave freely (64-frame tiles with
+// padded images until round 5: 78 KB, two per CU).  Octaves 0-2 (hop
 // >= 128, cqt_mfma_low_kernel below): their spans do not fit LDS as images.  Both write
 // per-(frame, octave) chroma partial rows; cqt_tail_kernel finishes the frames.
 //
@@ -654,8 +655,21 @@ __global__ __launch_bounds__(NT) void tuning_select_kernel(const float* peak_pit
 // step's MFMAs 748-765 against 730-745 us; octave 2 in a workgroup of its own 888-1012
 // against 879 us; the FFT CQT kernel for octaves 0-2 866 against 816-856 us (removed in
 // round 3).
-constexpr int CM_FR = 64;                          // frames per workgroup tile
+constexpr int CM_FR = 64;                          // frames per cqt_tail / partial-sum tile
 constexpr int CM_RT = CM_FR / 16;                  // row tiles per wave
+// Round 5: 32-frame tiles with swizzled (unpadded) images need 52 KB of LDS, three workgroups
+// (twelve waves) per CU instead of two at 78 KB: 343.0 -> 326.5 us per 224 chunks, bit-identical;
+// 32 frames with the pads (two per CU) 381.2, 64 frames swizzled 348.5, 64 unpadded (bank
+// conflicts) 345.3 (profiles/r5_cqt_high_tiles.txt)
+#ifndef CH_FR_
+#define CH_FR_ 32
+#endif
+#ifndef CH_MINB_
+#define CH_MINB_ 3
+#endif
+constexpr int CH_FR = CH_FR_;                      // frames per cqt_mfma_kernel workgroup tile
+constexpr int CH_RT = CH_FR / 16;                  // its row tiles per wave
+static_assert(CH_RT == 2 || CH_RT == 4, "tile rows");
 constexpr int CM_KS = kCqtNfft / 32;               // k-steps of 32 taps
 constexpr int CM_NT = 5;                           // column tiles (72 of 80 columns used)
 constexpr int CM_R = 2;                            // filter-slice ring slots
@@ -679,22 +693,37 @@ __host__ __device__ constexpr int cm_vmcnt(int n) { return (n & 15) | ((n >> 4) 
 // every octave and k-step (the round-2 pads, 8 halves when hop >= 16, gave 2-way conflicts
 // for octaves 3-5)
 __host__ __device__ constexpr int cm_hop(int o) { return 512 >> o; }
-__host__ __device__ constexpr int cm_pad(int o) { return cm_hop(o) >= 32 ? 16 : 0; }
-__host__ __device__ constexpr int cm_span(int o) { return (CM_FR - 1) * cm_hop(o) + kCqtNfft; }
+#ifndef CH_PAD_
+#define CH_PAD_ 16
+#endif
+// CH_SWZ_: no pads; instead 16-byte piece P of a hop-64 / hop-32 image sits at P ^ cm_swz(P),
+// an XOR of its low four bits keyed by its 256-byte block (conflict-free for every fragment
+// read by the bank model above, tests/test_lds_layout_cpu.py); hop 16 and 8 are conflict-free
+// unpadded
+#ifndef CH_SWZ_
+#define CH_SWZ_ 1
+#endif
+__host__ __device__ constexpr int cm_pad(int o) { return cm_hop(o) >= 32 && !CH_SWZ_ ? CH_PAD_ : 0; }
+// (key table, block-index mask) of octave o's swizzle: h[(P >> 4) & m] = (K >> 4 ((P >> 4) & m)) & 15
+__host__ __device__ constexpr unsigned cm_swz_k(int o) { return !CH_SWZ_ ? 0u : cm_hop(o) == 64 ? 0xC638u : cm_hop(o) == 32 ? 0xF8u : 0u; }
+__host__ __device__ constexpr int cm_swz_m(int o) { return cm_hop(o) == 64 ? 3 : 1; }
+__host__ __device__ __forceinline__ int cm_phys(int P, unsigned K, int m) { return P ^ (int)((K >> (((P >> 4) & m) << 2)) & 15u); }
+__host__ __device__ constexpr int cm_span(int o) { return (CH_FR - 1) * cm_hop(o) + kCqtNfft; }
 __host__ __device__ constexpr int cm_img(int o) {  // halves per hi (or lo) image, 16-byte multiple
-  return (cm_span(o) + (cm_span(o) / cm_hop(o)) * cm_pad(o) + 7) & ~7;
+  // (whole 256-byte blocks when swizzled: a piece of the last block may move anywhere in it)
+  return cm_swz_k(o) ? (cm_span(o) + 127) & ~127 : (cm_span(o) + (cm_span(o) / cm_hop(o)) * cm_pad(o) + 7) & ~7;
 }
 __host__ __device__ constexpr int cm_aoff(int o) {  // byte offset of octave o's image pair
   return o <= CM_LO ? 0 : cm_aoff(o - 1) + 4 * cm_img(o - 1);
 }
 // K-loop LDS: filter ring [CM_R][CM_SLICE] uint4 | images.  Epilogue overlay: octave rows
-// [CM_NW][CM_FR][36] f32
+// [CM_NW][CH_FR][36] f32
 constexpr int CM_BBYTES = CM_R * CM_SLICE * 16;
 // Image pieces per lane whose loads are issued together.  One session, cqt_chroma per 224
 // chunks: 1 / 2 / 4 / 8 -> 751-753 / 739 / 744-745 / 743 us.
 constexpr int CM_IMGU = 4;
 constexpr int CM_KBYTES = CM_BBYTES + cm_aoff(7);
-constexpr int CM_MBYTES = CM_NW * CM_FR * kCqtFilt * 4;
+constexpr int CM_MBYTES = CM_NW * CH_FR * kCqtFilt * 4;
 size_t cqm_lds_bytes() { return CM_KBYTES > CM_MBYTES ? CM_KBYTES : CM_MBYTES; }
 
 struct CqmArgs {
@@ -760,7 +789,7 @@ __device__ __forceinline__ void cm_split(const float (&v)[8], float s, cm_half8&
   lo = __builtin_bit_cast(cm_half8, l);
 }
 
-__global__ __launch_bounds__(CM_NTH, 2) void cqt_mfma_kernel(CqmArgs a) {
+__global__ __launch_bounds__(CM_NTH, CH_MINB_) void cqt_mfma_kernel(CqmArgs a) {
   const Span span_(a.span);
   extern __shared__ __attribute__((aligned(16))) char smem[];
   uint4* sB = reinterpret_cast<uint4*>(smem);  // [CM_R][CM_SLICE]
@@ -775,9 +804,9 @@ __global__ __launch_bounds__(CM_NTH, 2) void cqt_mfma_kernel(CqmArgs a) {
   // every descriptor read up front, unconditionally: one round trip of scalar loads
   const int T = a.n_frames[c], ti = a.tuning_idx[c], ex = a.oct_ex[c * 7 + oct];
   const int64_t yoff = a.oct_off[c * 7 + oct], Ly = a.oct_len[c * 7 + oct];
-  const int t0 = bx * CM_FR;
+  const int t0 = bx * CH_FR;
   if (t0 >= T) return;
-  const int nfr = min(CM_FR, T - t0);
+  const int nfr = min(CH_FR, T - t0);
   const uint4* bsrc = a.bfrag + (size_t)ti * (CM_KS * CM_SLICE);
   // the first filter slice is in flight while the image is built
   auto fetch_slice = [&](int ks) {
@@ -795,7 +824,7 @@ __global__ __launch_bounds__(CM_NTH, 2) void cqt_mfma_kernel(CqmArgs a) {
   const int hop = 512 >> oct;
   const float sx = ldexpf(1.0f, ex);
   const int64_t s0 = (int64_t)t0 * hop - 512;  // first sample of the tile's span
-  const int S = (CM_FR - 1) * hop + kCqtNfft;
+  const int S = (CH_FR - 1) * hop + kCqtNfft;
   const bool vec = s0 >= 0 && s0 + S <= Ly && (reinterpret_cast<uintptr_t>(y) & 15) == 0;
   const int kq = 8 * (lane >> 4);
 
@@ -803,6 +832,9 @@ __global__ __launch_bounds__(CM_NTH, 2) void cqt_mfma_kernel(CqmArgs a) {
   constexpr int aoffs[8] = {cm_aoff(0), cm_aoff(1), cm_aoff(2), cm_aoff(3), cm_aoff(4), cm_aoff(5), cm_aoff(6), cm_aoff(7)};
   const int pad = cm_pad(oct);
   const int img = cm_img(oct);
+  constexpr unsigned swk[8] = {cm_swz_k(0), cm_swz_k(1), cm_swz_k(2), cm_swz_k(3), cm_swz_k(4), cm_swz_k(5), cm_swz_k(6), cm_swz_k(7)};
+  const unsigned sk = swk[oct];
+  const int sm = cm_swz_m(oct);
   _Float16* aimg = reinterpret_cast<_Float16*>(smem + CM_BBYTES + aoffs[oct]);
   int ib = lane;
   if (vec) {
@@ -822,7 +854,7 @@ __global__ __launch_bounds__(CM_NTH, 2) void cqt_mfma_kernel(CqmArgs a) {
         const float v[8] = {u[k][0].x, u[k][0].y, u[k][0].z, u[k][0].w, u[k][1].x, u[k][1].y, u[k][1].z, u[k][1].w};
         cm_half8 h, l;
         cm_split(v, sx, h, l);
-        const int pos = 8 * i + (8 * i / hop) * pad;
+        const int pos = CH_SWZ_ ? 8 * cm_phys(i, sk, sm) : 8 * i + (8 * i / hop) * pad;
         *reinterpret_cast<cm_half8*>(aimg + pos) = h;
         *reinterpret_cast<cm_half8*>(aimg + img + pos) = l;
       }
@@ -844,17 +876,19 @@ __global__ __launch_bounds__(CM_NTH, 2) void cqt_mfma_kernel(CqmArgs a) {
     }
     cm_half8 h, l;
     cm_split(v, sx, h, l);
-    const int pos = 8 * i + (8 * i / hop) * pad;
+    const int pos = CH_SWZ_ ? 8 * cm_phys(i, sk, sm) : 8 * i + (8 * i / hop) * pad;
     *reinterpret_cast<cm_half8*>(aimg + pos) = h;
     *reinterpret_cast<cm_half8*>(aimg + img + pos) = l;
   }
-  int abase[CM_RT];
+  int abase[CH_RT];
 #pragma unroll
-  for (int rt = 0; rt < CM_RT; ++rt) abase[rt] = (16 * rt + (lane & 15)) * (hop + pad) + kq + (kq / hop) * pad;
+  for (int rt = 0; rt < CH_RT; ++rt)
+    abase[rt] = CH_SWZ_ ? ((16 * rt + (lane & 15)) * hop + kq) / 8  // the fragment's first piece
+                        : (16 * rt + (lane & 15)) * (hop + pad) + kq + (kq / hop) * pad;
 
-  cm_f4 acc[CM_RT][CM_NT];
+  cm_f4 acc[CH_RT][CM_NT];
 #pragma unroll
-  for (int rt = 0; rt < CM_RT; ++rt)
+  for (int rt = 0; rt < CH_RT; ++rt)
 #pragma unroll
     for (int nt = 0; nt < CM_NT; ++nt) acc[rt][nt] = cm_f4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll 1
@@ -872,33 +906,37 @@ __global__ __launch_bounds__(CM_NTH, 2) void cqt_mfma_kernel(CqmArgs a) {
     // fragments two column tiles ahead of their MFMAs
     const int kt = 32 * ks + (32 * ks / hop) * pad;
     const uint32_t sbl = lds_addr(sB + (ks % CM_R) * CM_SLICE + lane);
-    cm_u4 a0, a1, a2, a3, l0, l1, l2, l3, b[CM_NT][2];
-    static_assert(CM_RT == 4 && CM_NT == 5, "fragment schedule");
-    cm_rd<0>(a0, lds_addr(aimg + abase[0] + kt));
-    cm_rd<0>(a1, lds_addr(aimg + abase[1] + kt));
-    cm_rd<0>(a2, lds_addr(aimg + abase[2] + kt));
-    cm_rd<0>(a3, lds_addr(aimg + abase[3] + kt));
-    cm_rd<0>(l0, lds_addr(aimg + img + abase[0] + kt));
-    cm_rd<0>(l1, lds_addr(aimg + img + abase[1] + kt));
-    cm_rd<0>(l2, lds_addr(aimg + img + abase[2] + kt));
-    cm_rd<0>(l3, lds_addr(aimg + img + abase[3] + kt));
+    cm_u4 a4[CH_RT], l4[CH_RT], b[CM_NT][2];
+    static_assert(CM_NT == 5, "fragment schedule");
+#pragma unroll
+    for (int rt = 0; rt < CH_RT; ++rt)
+      cm_rd<0>(a4[rt], lds_addr(aimg + (CH_SWZ_ ? 8 * cm_phys(abase[rt] + 4 * ks, sk, sm) : abase[rt] + kt)));
+#pragma unroll
+    for (int rt = 0; rt < CH_RT; ++rt)
+      cm_rd<0>(l4[rt], lds_addr(aimg + img + (CH_SWZ_ ? 8 * cm_phys(abase[rt] + 4 * ks, sk, sm) : abase[rt] + kt)));
     cm_rd<0 * 1024>(b[0][0], sbl);
     cm_rd<1 * 1024>(b[0][1], sbl);
     cm_rd<2 * 1024>(b[1][0], sbl);
     cm_rd<3 * 1024>(b[1][1], sbl);
     cm_rd<4 * 1024>(b[2][0], sbl);
     cm_rd<5 * 1024>(b[2][1], sbl);
-    cm_wait<4>(a0, a1, a2, a3);  // A + tile 0 landed; tiles 1, 2 in flight
-    cm_wait<4>(l0, l1, l2, l3);
-    const cm_half8 ah[CM_RT] = {__builtin_bit_cast(cm_half8, a0), __builtin_bit_cast(cm_half8, a1),
-                                __builtin_bit_cast(cm_half8, a2), __builtin_bit_cast(cm_half8, a3)};
-    const cm_half8 al[CM_RT] = {__builtin_bit_cast(cm_half8, l0), __builtin_bit_cast(cm_half8, l1),
-                                __builtin_bit_cast(cm_half8, l2), __builtin_bit_cast(cm_half8, l3)};
+    if constexpr (CH_RT == 4) {
+      cm_wait<4>(a4[0], a4[1], a4[2], a4[3]);  // A + tile 0 landed; tiles 1, 2 in flight
+      cm_wait<4>(l4[0], l4[1], l4[2], l4[3]);
+    } else {
+      cm_wait<4>(a4[0], a4[1], l4[0], l4[1]);
+    }
+    cm_half8 ah[CH_RT], al[CH_RT];
+#pragma unroll
+    for (int rt = 0; rt < CH_RT; ++rt) {
+      ah[rt] = __builtin_bit_cast(cm_half8, a4[rt]);
+      al[rt] = __builtin_bit_cast(cm_half8, l4[rt]);
+    }
     auto tile = [&](int nt) {
       const cm_half8 bh = __builtin_bit_cast(cm_half8, b[nt][0]);
       const cm_half8 bl = __builtin_bit_cast(cm_half8, b[nt][1]);
 #pragma unroll
-      for (int rt = 0; rt < CM_RT; ++rt) {
+      for (int rt = 0; rt < CH_RT; ++rt) {
         acc[rt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[rt], bh, acc[rt][nt], 0, 0, 0);
         acc[rt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[rt], bl, acc[rt][nt], 0, 0, 0);
         acc[rt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al[rt], bh, acc[rt][nt], 0, 0, 0);
@@ -922,7 +960,7 @@ __global__ __launch_bounds__(CM_NTH, 2) void cqt_mfma_kernel(CqmArgs a) {
   __syncthreads();  // every wave's last ring / image reads done before the rows overlay them
 
   // |C| per (frame, row) into this wave's [64][36] region
-  float* mg = reinterpret_cast<float*>(smem) + wave * (CM_FR * kCqtFilt);
+  float* mg = reinterpret_cast<float*>(smem) + wave * (CH_FR * kCqtFilt);
   {
     const float oscale = (float)(1 << (oct >> 1)) * ((oct & 1) ? 0x1.6a09e6p+0f : 1.0f);
     const float* isl = a.cqt_isl + ti * kCqtBins + (kCqtBins - kCqtFilt * (oct + 1));
@@ -932,7 +970,7 @@ __global__ __launch_bounds__(CM_NTH, 2) void cqt_mfma_kernel(CqmArgs a) {
     const float inv2 = ldexpf(1.0f, -(ex + bx[32 + (col & 3)]));
     const float il0 = isl[col], il1 = isl[16 + col], il2 = isl[32 + (col & 3)];
 #pragma unroll
-    for (int rt = 0; rt < CM_RT; ++rt)
+    for (int rt = 0; rt < CH_RT; ++rt)
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int fr = 16 * rt + 4 * (lane >> 4) + i;  // row within the tile
@@ -1589,7 +1627,8 @@ int launch_chroma_mean(Context& ctx, const float* sig, const int64_t* chunk_off,
     KTimer kt_(ctx, "cqt_high", st);
     ma.span = kt_.span();
     for (int rep = 0; rep < NC_PROBE_REPS(5); ++rep)
-      hipLaunchKernelGGL(cqt_mfma_kernel, dim3(ntile, n), dim3(CM_NTH), cqm_lds_bytes(), st, ma);
+      hipLaunchKernelGGL(cqt_mfma_kernel, dim3((unsigned)((1 + max_chunk_len / 512 + CH_FR - 1) / CH_FR), n),
+                         dim3(CM_NTH), cqm_lds_bytes(), st, ma);
   }
   hipLaunchKernelGGL(cqt_tail_kernel, dim3(ntile, n), dim3(256), 0, st, w.gpart, w.tf_base, w.n_frames, w.partial);
   hipLaunchKernelGGL(chroma_finalize_kernel, dim3(n), dim3(64), 0, st, w.partial, w.tf_base, w.n_frames, n, CM_FR,

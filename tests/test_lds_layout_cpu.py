@@ -3,7 +3,8 @@ results), checked against a model of the hardware rules they were designed for:
 
 * `xcd_remap` (nc_device.h) must be a permutation of the workgroup ids for every grid size,
   or workgroups would be skipped or run twice;
-* the fragment reads of `cqt_mfma_kernel` (image pads `cm_pad`, cqt.hip) and of
+* the fragment reads of `cqt_mfma_kernel` (image pads `cm_pad`, or since round 5 the XOR
+  swizzle `cm_phys` of hop-64 / hop-32 images, cqt.hip) and of
   `cqt_mfma_low_kernel` (image swizzle `c2_sw`, round 5) must be free of LDS bank conflicts under the
   `ds_read_b128` lane groups of MI355X_MICROARCH.md (LDS table): one LDS cycle per group.
 
@@ -44,7 +45,7 @@ def cm_hop(o):
     return 512 >> o
 
 
-def cm_pad(o):  # cqt.hip
+def cm_pad(o):  # cqt.hip, the padded layout of CH_SWZ_=0 builds (the default until round 5)
     return 16 if cm_hop(o) >= 32 else 0
 
 
@@ -60,6 +61,52 @@ def test_octave_3_6_image_reads_conflict_free(octave):
                       for l in range(64)]
             assert all(h % 8 == 0 for h in halves)  # 16-byte aligned pieces
             assert b128_cycles([h // 2 for h in halves]) == 4, (octave, rt, ks)
+
+
+# cqt.hip cm_swz_k / cm_swz_m / cm_phys (the default since round 5): piece P of a hop-64 or hop-32
+# image sits at P ^ h[(P >> 4) & m]; hop 16 and 8 are unpadded and unswizzled
+CM_SWZ = {64: (0xC638, 3), 32: (0xF8, 1)}
+
+
+def cm_phys(P, hop):
+    if hop not in CM_SWZ:
+        return P
+    K, m = CM_SWZ[hop]
+    return P ^ ((K >> (((P >> 4) & m) << 2)) & 15)
+
+
+@pytest.mark.parametrize("frames", [32, 64])
+@pytest.mark.parametrize("octave", [3, 4, 5, 6])
+def test_octave_3_6_swizzled_image_reads_conflict_free(octave, frames):
+    """Fragment of row tile rt at k-step ks: lane l reads piece (16 rt + (l & 15)) hop / 8 +
+    l >> 4 + 4 ks through the swizzle (cqt_mfma_kernel abase / cm_phys)."""
+    hop = cm_hop(octave)
+    for rt in range(frames // 16):
+        for ks in range(32):
+            pieces = [cm_phys((16 * rt + (l & 15)) * hop // 8 + (l >> 4) + 4 * ks, hop) for l in range(64)]
+            assert b128_cycles([4 * p for p in pieces]) == 4, (octave, rt, ks)
+
+
+@pytest.mark.parametrize("frames", [32, 64])
+@pytest.mark.parametrize("octave", [3, 4, 5, 6])
+def test_octave_3_6_swizzle_is_a_permutation_inside_the_image(octave, frames):
+    """Every piece of the span lands on a distinct piece of the image (cm_img: whole 256-byte
+    blocks when swizzled), so no write overlaps another or leaves the octave's image."""
+    hop = cm_hop(octave)
+    span = (frames - 1) * hop + 1024
+    img = (span + 127) & ~127 if hop in CM_SWZ else (span + 7) & ~7
+    phys = [cm_phys(p, hop) for p in range(span // 8)]
+    assert len(set(phys)) == len(phys) and max(phys) < img // 8
+
+
+def test_octave_3_6_lds_fits_three_workgroups():
+    """cqm_lds_bytes at 32 frames swizzled: ring (2 slots x 10 KB) + the four images (hi + lo)."""
+    tot = 2 * 5 * 2 * 64 * 16
+    for o in range(3, 7):
+        hop = cm_hop(o)
+        span = 31 * hop + 1024
+        tot += 4 * ((span + 127) & ~127 if hop in CM_SWZ else (span + 7) & ~7)
+    assert 3 * tot <= 160 * 1024, tot
 
 
 SF_RS = 72  # spectral.hip spectral_frames_kernel: row stride (f64) of the frame-sum reduction
