@@ -7,6 +7,7 @@ import pickle
 import socket
 
 import numpy as np
+import pytest
 import torch.multiprocessing as mp
 
 from nightcore_analyzer import consensus as C
@@ -119,3 +120,29 @@ def test_one_rank_group_runs_the_collectives_with_collect_at_one():
     p.join(timeout=60)
     assert p.exitcode == 0
     assert got == [_key(_outcome(b)) for b in range(7)], got
+
+
+def test_outcomes_pickled_ahead_travel_the_same():
+    """sharded._PrePickle (the finished steps' interior outcomes pickled while the host waits on
+    the device): the gathered bytes decode to the same outcomes as items pickled at gather time,
+    and on_idle does one item per call."""
+    pre = S._PrePickle([3, 5, 6])
+    pre.on_batch(0, [_outcome(3), _outcome(5), _outcome(6)])
+    assert pre.on_idle() and pre.on_idle()          # pairs 3 and 5 of step 0 pickled
+    own = [(b, _outcome(b)) for b in (1, 3, 5, 6)]   # pair 1: a split pair, pickled at gather time
+    ahead = pre.step(0)
+    assert sorted(ahead) == [3, 5]
+    blob = S._dumps_outcomes(own, ahead)
+    assert not ahead                                   # every pre-pickled item was used
+    g = S.GatheredOutcomes(8, np.array([1, 0, 1, 0, 1, 0, 0, 1]), [], {0: memoryview(blob)})
+    for b in (1, 3, 5, 6):
+        assert _key(g[b]) == _key(_outcome(b))
+    assert pre.on_idle() and not pre.on_idle()       # pair 6 left, then nothing
+
+
+@pytest.mark.parametrize("sizes", [[5], [0, 7, 3], [300, 1, 0, 44]])
+def test_steps_pack_round_trip(sizes):
+    """analyze_sharded(steps=K) gathers the K steps' blobs as one: lengths table, then blobs."""
+    blobs = [bytes((i * 7 + j) % 256 for j in range(n)) for i, n in enumerate(sizes)]
+    got = S._unpack_steps(memoryview(S._pack_steps(blobs)), len(blobs))
+    assert [bytes(x) for x in got] == blobs

@@ -1,0 +1,100 @@
+#!/usr/bin/env python3
+"""One rank's share of the N > 1 window-sharded step, measured on the box's one GPU: a one-rank
+"nccl" (RCCL) group with sharded.Exchange.collect_at_one, so the step's outcome gather (pickle +
+byte all-gather) runs as on every rank of an 8-GPU job, against the same step without the
+gather and against Engine.analyze_batches (the N = 1 headline).  Rotated, minimum per variant.
+usage: tools/rank_step_probe.py [K] [ROUNDS]"""
+import os
+import socket
+import sys
+import time
+from pathlib import Path
+
+REPO = Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(REPO))
+sys.path.insert(0, str(REPO / "nightcore-to-flac-analyzer_amd"))
+
+
+def main():
+    K = int(sys.argv[1]) if len(sys.argv) > 1 else 10
+    R = int(sys.argv[2]) if len(sys.argv) > 2 else 3
+    import bench
+    pairs = bench.make_pairs(64, 180.0, 1000, 16)
+    import torch
+    import torch.distributed as dist
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(s.getsockname()[1]))
+    s.close()
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    from nightcore_analyzer import engine as E
+    from nightcore_analyzer import sharded as S
+    S.Exchange.collect_at_one = True
+    eng = E.get_engine(0)
+    flat = [a for nc, src in pairs for a in (nc, src)]
+    sig = eng.upload_signals(flat)
+    lengths = [len(a) for a in flat]
+    params = E.Params(compute_ibi=False)
+
+    def windows(gather):
+        return S.analyze_sharded(S.DeviceStages(eng, sig), params, lengths=lengths, gather=gather, steps=K)
+
+    def windows_late():   # every step's outcomes pickled at the gather (sharded.PREPICKLE off)
+        S.PREPICKLE = False
+        try:
+            return windows(True)
+        finally:
+            S.PREPICKLE = True
+
+    variants = {"analyze_batches": lambda: eng.analyze_batches([sig] * K, params),
+                "windows_gather": lambda: windows(True),
+                "windows_gather_late": windows_late,
+                "windows_nogather": lambda: windows(False)}
+    for f in variants.values():
+        f()
+    best = {k: [] for k in variants}
+    for _ in range(R):
+        for k, f in variants.items():
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            res = f()
+            torch.cuda.synchronize()
+            best[k].append((time.perf_counter() - t0) / K * 1e3)
+            del res
+    for k, v in best.items():
+        print(f"{k:>18}: {min(v):7.3f} ms/step (runs {[round(x, 3) for x in v]})", flush=True)
+    # where the gather's host time goes: one more windows_gather call with its parts timed
+    acc = {}
+
+    def timed(owner, name):
+        f = getattr(owner, name)
+
+        def w(*a, **kw):
+            t = time.perf_counter()
+            try:
+                return f(*a, **kw)
+            finally:
+                n, s_ = acc.get(name, (0, 0.0))
+                acc[name] = (n + 1, s_ + time.perf_counter() - t)
+        setattr(owner, name, w)
+        return f
+
+    saved = [(S, "_dumps_outcomes", timed(S, "_dumps_outcomes")),
+             (S.Exchange, "gather_bytes", timed(S.Exchange, "gather_bytes")),
+             (S._PrePickle, "on_idle", timed(S._PrePickle, "on_idle")),
+             (S._PrePickle, "on_batch", timed(S._PrePickle, "on_batch"))]
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    windows(True)
+    torch.cuda.synchronize()
+    tot = (time.perf_counter() - t0) / K * 1e3
+    for owner, name, f in saved:
+        setattr(owner, name, f)
+    print(f"windows_gather (parts timed) {tot:.3f} ms/step; per step: " +
+          ", ".join(f"{k} {v[1] / K * 1e3:.3f} ms ({v[0] / K:.1f} calls)" for k, v in acc.items()), flush=True)
+    dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()
