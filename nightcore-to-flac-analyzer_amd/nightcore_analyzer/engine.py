@@ -938,18 +938,11 @@ class Engine:
             except StopIteration as stop:
                 return stop.value
 
-    def _analyze_gen(self, batches: List[DeviceSignals], p: Params, group_pairs, log=None, on_batch=None,
-                     on_idle=None):
+    def _analyze_gen(self, batches: List[DeviceSignals], p: Params, group_pairs, log=None):
         """The body of ``_analyze_many`` as a generator that yields after each pair group is
         launched (the host is then free until the next ``next``): a caller can interleave
         other host work — the window-sharded record exchanges — with the pipelined groups
-        while up to GROUPS_IN_FLIGHT of them keep the device busy.  Returns the results.
-
-        ``on_batch(bi, outcomes)`` is called as soon as batch bi's last group is assembled.
-        ``on_idle()`` is called repeatedly where the host would otherwise block on the oldest
-        group's completion, while it is still running, until it returns False (one small piece
-        of the caller's host work per call: the window-sharded result gather pickles a finished
-        step's outcomes there)."""
+        while up to GROUPS_IN_FLIGHT of them keep the device busy.  Returns the results."""
         hs = self.host_stats
         launch = torch.cuda.current_stream(self.dev)
         # the signals are complete on the launch stream here; trims of later batches wait for
@@ -983,20 +976,6 @@ class Engine:
             if trace is not None:
                 trace.append((time.perf_counter(), label))
 
-        left = [None] * len(batches)        # groups of each batch not yet assembled
-
-        def finish(g):
-            bi = g["bi"]
-            results[bi] += self._finish_group(g, log)
-            left[bi] -= 1
-            if left[bi] == 0 and on_batch is not None:
-                on_batch(bi, results[bi])
-
-        def idle_until(g):
-            if on_idle is not None:
-                while not g["event"].query() and on_idle():
-                    pass
-
         nxt = None
         for bi, signals in enumerate(batches):
             t0 = time.perf_counter()
@@ -1004,7 +983,6 @@ class Engine:
             tr = nxt if nxt is not None else trim_begin(bi, False)
             nxt = None
             groups = tr["groups"]
-            left[bi] = len(groups)
             align = None
             if tr["split"]:
                 nF, f1 = signals.n_files, tr["f1"]
@@ -1042,20 +1020,17 @@ class Engine:
                     while pending and (len(pending) > self.MAX_GROUPS_IN_FLIGHT or
                                        (len(pending) > 1 and pending[0]["event"].query())):
                         g = pending.pop(0)
-                        idle_until(g)
                         mark(f"finish b{g['bi']} g{g['g0']}")
-                        finish(g)
+                        results[g["bi"]] += self._finish_group(g, log)
                 elif len(pending) > self.GROUPS_IN_FLIGHT:
                     g = pending.pop(0)
-                    idle_until(g)
                     mark(f"finish b{g['bi']} g{g['g0']}")
-                    finish(g)
+                    results[g["bi"]] += self._finish_group(g, log)
                 mark("yield")
                 yield
         for g in pending:
-            idle_until(g)
             mark(f"finish b{g['bi']} g{g['g0']}")
-            finish(g)
+            results[g["bi"]] += self._finish_group(g, log)
         mark("end")
         return results
 

@@ -189,24 +189,17 @@ class FakeStages:
             if root._left == 0:
                 raise RuntimeError(f"injected failure in {name}")
 
-    def pipeline(self, files, p, steps=1, on_batch=None, on_idle=None):
-        """Engine._analyze_gen's shape: two yields per step; each step's outcomes handed to
-        on_batch when the step is done, and on_idle polled between the yields."""
+    def pipeline(self, files, p, steps=1):
         n = len(files) // 2
         fail = self.fail_in == "pipeline"
 
         def gen():
             from nightcore_analyzer.engine import PairOutcome
-            res = [[PairOutcome() for _ in range(n)] for _ in range(steps)]
-            for i in range(2 * steps):
+            for _ in range(2 * steps):
                 yield
                 if fail:
                     raise RuntimeError("injected failure in pipeline")
-                if on_idle is not None:
-                    on_idle()
-                if i % 2 == 1 and on_batch is not None:
-                    on_batch(i // 2, res[i // 2])
-            return res
+            return [[PairOutcome() for _ in range(n)] for _ in range(steps)]
         return gen()
 
     def trim(self, p):

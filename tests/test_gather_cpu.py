@@ -122,22 +122,16 @@ def test_one_rank_group_runs_the_collectives_with_collect_at_one():
     assert got == [_key(_outcome(b)) for b in range(7)], got
 
 
-def test_outcomes_pickled_ahead_travel_the_same():
-    """sharded._PrePickle (the finished steps' interior outcomes pickled while the host waits on
-    the device): the gathered bytes decode to the same outcomes as items pickled at gather time,
-    and on_idle does one item per call."""
-    pre = S._PrePickle([3, 5, 6])
-    pre.on_batch(0, [_outcome(3), _outcome(5), _outcome(6)])
-    assert pre.on_idle() and pre.on_idle()          # pairs 3 and 5 of step 0 pickled
-    own = [(b, _outcome(b)) for b in (1, 3, 5, 6)]   # pair 1: a split pair, pickled at gather time
-    ahead = pre.step(0)
-    assert sorted(ahead) == [3, 5]
-    blob = S._dumps_outcomes(own, ahead)
-    assert not ahead                                   # every pre-pickled item was used
-    g = S.GatheredOutcomes(8, np.array([1, 0, 1, 0, 1, 0, 0, 1]), [], {0: memoryview(blob)})
-    for b in (1, 3, 5, 6):
-        assert _key(g[b]) == _key(_outcome(b))
-    assert pre.on_idle() and not pre.on_idle()       # pair 6 left, then nothing
+def test_fast_pickler_round_trips_arrays():
+    """sharded._OutcomePickler sends numeric arrays as (dtype, shape, bytes): same values,
+    dtypes and shapes after unpickling, writable copies."""
+    x = {"a": np.arange(12, dtype=np.float32).reshape(3, 4), "b": np.array([1, -2], np.int32),
+         "c": np.zeros((0,), np.float64), "d": np.array([True, False]), "s": "text"}
+    y = pickle.loads(S._pickle_fast(x))
+    for k in "abcd":
+        assert y[k].dtype == x[k].dtype and y[k].shape == x[k].shape and np.array_equal(y[k], x[k])
+        assert y[k].flags.writeable
+    assert y["s"] == "text"
 
 
 @pytest.mark.parametrize("sizes", [[5], [0, 7, 3], [300, 1, 0, 44]])

@@ -40,16 +40,8 @@ def main():
     def windows(gather):
         return S.analyze_sharded(S.DeviceStages(eng, sig), params, lengths=lengths, gather=gather, steps=K)
 
-    def windows_late():   # every step's outcomes pickled at the gather (sharded.PREPICKLE off)
-        S.PREPICKLE = False
-        try:
-            return windows(True)
-        finally:
-            S.PREPICKLE = True
-
     variants = {"analyze_batches": lambda: eng.analyze_batches([sig] * K, params),
                 "windows_gather": lambda: windows(True),
-                "windows_gather_late": windows_late,
                 "windows_nogather": lambda: windows(False)}
     for f in variants.values():
         f()
@@ -81,9 +73,7 @@ def main():
         return f
 
     saved = [(S, "_dumps_outcomes", timed(S, "_dumps_outcomes")),
-             (S.Exchange, "gather_bytes", timed(S.Exchange, "gather_bytes")),
-             (S._PrePickle, "on_idle", timed(S._PrePickle, "on_idle")),
-             (S._PrePickle, "on_batch", timed(S._PrePickle, "on_batch"))]
+             (S.Exchange, "gather_bytes", timed(S.Exchange, "gather_bytes"))]
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     windows(True)
