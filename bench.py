@@ -261,8 +261,9 @@ def main():
     def run_windows(k, split_offset=0.0, gather=True):
         """k steps of the window-sharded analysis (interior groups pipelined across steps).
         gather=True is analyze_sharded's default: every step's outcomes of all pairs end on
-        every rank (one byte all-gather per step after the step's last record exchange; the
-        other ranks' outcomes unpickled on first access: sharded.GatheredOutcomes).  Returns
+        every rank (one byte all-gather of record tables per call after the last record
+        exchange: result rows readable at once, the other ranks' outcomes rebuilt from their
+        records on first access: sharded.GatheredOutcomes).  Returns
         one sequence of outcomes per step (gather) or of this rank's (pair, outcome)."""
         from nightcore_analyzer.sharded import DeviceStages, analyze_sharded
         res = analyze_sharded(DeviceStages(eng, signals), params, lengths=lengths, local_pairs=ids,
@@ -313,10 +314,14 @@ def main():
     # separate analyze calls (reported beside it as single_call_ms_per_step).  Window mode:
     # one analyze_sharded call of K steps (its interior groups pipelined the same way)
     pipelined = not args.no_pipeline
-    gather_unpickle_ms = None
+    gather_rebuild = None
     t0 = time.perf_counter()
     if win_mode:
         res = run_windows(args.steps)
+        # the caller's read of every step's results on every rank, inside the timed region: each
+        # pair's result row (ratios, CIs, counts) straight from the gathered records
+        # (sharded.GatheredOutcomes.table; the whole outcome is rebuilt only on access, below)
+        tabs = [r.table() for r in res]
     elif pipelined:
         res = eng.analyze_batches([own] * args.steps, params)
     else:
@@ -330,17 +335,28 @@ def main():
     if win_mode:
         if any(len(r) != world * P for r in res):
             raise RuntimeError("a window-sharded step returned an incomplete result")
-        # the received outcomes unpickled, outside the timed region (its cost reported beside it)
+        if any(not (t[:, 0] == 1.0).all() for t in tabs):
+            raise RuntimeError("a window-sharded step failed")
+        if rank == 0 and (tabs[0][0, 1] != tr or tabs[0][0, 4] != pr):
+            raise RuntimeError("the window-sharded result of pair 0 differs from the single-GPU engine's")
+        from nightcore_analyzer.sharded import result_row
+        # every outcome of the first step rebuilt from the records (report text, logs, detail:
+        # assemble_pair on the receiving rank), after the timed region, per received pair
         tu = time.perf_counter()
-        decoded = [list(r) for r in res]
-        gather_unpickle_ms = max_over_ranks((time.perf_counter() - tu) / args.steps * 1e3)
-        mine = decoded[0]                       # gather=True: every pair's outcome on every rank
-        if any(o.error is not None for r in decoded for o in r):
+        mine = list(res[0])                     # gather=True: every pair's outcome on every rank
+        n_recv = sum(1 for b in range(len(mine)) if int(res[0]._owner[b]) != rank)
+        gather_rebuild = {"ms_per_received_pair": max_over_ranks((time.perf_counter() - tu) * 1e3 / max(1, n_recv)),
+                          "received_pairs_per_rank_step": n_recv,
+                          "how": "outside the timed region: one step's outcomes of the other ranks' pairs rebuilt "
+                                 "from the gathered records by assemble_pair (engine.AsmContext), as a caller pays "
+                                 "on first access to a pair's report or logs; the timed steps read every pair's "
+                                 "result row (GatheredOutcomes.table)"}
+        if any(o.error is not None for o in mine):
             raise RuntimeError("a window-sharded step failed")
         win_total = sum(o.detail["energy_src"].size + o.detail["energy_nc"].size for o in mine)
-        if rank == 0 and (mine[0].result.tempo_ratio != tr or mine[0].result.pitch_ratio != pr):
-            raise RuntimeError("the window-sharded result of pair 0 differs from the single-GPU engine's")
-        del res, mine, decoded                  # not kept (see below)
+        if any(not np.array_equal(tabs[0][b], result_row(o), equal_nan=True) for b, o in enumerate(mine)):
+            raise RuntimeError("a gathered result row differs from its rebuilt outcome")
+        del res, mine, tabs                     # not kept (see below)
     elif pipelined:
         if len(res) != args.steps or any(len(r) != len(outs) for r in res):
             raise RuntimeError("analyze_batches returned an incomplete result")
@@ -395,15 +411,20 @@ def main():
             t1 = time.perf_counter()
             if off is None:
                 eng.analyze_batches([own] * args.steps, params)
-                n_win = world * win_per_step
             else:
                 r_ = run_windows(args.steps, off, gat)
-                n_win = (sum(o.detail["energy_src"].size + o.detail["energy_nc"].size for o in r_[0]) if gat else
-                         sum_over_ranks(sum(o.detail["energy_src"].size + o.detail["energy_nc"].size
-                                            for _, o in r_[0])))
+                if gat:
+                    tabs_ = [r.table() for r in r_]     # the caller's read, as in the headline
             torch.cuda.synchronize()
             barrier()
             e1 = max_over_ranks(time.perf_counter() - t1)
+            # windows counted after the clock (a gathered outcome's detail is rebuilt on access)
+            if off is None:
+                n_win = world * win_per_step
+            else:
+                n_win = (sum(o.detail["energy_src"].size + o.detail["energy_nc"].size for o in r_[0]) if gat else
+                         sum_over_ranks(sum(o.detail["energy_src"].size + o.detail["energy_nc"].size
+                                            for _, o in r_[0])))
             modes[name] = {"value": n_win * args.steps / e1, "ms_per_step": e1 / args.steps * 1e3}
         from nightcore_analyzer.sharded import shard_plan
         sp = shard_plan(lengths, params, world, 0.5)
@@ -542,7 +563,41 @@ def main():
                "ms_per_step": t_up / n_up * 1e3, "bytes_per_step": int(host.numel() * 4),
                "h2d_ms_per_step_alone": h2d_ms, "h2d_gb_per_s": host.numel() * 4 / (h2d_ms * 1e-3) / 1e9,
                "how": "pinned host staging, H2D on its own stream, double-buffered against the analysis"}
-        del host, bufs
+        del host
+
+        # the same with 16-bit PCM sources (a mono 16-bit WAV as io.load_audio(keep_pcm16=True)
+        # keeps it): the batch quantized to int16, its 2-byte samples copied host -> HBM and
+        # widened on the copy stream (nc_pcm16_to_f32, k / 32768), half the PCIe bytes
+        q16 = torch.clamp(torch.round(signals.buf * 32768.0), -32768, 32767).to(torch.int16)
+        host16 = q16.cpu().pin_memory()
+        raw = [q16, torch.empty_like(q16)]
+        bufs = [torch.empty_like(signals.buf), torch.empty_like(signals.buf)]   # the resident batch kept
+
+        def upload16(j):
+            with torch.cuda.stream(cs):
+                raw[j % 2].copy_(host16, non_blocking=True)
+                eng.call("nc_pcm16_to_f32", raw[j % 2].data_ptr(), raw[j % 2].numel(), bufs[j % 2].data_ptr(),
+                         cs.cuda_stream)
+                evs[j % 2].record(cs)
+        upload16(0)
+        torch.cuda.synchronize()
+        eng.analyze(signals=E.DeviceSignals(bufs[0], own.off, own.length), params=params)   # warm
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        upload16(0)
+        for j in range(n_up):
+            if j + 1 < n_up:
+                upload16(j + 1)
+            torch.cuda.current_stream(eng.dev).wait_event(evs[j % 2])
+            eng.analyze(signals=E.DeviceSignals(bufs[j % 2], own.off, own.length), params=params)
+        torch.cuda.synchronize()
+        t16 = time.perf_counter() - t1
+        upl["pcm16"] = {"value": world * win_per_step * n_up / t16, "ms_per_step": t16 / n_up * 1e3,
+                        "bytes_per_step": int(host16.numel() * 2),
+                        "vs_f32_upload": (world * win_per_step * n_up / t16) / upl["value"],
+                        "how": "the batch quantized to 16-bit PCM (a 16-bit WAV source), int16 staged in pinned "
+                               "memory, H2D + nc_pcm16_to_f32 widening on the copy stream, double-buffered"}
+        del host16, raw, q16, bufs
 
     ibi = None
     if not args.no_ibi and rank == 0:
@@ -750,10 +805,9 @@ def main():
         if modes is not None:
             line["modes"] = modes
         if win_mode:
-            # the timed steps end with every rank holding every pair's outcome as the bytes of
-            # the step's all-gather; unpickling the other ranks' outcomes happens on access
-            # (sharded.GatheredOutcomes), here all of them after the timed region, per step
-            line["gather_unpickle_ms_per_step"] = gather_unpickle_ms
+            # the timed steps end with every rank holding every pair's result rows (read in the
+            # region) and the records its whole outcome is rebuilt from on access (cost here)
+            line["gather_rebuild"] = gather_rebuild
         if upl is not None:
             line["upload_included"] = upl
         if ibi is not None:

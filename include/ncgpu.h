@@ -35,7 +35,7 @@ extern "C" {
 
 typedef struct nc_ctx nc_ctx;
 
-#define NCGPU_ABI_VERSION 4  /* 4: nc_melodia_salience; 3: tuning decision margins, nc_xcorr_peak */
+#define NCGPU_ABI_VERSION 5  /* 5: nc_pcm16_to_f32; 4: nc_melodia_salience; 3: tuning decision margins, nc_xcorr_peak */
 
 int nc_abi_version(void);
 const char* nc_last_error(void);
@@ -378,6 +378,15 @@ int nc_spectral_stats(nc_ctx* ctx, const float* sig, const int64_t* file_off, co
 int nc_resample_poly(nc_ctx* ctx, const float* x, const int64_t* in_off, const int64_t* in_len, int n_files,
                      float* y, const int64_t* out_off, const int64_t* out_len, int64_t max_out,
                      const double* h, int h_len, int up, int down, int64_t pre_remove, void* stream);
+
+/* -------------------------------------------------------------------------
+ * R1b 16-bit PCM upload — replaces the int16 -> float32 scaling inside
+ *     io.load_audio (io.py:44-55: librosa.load -> soundfile, sample k -> k / 32768)
+ *     for mono 16-bit WAV files: the host uploads the stored 2-byte samples and
+ *     y[i] = x[i] / 32768 (exact in f32) is computed in HBM.  x and y 16-byte
+ *     aligned, n samples.  (ABI 5)
+ * ------------------------------------------------------------------------- */
+int nc_pcm16_to_f32(nc_ctx* ctx, const int16_t* x, int64_t n, float* y, void* stream);
 
 /* -------------------------------------------------------------------------
  * MELODIA front end (opt-in; replaces the frame-level part of essentia's

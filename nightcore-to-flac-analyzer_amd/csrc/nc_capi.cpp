@@ -89,6 +89,7 @@ int launch_spectral(Context& ctx, const float* sig, const int64_t* file_off, con
                     int64_t total_frames, int64_t max_frames, float roll_percent, float* rms_out,
                     double* stats_out, double* bin_db_out, void* ws, size_t ws_bytes, hipStream_t st);
 
+int launch_pcm16_to_f32(const int16_t* x, int64_t n, float* y, hipStream_t st);
 int launch_resample_poly(const float* x, const int64_t* in_off, const int64_t* in_len, int n_files,
                          float* y, const int64_t* out_off, const int64_t* out_len, int64_t max_out,
                          const double* h, int h_len, int up, int down, int64_t pre_remove, hipStream_t st);
@@ -527,6 +528,12 @@ int nc_resample_poly(nc_ctx* ctx, const float* x, const int64_t* in_off, const i
   SET_DEVICE(ctx);
   return nc::launch_resample_poly(x, in_off, in_len, n_files, y, out_off, out_len, max_out, h, h_len, up, down,
                                   pre_remove, (hipStream_t)stream);
+}
+
+int nc_pcm16_to_f32(nc_ctx* ctx, const int16_t* x, int64_t n, float* y, void* stream) {
+  CHECK_CTX(ctx);
+  SET_DEVICE(ctx);
+  return nc::launch_pcm16_to_f32(x, n, y, (hipStream_t)stream);
 }
 
 int nc_melodia_salience(nc_ctx* ctx, const float* sig, const int64_t* file_off, const int64_t* file_len,

@@ -111,4 +111,46 @@ int launch_resample_poly(const float* x, const int64_t* in_off, const int64_t* i
   return 0;
 }
 
+// 16-bit PCM -> f32 (io.load_audio of a mono 16-bit WAV, io.py:44-55: soundfile scales sample k
+// to k / 32768, exact in f32).  The host uploads the file's own 2-byte samples (half the bytes of
+// f32 over PCIe) and this kernel widens them in HBM.  HBM-bound: each thread reads 16 B (8
+// samples) and writes 32 B; a grid-stride loop over the buffer.
+__global__ __launch_bounds__(256) void pcm16_to_f32_kernel(const int16_t* __restrict__ x, int64_t n,
+                                                           float* __restrict__ y) {
+  const int64_t n8 = n >> 3;
+  const float s = 1.0f / 32768.0f;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n8; i += (int64_t)gridDim.x * 256) {
+    const int4 v = reinterpret_cast<const int4*>(x)[i];
+    const int w[4] = {v.x, v.y, v.z, v.w};
+    float4 lo, hi;
+    lo.x = (float)(int16_t)(w[0] & 0xffff) * s;
+    lo.y = (float)(int16_t)(w[0] >> 16) * s;
+    lo.z = (float)(int16_t)(w[1] & 0xffff) * s;
+    lo.w = (float)(int16_t)(w[1] >> 16) * s;
+    hi.x = (float)(int16_t)(w[2] & 0xffff) * s;
+    hi.y = (float)(int16_t)(w[2] >> 16) * s;
+    hi.z = (float)(int16_t)(w[3] & 0xffff) * s;
+    hi.w = (float)(int16_t)(w[3] >> 16) * s;
+    reinterpret_cast<float4*>(y)[2 * i] = lo;
+    reinterpret_cast<float4*>(y)[2 * i + 1] = hi;
+  }
+  if (blockIdx.x == 0 && threadIdx.x < (n & 7)) {
+    const int64_t k = (n8 << 3) + threadIdx.x;
+    y[k] = (float)x[k] * s;
+  }
+}
+
+int launch_pcm16_to_f32(const int16_t* x, int64_t n, float* y, hipStream_t st) {
+  if (n <= 0) return 0;
+  if ((reinterpret_cast<uintptr_t>(x) & 15) || (reinterpret_cast<uintptr_t>(y) & 15)) {
+    set_error("pcm16_to_f32: buffers must be 16-byte aligned");
+    return -2;
+  }
+  const int64_t n8 = n >> 3;
+  const int grid = (int)std::max<int64_t>(1, std::min<int64_t>((n8 + 255) / 256, 256 * 16));
+  hipLaunchKernelGGL(pcm16_to_f32_kernel, dim3(grid), dim3(256), 0, st, x, n, y);
+  NC_HIP(hipGetLastError());
+  return 0;
+}
+
 }  // namespace nc

@@ -248,6 +248,11 @@ class PairOutcome:
     error: Optional[BaseException] = None
     _log_ops: list = field(default_factory=list)
     detail: dict = field(default_factory=dict)
+    # (AsmContext, pair index in it): the inputs assemble_pair read, kept for the window-sharded
+    # result gather (sharded.GatheredOutcomes), which sends them as plain arrays and re-runs
+    # assemble_pair on the receiving rank; the MELODIA hook's (pick, lines) when it ran
+    _asm: Optional[tuple] = field(default=None, repr=False, compare=False)
+    _melodia: Optional[tuple] = field(default=None, repr=False, compare=False)
 
     @property
     def logs(self) -> List[str]:
@@ -261,6 +266,38 @@ class PairOutcome:
                     lines.extend(r) if isinstance(r, list) else lines.append(r)
             self._log_ops[:] = lines        # in place: assemble_pair keeps appending to this list
         return self._log_ops
+
+
+@dataclass(eq=False)
+class AsmContext:
+    """What ``assemble_pair`` reads for the pairs of one group: the group's host result arrays
+    (``h``: the device arena's views, or the split-pair path's record columns), the hop-64 IBI
+    results, and the host plan.  Every outcome keeps a reference to its group's context, so the
+    window-sharded gather can send the context as plain arrays and the receiving rank rebuilds
+    the outcome with the same ``assemble_pair`` call (sharded.GatheredOutcomes)."""
+    h: dict
+    ibi: Optional[dict]
+    starts: list
+    w0: list
+    w1: list
+    f_len: np.ndarray
+    strip_len: np.ndarray
+    lead: np.ndarray
+    trail: np.ndarray
+    intro: list
+    win_n: int
+    pair_chunks: list
+    n_cp: int
+    nj: int
+    n_pitch_jobs: int
+    align: Optional[list]
+
+    def assemble(self, b: int, p: "Params", out: Optional["PairOutcome"] = None, wait=None, span=None) -> "PairOutcome":
+        o = assemble_pair(b, p, self.h, self.ibi, self.starts, self.w0, self.w1, self.f_len, self.strip_len,
+                          self.lead, self.trail, self.intro[b], self.win_n, self.pair_chunks, self.n_cp, self.nj,
+                          self.n_pitch_jobs, self.align[b] if self.align else None, out=out, wait=wait, span=span)
+        o._asm = (self, b)
+        return o
 
 
 @dataclass
@@ -665,17 +702,26 @@ class Engine:
         return [(names[idx[i]], float(st[i]), float(en[i])) for i in range(n.value)]
 
     def upload_signals(self, arrays: Sequence[np.ndarray]) -> DeviceSignals:
+        """The files into one f32 HBM buffer (64-sample aligned offsets).  When every file is
+        16-bit PCM as stored (``io.Pcm16``) the 2-byte samples are uploaded and widened on the
+        device (``nc_pcm16_to_f32``, k / 32768 exactly): half the host -> HBM bytes."""
+        from .io import Pcm16, as_f32
         lens = np.array([len(a) for a in arrays], dtype=np.int64)
         offs = np.zeros(len(arrays), dtype=np.int64)
         tot = 0
         for i, n in enumerate(lens):
             offs[i] = tot
             tot += (int(n) + _ALIGN - 1) // _ALIGN * _ALIGN
-        host = torch.zeros(max(_ALIGN, tot), dtype=torch.float32, pin_memory=True)
+        pcm = bool(arrays) and all(isinstance(a, Pcm16) for a in arrays)
+        host = torch.zeros(max(_ALIGN, tot), dtype=torch.int16 if pcm else torch.float32, pin_memory=True)
         hv = host.numpy()
         for a, o in zip(arrays, offs):
-            hv[o:o + len(a)] = np.asarray(a, dtype=np.float32)
-        buf = host.to(self.dev, non_blocking=True)
+            hv[o:o + len(a)] = a.view(np.ndarray) if pcm else as_f32(a)
+        if not pcm:
+            return DeviceSignals(host.to(self.dev, non_blocking=True), offs, lens)
+        raw = host.to(self.dev, non_blocking=True)
+        buf = torch.empty(raw.numel(), dtype=torch.float32, device=self.dev)
+        self.call("nc_pcm16_to_f32", raw.data_ptr(), raw.numel(), buf.data_ptr(), self.stream())
         return DeviceSignals(buf, offs, lens)
 
     # -------------------------------------------------------------- bootstrap (generic)
@@ -1395,16 +1441,16 @@ class Engine:
         g["starts_l"] = [x.tolist() for x in g["starts"]]
         g["w0"], g["w1"] = g["w0"].tolist(), g["w1"].tolist()
         ibi = {k[4:]: v for k, v in g["host"].items() if k.startswith("ibi_")} if g["has_ibi"] else None
+        ctx = AsmContext(h, ibi, g["starts_l"], g["w0"], g["w1"], g["f_len"], g["strip_len"], g["lead"], g["trail"],
+                         g["intro"], g["win_n"], g["pair_chunks"], g["n_cp"], g["nj"], g["n_pitch_jobs"], g["align"])
         out = []
         for b in range(g["B"]):
             o = PairOutcome()
             wait = None
             if log is not None:
                 wait = _StageWaiter(o, g, h, lambda line, i=g["g0"] + b: log(i, line))
-            assemble_pair(b, g["p"], h, ibi, g["starts_l"], g["w0"], g["w1"], g["f_len"], g["strip_len"], g["lead"],
-                          g["trail"], g["intro"][b], g["win_n"], g["pair_chunks"], g["n_cp"], g["nj"],
-                          g["n_pitch_jobs"], g["align"][b] if g["align"] else None, out=o, wait=wait,
-                          span=(g["g0"] + b, g["spans"][b]) if g.get("spans") else None)
+            ctx.assemble(b, g["p"], out=o, wait=wait,
+                         span=(g["g0"] + b, g["spans"][b]) if g.get("spans") else None)
             if wait is not None:
                 wait.flush()
             out.append(o)
@@ -1615,6 +1661,7 @@ def assemble_pair(b, p: Params, h, ibi, starts, w0, w1, f_len, strip_len, lead, 
         else:
             lines: List[str] = []
             pick = p.melodia(span[0], point_st, lines.append, span[1])   # batch pair index, trimmed spans
+            out._melodia = (pick, list(lines), None)
             for x in lines:
                 L(x)
         method = "chroma+melodia" if pick is not None else "chroma_xcorr"
@@ -1674,7 +1721,10 @@ def assemble_pair(b, p: Params, h, ibi, starts, w0, w1, f_len, strip_len, lead, 
     if p.compute_pitch and method == "chroma+melodia":
         vs, vn = C._valid(src_p), C._valid(nc_p)
         if len(vs) >= C.MIN_VALID and len(vn) >= C.MIN_VALID:
-            pitch_boot = C._bootstrap_ratio(vn, vs)      # consensus.py:550-553 on the MELODIA lists
+            # consensus.py:550-553 on the MELODIA lists (a gathered outcome rebuilt on another
+            # rank replays the owner's answer: sharded._MelodiaReplay)
+            pitch_boot = getattr(p.melodia, "pitch_boot", None) or C._bootstrap_ratio(vn, vs)
+            out._melodia = out._melodia[:2] + (pitch_boot,)
     elif p.compute_pitch:
         pj = len(w0) // 2 + b     # pitch job index: after the B tempo jobs
         bo = h["bout_l"]

@@ -47,11 +47,30 @@ def _rms_db(audio: np.ndarray) -> float:
 _WAVE_PCM, _WAVE_FLOAT, _WAVE_EXTENSIBLE = 1, 3, 0xFFFE
 
 
-def _read_wav(path: Path):
+class Pcm16(np.ndarray):
+    """Mono 16-bit PCM as the file stores it: int16 sample k stands for k / 32768 (soundfile's
+    scaling, exact in float32).  ``load_audio(..., keep_pcm16=True)`` returns one for a mono
+    16-bit WAV at the requested rate; the engine uploads its 2-byte samples (half the host ->
+    HBM bytes of float32) and widens them on the device (``nc_pcm16_to_f32``), so the analysis
+    sees exactly the float32 array ``load_audio`` would have returned.  Slices stay Pcm16."""
+
+    def f32(self) -> np.ndarray:
+        return self.view(np.ndarray).astype(np.float32) / np.float32(32768.0)
+
+
+def as_f32(a) -> np.ndarray:
+    """The float32 samples of ``a``: a Pcm16 scaled by 1 / 32768, anything else as float32."""
+    if isinstance(a, Pcm16):
+        return a.f32()
+    return np.asarray(a, dtype=np.float32)
+
+
+def _read_wav(path: Path, keep_pcm16: bool = False):
     """RIFF/WAVE -> (mono float32, rate): PCM 8 (unsigned) / 16 / 24 / 32-bit and IEEE float
     32 / 64-bit, plain or WAVE_FORMAT_EXTENSIBLE (the sub-format GUID's first two bytes
     carry the format tag), scaled to [-1, 1) as soundfile does and averaged over channels
-    (librosa.load(mono=True))."""
+    (librosa.load(mono=True)).  ``keep_pcm16``: a mono 16-bit PCM file comes back as its
+    stored samples (Pcm16)."""
     data = Path(path).read_bytes()
     if len(data) < 12 or data[:4] not in (b"RIFF", b"RF64") or data[8:12] != b"WAVE":
         raise ValueError(f"{path}: not a RIFF/WAVE file")
@@ -84,6 +103,8 @@ def _read_wav(path: Path):
     elif tag == _WAVE_PCM and width == 1:
         x = (np.frombuffer(raw, np.uint8).astype(np.float32) - 128.0) / 128.0
     elif tag == _WAVE_PCM and width == 2:
+        if keep_pcm16 and ch == 1:
+            return np.frombuffer(raw, "<i2").astype(np.int16).view(Pcm16), sr
         x = np.frombuffer(raw, "<i2").astype(np.float32) / 32768.0
     elif tag == _WAVE_PCM and width == 3:
         b = np.frombuffer(raw, np.uint8).reshape(-1, 3).astype(np.int32)
@@ -97,17 +118,23 @@ def _read_wav(path: Path):
     return x.reshape(-1, ch).mean(axis=1).astype(np.float32), sr
 
 
-def load_audio(path: str, sr: Optional[int] = SAMPLE_RATE) -> tuple[np.ndarray, int]:
+def load_audio(path: str, sr: Optional[int] = SAMPLE_RATE, *, keep_pcm16: bool = False) -> tuple[np.ndarray, int]:
     """Decode *path* to mono float32 at *sr* Hz (io.py:44-55; decode stays on the CPU).
     ``sr=None`` keeps the file's own rate (librosa.load(sr=None), spectral.py:52); a .npy
-    file carries no rate and is taken to be at SAMPLE_RATE."""
+    file carries no rate and is taken to be at SAMPLE_RATE.  ``keep_pcm16`` (the engine's
+    loaders, pipeline.run): a mono 16-bit WAV already at *sr* is returned as its stored
+    samples (``Pcm16``: the same values as float32 once scaled by 1 / 32768, on the device)."""
     p = Path(path)
     if p.suffix.lower() == ".npy":
         y, file_sr = np.load(p, allow_pickle=False).astype(np.float32), sr or SAMPLE_RATE
         if y.ndim > 1:
             y = y.mean(axis=0).astype(np.float32)
     elif p.suffix.lower() == ".wav":
-        y, file_sr = _read_wav(p)
+        y, file_sr = _read_wav(p, keep_pcm16)
+        if isinstance(y, Pcm16):
+            if sr is None or file_sr == sr:
+                return y, file_sr
+            y = y.f32()
     else:
         raise NotImplementedError(
             f"{p.suffix} decoding is outside the engine (the reference uses librosa.load/soundfile, "

@@ -31,11 +31,13 @@ def _params(window_sec, hop_sec, energy_gate_db, silence_strip_db, src_trim_sec,
 
 
 def _load(x: PathOrArray, log, what: str, sr: int = 22050):
+    """A file decoded as load_audio does (a mono 16-bit WAV kept as its stored samples,
+    io.Pcm16, and widened on the device at upload: half the PCIe bytes), or an array."""
     log(f"Loading {what} audio…")
     if isinstance(x, np.ndarray):
         y = np.ascontiguousarray(x, dtype=np.float32)
     else:
-        y, sr = load_audio(x, sr=sr)
+        y, sr = load_audio(x, sr=sr, keep_pcm16=True)
     log(f"  {len(y) / sr:.1f} s  ({len(y):,} samples @ {sr} Hz)")
     return y
 
@@ -76,8 +78,9 @@ def _melodia_hook(pairs):
         return None
 
     def hook(b, chroma_st, log, span):         # b: pair index in `pairs`; span: trimmed (src, nc)
+        from .io import as_f32
         (so, sl), (no, nl) = span
-        nc, src = pairs[b]
+        nc, src = (as_f32(a) for a in pairs[b])
         mel = pitch.estimate_pitch_melodia(src[so:so + sl], nc[no:no + nl], 22050, log=log)
         return pitch.melodia_choice(mel, chroma_st, log)
     return hook

@@ -33,10 +33,12 @@ xGMI before consensus".  SURVEY.md §8(e) lays the split out and this module fol
     3. the owner runs the bootstraps (consensus.py:243-312, pitch.py:143-150), the hop-64
        IBI pass (tempo.py:120-173) and the host assembly (report, warnings, logs).
 * The results of every pair are gathered to every rank (``gather=True``, the API
-  default): each rank pickles its owned outcomes once (log lines still unrendered:
-  ``engine._Lines``), one all-gather moves every rank's bytes to every rank (device tensors
-  over RCCL), and a rank unpickles another rank's outcomes on first access
-  (``GatheredOutcomes``).  The benchmark's N > 1 headline times this default.
+  default) as record tables, no pickle: per pair a fixed-size result row and, per assembly
+  group, the inputs ``assemble_pair`` read (``pack_outcomes``).  One all-gather moves every
+  rank's bytes to every rank (device tensors over RCCL); a rank reads all result rows as one
+  table (``GatheredOutcomes.table``) and rebuilds another rank's whole outcome (report,
+  logs, detail) with the same ``assemble_pair`` call on first access.  The benchmark's N > 1
+  headline times the gather and the table read of every step.
 
 The records are fixed-size f64 rows.  They are assembled on the host from the stage
 results (a few hundred bytes per window), copied to the exchange device on the split-pair
@@ -63,11 +65,10 @@ from __future__ import annotations
 
 import collections.abc
 import contextlib
-import io
 import dataclasses
 import gc
 import math
-import pickle
+import json
 from dataclasses import dataclass
 from typing import Dict, List, Optional, Sequence, Tuple
 
@@ -77,8 +78,8 @@ import torch.distributed as dist
 
 from . import consensus as C
 from .distributed import shard_range
-from .engine import (CHUNK_SEC, HOP_LENGTH, IBI_HOP, MIN_BEATS, MIN_CHUNKS, REF_HZ, SR, DeviceSignals, Engine,
-                     PairOutcome, Params, _Upload, assemble_pair, plan_batch)
+from .engine import (CHUNK_SEC, HOP_LENGTH, IBI_HOP, MIN_BEATS, MIN_CHUNKS, REF_HZ, SR, AsmContext, DeviceSignals,
+                     Engine, PairOutcome, Params, _HostViews, _Upload, plan_batch)
 
 # exchanged window record: exists, energy_db, bpm, nbeats, tempo lag, decision margin
 R_EXISTS, R_ENERGY, R_BPM, R_NBEATS, R_LAG, R_MARGIN = range(6)
@@ -305,19 +306,28 @@ class Exchange:
             out.extend(part)
         return out
 
-    def gather_bytes(self, blob: bytes) -> List[memoryview]:
+    def gather_bytes(self, blob: bytes, failed: Optional[BaseException] = None) -> List[memoryview]:
         """Every rank's byte string, in rank order: one all_gather_into_tensor of the lengths
         and one of the strings padded to the longest (uint8; device tensors under RCCL, on the
-        split-pair stream).  The parts are views of one host buffer: nothing is copied per rank."""
+        split-pair stream).  The parts are views of one host buffer: nothing is copied per rank.
+        Fail together: a rank with ``failed`` sends length -1 instead, and every rank raises
+        after the first collective (that rank its own exception, the others ShardError)."""
         if self.local:
+            if failed is not None:
+                raise failed
             return [memoryview(blob)]
         ctx = torch.cuda.stream(self.stream) if self.dev.type == "cuda" and self.stream is not None \
             else contextlib.nullcontext()
         with ctx:
-            n = torch.tensor([len(blob)], dtype=torch.int64).to(self.dev)
+            n = torch.tensor([-1 if failed is not None else len(blob)], dtype=torch.int64).to(self.dev)
             ns = torch.empty(self.world, dtype=torch.int64, device=self.dev)
             dist.all_gather_into_tensor(ns, n, group=self.group)
             sizes = ns.cpu().tolist()
+            if failed is not None:
+                raise failed
+            bad = [q for q in range(self.world) if sizes[q] < 0]
+            if bad:
+                raise ShardError(f"window-sharded result gather failed on rank(s) {bad}")
             S = max(1, int(max(sizes)))
             mine = np.zeros(S, np.uint8)
             mine[:len(blob)] = np.frombuffer(blob, np.uint8)
@@ -328,67 +338,243 @@ class Exchange:
         return [h[q * S:q * S + int(sizes[q])] for q in range(self.world)]
 
 
-def _rebuild_array(dt: str, shape: tuple, raw: bytes) -> np.ndarray:
-    return np.frombuffer(raw, dtype=dt).reshape(shape).copy()
+# ------------------------------------------------------------------------------ result records
+# The gather of every pair's outcome to every rank (gather=True) sends plain arrays, no pickle:
+# per owned pair a fixed-size result row (RES_FIELDS: the AnalysisResult numbers a caller reads
+# first) and, per assembly group, the inputs assemble_pair read (engine.AsmContext: the group's
+# host result arrays and plan).  A receiving rank reads the result rows as one table
+# (GatheredOutcomes.table) and rebuilds a whole PairOutcome (report text, warnings, logs, detail)
+# with the same assemble_pair call on first access.
+RES_FIELDS = ("ok", "tempo_ratio", "tempo_lo", "tempo_hi", "pitch_ratio", "pitch_lo", "pitch_hi", "ibi_ratio",
+              "ibi_lo", "ibi_hi", "n_source_pitch_windows", "n_nc_pitch_windows", "n_source_tempo_windows",
+              "n_nc_tempo_windows", "nc_duration", "src_duration", "nc_median_bpm", "src_median_bpm",
+              "intro_offset_sec")
+_NAN = float("nan")
 
 
-class _OutcomePickler(pickle.Pickler):
-    """The gather's pickler: numeric ndarrays (the outcomes' detail arrays and deferred log
-    arguments) as (dtype, shape, raw bytes), which pickles a config-3 batch's 64 outcomes in
-    2.9 ms against 3.9 with numpy's own reduce (profiled on the build host)."""
-
-    def reducer_override(self, obj):
-        if type(obj) is np.ndarray and obj.dtype.kind in "fiub":
-            return _rebuild_array, (obj.dtype.str, obj.shape, obj.tobytes())
-        return NotImplemented
+def _opt(v) -> float:
+    return _NAN if v is None else float(v)
 
 
-def _pickle_fast(x) -> bytes:
-    f = io.BytesIO()
-    _OutcomePickler(f, protocol=pickle.HIGHEST_PROTOCOL).dump(x)
-    return f.getvalue()
+def result_row(o: PairOutcome) -> List[float]:
+    """The RES_FIELDS row of one outcome (NaN for None; ok = 0 for an error outcome)."""
+    r = o.result
+    if r is None:
+        return [0.0] + [_NAN] * (len(RES_FIELDS) - 1)
+    ic = r.ibi_ci or (None, None)
+    return [1.0, r.tempo_ratio, r.tempo_ci[0], r.tempo_ci[1], r.pitch_ratio, r.pitch_ci[0], r.pitch_ci[1],
+            _opt(r.ibi_ratio), _opt(ic[0]), _opt(ic[1]), r.n_source_pitch_windows, r.n_nc_pitch_windows,
+            r.n_source_tempo_windows, r.n_nc_tempo_windows, _opt(r.nc_duration), _opt(r.src_duration),
+            _opt(r.nc_median_bpm), _opt(r.src_median_bpm), _opt(r.intro_offset_sec)]
 
 
-def _dumps_outcomes(outs: List[Tuple[int, PairOutcome]]) -> bytes:
-    """A rank's [(pair, outcome)] pickled for the result gather.  An outcome that does not
-    pickle (an exception type that cannot be rebuilt) travels with its error as a
-    RuntimeError of the same text and its log lines rendered."""
-    try:
-        return _pickle_fast(outs)
-    except Exception:                    # noqa: BLE001
-        safe = []
-        for b, o in outs:
-            try:
-                _pickle_fast(o)
-                safe.append((b, o))
-            except Exception:            # noqa: BLE001
-                err = None if o.error is None else RuntimeError(f"{type(o.error).__name__}: {o.error}")
-                safe.append((b, PairOutcome(result=o.result, error=err, _log_ops=list(o.logs))))
-        return _pickle_fast(safe)
+def pack_tables(tables: Dict[str, np.ndarray]) -> bytes:
+    """Named numeric arrays as one byte string: an 8-byte header length, a JSON header (name,
+    dtype, shape, offset of each array) and the raw bytes, each array 8-byte aligned."""
+    meta, chunks, off = [], [], 0
+    for name, a in tables.items():
+        a = np.asarray(a)
+        a = a if a.flags.c_contiguous else a.copy()       # (ascontiguousarray would make 0-d 1-d)
+        if a.dtype.kind not in "biuf":
+            raise TypeError(f"record table {name!r}: dtype {a.dtype} is not numeric")
+        meta.append((name, a.dtype.str, list(a.shape), off))
+        chunks.append(a.tobytes())
+        pad = -a.nbytes % 8
+        if pad:
+            chunks.append(b"\0" * pad)
+        off += a.nbytes + pad
+    head = json.dumps(meta, separators=(",", ":")).encode()
+    head += b" " * (-len(head) % 8)
+    return np.array([len(head)], np.int64).tobytes() + head + b"".join(chunks)
+
+
+def unpack_tables(buf) -> Dict[str, np.ndarray]:
+    """pack_tables' arrays as read-only views of ``buf`` (nothing is copied)."""
+    mv = memoryview(buf)
+    n = int(np.frombuffer(mv[:8], np.int64)[0])
+    base = 8 + n
+    out = {}
+    for name, dt, shape, off in json.loads(bytes(mv[8:base])):
+        dt = np.dtype(dt)
+        cnt = int(np.prod(shape)) if shape else 1
+        out[name] = np.frombuffer(mv, dt, cnt, base + off).reshape(tuple(shape))
+    return out
+
+
+def _list_array(v) -> np.ndarray:
+    a = np.asarray(v)
+    if a.dtype.kind not in "biuf":
+        raise TypeError(f"assembly list of dtype {a.dtype} cannot travel as a record")
+    return a if a.size else np.zeros(0, np.float64)
+
+
+def _ctx_tables(ctx: AsmContext, pre: str, out: Dict[str, np.ndarray]) -> None:
+    """An assembly context as arrays (keys prefixed ``pre``).  Host views: every array, not the
+    derived python lists ("x_l" is rebuilt from "x" by _HostViews) nor the engine's boolean
+    screens; a list with no array behind it (the split-pair path's "clag_l", ...) as its array."""
+    h = ctx.h
+    for k, v in h.items():
+        if k.startswith("ibi_") or isinstance(v, bool):
+            continue
+        if k.endswith("_l"):
+            if k[:-2] not in h:
+                out[pre + "h." + k[:-2]] = _list_array(v)
+            continue
+        out[pre + "h." + k] = np.asarray(v)
+    if ctx.ibi is not None:
+        for k, v in ctx.ibi.items():
+            out[pre + "i." + k] = np.asarray(v)
+    starts = [np.asarray(s, np.int64) for s in ctx.starts]
+    out[pre + "starts"] = np.concatenate(starts) if starts else np.zeros(0, np.int64)
+    out[pre + "starts_n"] = np.array([len(s) for s in starts], np.int64)
+    out[pre + "w0"] = np.asarray(ctx.w0, np.int64)
+    out[pre + "w1"] = np.asarray(ctx.w1, np.int64)
+    for k in ("f_len", "strip_len", "lead", "trail"):
+        out[pre + k] = np.asarray(getattr(ctx, k))
+    out[pre + "intro"] = np.array([_opt(v) for v in ctx.intro], np.float64)
+    out[pre + "intro_none"] = np.array([v is None for v in ctx.intro], np.bool_)
+    if ctx.align is not None:
+        out[pre + "align"] = np.array([(_NAN, _NAN) if a is None else a for a in ctx.align], np.float64).reshape(-1, 2)
+        out[pre + "align_none"] = np.array([a is None for a in ctx.align], np.bool_)
+    out[pre + "chunks"] = np.array(ctx.pair_chunks, np.int64).reshape(-1, 2)
+    out[pre + "scal"] = np.array([ctx.win_n, ctx.n_cp, ctx.nj, ctx.n_pitch_jobs, ctx.ibi is not None], np.int64)
+
+
+def _ctx_from_tables(t: Dict[str, np.ndarray], pre: str) -> AsmContext:
+    """_ctx_tables' inverse: the same values, types and python lists assemble_pair reads."""
+    n = len(pre)
+    h = _HostViews({k[n + 2:]: v for k, v in t.items() if k.startswith(pre + "h.")})
+    win_n, n_cp, nj, n_pj, has_ibi = t[pre + "scal"].tolist()
+    ibi = {k[n + 2:]: v for k, v in t.items() if k.startswith(pre + "i.")} if has_ibi else None
+    flat, cnt = t[pre + "starts"].tolist(), t[pre + "starts_n"].tolist()
+    starts, o = [], 0
+    for c in cnt:
+        starts.append(flat[o:o + c])
+        o += c
+    intro = [None if none else v for v, none in zip(t[pre + "intro"].tolist(), t[pre + "intro_none"].tolist())]
+    align = None
+    if pre + "align" in t:
+        align = [None if none else tuple(a) for a, none in zip(t[pre + "align"].tolist(), t[pre + "align_none"].tolist())]
+    chunks = [tuple(c) for c in t[pre + "chunks"].tolist()]
+    return AsmContext(h, ibi, starts, t[pre + "w0"].tolist(), t[pre + "w1"].tolist(), t[pre + "f_len"],
+                      t[pre + "strip_len"], t[pre + "lead"], t[pre + "trail"], intro, win_n, chunks, n_cp, nj, n_pj,
+                      align)
+
+
+def _melodia_tables(rec, pre: str, out: Dict[str, np.ndarray]) -> None:
+    """The MELODIA hook's answer on the owner (engine.assemble_pair): its (src, nc) Hz lists or
+    None, its log lines, and the bootstrap of the accepted lists."""
+    pick, lines, boot = rec
+    out[pre + "lines"] = np.frombuffer("\0".join(lines).encode(), np.uint8)
+    out[pre + "nlines"] = np.array([len(lines)], np.int64)
+    if pick is not None:
+        for side, vals in zip(("src", "nc"), pick):
+            out[pre + side] = np.array([_opt(v) for v in vals], np.float64)
+            out[pre + side + "_none"] = np.array([v is None for v in vals], np.bool_)
+    if boot is not None:
+        out[pre + "boot"] = np.array([boot[0], boot[1][0], boot[1][1]], np.float64)
+
+
+class _MelodiaReplay:
+    """The receiving rank's MELODIA hook: the owner's lines and answer, and its bootstrap."""
+
+    def __init__(self, t: Dict[str, np.ndarray], pre: str):
+        self.lines = bytes(t[pre + "lines"]).decode().split("\0") if int(t[pre + "nlines"][0]) else []
+        self.pick = None
+        if pre + "src" in t:
+            self.pick = tuple([None if none else v for v, none in zip(t[pre + s].tolist(),
+                                                                      t[pre + s + "_none"].tolist())]
+                              for s in ("src", "nc"))
+        self.pitch_boot = None
+        if pre + "boot" in t:
+            pt, lo, hi = t[pre + "boot"].tolist()
+            self.pitch_boot = (pt, (lo, hi))
+
+    def __call__(self, _b, _point_st, log, _span):
+        for x in self.lines:
+            log(x)
+        return self.pick
+
+
+def pack_outcomes(outs: List[Tuple[int, PairOutcome]]) -> bytes:
+    """A rank's owned [(global pair index, outcome)] of one step as record tables: "pairs"
+    (pair, context, index in the context), "res" (RES_FIELDS rows), each distinct assembly
+    context once ("c<k>.…") and the MELODIA hook's recorded answer where it ran ("m<i>.…")."""
+    ctx_id: Dict[int, int] = {}
+    tables: Dict[str, np.ndarray] = {}
+    rows, res = [], []
+    for i, (b, o) in enumerate(outs):
+        if o._asm is None:
+            if o != PairOutcome():
+                raise ValueError(f"pair {b}'s outcome was not built by assemble_pair: it cannot travel as records")
+            rows.append((b, -1, 0))            # an empty outcome (nothing to rebuild)
+            res.append(result_row(o))
+            continue
+        ctx, j = o._asm
+        k = ctx_id.get(id(ctx))
+        if k is None:
+            k = ctx_id[id(ctx)] = len(ctx_id)
+            _ctx_tables(ctx, f"c{k}.", tables)
+        rows.append((b, k, j))
+        res.append(result_row(o))
+        if o._melodia is not None:
+            _melodia_tables(o._melodia, f"m{i}.", tables)
+    tables["pairs"] = np.array(rows, np.int64).reshape(-1, 3)
+    tables["res"] = np.array(res, np.float64).reshape(-1, len(RES_FIELDS))
+    return pack_tables(tables)
+
+
+class _Part:
+    """One rank's record tables of one step, parsed on first use."""
+    __slots__ = ("raw", "t", "ctx", "where")
+
+    def __init__(self, raw):
+        self.raw, self.t, self.ctx, self.where = raw, None, {}, None
+
+    def tables(self) -> Dict[str, np.ndarray]:
+        if self.t is None:
+            self.t = unpack_tables(self.raw)
+            self.where = {int(b): i for i, b in enumerate(self.t["pairs"][:, 0].tolist())}
+        return self.t
+
+    def outcome(self, b: int, p: Params) -> Optional[PairOutcome]:
+        t = self.tables()
+        i = self.where.get(b)
+        if i is None:
+            return None
+        _, k, j = t["pairs"][i].tolist()
+        if k < 0:
+            return PairOutcome()
+        ctx = self.ctx.get(k)
+        if ctx is None:
+            ctx = self.ctx[k] = _ctx_from_tables(t, f"c{k}.")
+        span, q = None, p
+        if f"m{i}.nlines" in t:        # replay the owner's MELODIA answer and lines
+            q, span = dataclasses.replace(p, melodia=_MelodiaReplay(t, f"m{i}.")), (b, None)
+        elif p.melodia is not None:
+            q = dataclasses.replace(p, melodia=None)
+        return ctx.assemble(j, q, span=span)
 
 
 class GatheredOutcomes(collections.abc.Sequence):
     """Every pair's outcome on every rank, in pair order (``analyze_sharded`` with
-    ``gather=True``).  This rank's own outcomes are the objects it assembled; the other
-    ranks' arrived as the bytes of one all-gather (``Exchange.gather_bytes``) and are
-    unpickled a rank at a time, on the first access to one of its pairs (a config-4 step:
-    64 pairs per rank, about a millisecond each).  Indexing, slicing, iteration, ``len`` and
+    ``gather=True``).  This rank's own outcomes are the objects it assembled; the other ranks'
+    arrived as record tables (``pack_outcomes``, one byte all-gather per call) and are rebuilt by
+    assemble_pair on first access to one of their pairs.  ``table()`` returns every pair's
+    RES_FIELDS row without rebuilding anything.  Indexing, slicing, iteration, ``len`` and
     comparison with a list behave as on the list of outcomes."""
 
     def __init__(self, n: int, owner: np.ndarray, own: Sequence[Tuple[int, PairOutcome]],
-                 parts: Dict[int, memoryview]):
+                 parts: Dict[int, memoryview], p: Optional[Params] = None):
         self._n = int(n)
         self._owner = np.asarray(owner)
         self._items: Dict[int, PairOutcome] = dict(own)
-        self._parts = dict(parts)
+        self._parts = {q: _Part(v) for q, v in parts.items()}
+        self._p = p or Params()
+        self._table = None
 
     def __len__(self) -> int:
         return self._n
-
-    def _load(self, q: int) -> None:
-        part = self._parts.pop(q, None)
-        if part is not None:
-            self._items.update(pickle.loads(part))
 
     def __getitem__(self, i):
         if isinstance(i, slice):
@@ -400,10 +586,11 @@ class GatheredOutcomes(collections.abc.Sequence):
             raise IndexError("pair index out of range")
         o = self._items.get(i)
         if o is None:
-            self._load(int(self._owner[i]))
-            o = self._items.get(i)
+            part = self._parts.get(int(self._owner[i]))
+            o = part.outcome(i, self._p) if part is not None else None
             if o is None:
                 raise ShardError(f"pair {i} is missing from rank {int(self._owner[i])}'s gathered outcomes")
+            self._items[i] = o
         return o
 
     def __iter__(self):
@@ -413,12 +600,26 @@ class GatheredOutcomes(collections.abc.Sequence):
     def __eq__(self, other):
         return isinstance(other, collections.abc.Sequence) and list(self) == list(other)
 
+    def table(self) -> np.ndarray:
+        """[pair][RES_FIELDS] f64 (NaN for None): the other ranks' rows straight from their
+        records, this rank's from its own outcomes."""
+        if self._table is None:
+            tab = np.full((self._n, len(RES_FIELDS)), np.nan)
+            for part in self._parts.values():
+                t = part.tables()
+                tab[t["pairs"][:, 0]] = t["res"]
+            own = [(b, o) for b, o in self._items.items() if int(self._owner[b]) not in self._parts]
+            if own:
+                tab[[b for b, _ in own]] = [result_row(o) for _, o in own]
+            self._table = tab
+        return self._table
+
     def decoded(self) -> int:
-        """How many of the other ranks' parts are still bytes (diagnostics)."""
-        return len(self._parts)
+        """How many pairs are still only records (diagnostics)."""
+        return self._n - len(self._items)
 
     def __repr__(self) -> str:
-        return f"GatheredOutcomes({self._n} pairs, {len(self._parts)} rank part(s) not yet unpickled)"
+        return f"GatheredOutcomes({self._n} pairs, {self.decoded()} not yet rebuilt from records)"
 
 
 # Fault-injection points of the fail-together tests (tests/test_sharded_cpu.py): host-only
@@ -849,13 +1050,14 @@ def _analyze_sharded(stages, p, group, lengths, local_pairs, split_offset, gathe
     elif ex.local:
         result = [[o for _, o in outs] for outs in per_step]
     else:
-        # every rank's owned outcomes to every rank: one byte all-gather for the call's steps
-        # (the log lines travel unrendered, engine._Lines; a rank's part is its steps' blobs
-        # behind a table of their lengths); the others' parts unpickled on access
-        blobs = [_dumps_outcomes(outs) for outs in per_step]
-        parts = ex.gather_bytes(_pack_steps(blobs))
+        # every rank's owned outcomes to every rank as record tables (pack_outcomes: result rows
+        # and the assembly inputs, plain arrays): one byte all-gather for the call's steps (a
+        # rank's part is its steps' blobs behind a table of their lengths); the other ranks'
+        # outcomes rebuilt by assemble_pair on access, their result rows readable at once
+        blobs, err = _try(lambda: _pack_steps([pack_outcomes(outs) for outs in per_step]))
+        parts = ex.gather_bytes(blobs or b"", err)          # a packing error raises on every rank
         mine = {q: _unpack_steps(parts[q], len(per_step)) for q in range(world) if q != r}
-        result = [GatheredOutcomes(sp.B, sp.owner, outs, {q: mine[q][k] for q in mine})
+        result = [GatheredOutcomes(sp.B, sp.owner, outs, {q: mine[q][k] for q in mine}, p)
                   for k, outs in enumerate(per_step)]
     return result[0] if steps == 1 else result
 
@@ -1219,10 +1421,9 @@ def _consensus(stages, p: Params, pl, align, active, energy, full, prior, cps, o
         rel = lambda f: (int(pl.f_off[f] - stages.off[f]), int(pl.f_len[f]))
         return (index[b] if index is not None else b, (rel(fs), rel(fn)))
 
-    return [assemble_pair(b, p, h, ibi, starts_l, w0l, w1l, pl.f_len, pl.strip_len, pl.lead, pl.trail,
-                          pl.intro[b], pl.win_n, pl.pair_chunks, n_cp, nj, n_pj, align[b] if align else None,
-                          span=span(b))
-            for b in owned]
+    ctx = AsmContext(h, ibi, starts_l, w0l, w1l, pl.f_len, pl.strip_len, pl.lead, pl.trail, list(pl.intro),
+                     pl.win_n, pl.pair_chunks, n_cp, nj, n_pj, align)
+    return [ctx.assemble(b, p, span=span(b)) for b in owned]
 
 
 def run_window_sharded(pairs: Sequence[Tuple[np.ndarray, np.ndarray]], p: Optional[Params] = None,
@@ -1237,7 +1438,8 @@ def run_window_sharded(pairs: Sequence[Tuple[np.ndarray, np.ndarray]], p: Option
     rank = dist.get_rank(group) if dist.is_available() and dist.is_initialized() else 0
     lengths = [len(a) for nc, src in pairs for a in (nc, src)]
     touched = shard_plan(lengths, p, world, split_offset).needed(rank, p.compute_ibi and world > 1)
-    flat = [np.asarray(a, np.float32) for b in touched for a in pairs[b]]
+    from .io import Pcm16
+    flat = [a if isinstance(a, Pcm16) else np.asarray(a, np.float32) for b in touched for a in pairs[b]]
     sig = eng.upload_signals(flat) if flat else DeviceSignals(torch.zeros(64, device=eng.dev),
                                                              np.zeros(0, np.int64), np.zeros(0, np.int64))
     return analyze_sharded(DeviceStages(eng, sig), p, group, lengths=lengths, local_pairs=touched,

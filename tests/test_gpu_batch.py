@@ -75,9 +75,10 @@ def oracle_pool(seeds, reserve: int = 2):
     return pool, pool.map_async(_oracle, list(seeds), chunksize=1)
 
 
-def check_against_oracle(o: E.PairOutcome, pair, ref: dict, tag=""):
-    """One outcome of Params(compute_ibi=False) against refglue.run_arrays of the same pair:
-    tempo lists, chunk lags, nc prior, ratios, CIs, classification, counts, exact duration ratio."""
+def check_against_oracle(o: E.PairOutcome, pair, ref: dict, tag="", ibi: bool = False):
+    """One outcome against refglue.run_arrays of the same pair: tempo lists, chunk lags, nc
+    prior, ratios, CIs, classification, counts, exact duration ratio; with ``ibi`` (outcomes of
+    run()'s defaults) also the hop-64 IBI ratio and its CI."""
     assert o.error is None, (tag, o.error)
     r, d = o.result, o.detail
     assert r.src_tempos_raw == ref["src_tempos"] and r.nc_tempos_raw == ref["nc_tempos"], tag
@@ -89,6 +90,10 @@ def check_against_oracle(o: E.PairOutcome, pair, ref: dict, tag=""):
     assert tuple(r.tempo_ci) == tuple(ref["tempo_ci"]) and tuple(r.pitch_ci) == tuple(ref["pitch_ci"]), tag
     nc, src = pair
     assert r.src_duration / r.nc_duration == len(src) / len(nc)          # exact sample-count ratio
+    if ibi:
+        assert r.ibi_ratio == ref["ibi_ratio"], (tag, "ibi_ratio", r.ibi_ratio, ref["ibi_ratio"])
+        assert (None if r.ibi_ci is None else tuple(r.ibi_ci)) == \
+            (None if ref["ibi_ci"] is None else tuple(ref["ibi_ci"])), (tag, "ibi_ci")
 
 
 @pytest.fixture(scope="module")

@@ -15,8 +15,11 @@ exchanges):
   outcomes, so every rank holds all 512 (the same list on every rank, checked by digest).
 
 Every rank compares each outcome it owns with ``Engine.analyze`` of the same pairs on
-that rank alone, field for field (results, report text, logs, per-window detail), and
-the owners of pairs 0 and 511 compare them with the CPU oracle (refglue.run_arrays).
+that rank alone, field for field (results, report text, logs, per-window detail).  Against
+the CPU oracle (refglue.run_arrays): the owners of pairs 0 and 511 at split_offset 0, and
+the owners of the 7 cut pairs at split_offset 0.5, whose windows, chunk pairs and hop-64
+IBI pass were split over two ranks and exchanged (IBI ratio and CI included; VERDICT r5
+item 5).
 """
 import dataclasses
 import hashlib
@@ -101,18 +104,23 @@ def _worker(rank, world, port, q):
                                split=int(sp.split.sum()), split_owned=[b for b in owned if sp.split[b]],
                                n_all=n_all, digest=digest))
             if off == 0.0:
-                keep = {b: o for b, o in got if b in ORACLE_PAIRS}
+                keep = {b: (o, False) for b, o in got if b in ORACLE_PAIRS}
+            else:                                          # the cut pairs this rank owns
+                keep.update({b: (o, True) for b, o in got if sp.split[b]})
             print(f"[config4 rank {rank}] split_offset {off}: {len(got)} owned, {len(mism)} mismatches", flush=True)
             del sig
         oracle = []
-        for b, o in keep.items():                          # the owners of pairs 0 and 511
+        for b, (o, ibi) in keep.items():                   # pairs 0 and 511; the cut pairs with IBI
             from oracle import refglue
             nc, src = arrays[b]
             try:
-                check_against_oracle(o, (nc, src), refglue.run_arrays(nc, src, compute_ibi=False), tag=f"pair {b}")
-                oracle.append((b, None))
+                check_against_oracle(o, (nc, src), refglue.run_arrays(nc, src, compute_ibi=ibi), tag=f"pair {b}",
+                                     ibi=ibi)
+                oracle.append((b, ibi, None))
             except AssertionError as exc:
-                oracle.append((b, repr(exc)))
+                oracle.append((b, ibi, repr(exc)))
+            print(f"[config4 rank {rank}] pair {b} against the oracle (ibi {ibi}): "
+                  f"{'ok' if oracle[-1][2] is None else 'MISMATCH'}", flush=True)
         q.put((rank, dict(cases=report, oracle=oracle)))
     except Exception as exc:          # noqa: BLE001
         import traceback
@@ -153,9 +161,9 @@ def test_config4_512_pairs_eight_ranks_equal_engine():
             assert not c["mism"], (r, c["off"], c["mism"])
             owned_all[c["off"]] += c["owned"]
             split_all[c["off"]] += c["split_owned"]
-        for b, err in res[r]["oracle"]:
+        for b, ibi, err in res[r]["oracle"]:
             assert err is None, (r, b, err)
-            oracle_seen.append(b)
+            oracle_seen.append((b, ibi))
     for off, _ in CASES:
         assert sorted(owned_all[off]) == list(range(N_PAIRS)), off       # every pair owned exactly once
     # gather=True (split_offset 0.5): every rank holds all 512 outcomes, the same list on every rank
@@ -164,4 +172,6 @@ def test_config4_512_pairs_eight_ranks_equal_engine():
     assert [c["n_all"] for c in gathered] == [N_PAIRS] * WORLD
     assert len({c["digest"] for c in gathered}) == 1
     assert split_all[0.0] == [] and len(split_all[0.5]) == WORLD - 1       # 0: no exchange; 0.5: 7 cut pairs
-    assert sorted(oracle_seen) == list(ORACLE_PAIRS)
+    # pairs 0 and 511 (interior, split_offset 0) and the 7 cut pairs of split_offset 0.5 (IBI on)
+    assert sorted(b for b, ibi in oracle_seen if not ibi) == list(ORACLE_PAIRS)
+    assert sorted(b for b, ibi in oracle_seen if ibi) == sorted(split_all[0.5])

@@ -45,7 +45,7 @@ def test_abi_version_and_loud_failure_without_device():
         pytest.skip("libncgpu.so not built")
     import torch
     lib = _native.load()
-    assert lib.nc_abi_version() == 4
+    assert lib.nc_abi_version() == 5
     if torch.cuda.is_available():
         pytest.skip("a device is visible; the no-device path is exercised on CPU hosts")
     with pytest.raises(_native.NativeUnavailable):

@@ -72,3 +72,39 @@ def test_not_a_wav(tmp_path):
     p.write_bytes(b"fLaC\x00\x00\x00\x22")
     with pytest.raises(ValueError):
         nio._read_wav(p)
+
+
+@pytest.mark.parametrize("extensible", [False, True])
+def test_keep_pcm16_returns_the_stored_samples(tmp_path, extensible):
+    """load_audio(keep_pcm16=True) on a mono 16-bit WAV at the requested rate: the stored
+    samples (io.Pcm16), whose float32 view is exactly what load_audio returns by default (the
+    engine uploads the 2-byte samples and widens them on the device, nc_pcm16_to_f32)."""
+    x = np.random.default_rng(7).integers(-32768, 32768, size=(5000, 1))
+    x[:4, 0] = [-32768, 32767, 0, -1]
+    f = tmp_path / "m16.wav"
+    f.write_bytes(_wav_bytes(x, 16, 22050, extensible))
+    y, sr = nio.load_audio(str(f), keep_pcm16=True)
+    ref, sr0 = nio.load_audio(str(f))
+    assert isinstance(y, nio.Pcm16) and y.dtype == np.int16 and sr == sr0 == 22050
+    assert np.array_equal(y.view(np.ndarray), x[:, 0].astype(np.int16))
+    f32 = nio.as_f32(y)
+    assert f32.dtype == np.float32 and np.array_equal(f32, ref) and not isinstance(f32, nio.Pcm16)
+    assert isinstance(y[10:20], nio.Pcm16) and np.array_equal(nio.as_f32(y[10:20]), ref[10:20])
+    assert np.array_equal(nio.as_f32(ref), ref)
+
+
+def test_keep_pcm16_only_for_mono_16bit_at_the_rate(tmp_path):
+    """Stereo, other widths and files that need the load-time resample stay float32."""
+    rng = np.random.default_rng(8)
+    st = tmp_path / "s16.wav"
+    st.write_bytes(_wav_bytes(rng.integers(-32768, 32768, size=(800, 2)), 16, 22050, False))
+    m24 = tmp_path / "m24.wav"
+    m24.write_bytes(_wav_bytes(rng.integers(-(1 << 23), 1 << 23, size=(800, 1)), 24, 22050, False))
+    for f in (st, m24):
+        y, _ = nio.load_audio(str(f), keep_pcm16=True)
+        assert type(y) is np.ndarray and y.dtype == np.float32
+        assert np.array_equal(y, nio.load_audio(str(f))[0])
+    m16 = tmp_path / "m16_48k.wav"
+    m16.write_bytes(_wav_bytes(rng.integers(-32768, 32768, size=(800, 1)), 16, 48000, False))
+    y, sr = nio.load_audio(str(m16), sr=None, keep_pcm16=True)     # its own rate: kept
+    assert isinstance(y, nio.Pcm16) and sr == 48000

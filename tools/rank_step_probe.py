@@ -1,8 +1,11 @@
 #!/usr/bin/env python3
 """One rank's share of the N > 1 window-sharded step, measured on the box's one GPU: a one-rank
-"nccl" (RCCL) group with sharded.Exchange.collect_at_one, so the step's outcome gather (pickle +
-byte all-gather) runs as on every rank of an 8-GPU job, against the same step without the
-gather and against Engine.analyze_batches (the N = 1 headline).  Rotated, minimum per variant.
+"nccl" (RCCL) group with sharded.Exchange.collect_at_one, so the step's outcome gather (record
+tables + byte all-gather + the caller's read of every result row) runs as on every rank of an
+8-GPU job, against the same step without the gather and against Engine.analyze_batches (the
+N = 1 headline).  Rotated, minimum per variant.  Then the receive side of an 8-GPU rank: the
+other seven ranks' parts (here: this rank's own records, seven times) read as result tables,
+and the cost of rebuilding a whole outcome from the records (assemble_pair) per pair.
 usage: tools/rank_step_probe.py [K] [ROUNDS]"""
 import os
 import socket
@@ -38,7 +41,11 @@ def main():
     params = E.Params(compute_ibi=False)
 
     def windows(gather):
-        return S.analyze_sharded(S.DeviceStages(eng, sig), params, lengths=lengths, gather=gather, steps=K)
+        res = S.analyze_sharded(S.DeviceStages(eng, sig), params, lengths=lengths, gather=gather, steps=K)
+        if gather:
+            for r in res:
+                r.table()                   # the caller's read of every pair's result row
+        return res
 
     variants = {"analyze_batches": lambda: eng.analyze_batches([sig] * K, params),
                 "windows_gather": lambda: windows(True),
@@ -72,7 +79,7 @@ def main():
         setattr(owner, name, w)
         return f
 
-    saved = [(S, "_dumps_outcomes", timed(S, "_dumps_outcomes")),
+    saved = [(S, "pack_outcomes", timed(S, "pack_outcomes")),
              (S.Exchange, "gather_bytes", timed(S.Exchange, "gather_bytes"))]
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -83,6 +90,33 @@ def main():
         setattr(owner, name, f)
     print(f"windows_gather (parts timed) {tot:.3f} ms/step; per step: " +
           ", ".join(f"{k} {v[1] / K * 1e3:.3f} ms ({v[0] / K:.1f} calls)" for k, v in acc.items()), flush=True)
+    # the receive side of one rank of an 8-GPU job: 7 parts of 64 pairs per step read as tables
+    own = windows(False)
+    blobs = [S.pack_outcomes(outs) for outs in own]
+    import numpy as np
+    B = 8 * 64
+    owner = np.repeat(np.arange(8), 64)
+    t0 = time.perf_counter()
+    for k in range(K):
+        parts = {q: memoryview(blobs[k]) for q in range(1, 8)}
+        g = S.GatheredOutcomes(B, owner, [], parts, params)
+        # rank q's part holds pairs 0..63 of its own numbering: shift to the global indices
+        for q, part in g._parts.items():
+            t = part.tables()
+            t["pairs"] = t["pairs"].copy()
+            t["pairs"][:, 0] += 64 * q
+            part.where = {int(b): i for i, b in enumerate(t["pairs"][:, 0].tolist())}
+        tab = g.table()
+    rx = (time.perf_counter() - t0) / K * 1e3
+    t0 = time.perf_counter()
+    n = 0
+    for b in range(64, 128):
+        g[b]
+        n += 1
+    rb = (time.perf_counter() - t0) / n * 1e3
+    print(f"receive (7 parts x 64 pairs as result tables): {rx:.3f} ms/step; {np.isnan(tab[64:, 1]).sum()} missing "
+          f"rows; whole-outcome rebuild from records: {rb:.3f} ms per pair; "
+          f"blob {len(blobs[0]) / 1024:.1f} KiB per rank-step", flush=True)
     dist.destroy_process_group()
 
 
