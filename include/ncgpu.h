@@ -92,6 +92,16 @@ int nc_trim_bounds(nc_ctx* ctx, const float* sig, const int64_t* file_off, const
                    int n_files, int64_t max_frames, float top_db, int64_t* out_start,
                    int64_t* out_end, void* ws, size_t ws_bytes, void* stream);
 
+/* K1b' window energies from a finished nc_trim_bounds workspace (ABI 5) — replaces
+ * io._rms_db (io.py:38-40) for windows of the trimmed files: window w of file
+ * win_file[w] (an index into that trim call's files, whose untrimmed offsets are
+ * file_off) at sig + win_off[w], win_len samples; energy_out[w] = RMS dB (f64) from
+ * the trim's f64 512-sample block sums plus the partial blocks at the window ends.
+ * The per-window stage then runs with energy_out = NULL (no per-frame energy). */
+int nc_window_energy_blocks(nc_ctx* ctx, const float* sig, const void* trim_ws, int n_files, const int64_t* file_off,
+                            const int64_t* win_off, const int* win_file, int n_win, int win_len, double* energy_out,
+                            void* stream);
+
 /* ---------------------------------------------------------------------------
  * K1b+K2..K5  per-window stage — replaces io._rms_db (io.py:38-40) and, inside
  * tempo.estimate_tempo (tempo.py:27-77), librosa.onset.onset_strength
@@ -100,7 +110,8 @@ int nc_trim_bounds(nc_ctx* ctx, const float* sig, const int64_t* file_off, const
  * Window w = win_len samples at sig + win_off[w] (hop must be 512).
  * Outputs: onset_out[w*T + t] (T = 1 + win_len/512), tg_out[w*acw + k]
  * (acw = 344: mean over frames of the inf-normalised tempogram),
- * energy_out[w] (RMS dB, float64).  `active` (nullable) skips windows.
+ * energy_out[w] (RMS dB, float64; nullable since ABI 5: then no energy is computed,
+ * nc_window_energy_blocks gives it from the trim).  `active` (nullable) skips windows.
  * ------------------------------------------------------------------------- */
 size_t nc_window_stage_workspace_bytes(const nc_ctx* ctx, int n_win, int win_len, int hop);
 int nc_window_stage(nc_ctx* ctx, const float* sig, const int64_t* win_off, const uint8_t* active,

@@ -1109,11 +1109,20 @@ struct C2 {
   }
 };
 
-// vmcnt(younger(q, last)): retires this wave's pieces of slice n (this step's slot)
+// vmcnt(younger(q, last)): retires this wave's pieces of slice n (this step's slot).
+// C2_SAFE_=1 (probe): vmcnt(0) wherever a block load is younger than the slice
+#ifndef C2_SAFE_
+#define C2_SAFE_ 0
+#endif
 template <int OCT, int Q>
 __device__ __forceinline__ void c2_wait_slice(bool last) {
-  if (last) c2_vmwait<C2<OCT>::younger(Q, true)>();
-  else c2_vmwait<C2<OCT>::younger(Q, false)>();
+  if (C2_SAFE_) {
+    if (last) c2_vmwait<C2<OCT>::staged(Q, 1, true) ? 0 : C2<OCT>::younger(Q, true)>();
+    else c2_vmwait<C2<OCT>::staged(Q, 1, false) ? 0 : C2<OCT>::younger(Q, false)>();
+  } else {
+    if (last) c2_vmwait<C2<OCT>::younger(Q, true)>();
+    else c2_vmwait<C2<OCT>::younger(Q, false)>();
+  }
 }
 
 // Block g of this wave's tile into registers: 8-sample unit u = 64 k + lane is row min(u / 4,
@@ -1577,7 +1586,7 @@ int launch_chroma_mean(Context& ctx, const float* sig, const int64_t* chunk_off,
   {
     const size_t lds = (((TpTw::size + 1) & ~1) + 1024 + (size_t)TP_WAVES * LdsSize<1024>::value) * sizeof(float2);
     const int64_t groups = (pa.total_tframes + TP_WAVES - 1) / TP_WAVES;
-    const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(groups, ctx.num_cu));
+    const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(groups, ctx.chroma_cus > 0 ? ctx.chroma_cus : ctx.num_cu));
     {
       KTimer kt_(ctx, "tuning_peaks", st);
       pa.span = kt_.span();

@@ -1,4 +1,5 @@
 // nc_capi.cpp — extern "C" entry points of libncgpu.so (declared in include/ncgpu.h).
+#include <cstdlib>
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -90,6 +91,9 @@ int launch_spectral(Context& ctx, const float* sig, const int64_t* file_off, con
                     double* stats_out, double* bin_db_out, void* ws, size_t ws_bytes, hipStream_t st);
 
 int launch_pcm16_to_f32(const int16_t* x, int64_t n, float* y, hipStream_t st);
+int launch_window_energy_blocks(const float* sig, const void* trim_ws, int n_files, const int64_t* file_off,
+                                const int64_t* win_off, const int* win_file, int n_win, int win_len, double* out,
+                                hipStream_t st);
 int launch_resample_poly(const float* x, const int64_t* in_off, const int64_t* in_len, int n_files,
                          float* y, const int64_t* out_off, const int64_t* out_len, int64_t max_out,
                          const double* h, int h_len, int up, int down, int64_t pre_remove, hipStream_t st);
@@ -150,6 +154,8 @@ int nc_create(int device, nc_ctx** out) {
   int cu = 0;
   if (hipDeviceGetAttribute(&cu, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && cu > 0)
     c->c.num_cu = cu;
+  if (const char* v = std::getenv("NC_STFT_CUS")) c->c.stft_cus = std::max(0, std::atoi(v));
+  if (const char* v = std::getenv("NC_CHROMA_CUS")) c->c.chroma_cus = std::max(0, std::atoi(v));
   nc::build_tables(c->c);
   if (!c->c.t.tw || !c->c.t.cqt_w || !c->c.t.halfband) {
     nc::free_tables(c->c);
@@ -528,6 +534,15 @@ int nc_resample_poly(nc_ctx* ctx, const float* x, const int64_t* in_off, const i
   SET_DEVICE(ctx);
   return nc::launch_resample_poly(x, in_off, in_len, n_files, y, out_off, out_len, max_out, h, h_len, up, down,
                                   pre_remove, (hipStream_t)stream);
+}
+
+int nc_window_energy_blocks(nc_ctx* ctx, const float* sig, const void* trim_ws, int n_files, const int64_t* file_off,
+                            const int64_t* win_off, const int* win_file, int n_win, int win_len, double* energy_out,
+                            void* stream) {
+  CHECK_CTX(ctx);
+  SET_DEVICE(ctx);
+  return nc::launch_window_energy_blocks(sig, trim_ws, n_files, file_off, win_off, win_file, n_win, win_len,
+                                         energy_out, (hipStream_t)stream);
 }
 
 int nc_pcm16_to_f32(nc_ctx* ctx, const int16_t* x, int64_t n, float* y, void* stream) {

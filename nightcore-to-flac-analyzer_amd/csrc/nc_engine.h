@@ -67,6 +67,10 @@ struct KernelTimers;  // nc_prof.cpp
 struct Context {
   int device = 0;
   int num_cu = 256;
+  // persistent grids of the window chain's STFT and the chroma chain's tuning FFT (0: num_cu).
+  // Measurement knobs (NC_STFT_CUS / NC_CHROMA_CUS at nc_create) for CU-masked streams: a
+  // persistent kernel sized to the CUs its stream may use (round 6)
+  int stft_cus = 0, chroma_cus = 0;
   hipStream_t stream = nullptr;
   Tables t;
   KernelTimers* timers = nullptr;  // non-null while per-kernel profiling is enabled

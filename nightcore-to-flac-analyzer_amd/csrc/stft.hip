@@ -41,6 +41,9 @@ constexpr int SM_HALF = 528;  // float2 per half-size slot: 512 exchange element
 // waves at 96 VGPRs with a 120 KB reserve ran the step at 9.36-10.40 ms against 9.22-9.61 (16 waves,
 // 150 KB) and 16 waves with a 120 KB reserve at 9.31-9.72 (profiles/r5_stft_coresidency_ab.txt)
 constexpr size_t SM_LDS_RESERVE = 150 * 1024;
+#ifndef SM_NOEN_
+#define SM_NOEN_ 0  // timing probe: the frame energies left out even when asked for (outputs wrong)
+#endif
 using SmTw = StagedTw<1024>;  // per-stage twiddle table in LDS (conflict-free reads)
 
 // Mel band loops with compile-time trip counts, unrolled in load batches: 562-576 against
@@ -212,7 +215,9 @@ __device__ __forceinline__ void sm_exchange2(const float2 (&v)[16], float2 (&o)[
 // Hann taps held in registers across frames (124 VGPRs, still four waves per SIMD) instead of 16
 // LDS reads per frame: 483.3 -> 472.6 us per 560 windows, bit-identical (round 5,
 // profiles/r5_stft_variants.txt; either change alone 483.8 / 479.1)
-template <bool H512>
+// EN: the f64 hop-slice energy of each frame (a.frame_energy); without it the window energies come
+// from the silence trim's 512-sample block sums (nc_window_energy_blocks)
+template <bool H512, bool EN>
 __global__ __launch_bounds__(SM_THREADS) void stft_mel_kernel(StftMelArgs a) {
   const Span span_(a.span);
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -297,7 +302,7 @@ __global__ __launch_bounds__(SM_THREADS) void stft_mel_kernel(StftMelArgs a) {
         const int n = jin + 64 * r;
         const float2 v = xv[r];
         const float2 h = hw[r];
-        if (r >= 8 && r < 12) {
+        if (EN && r >= 8 && r < 12) {
           const bool in_hop = H512 || 2 * n - 1024 < a.hop;
           const double dx = in_hop ? (double)v.x : 0.0, dy = in_hop ? (double)v.y : 0.0;
           e = fma(dx, dx, e);
@@ -312,7 +317,7 @@ __global__ __launch_bounds__(SM_THREADS) void stft_mel_kernel(StftMelArgs a) {
         const int64_t i0 = s0 + 2 * n;
         const float x0 = (i0 >= 0 && i0 < L) ? x[i0] : 0.0f;
         const float x1 = (i0 + 1 >= 0 && i0 + 1 < L) ? x[i0 + 1] : 0.0f;
-        if (r >= 8 && r < 12) {
+        if (EN && r >= 8 && r < 12) {
           const int q = 2 * n - 1024;
           if (q < a.hop) {
             e = fma((double)x0, (double)x0, e);
@@ -322,7 +327,7 @@ __global__ __launch_bounds__(SM_THREADS) void stft_mel_kernel(StftMelArgs a) {
         in[r] = make_float2(x0 * hann[2 * n], x1 * hann[2 * n + 1]);
       }
     }
-    if (a.frame_energy) {
+    if (EN) {
       e = wave_sum_u(e);
       if (lane == 0) a.frame_energy[g] = e;
     }
@@ -454,14 +459,20 @@ int launch_stft_mel(Context& ctx, const StftMelArgs& args, hipStream_t st) {
     return -2;
   }
   const int64_t n_groups = (a.total_frames + SM_WAVES - 1) / SM_WAVES;
-  const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(n_groups, (int64_t)ctx.num_cu * (lds <= 80 * 1024 ? 2 : 1)));
+  const int cus = ctx.stft_cus > 0 ? ctx.stft_cus : ctx.num_cu;
+  const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(n_groups, (int64_t)cus * (lds <= 80 * 1024 ? 2 : 1)));
   {
     KTimer kt_(ctx, "stft_mel", st);
     a.span = kt_.span();
-    if (a.hop == 512)
-      hipLaunchKernelGGL(stft_mel_kernel<true>, dim3(grid), dim3(SM_THREADS), lds, st, a);
+    const bool en = a.frame_energy != nullptr && !SM_NOEN_;
+    if (a.hop == 512 && en)
+      hipLaunchKernelGGL((stft_mel_kernel<true, true>), dim3(grid), dim3(SM_THREADS), lds, st, a);
+    else if (a.hop == 512)
+      hipLaunchKernelGGL((stft_mel_kernel<true, false>), dim3(grid), dim3(SM_THREADS), lds, st, a);
+    else if (en)
+      hipLaunchKernelGGL((stft_mel_kernel<false, true>), dim3(grid), dim3(SM_THREADS), lds, st, a);
     else
-      hipLaunchKernelGGL(stft_mel_kernel<false>, dim3(grid), dim3(SM_THREADS), lds, st, a);
+      hipLaunchKernelGGL((stft_mel_kernel<false, false>), dim3(grid), dim3(SM_THREADS), lds, st, a);
   }
   NC_HIP(hipGetLastError());
   return 0;

@@ -187,4 +187,54 @@ int launch_trim(Context& ctx, const float* sig, const int64_t* file_off, const i
   return 0;
 }
 
+// Window energies from the trim's block sums (io.slice_windows' energy_db, io.py:38-40):
+//   E = sum over [s, s + L) of x^2,  s = win_off[w] - file_off[f],  f = win_file[w]
+// the full 512-sample blocks of file f inside the window from blk (trim_blocks_kernel's f64 sums
+// of exactly these samples), the partial blocks at either end from the samples themselves; one
+// wave per window, each lane's f64 partials in a fixed order, then the wave sum (deterministic).
+// energy_db = 20 log10(max(sqrt(E / L), 1e-10)).  stft_mel then needs no per-frame energy.
+__global__ __launch_bounds__(256) void window_energy_blocks_kernel(const float* sig, const int64_t* trim_ws, int n_files,
+                                                                   const int64_t* file_off, const int64_t* win_off,
+                                                                   const int* win_file, int n_win, int L,
+                                                                   double* out) {
+  const int lane = threadIdx.x & 63;
+  const int w = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (w >= n_win) return;
+  const int f = win_file[w];
+  const int64_t* frame_base = trim_ws;
+  const double* blk = reinterpret_cast<const double*>(trim_ws + 2 * (n_files + 1)) + frame_base[f];
+  const int64_t fo = file_off[f];
+  const int64_t s = win_off[w] - fo, e = s + L;
+  int64_t b0 = (s + 511) / 512, b1 = e / 512;  // full blocks [b0, b1)
+  if (b1 < b0) b1 = b0;
+  const int64_t h1 = min(e, 512 * b0), t0 = max(h1, 512 * b1);  // head [s, h1), tail [t0, e)
+  const float* x = sig + fo;
+  double acc = 0.0;
+  for (int64_t b = b0 + lane; b < b1; b += 64) acc += blk[b];
+  for (int64_t i = s + lane; i < h1; i += 64) {
+    const double v = (double)x[i];
+    acc = fma(v, v, acc);
+  }
+  for (int64_t i = t0 + lane; i < e; i += 64) {
+    const double v = (double)x[i];
+    acc = fma(v, v, acc);
+  }
+  acc = wave_sum(acc);
+  if (lane == 0) out[w] = 20.0 * log10(fmax(sqrt(acc / (double)L), 1e-10));
+}
+
+int launch_window_energy_blocks(const float* sig, const void* trim_ws, int n_files, const int64_t* file_off,
+                                const int64_t* win_off, const int* win_file, int n_win, int win_len, double* out,
+                                hipStream_t st) {
+  if (n_win <= 0) return 0;
+  if (n_files <= 0 || win_len <= 0) {
+    set_error("window_energy_blocks: need trimmed files and a positive window length");
+    return -2;
+  }
+  hipLaunchKernelGGL(window_energy_blocks_kernel, dim3((n_win + 3) / 4), dim3(256), 0, st, sig,
+                     static_cast<const int64_t*>(trim_ws), n_files, file_off, win_off, win_file, n_win, win_len, out);
+  NC_HIP(hipGetLastError());
+  return 0;
+}
+
 }  // namespace nc

@@ -76,11 +76,13 @@ __device__ __forceinline__ void wtg_onset(const WinTgArgs& a, int w, double* sh_
   double e = 0.0;
   for (int i = tid; i < T; i += NT) {
     m = fmaxf(m, a.frame_max[g0 + i]);
-    e += a.frame_energy[g0 + i];
+    if (a.frame_energy) e += a.frame_energy[g0 + i];
   }
   const float gmax = (float)block_max((double)m, red);
-  const double esum = block_sum(e, red);
-  if (tid == 0) a.energy_out[w] = 20.0 * log10(fmax(sqrt(esum / (double)a.win_len), 1e-10));
+  if (a.frame_energy) {  // else nc_window_energy_blocks gives the energy from the trim's block sums
+    const double esum = block_sum(e, red);
+    if (tid == 0) a.energy_out[w] = 20.0 * log10(fmax(sqrt(esum / (double)a.win_len), 1e-10));
+  }
   const float c = gmax - 80.0f;
 
   constexpr int FB = 8, NW = NT / 64;
@@ -336,7 +338,7 @@ int launch_window_stage(Context& ctx, const float* sig, const int64_t* win_off, 
   s.hop = hop;
   s.sdb = sdb;
   s.frame_max = fmax_;
-  s.frame_energy = fen;
+  s.frame_energy = energy_out ? fen : nullptr;
   if (win_chunk) {
     // a shared frame must see no right-edge padding of the window: t hop + n_fft / 2 <= win_len
     if (!chunk_tf_base || !peak_pitch || !peak_mag || !chunk_npk || tp_frames < 0 || tp_frames > T ||
@@ -359,7 +361,7 @@ int launch_window_stage(Context& ctx, const float* sig, const int64_t* win_off, 
   WinTgArgs a;
   a.sdb = sdb;
   a.frame_max = fmax_;
-  a.frame_energy = fen;
+  a.frame_energy = energy_out ? fen : nullptr;
   a.active = active;
   a.n_win = n_win;
   a.T = T;

@@ -75,6 +75,7 @@ SIGNATURES = {
     "nc_spectral_stats": (I32, [P, P, P, P, P, P, P, I32, I64, I64, F32, P, P, P, P, SZ, P]),
     "nc_resample_poly": (I32, [P, P, P, P, I32, P, P, P, I64, P, I32, I32, I32, I64, P]),
     "nc_pcm16_to_f32": (I32, [P, P, I64, P, P]),
+    "nc_window_energy_blocks": (I32, [P, P, P, I32, P, P, P, I32, I32, P, P]),
     "nc_melodia_salience": (I32, [P, P, P, P, P, I32, I64, I32, F32, P, I32, P, P, P, P]),
 }
 

@@ -268,6 +268,51 @@ class PairOutcome:
         return self._log_ops
 
 
+def cu_masks(spec: str, num_cu: int) -> Tuple[List[int], List[int]]:
+    """(window-chain mask, chroma-chain mask) as 32-bit words for NC_CU_SPLIT=k[:form]: "even"
+    (default) gives the window chain k / words CUs of every 32-CU word, "low" the first k CUs."""
+    k, form = (spec.split(":") + ["even"])[:2]
+    k, words = int(k), (num_cu + 31) // 32
+    if form == "low":
+        bits = [min(32, max(0, k - 32 * i)) for i in range(words)]
+    else:
+        bits = [k // words + (1 if i < k % words else 0) for i in range(words)]
+    full = (1 << 32) - 1
+    win = [((1 << b) - 1) & full for b in bits]
+    return win, [full ^ m for m in win]
+
+
+def _cu_masked_streams(spec: str, num_cu: int, dev: torch.device):
+    """Two HIP streams restricted to complementary CU sets (hipExtStreamCreateWithCUMask of the
+    HIP runtime torch loaded), wrapped as torch streams."""
+    import ctypes as _C
+    lib = _C.CDLL("libamdhip64.so")
+    fn = lib.hipExtStreamCreateWithCUMask
+    fn.restype = _C.c_int
+    fn.argtypes = [_C.POINTER(_C.c_void_p), _C.c_uint32, _C.POINTER(_C.c_uint32)]
+    out = []
+    for m in cu_masks(spec, num_cu):
+        h = _C.c_void_p()
+        arr = (_C.c_uint32 * len(m))(*m)
+        with torch.cuda.device(dev):
+            rc = fn(_C.byref(h), len(m), arr)
+        if rc != 0:
+            raise _native.NativeError(f"hipExtStreamCreateWithCUMask failed ({rc})")
+        out.append(torch.cuda.ExternalStream(h.value, device=dev))
+    return out
+
+
+@dataclass(eq=False)
+class _TrimBlocks:
+    """A finished (or queued) nc_trim_bounds call: its workspace (the f64 512-sample block sums
+    of files [f0, f1) of the batch), the device offsets of those files and the trim's event."""
+    ws: torch.Tensor
+    off: "_DevSpan"
+    f0: int
+    f1: int
+    event: Optional[torch.cuda.Event]
+
+
 @dataclass(eq=False)
 class AsmContext:
     """What ``assemble_pair`` reads for the pairs of one group: the group's host result arrays
@@ -573,6 +618,15 @@ class Engine:
         # leading tuning frames of a chunk computed inside the window STFT (nc_window_stage_tuning);
         # NC_SHARE_TUNING=0 runs every tuning frame in the chroma chain instead (same results)
         self.share_tuning = os.environ.get("NC_SHARE_TUNING", "1") != "0"
+        # NC_CU_SPLIT=k[:form] (measurement): the window chain on a stream of k
+        # CUs and the chroma chain on a stream of the others (hipExtStreamCreateWithCUMask), the
+        # persistent STFT / tuning grids sized to them (NC_STFT_CUS / NC_CHROMA_CUS, set by the caller
+        # before the context is created).  The masked window stream becomes torch's current stream
+        split = os.environ.get("NC_CU_SPLIT")
+        if split:
+            w, c = _cu_masked_streams(split, self.num_cu, self.dev)
+            torch.cuda.set_stream(w)
+            self.chroma_stream = c
 
     def close(self) -> None:
         """Wait for this engine's streams, then drop its workspaces and its context (tables)."""
@@ -1035,8 +1089,10 @@ class Engine:
                 start = np.zeros(nF, np.int64)
                 end = np.zeros(nF, np.int64)
                 start[:f1], end[:f1] = self._trim_wait(tr["first"])
+                blocks = [tr["first"][3], tr["rest"][3]]
             else:
-                start, end = self._trim_all(signals, p)
+                start, end, tb = self._trim_all(signals, p)
+                blocks = [tb] if tb is not None else []
                 if p.auto_align and p.src_trim_sec == 0.0:  # pipeline.py:111-125 (manual trim has priority)
                     align = self.align_offsets(signals.buf, signals.off[1::2] + start[1::2], end[1::2] - start[1::2],
                                                signals.off[0::2] + start[0::2], end[0::2] - start[0::2])
@@ -1050,8 +1106,10 @@ class Engine:
                 sub = DeviceSignals(signals.buf, signals.off[sl], signals.length[sl])
                 t0 = time.perf_counter()
                 mark(f"b{bi} g{gi} launch")
+                tb = next((b for b in blocks if b.f0 <= 2 * g0 and 2 * g1 <= b.f1), None)
                 g = self._launch_group(sub, p, start[sl].copy(), end[sl].copy(),
-                                       align[g0:g1] if align is not None else None, log is not None)
+                                       align[g0:g1] if align is not None else None, log is not None,
+                                       blocks=(tb, 2 * g0 - tb.f0) if tb is not None else None)
                 g["g0"], g["bi"] = g0, bi
                 pending.append(g)
                 if gi == len(groups) - 1 and bi + 1 < len(batches):
@@ -1101,8 +1159,10 @@ class Engine:
             up.add("len", lens, np.int64)
             d0 = up.commit(dev, spans=True)
             wsb = self.ctx.lib.nc_trim_workspace_bytes(lens.ctypes.data, n)
-            ws = self.workspace(ws_name, wsb)
-            ws.record_stream(stream)
+            # a fresh workspace per launch (not a named one): its 512-sample block sums give the
+            # batch's window energies later (nc_window_energy_blocks), while the next batch's trim
+            # already runs ahead on the trim stream
+            ws = torch.empty(wsb, dtype=torch.uint8, device=dev)
             se = torch.empty(2 * n, dtype=torch.int64, device=dev)
             self.call("nc_trim_bounds", signals.buf.data_ptr(), d0["off"].data_ptr(), d0["len"].data_ptr(), n,
                       int(np.sum(1 + lens // 512)), float(p.silence_strip_db), se[:n].data_ptr(),
@@ -1111,21 +1171,22 @@ class Engine:
             host.copy_(se, non_blocking=True)
             ev = torch.cuda.Event()
             ev.record(stream)
-        return ev, host, (d0, se)
+        return ev, host, (d0, se), _TrimBlocks(ws, d0["off"], f0, f1, ev)
 
     @staticmethod
     def _trim_wait(launched) -> Tuple[np.ndarray, np.ndarray]:
-        ev, host, _ = launched
+        ev, host, _, _ = launched
         ev.synchronize()
         h = host.numpy()
         n = len(h) // 2
         return h[:n].copy(), h[n:].copy()
 
-    def _trim_all(self, signals: DeviceSignals, p: Params) -> Tuple[np.ndarray, np.ndarray]:
-        """io.strip_silence bounds of every file (sync 1)."""
+    def _trim_all(self, signals: DeviceSignals, p: Params):
+        """io.strip_silence bounds of every file (sync 1), and the trim's block sums
+        (_TrimBlocks; None without a silence trim)."""
         nF = signals.n_files
         if p.silence_strip_db is None:
-            return np.zeros(nF, np.int64), signals.length.copy()
+            return np.zeros(nF, np.int64), signals.length.copy(), None
         dev, st = self.dev, self.stream()
         up = _Upload()
         up.add("off", signals.off, np.int64)
@@ -1135,17 +1196,20 @@ class Engine:
         lens = np.ascontiguousarray(signals.length, np.int64)
         # a plain address (ndarray.ctypes.data_as would build a ctypes.cast reference cycle)
         wsb = self.ctx.lib.nc_trim_workspace_bytes(lens.ctypes.data, nF)
-        ws = self.workspace("trim", wsb)
+        ws = torch.empty(wsb, dtype=torch.uint8, device=dev)     # fresh: its block sums outlive the call
         se = torch.empty(2 * nF, dtype=torch.int64, device=dev)
         self.call("nc_trim_bounds", signals.buf.data_ptr(), d0["off"].data_ptr(), d0["len"].data_ptr(), nF,
                   tot_frames, float(p.silence_strip_db), se[:nF].data_ptr(), se[nF:].data_ptr(),
                   ws.data_ptr(), ws.numel(), st)
         se_h = se.cpu().numpy()
-        return se_h[:nF].copy(), se_h[nF:].copy()
+        return se_h[:nF].copy(), se_h[nF:].copy(), _TrimBlocks(ws, d0["off"], 0, nF, None)
 
     def _launch_group(self, signals: DeviceSignals, p: Params, start: np.ndarray, end: np.ndarray,
-                      align: Optional[List[Tuple[float, float]]] = None, stream_logs: bool = False) -> dict:
-        """Queue the whole device pipeline of one group of pairs; returns the pending group."""
+                      align: Optional[List[Tuple[float, float]]] = None, stream_logs: bool = False,
+                      blocks: Optional[Tuple["_TrimBlocks", int]] = None) -> dict:
+        """Queue the whole device pipeline of one group of pairs; returns the pending group.
+        ``blocks``: the silence trim holding this group's files and the index of its first file
+        there; the window energies then come from the trim's block sums, not from the STFT."""
         dev, st = self.dev, self.stream()
         pl = plan_batch(signals.off, signals.length, start, end, p, align)
         nF, B = pl.nF, pl.B
@@ -1193,6 +1257,11 @@ class Engine:
         # device by nc_collect_valid) | chunk counts of the pitch jobs]
         up = _Upload()
         up.add("win_off", win_abs if n_win else [0], np.int64)
+        if blocks is not None and n_win:
+            # each window's file as an index into the trim call that holds the group's files
+            w0a, w1a = np.asarray(w0, np.int64), np.asarray(w1, np.int64)
+            order = np.argsort(w0a, kind="stable")
+            up.add("win_file", np.repeat(order, (w1a - w0a)[order]) + blocks[1], np.int32)
         up.add("w0", w0, np.int32)
         up.add("w1", w1, np.int32)
         up.add("nc_w0", [w0[2 * b] for b in range(B)], np.int32)
@@ -1290,14 +1359,24 @@ class Engine:
             tg = torch.empty(n_win * acw, dtype=torch.float64, device=dev)
             wsb = self.ctx.lib.nc_window_stage_workspace_bytes(self.ctx.h, n_win, win_n, HOP_LENGTH)
             ws = self.workspace("win", wsb)
+            # window energies (io._rms_db): from the silence trim's f64 block sums when the batch
+            # was trimmed (the STFT then skips its per-frame energy), else fused into the STFT
+            en_ptr = energy.data_ptr()
+            if blocks is not None:
+                tb = blocks[0]
+                self.call("nc_window_energy_blocks", signals.buf.data_ptr(), tb.ws.data_ptr(), tb.f1 - tb.f0,
+                          tb.off.data_ptr(), d["win_off"].data_ptr(), d["win_file"].data_ptr(), n_win, win_n,
+                          en_ptr, st)
+                tb.ws.record_stream(torch.cuda.current_stream(dev))
+                en_ptr = None
             if share:
                 self.call("nc_window_stage_tuning", signals.buf.data_ptr(), d["win_off"].data_ptr(), None, n_win,
-                          win_n, HOP_LENGTH, onset.data_ptr(), tg.data_ptr(), energy.data_ptr(),
+                          win_n, HOP_LENGTH, onset.data_ptr(), tg.data_ptr(), en_ptr,
                           d["win_chunk"].data_ptr(), d["tf_base"].data_ptr(), tp, peaks[0].data_ptr(),
                           peaks[1].data_ptr(), o["npk"].data_ptr(), ev_stft.cuda_event, ws.data_ptr(), ws.numel(), st)
             else:
                 self.call("nc_window_stage", signals.buf.data_ptr(), d["win_off"].data_ptr(), None, n_win, win_n,
-                          HOP_LENGTH, onset.data_ptr(), tg.data_ptr(), energy.data_ptr(), ws.data_ptr(), ws.numel(),
+                          HOP_LENGTH, onset.data_ptr(), tg.data_ptr(), en_ptr, ws.data_ptr(), ws.numel(),
                           st)
 
         # ---------------------------------------------------------------- 3b. chroma (stream 2)

@@ -79,7 +79,7 @@ import torch.distributed as dist
 from . import consensus as C
 from .distributed import shard_range
 from .engine import (CHUNK_SEC, HOP_LENGTH, IBI_HOP, MIN_BEATS, MIN_CHUNKS, REF_HZ, SR, AsmContext, DeviceSignals,
-                     Engine, PairOutcome, Params, _HostViews, _Upload, plan_batch)
+                     Engine, PairOutcome, Params, _HostViews, _TrimBlocks, _Upload, plan_batch)
 
 # exchanged window record: exists, energy_db, bpm, nbeats, tempo lag, decision margin
 R_EXISTS, R_ENERGY, R_BPM, R_NBEATS, R_LAG, R_MARGIN = range(6)
@@ -657,6 +657,7 @@ class DeviceStages:
         self.off = signals.off
         self.length = signals.length
         self._win = None
+        self._blocks = None     # the last trim's block sums (the window energies come from them)
         if stream is None:
             stream = getattr(eng, "_split_stream", None) or torch.cuda.Stream(eng.dev)
             eng._split_stream = stream
@@ -683,11 +684,15 @@ class DeviceStages:
             up.add("len", self.length, np.int64)
             d0 = up.commit(eng.dev)
             lens = np.ascontiguousarray(self.length, np.int64)
-            ws = eng.workspace("sp_trim", eng.ctx.lib.nc_trim_workspace_bytes(lens.ctypes.data, nF))
+            # a fresh workspace, kept: its block sums give the window energies (windows()), as
+            # in the engine's pipelined groups
+            ws = torch.empty(eng.ctx.lib.nc_trim_workspace_bytes(lens.ctypes.data, nF), dtype=torch.uint8,
+                             device=eng.dev)
             se = torch.empty(2 * nF, dtype=torch.int64, device=eng.dev)
             eng.call("nc_trim_bounds", self.sig.buf.data_ptr(), d0["off"].data_ptr(), d0["len"].data_ptr(), nF,
                      int(np.sum(1 + lens // 512)), float(p.silence_strip_db), se[:nF].data_ptr(), se[nF:].data_ptr(),
                      ws.data_ptr(), ws.numel(), eng.stream())
+            self._blocks = _TrimBlocks(ws, d0["off"], 0, nF, None)
             h = se.cpu().numpy()
         return h[:nF].copy(), h[nF:].copy()
 
@@ -711,8 +716,16 @@ class DeviceStages:
             tg = torch.empty(n * acw, dtype=torch.float64, device=eng.dev)
             en = torch.empty(n, dtype=torch.float64, device=eng.dev)
             ws = eng.workspace("sp_win", eng.ctx.lib.nc_window_stage_workspace_bytes(eng.ctx.h, n, win_n, HOP_LENGTH))
+            en_ptr = en.data_ptr()
+            tb = self._blocks
+            if tb is not None:          # energies from the trim's block sums (engine._launch_group)
+                wf = np.searchsorted(np.asarray(self.off, np.int64), np.asarray(win_abs, np.int64), side="right") - 1
+                wf_d = torch.from_numpy(wf.astype(np.int32)).to(eng.dev)
+                eng.call("nc_window_energy_blocks", self.sig.buf.data_ptr(), tb.ws.data_ptr(), tb.f1 - tb.f0,
+                         tb.off.data_ptr(), off.data_ptr(), wf_d.data_ptr(), n, win_n, en_ptr, eng.stream())
+                en_ptr = None
             eng.call("nc_window_stage", self.sig.buf.data_ptr(), off.data_ptr(), None, n, win_n, HOP_LENGTH,
-                     onset.data_ptr(), tg.data_ptr(), en.data_ptr(), ws.data_ptr(), ws.numel(), eng.stream())
+                     onset.data_ptr(), tg.data_ptr(), en_ptr, ws.data_ptr(), ws.numel(), eng.stream())
             self._win = dict(onset=onset, tg=tg, T=T, acw=acw)
             return en.cpu().numpy()
 

@@ -13,9 +13,10 @@ these tests check, on batches that take it:
   (oracle/refglue.run_arrays: the port of pipeline.py:23-216), run in a process
   pool that starts with the module so it overlaps the GPU tests;
 * every PIPELINE_CASES golden (the reference's own pipeline.run outputs) inside a
-  17-pair batch, with the default schedule and with group_pairs=3 (6 groups, more
-  than the peak ring's 4 slots), equals the fixture field for field, including
-  str(result), the logs and the CLI JSON.
+  17-pair batch, with the default schedule and with group_pairs=2 (9 groups, more
+  than the peak ring's max(GROUPS_IN_FLIGHT, MAX_GROUPS_IN_FLIGHT) + 1 = 6 slots, the
+  ring reset before the call so it wraps within it), equals the fixture field for
+  field, including str(result), the logs and the CLI JSON.
 """
 import dataclasses
 import math
@@ -134,7 +135,8 @@ def _key(o: E.PairOutcome):
 
 def test_group_schedule_is_multi_group():
     assert [b - a for a, b in E._group_bounds(N_PAIRS, None)] == [16, 16, 16, 16]
-    assert len(E._group_bounds(17, 3)) == 6 > E.Engine.GROUPS_IN_FLIGHT + 1
+    ring = max(E.Engine.GROUPS_IN_FLIGHT, E.Engine.MAX_GROUPS_IN_FLIGHT) + 1
+    assert len(E._group_bounds(17, 2)) == 9 > ring + 1
 
 
 def test_config3_batch_equals_single_pair_runs(eng, bench_pairs):
@@ -157,7 +159,7 @@ def _kw_classes():
     return sorted(out.items(), key=lambda kv: kv[1][0])
 
 
-@pytest.mark.parametrize("group_pairs", [None, 3])
+@pytest.mark.parametrize("group_pairs", [None, 2])
 @pytest.mark.parametrize("kw_names", _kw_classes(), ids=lambda kv: "+".join(kv[1]))
 def test_goldens_inside_multi_group_batch(eng, bench_pairs, golden_pipeline, kw_names, group_pairs):
     kwkey, names = kw_names
@@ -174,6 +176,7 @@ def test_goldens_inside_multi_group_batch(eng, bench_pairs, golden_pipeline, kw_
     for n, c in zip(names, cases):
         pos[n] = next(j for j, b in enumerate(batch) if b is c)
     assert len(batch) >= 17
+    eng._peak_ring = -1                 # the ring's slot 0 first: 9 groups wrap it within this call
     outs = eng.analyze(batch, p, group_pairs=group_pairs)
     for n in names:
         g = golden_pipeline[n]

@@ -49,6 +49,40 @@ def test_slice_windows_energies(eng):
     assert [w.start_sec for w in nio.energy_gate(wins)] == [w.start_sec for w in refglue.energy_gate(ref)]
 
 
+def test_window_energy_from_trim_blocks(eng):
+    """nc_window_energy_blocks (round 6): io._rms_db of windows at any sample offset of their
+    (untrimmed) file, from the silence trim's f64 512-sample block sums plus the partial blocks
+    at the window ends, equals the direct f64 sum of the window's samples (nc_window_energy) and
+    the oracle to 1e-9 dB; the engine's pipelined groups take their energies from it."""
+    cases = _silence_cases()[:3] + [synth.make_pair(45.0, 1010)[0]]
+    sig = eng.upload_signals(cases)
+    start, end, tb = eng._trim_all(sig, E.Params())
+    assert tb is not None and (tb.f0, tb.f1) == (0, len(cases))
+    rng = np.random.default_rng(4)
+    win_off, win_file, ref = [], [], []
+    L = 22050 * 2 + 333
+    for f, y in enumerate(cases):
+        if len(y) < L:
+            continue
+        for s in sorted({0, 1, 511, 512, 513, len(y) - L, *rng.integers(0, len(y) - L, 6).tolist()}):
+            win_off.append(int(sig.off[f]) + s)
+            win_file.append(f)
+            ref.append(refglue.rms_db(y[s:s + L]))
+    n = len(win_off)
+    d_off = torch.tensor(win_off, dtype=torch.int64, device=eng.dev)
+    d_file = torch.tensor(win_file, dtype=torch.int32, device=eng.dev)
+    out = torch.empty(n, dtype=torch.float64, device=eng.dev)
+    eng.call("nc_window_energy_blocks", sig.buf.data_ptr(), tb.ws.data_ptr(), tb.f1 - tb.f0, tb.off.data_ptr(),
+             d_off.data_ptr(), d_file.data_ptr(), n, L, out.data_ptr(), eng.stream())
+    got = out.cpu().numpy()
+    assert np.max(np.abs(got - np.array(ref))) < 1e-9
+    # the same windows through nc_window_energy (direct f64 sums over the samples)
+    for f in sorted(set(win_file)):
+        idx = [i for i in range(n) if win_file[i] == f]
+        d = ops.window_energies(eng, cases[f], np.array([win_off[i] - int(sig.off[f]) for i in idx]), L)
+        assert np.max(np.abs(np.asarray(d) - got[idx])) < 1e-9
+
+
 def test_batch_estimate_tempo_and_logs(eng):
     nc, src = synth.make_pair(40.0, 1009)
     wins = nio.slice_windows(nc, 22050)
