@@ -44,6 +44,11 @@ const char* nc_last_error(void);
  * twiddles, Hann windows, Slaney mel bank, CQT bases for the 100-value tuning
  * grid, the half-band decimator). */
 int nc_create(int device, nc_ctx** out);
+/* The same for audio at `sample_rate` Hz (ABI 5; 8000..48000): the mel bank and the tempogram
+ * windows are built for that rate, so the per-window stage, the beat tracker and the hop-64 IBI
+ * pass follow tempo.py:27-173 at that sr (librosa passes sr through).  The CQT / tuning tables
+ * stay at 22 050 Hz: the chroma entry points and the shared tuning frames need nc_create. */
+int nc_create_rate(int device, int sample_rate, nc_ctx** out);
 int nc_destroy(nc_ctx* ctx);
 /* number of compute units seen by the context (256 on MI355X) */
 int nc_num_cu(const nc_ctx* ctx);

@@ -650,7 +650,7 @@ int launch_tempo_beats(Context& ctx, BeatArgs a, int n_seq, int max_len, hipStre
   a.max_len = max_len;
   a.max_tempo = 320.0;
   a.tightness = 100.0f;
-  a.sr = a.sr ? a.sr : kSR;
+  a.sr = a.sr ? a.sr : ctx.sr;
   // longest possible window table / penalty table: 2P+1 with P <= acw-1
   a.tab_cap = 2 * (a.acw - 1) + 2;
   const size_t tab = al16((size_t)a.tab_cap * sizeof(double));
@@ -693,18 +693,18 @@ int launch_tempo_beats(Context& ctx, BeatArgs a, int n_seq, int max_len, hipStre
 
 int launch_nc_prior(const double* bpm, const int* nbeats, const uint8_t* active, const int* src_w0,
                     const int* src_w1, const int64_t* src_len, const int64_t* nc_len, int n_pairs,
-                    double* prior_out, hipStream_t st) {
+                    double* prior_out, hipStream_t st, int sr) {
   if (n_pairs <= 0) return 0;
   hipLaunchKernelGGL((nc_prior_kernel<256>), dim3(n_pairs), dim3(256), 0, st, bpm, nbeats, active, src_w0,
-                     src_w1, src_len, nc_len, kSR, 4, prior_out);
+                     src_w1, src_len, nc_len, sr, 4, prior_out);
   NC_HIP(hipGetLastError());
   return 0;
 }
 
 int launch_ibi_from_beats(const int* beats, const int64_t* off, const int* nbeats, int n_seq, int hop,
-                          int min_ibis, double* ibi_out, int* n_ibi, hipStream_t st) {
+                          int min_ibis, double* ibi_out, int* n_ibi, hipStream_t st, int sr) {
   if (n_seq <= 0) return 0;
-  hipLaunchKernelGGL((ibi_from_beats_kernel<256>), dim3(n_seq), dim3(256), 0, st, beats, off, nbeats, kSR,
+  hipLaunchKernelGGL((ibi_from_beats_kernel<256>), dim3(n_seq), dim3(256), 0, st, beats, off, nbeats, sr,
                      hop, min_ibis, ibi_out, n_ibi);
   NC_HIP(hipGetLastError());
   return 0;
@@ -727,7 +727,7 @@ int launch_tempo_beats_c(Context& ctx, const float* onset, const int64_t* off, c
   a.start_bpm = start_bpm;
   a.prior_idx = prior_idx;
   a.active = active;
-  a.sr = kSR;
+  a.sr = ctx.sr;
   a.hop = hop;
   a.trim = trim;
   a.bpm_out = bpm_out;

@@ -32,9 +32,9 @@ int launch_tempo_beats_c(Context& ctx, const float* onset, const int64_t* off, c
                          int64_t total_frames, void* ws, size_t ws_bytes, hipStream_t st);
 int launch_nc_prior(const double* bpm, const int* nbeats, const uint8_t* active, const int* src_w0,
                     const int* src_w1, const int64_t* src_len, const int64_t* nc_len, int n_pairs,
-                    double* prior_out, hipStream_t st);
+                    double* prior_out, hipStream_t st, int sr);
 int launch_ibi_from_beats(const int* beats, const int64_t* off, const int* nbeats, int n_seq, int hop,
-                          int min_ibis, double* ibi_out, int* n_ibi, hipStream_t st);
+                          int min_ibis, double* ibi_out, int* n_ibi, hipStream_t st, int sr);
 size_t trim_ws_bytes(const int64_t* host_file_len, int n_files);
 int launch_trim(Context& ctx, const float* sig, const int64_t* file_off, const int64_t* file_len, int n_files,
                 int64_t max_frames, float top_db, int64_t* out_start, int64_t* out_end, void* ws,
@@ -133,7 +133,9 @@ extern "C" {
 int nc_abi_version(void) { return NCGPU_ABI_VERSION; }
 const char* nc_last_error(void) { return nc::g_err.c_str(); }
 
-int nc_create(int device, nc_ctx** out) {
+int nc_create(int device, nc_ctx** out) { return nc_create_rate(device, nc::kSR, out); }
+
+int nc_create_rate(int device, int sample_rate, nc_ctx** out) {
   if (!out) {
     nc::set_error("nc_create: null out");
     return -1;
@@ -149,8 +151,13 @@ int nc_create(int device, nc_ctx** out) {
     return -1;
   }
   NC_HIP(hipSetDevice(device));
+  if (sample_rate < 8000 || sample_rate > 48000) {
+    nc::set_error("nc_create_rate: sample rate outside 8000..48000 Hz");
+    return -2;
+  }
   nc_ctx* c = new nc_ctx();
   c->c.device = device;
+  c->c.sr = sample_rate;
   int cu = 0;
   if (hipDeviceGetAttribute(&cu, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && cu > 0)
     c->c.num_cu = cu;
@@ -293,7 +300,7 @@ int nc_tempo_prior(nc_ctx* ctx, const double* bpm, const int* nbeats, const uint
   CHECK_CTX(ctx);
   SET_DEVICE(ctx);
   return nc::launch_nc_prior(bpm, nbeats, active, src_w0, src_w1, src_len, nc_len, n_pairs, prior_out,
-                             (hipStream_t)stream);
+                             (hipStream_t)stream, ctx->c.sr);
 }
 
 int nc_ibi_from_beats(nc_ctx* ctx, const int* beats, const int64_t* off, const int* nbeats, int n_seq, int hop,
@@ -301,7 +308,7 @@ int nc_ibi_from_beats(nc_ctx* ctx, const int* beats, const int64_t* off, const i
   CHECK_CTX(ctx);
   SET_DEVICE(ctx);
   return nc::launch_ibi_from_beats(beats, off, nbeats, n_seq, hop, min_ibis, ibi_out, n_ibi,
-                                   (hipStream_t)stream);
+                                   (hipStream_t)stream, ctx->c.sr);
 }
 
 size_t nc_chroma_workspace_bytes(const nc_ctx* ctx, int n_chunks, int64_t total_len) {
@@ -314,6 +321,10 @@ int nc_chroma_mean(nc_ctx* ctx, const float* sig, const int64_t* chunk_off, cons
                    int* out_tuning_idx, int* out_tuning_margin, void* ws, size_t ws_bytes, void* stream) {
   CHECK_CTX(ctx);
   SET_DEVICE(ctx);
+  if (ctx->c.sr != nc::kSR) {
+    nc::set_error("chroma: the CQT and tuning tables are built for 22050 Hz (nc_create)");
+    return -2;
+  }
   return nc::launch_chroma_mean(ctx->c, sig, chunk_off, chunk_len, n_chunks, total_len, max_chunk_len, out_chroma,
                                 out_tuning, out_tuning_idx, out_tuning_margin, nullptr, 0, nullptr, nullptr, nullptr, nullptr, ws,
                                 ws_bytes, (hipStream_t)stream);
@@ -326,6 +337,10 @@ int nc_chroma_mean_shared(nc_ctx* ctx, const float* sig, const int64_t* chunk_of
                           void* wait_event, void* ws, size_t ws_bytes, void* stream) {
   CHECK_CTX(ctx);
   SET_DEVICE(ctx);
+  if (ctx->c.sr != nc::kSR) {
+    nc::set_error("chroma: the CQT and tuning tables are built for 22050 Hz (nc_create)");
+    return -2;
+  }
   return nc::launch_chroma_mean(ctx->c, sig, chunk_off, chunk_len, n_chunks, total_len, max_chunk_len, out_chroma,
                                 out_tuning, out_tuning_idx, out_tuning_margin, tf_skip, tf_skip_total, peak_pitch, peak_mag, chunk_npk,
                                 wait_event, ws, ws_bytes, (hipStream_t)stream);

@@ -71,6 +71,10 @@ struct Context {
   // Measurement knobs (NC_STFT_CUS / NC_CHROMA_CUS at nc_create) for CU-masked streams: a
   // persistent kernel sized to the CUs its stream may use (round 6)
   int stft_cus = 0, chroma_cus = 0;
+  // sample rate the rate-dependent tables are built for (nc_create_rate, ABI 5): the mel
+  // filterbank and the tempogram windows (tempo.py:27-173 at any sr); the CQT / tuning / trim
+  // tables stay at kSR and their entry points need sr == kSR
+  int sr = kSR;
   hipStream_t stream = nullptr;
   Tables t;
   KernelTimers* timers = nullptr;  // non-null while per-kernel profiling is enabled

@@ -141,8 +141,9 @@ void build_tables(Context& ctx) {
   }
   t.tw = upload(tw);
   t.hann2048 = upload(to_f32(hann_periodic(kNFFT)));
-  t.ac512 = (int)((int)(8.0 * kSR) / 512);
-  t.ac64 = (int)((int)(8.0 * kSR) / 64);
+  const int sr = ctx.sr;
+  t.ac512 = (int)((int)(8.0 * sr) / 512);
+  t.ac64 = (int)((int)(8.0 * sr) / 64);
   t.hann_ac512 = upload(to_f32(hann_periodic(t.ac512)));
   t.hann_ac64 = upload(to_f32(hann_periodic(t.ac64)));
   {
@@ -157,13 +158,13 @@ void build_tables(Context& ctx) {
   // mel filterbank (oracle/ncref.py mel_filter)
   {
     const int nb = 1 + kNFFT / 2, nm = kNMels;
-    const double fmin = 0.0, fmax = kSR / 2.0;
+    const double fmin = 0.0, fmax = sr / 2.0;
     const double mmin = hz_to_mel(fmin), mmax = hz_to_mel(fmax);
     std::vector<double> mel_f(nm + 2);
     const double step = (mmax - mmin) / (double)(nm + 1);
     for (int j = 0; j < nm + 2; ++j) mel_f[j] = mel_to_hz(j == nm + 1 ? mmax : (double)j * step + mmin);
     std::vector<double> fft_f(nb);
-    for (int k = 0; k < nb; ++k) fft_f[k] = (double)k * ((double)kSR / (double)kNFFT);
+    for (int k = 0; k < nb; ++k) fft_f[k] = (double)k * ((double)sr / (double)kNFFT);
     std::vector<int> lo(nm), len(nm), offs(nm);
     std::vector<float> wts;
     for (int i = 0; i < nm; ++i) {
@@ -214,6 +215,15 @@ void build_tables(Context& ctx) {
         nj4[sl * 64 + l] = bnj[b];
         jmax[sl] = std::max(jmax[sl], bnj[b]);
       }
+    }
+    // the stft_mel instance's compile-time step counts (stft.hip kMelJ: 3 / 14 at 22 050 Hz, 4 / 17
+    // covers 16-48 kHz): the weights are zero-padded to them
+    if (jmax[0] <= 3 && jmax[1] <= 14) {
+      jmax[0] = 3;
+      jmax[1] = 14;
+    } else if (jmax[0] <= 4 && jmax[1] <= 17) {
+      jmax[0] = 4;
+      jmax[1] = 17;
     }
     t.mel_j0 = jmax[0];
     t.mel_j1 = jmax[1];

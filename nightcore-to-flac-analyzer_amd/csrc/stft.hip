@@ -48,7 +48,10 @@ using SmTw = StagedTw<1024>;  // per-stage twiddle table in LDS (conflict-free r
 
 // Mel band loops with compile-time trip counts, unrolled in load batches: 562-576 against
 // 577-596 us per 560 windows (round 3, same session), bit-identical.
-constexpr int kMelJ0 = 3, kMelJ1 = 14;  // float4 steps of the short / long band of a lane (nc_tables.cpp)
+// float4 steps of the short / long band of a lane (nc_tables.cpp): 3 / 14 at 22 050 Hz; the 4 / 17
+// instance serves contexts built for other rates (16-48 kHz, nc_create_rate)
+constexpr int kMelJ0 = 3, kMelJ1 = 14;
+constexpr int kMelJ0w = 4, kMelJ1w = 17;
 constexpr int kMelB = 7;                // steps per load batch
 
 // acc = the fmaf chain of mel_loop over j < nj (< J), in the same order: batches of kMelB
@@ -217,7 +220,7 @@ __device__ __forceinline__ void sm_exchange2(const float2 (&v)[16], float2 (&o)[
 // profiles/r5_stft_variants.txt; either change alone 483.8 / 479.1)
 // EN: the f64 hop-slice energy of each frame (a.frame_energy); without it the window energies come
 // from the silence trim's 512-sample block sums (nc_window_energy_blocks)
-template <bool H512, bool EN>
+template <bool H512, bool EN, int J0 = kMelJ0, int J1 = kMelJ1>
 __global__ __launch_bounds__(SM_THREADS) void stft_mel_kernel(StftMelArgs a) {
   const Span span_(a.span);
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -388,8 +391,8 @@ __global__ __launch_bounds__(SM_THREADS) void stft_mel_kernel(StftMelArgs a) {
     // aligned first bin with zero-padded weights (fmaf chain in bin order, as the CSR form)
     float acc0 = 0.0f, acc1 = 0.0f;
     const int mt0 = sh_mt[lane], mt1 = sh_mt[64 + lane];
-    mel_unrolled<kMelJ0>(pw, mw4, mt0 & 2047, (mt0 >> 11) & 31, lane, acc0);
-    mel_unrolled<kMelJ1>(pw, mw4 + kMelJ0 * 64, mt1 & 2047, (mt1 >> 11) & 31, lane, acc1);
+    mel_unrolled<J0>(pw, mw4, mt0 & 2047, (mt0 >> 11) & 31, lane, acc0);
+    mel_unrolled<J1>(pw, mw4 + J0 * 64, mt1 & 2047, (mt1 >> 11) & 31, lane, acc1);
     const float db0 = 10.0f * log10f(fmaxf(1e-10f, acc0));
     const float db1 = 10.0f * log10f(fmaxf(1e-10f, acc1));
     float* row = a.sdb + g * 128;
@@ -445,8 +448,13 @@ int launch_stft_mel(Context& ctx, const StftMelArgs& args, hipStream_t st) {
     set_error("stft_mel: hop must be even and <= 512");
     return -2;
   }
-  if (a.mel_j0 != kMelJ0 || a.mel_j1 != kMelJ1) {
+  const bool wide = a.mel_j0 == kMelJ0w && a.mel_j1 == kMelJ1w;
+  if (!(a.mel_j0 == kMelJ0 && a.mel_j1 == kMelJ1) && !wide) {
     set_error("stft_mel: mel table trip counts differ from the kernel's compile-time ones");
+    return -2;
+  }
+  if (a.chunk_tf_base && ctx.sr != kSR) {
+    set_error("stft_mel: the shared tuning frames (piptrack) are built for 22050 Hz");
     return -2;
   }
   const size_t lds = std::max<size_t>(stft_mel_lds_bytes(a.mel_j0 + a.mel_j1), SM_LDS_RESERVE);
@@ -465,7 +473,16 @@ int launch_stft_mel(Context& ctx, const StftMelArgs& args, hipStream_t st) {
     KTimer kt_(ctx, "stft_mel", st);
     a.span = kt_.span();
     const bool en = a.frame_energy != nullptr && !SM_NOEN_;
-    if (a.hop == 512 && en)
+    if (wide) {  // a context at another sample rate (nc_create_rate): tempo seams only
+      if (a.hop == 512 && en)
+        hipLaunchKernelGGL((stft_mel_kernel<true, true, kMelJ0w, kMelJ1w>), dim3(grid), dim3(SM_THREADS), lds, st, a);
+      else if (a.hop == 512)
+        hipLaunchKernelGGL((stft_mel_kernel<true, false, kMelJ0w, kMelJ1w>), dim3(grid), dim3(SM_THREADS), lds, st, a);
+      else if (en)
+        hipLaunchKernelGGL((stft_mel_kernel<false, true, kMelJ0w, kMelJ1w>), dim3(grid), dim3(SM_THREADS), lds, st, a);
+      else
+        hipLaunchKernelGGL((stft_mel_kernel<false, false, kMelJ0w, kMelJ1w>), dim3(grid), dim3(SM_THREADS), lds, st, a);
+    } else if (a.hop == 512 && en)
       hipLaunchKernelGGL((stft_mel_kernel<true, true>), dim3(grid), dim3(SM_THREADS), lds, st, a);
     else if (a.hop == 512)
       hipLaunchKernelGGL((stft_mel_kernel<true, false>), dim3(grid), dim3(SM_THREADS), lds, st, a);

@@ -75,6 +75,7 @@ SIGNATURES = {
     "nc_spectral_stats": (I32, [P, P, P, P, P, P, P, I32, I64, I64, F32, P, P, P, P, SZ, P]),
     "nc_resample_poly": (I32, [P, P, P, P, I32, P, P, P, I64, P, I32, I32, I32, I64, P]),
     "nc_pcm16_to_f32": (I32, [P, P, I64, P, P]),
+    "nc_create_rate": (I32, [I32, I32, C.POINTER(P)]),
     "nc_window_energy_blocks": (I32, [P, P, P, I32, P, P, P, I32, I32, P, P]),
     "nc_melodia_salience": (I32, [P, P, P, P, P, I32, I64, I32, F32, P, I32, P, P, P, P]),
 }
@@ -130,16 +131,18 @@ def check(rc: int, what: str) -> None:
 class Context:
     """One engine context per (device, thread) — holds the read-only tables."""
 
-    def __init__(self, device: int = 0):
+    def __init__(self, device: int = 0, sr: int = 22050):
         lib = load()
         h = P()
-        rc = lib.nc_create(int(device), C.byref(h))
+        rc = lib.nc_create(int(device), C.byref(h)) if sr == 22050 else \
+            lib.nc_create_rate(int(device), int(sr), C.byref(h))
         if rc != 0:
             msg = lib.nc_last_error()
-            raise NativeUnavailable(f"nc_create(device={device}) failed: {msg.decode() if msg else rc}")
+            raise NativeUnavailable(f"nc_create(device={device}, sr={sr}) failed: {msg.decode() if msg else rc}")
         self.lib = lib
         self.h = h
         self.device = device
+        self.sr = int(sr)
 
     def close(self):
         if getattr(self, "h", None):

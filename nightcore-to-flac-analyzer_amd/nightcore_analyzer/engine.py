@@ -586,12 +586,17 @@ class _StageWaiter:
 
 # ------------------------------------------------------------------------------ engine
 class Engine:
-    def __init__(self, device: int = 0):
+    def __init__(self, device: int = 0, sr: int = SR):
+        """``sr`` (round 6): an engine whose context's rate-dependent tables (mel bank,
+        tempogram windows) are built for that sample rate serves the tempo seams at it
+        (tempo.py:27-173 pass sr through to librosa); the batched pipeline, the chroma and the
+        tuning need the default 22 050 Hz."""
         if not torch.cuda.is_available():
             raise _native.NativeUnavailable("no HIP device visible to torch (ROCm); the engine has no CPU path")
         self.device_index = device
         self.dev = torch.device("cuda", device)
-        self.ctx = _native.Context(device)
+        self.sr = int(sr)
+        self.ctx = _native.Context(device, self.sr)
         self._ws: Dict[str, torch.Tensor] = {}
         self.num_cu = self.ctx.lib.nc_num_cu(self.ctx.h)
         self.timers: Optional[Dict[str, list]] = None
@@ -1553,7 +1558,7 @@ class Engine:
         ws = self.workspace(ws_tag + "ibi_on", wsb)
         self.call("nc_ibi_onset", buf.data_ptr(), d_off.data_ptr(), d_len.data_ptr(), nF, total, hop,
                   onset.data_ptr(), fbase.data_ptr(), ws.data_ptr(), ws.numel(), st)
-        acw = int(int(8.0 * SR) // hop)
+        acw = int(int(8.0 * self.sr) // hop)
         tg = torch.empty(nF * acw, dtype=torch.float64, device=dev)
         fmax = int(frames.max())
         wsb = self.ctx.lib.nc_ibi_tempogram_workspace_bytes(self.ctx.h, nF, total, fmax, hop)
@@ -1844,20 +1849,22 @@ _tls = threading.local()
 _live: "weakref.WeakSet[Engine]" = weakref.WeakSet()     # engines not yet collected (tests, diagnostics)
 
 
-def get_engine(device: Optional[int] = None) -> Engine:
+def get_engine(device: Optional[int] = None, sr: int = SR) -> Engine:
     """This thread's engine for ``device`` — contexts are not shared across threads.  The
     engine lives in thread-local storage, so it (its context, streams and HBM workspaces) is
     released when the thread ends: the reference's GUI starts a fresh QThread per analysis
     (gui/worker.py:16-56), and a long session must not keep one engine per finished thread.
-    ``release_engine`` frees it earlier."""
+    ``release_engine`` frees it earlier.  ``sr``: an engine whose tables are built for that
+    sample rate (the tempo seams at other rates), kept beside the 22 050 Hz one."""
     if device is None:
         device = torch.cuda.current_device() if torch.cuda.is_available() else 0
     engines = getattr(_tls, "engines", None)
     if engines is None:
         engines = _tls.engines = {}
-    e = engines.get(device)
+    key = device if int(sr) == SR else (device, int(sr))
+    e = engines.get(key)
     if e is None:
-        e = engines[device] = Engine(device)
+        e = engines[key] = Engine(device, int(sr))
         _live.add(e)
     return e
 
@@ -1866,7 +1873,7 @@ def release_engine(device: Optional[int] = None) -> None:
     """Close this thread's engine for ``device`` (every device when None) after its queued
     work: the next get_engine on this thread builds a new one."""
     engines = getattr(_tls, "engines", None) or {}
-    for d in [d for d in engines if device is None or d == device]:
+    for d in [d for d in engines if device is None or (d[0] if isinstance(d, tuple) else d) == device]:
         engines.pop(d).close()
 
 

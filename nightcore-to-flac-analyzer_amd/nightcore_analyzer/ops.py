@@ -53,7 +53,7 @@ def window_tempos(eng: Engine, audios: Sequence[np.ndarray], start_bpms: Sequenc
     by_len: dict = {}
     for i, a in enumerate(audios):
         by_len.setdefault(len(a), []).append(i)
-    acw = int(int(8.0 * SR) // HOP)
+    acw = int(int(8.0 * eng.sr) // HOP)     # the tempogram window of the engine's rate
     for L, idx in by_len.items():
         if L == 0:
             continue

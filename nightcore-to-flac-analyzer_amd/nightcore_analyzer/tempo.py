@@ -23,33 +23,50 @@ IBI_HOP_LENGTH: int = 64
 IBI_MIN_IBIS: int = 4
 
 
+MIN_RATE, MAX_RATE = 8000, 48000   # rates the per-rate tables are built for (nc_create_rate)
+
+
 def require_rate(sr, what: str) -> None:
-    """The engine's STFT / mel / tempogram / CQT tables are built for io.SAMPLE_RATE (the
-    rate io.load_audio returns, io.py:44-55).  Another rate raises instead of being
-    analysed with the wrong tables."""
+    """The chroma / CQT / tuning tables are built for io.SAMPLE_RATE (the rate io.load_audio
+    returns, io.py:44-55): the pitch seams raise for another rate instead of analysing with
+    the wrong tables.  (The tempo seams take any rate in MIN_RATE..MAX_RATE: rate_engine.)"""
     if int(sr) != SAMPLE_RATE:
         raise ValueError(f"{what}: sample rate {sr} Hz is not supported by the MI355X engine, whose tables "
                          f"are built for {SAMPLE_RATE} Hz; load or resample the audio at {SAMPLE_RATE} Hz "
                          f"(io.load_audio(path, sr={SAMPLE_RATE}))")
 
 
+def rate_engine(sr, what: str):
+    """This thread's engine for audio at ``sr`` Hz: the reference passes sr through to librosa
+    (tempo.py:44-50, 139-164), so the mel bank and the tempogram windows are built for that rate
+    (engine.get_engine(sr=...), a context from nc_create_rate) rather than resampling."""
+    from .engine import get_engine
+    sr = int(sr)
+    if not MIN_RATE <= sr <= MAX_RATE:
+        raise ValueError(f"{what}: sample rate {sr} Hz is outside the engine's {MIN_RATE}..{MAX_RATE} Hz")
+    return get_engine(sr=sr)
+
+
 def estimate_tempo(window: AudioWindow, start_bpm: float = 120.0) -> Optional[float]:
     """tempo.py:27-77 for one window, at window.sample_rate."""
-    from .engine import get_engine
     from .ops import window_tempos
-    require_rate(window.sample_rate, "estimate_tempo")
-    return window_tempos(get_engine(), [window.audio], [start_bpm])[0]
+    return window_tempos(rate_engine(window.sample_rate, "estimate_tempo"), [window.audio], [start_bpm])[0]
 
 
 def batch_estimate_tempo(windows: List[AudioWindow], log: Optional[Callable[[str], None]] = None,
                          start_bpm: float = 120.0) -> List[Optional[float]]:
-    """All windows in one device batch; the same log lines as tempo.py:102-110."""
-    from .engine import get_engine
+    """All windows in one device batch per sample rate; the same log lines as tempo.py:102-110."""
     from .ops import window_tempos
     n = len(windows)
-    for w in windows:
-        require_rate(w.sample_rate, "batch_estimate_tempo")
-    res = window_tempos(get_engine(), [w.audio for w in windows], [start_bpm] * n) if n else []
+    res: List[Optional[float]] = [None] * n
+    by_rate: dict = {}
+    for i, w in enumerate(windows):
+        by_rate.setdefault(int(w.sample_rate), []).append(i)
+    for sr, idx in by_rate.items():
+        got = window_tempos(rate_engine(sr, "batch_estimate_tempo"), [windows[i].audio for i in idx],
+                            [start_bpm] * len(idx))
+        for i, g in zip(idx, got):
+            res[i] = g
     if log:
         for i, w in enumerate(windows):
             log(f"    tempo window {i + 1}/{n}  [{w.start_sec:.1f}–{w.end_sec:.1f} s]")
@@ -57,9 +74,18 @@ def batch_estimate_tempo(windows: List[AudioWindow], log: Optional[Callable[[str
     return res
 
 
+# the hop-64 beat tracker keeps its DP ring and penalty table (both ~ the 8 s tempogram window in
+# frames) in LDS: up to ~26 kHz at hop 64 (beat.hip launch_tempo_beats); a higher rate runs the
+# pass at hop_length=512 (the streamed tempogram supports hops 64 and 512, ibi.hip tg_acw)
+IBI_MAX_WINDOW_FRAMES = 3276
+
+
 def estimate_ibis_global(y: np.ndarray, sr: int, hop_length: int = IBI_HOP_LENGTH,
                          min_ibis: int = IBI_MIN_IBIS, start_bpm: float = 120.0) -> Optional[np.ndarray]:
-    from .engine import get_engine
     from .ops import ibis
-    require_rate(sr, "estimate_ibis_global")
-    return ibis(get_engine(), [y], [start_bpm], hop=hop_length, min_ibis=min_ibis)[0]
+    eng = rate_engine(sr, "estimate_ibis_global")
+    if int(8.0 * int(sr)) // int(hop_length) > IBI_MAX_WINDOW_FRAMES:
+        raise ValueError(f"estimate_ibis_global: an 8 s tempogram window at {sr} Hz / hop {hop_length} is "
+                         f"{int(8.0 * int(sr)) // int(hop_length)} frames, more than the beat tracker's "
+                         f"{IBI_MAX_WINDOW_FRAMES}; use hop_length=512")
+    return ibis(eng, [y], [start_bpm], hop=hop_length, min_ibis=min_ibis)[0]

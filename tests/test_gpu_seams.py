@@ -84,3 +84,57 @@ def test_engine_released_with_its_thread():
     assert not errs, errs[0]
     assert max(live) == base, (base, live)             # each thread's engine went with its thread
     assert reserved[-1] <= reserved[2], reserved      # flat after the first threads warmed the allocator
+
+
+# ---- tempo seams at other sample rates: the reference passes sr through to
+# librosa (tempo.py:44-50, 139-164); an engine whose mel bank and tempogram windows are built for
+# the rate (nc_create_rate) equals the oracle at that rate, with no resampling
+def _at(sr, seconds, seed):
+    import scipy.signal
+    src = synth.make_source(seconds, seed)
+    from math import gcd
+    g = gcd(sr, 22050)
+    return scipy.signal.resample_poly(src, sr // g, 22050 // g).astype(np.float32)
+
+
+@pytest.mark.parametrize("sr", [44100, 48000, 16000])
+def test_estimate_tempo_at_other_rates_equals_oracle(eng, sr):
+    from nightcore_analyzer import io as nio, tempo
+    from oracle import refglue
+    y = _at(sr, 40.0, 1012)
+    wins = [nio.AudioWindow(audio=y[s:s + 10 * sr], sample_rate=sr, start_sec=s / sr, end_sec=s / sr + 10.0,
+                            energy_db=0.0) for s in range(0, len(y) - 10 * sr + 1, 5 * sr)]
+    for bpm in (120.0, 150.0):
+        got = [tempo.estimate_tempo(w, start_bpm=bpm) for w in wins]
+        ref = [refglue.estimate_tempo(w.audio, sr, bpm) for w in wins]
+        assert got == ref, (sr, bpm, got, ref)
+    # one call over windows of two rates: each rate on its own engine, in the caller's order
+    mixed = wins[:2] + [nio.AudioWindow(audio=_at(22050, 10.0, 1013), sample_rate=22050, start_sec=0.0,
+                                        end_sec=10.0, energy_db=0.0)]
+    got = tempo.batch_estimate_tempo(mixed, start_bpm=120.0)
+    assert got == [refglue.estimate_tempo(w.audio, w.sample_rate, 120.0) for w in mixed]
+    assert E.get_engine(sr=sr) is not E.get_engine() and E.get_engine(sr=sr).sr == sr
+
+
+@pytest.mark.parametrize("sr,hop", [(16000, 64), (44100, 512)])
+def test_ibis_at_other_rates_equal_oracle(eng, sr, hop):
+    """The IBI pass (tempo.py:120-173) at 16 kHz hop 64, and at 44.1 kHz hop 512 (at hop 64 its
+    5 512-frame tempogram window exceeds the beat tracker's LDS ring: ValueError)."""
+    from nightcore_analyzer import tempo
+    from oracle import refglue
+    y = _at(sr, 20.0, 1014)
+    got = tempo.estimate_ibis_global(y, sr, hop_length=hop, start_bpm=120.0)
+    ref = refglue.estimate_ibis_global(y, sr, hop_length=hop, start_bpm=120.0)
+    assert (got is None) == (ref is None)
+    if ref is not None:
+        assert len(got) == len(ref) and np.array_equal(got, ref)
+    if sr == 44100:
+        with pytest.raises(ValueError, match="use hop_length=512"):
+            tempo.estimate_ibis_global(y, sr, hop_length=64)
+
+
+def test_chroma_needs_the_22k_context(eng):
+    from nightcore_analyzer import ops, _native
+    e44 = E.get_engine(sr=44100)
+    with pytest.raises(_native.NativeError, match="22050"):
+        ops.chroma_means(e44, [np.zeros(441000, np.float32)])

@@ -1,6 +1,8 @@
 """The drop-in seams called with the reference's own signatures, on the CPU (no device
-work reaches the engine): a sample rate other than io.SAMPLE_RATE raises ValueError
-instead of being analysed with the 22 050 Hz tables (tempo.py:41-44,158; pitch.py:55-62),
+work reaches the engine): the pitch seams raise ValueError for a sample rate other than
+io.SAMPLE_RATE instead of being analysed with the 22 050 Hz CQT tables (pitch.py:55-62), the
+tempo seams for a rate outside the 8-48 kHz their per-rate tables cover (tempo.py:41-44,158;
+44.1 kHz runs on the device: tests/test_gpu_seams.py),
 session.set_many takes the reference's dict (session.py:37-41), and MELODIA runs
 essentia's algorithm when essentia is importable (pitch.py:187-241; a stand-in module
 here, since essentia is absent: parity unpinned)."""
@@ -23,11 +25,6 @@ def _window(sr):
 
 
 @pytest.mark.parametrize("call", [
-    lambda: tempo.estimate_tempo(_window(SR44)),
-    lambda: tempo.estimate_tempo(_window(SR44), start_bpm=150.0),
-    lambda: tempo.batch_estimate_tempo([_window(SR44)], log=None, start_bpm=120.0),
-    lambda: tempo.estimate_ibis_global(np.zeros(SR44 * 20, np.float32), SR44, hop_length=64, min_ibis=4,
-                                       start_bpm=120.0),
     lambda: pitch._mean_chroma(np.zeros(SR44 * 20, np.float32), SR44),
     lambda: pitch._chroma_shift_for_chunk(np.zeros(SR44 * 20, np.float32), np.zeros(SR44 * 20, np.float32), SR44),
     lambda: pitch.estimate_pitch_chroma(np.zeros(SR44 * 60, np.float32), np.zeros(SR44 * 60, np.float32), SR44,
@@ -38,6 +35,18 @@ def _window(sr):
 def test_other_sample_rates_raise_value_error(call):
     with pytest.raises(ValueError, match="44100 Hz"):
         call()
+
+
+@pytest.mark.parametrize("sr", [4000, 96000])
+@pytest.mark.parametrize("call", [
+    lambda sr: tempo.estimate_tempo(_window(sr)),
+    lambda sr: tempo.batch_estimate_tempo([_window(sr)], log=None, start_bpm=120.0),
+    lambda sr: tempo.estimate_ibis_global(np.zeros(sr * 20, np.float32), sr, hop_length=64, min_ibis=4,
+                                          start_bpm=120.0),
+])
+def test_tempo_seams_outside_the_table_rates_raise(call, sr):
+    with pytest.raises(ValueError, match=f"{sr} Hz is outside"):
+        call(sr)
 
 
 def test_session_set_many_takes_a_dict(tmp_path, monkeypatch):
