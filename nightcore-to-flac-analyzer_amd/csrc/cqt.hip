@@ -1008,10 +1008,14 @@ __global__ __launch_bounds__(CM_NTH, CH_MINB_) void cqt_mfma_kernel(CqmArgs a) {
 //    and retired by a counted vmcnt at step n + 1's top (the block loads stay in flight): every
 //    wave issues the same vector-memory sequence (5 slice pieces per step, 10 block loads at a
 //    group's first step), so the count of younger operations is static per position in the
-//    group (C2::younger).  The block itself is waited for with vmcnt(0): a counted wait that
-//    left younger L2-hit slice pieces in flight behind the (HBM) block loads returned before the
-//    loads had landed (NaNs from fresh workspace contents in tools/det_check.py, round 5), so on
-//    gfx950 vmcnt is not retired in issue order across global_load and global_load_lds;
+//    group (C2::younger).  The counted wait relies on vmcnt retiring in issue order across
+//    global_load_lds and global_load: round 6 measured that directly (tools/probe/vmcnt_order.hip:
+//    an LDS-DMA piece from an HBM-cold line, then 4 L2-hot register loads, vmcnt(4), the LDS read;
+//    and the reverse, a cold register load then 4 hot LDS-DMA pieces: 0 stale of 3.4e8 lane-trials
+//    each, profiles/r6_vmcnt_order.txt), as MI355X_MICROARCH.md states.  (Round 5 had blamed out-of-
+//    order retirement for NaNs from a counted wait on the block loads; the block wait stays
+//    vmcnt(0).  C2_SAFE_=1, vmcnt(0) wherever a block load is younger than the slice, measured
+//    the same: 353.3 against 352.7 us per 224 chunks, profiles/r6_var_bench.txt);
 //  * block loads are dword-aligned dwordx4 (gfx950 serves unaligned global loads), so an
 //    unaligned chunk issues the same instructions; an edge tile loads clamped pieces and zeroes
 //    the samples outside the signal when it splits.

@@ -75,8 +75,8 @@ def batch_estimate_tempo(windows: List[AudioWindow], log: Optional[Callable[[str
 
 
 # the hop-64 beat tracker keeps its DP ring and penalty table (both ~ the 8 s tempogram window in
-# frames) in LDS: up to ~26 kHz at hop 64 (beat.hip launch_tempo_beats); a higher rate runs the
-# pass at hop_length=512 (the streamed tempogram supports hops 64 and 512, ibi.hip tg_acw)
+# frames) in LDS: up to ~26 kHz at hop 64 (beat.hip launch_tempo_beats); the streamed tempogram
+# runs hops 64 and 512 with an even window (ibi.hip tg_acw): e.g. 48 kHz at hop 512
 IBI_MAX_WINDOW_FRAMES = 3276
 
 
@@ -84,8 +84,11 @@ def estimate_ibis_global(y: np.ndarray, sr: int, hop_length: int = IBI_HOP_LENGT
                          min_ibis: int = IBI_MIN_IBIS, start_bpm: float = 120.0) -> Optional[np.ndarray]:
     from .ops import ibis
     eng = rate_engine(sr, "estimate_ibis_global")
-    if int(8.0 * int(sr)) // int(hop_length) > IBI_MAX_WINDOW_FRAMES:
+    win = int(8.0 * int(sr)) // int(hop_length)
+    if win > IBI_MAX_WINDOW_FRAMES:
         raise ValueError(f"estimate_ibis_global: an 8 s tempogram window at {sr} Hz / hop {hop_length} is "
-                         f"{int(8.0 * int(sr)) // int(hop_length)} frames, more than the beat tracker's "
-                         f"{IBI_MAX_WINDOW_FRAMES}; use hop_length=512")
+                         f"{win} frames, more than the beat tracker's {IBI_MAX_WINDOW_FRAMES}; use hop_length=512")
+    if int(hop_length) not in (64, 512) or win % 2:
+        raise ValueError(f"estimate_ibis_global: the streamed tempogram runs hop_length 64 or 512 with an even "
+                         f"8 s window; {sr} Hz / hop {hop_length} gives {win} frames")
     return ibis(eng, [y], [start_bpm], hop=hop_length, min_ibis=min_ibis)[0]

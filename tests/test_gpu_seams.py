@@ -116,10 +116,11 @@ def test_estimate_tempo_at_other_rates_equals_oracle(eng, sr):
     assert E.get_engine(sr=sr) is not E.get_engine() and E.get_engine(sr=sr).sr == sr
 
 
-@pytest.mark.parametrize("sr,hop", [(16000, 64), (44100, 512)])
+@pytest.mark.parametrize("sr,hop", [(16000, 64), (48000, 512)])
 def test_ibis_at_other_rates_equal_oracle(eng, sr, hop):
-    """The IBI pass (tempo.py:120-173) at 16 kHz hop 64, and at 44.1 kHz hop 512 (at hop 64 its
-    5 512-frame tempogram window exceeds the beat tracker's LDS ring: ValueError)."""
+    """The IBI pass (tempo.py:120-173) at 16 kHz hop 64 and 48 kHz hop 512; 44.1 kHz raises
+    ValueError: at hop 64 its 5 512-frame tempogram window exceeds the beat tracker's LDS ring,
+    at hop 512 the 689-frame window is odd (the streamed tempogram pairs lags)."""
     from nightcore_analyzer import tempo
     from oracle import refglue
     y = _at(sr, 20.0, 1014)
@@ -128,9 +129,11 @@ def test_ibis_at_other_rates_equal_oracle(eng, sr, hop):
     assert (got is None) == (ref is None)
     if ref is not None:
         assert len(got) == len(ref) and np.array_equal(got, ref)
-    if sr == 44100:
-        with pytest.raises(ValueError, match="use hop_length=512"):
-            tempo.estimate_ibis_global(y, sr, hop_length=64)
+    y44 = _at(44100, 12.0, 1015)
+    with pytest.raises(ValueError, match="use hop_length=512"):
+        tempo.estimate_ibis_global(y44, 44100, hop_length=64)
+    with pytest.raises(ValueError, match="689 frames"):
+        tempo.estimate_ibis_global(y44, 44100, hop_length=512)
 
 
 def test_chroma_needs_the_22k_context(eng):

@@ -149,9 +149,10 @@ int main(int argc, char** argv) {
   CK(hipDeviceSynchronize());
   unsigned long long h[4];
   CK(hipMemcpy(h, cnt, sizeof(h), hipMemcpyDeviceToHost));
-  std::printf("case A (LDS-DMA cold, then 4 register loads hot, vmcnt(4), read LDS): %llu stale of %llu wave-trials x 64 lanes\n",
+  // every lane adds its own stale count and its TRIALS: both totals are per lane-trial
+  std::printf("case A (LDS-DMA cold, then 4 register loads hot, vmcnt(4), read LDS): %llu stale of %llu lane-trials\n",
               h[0], h[1]);
-  std::printf("case B (register load cold, then 4 LDS-DMA hot, vmcnt(4), read register): %llu stale of %llu wave-trials x 64 lanes\n",
+  std::printf("case B (register load cold, then 4 LDS-DMA hot, vmcnt(4), read register): %llu stale of %llu lane-trials\n",
               h[2], h[3]);
   CK(hipFree(cold));
   CK(hipFree(hot));

@@ -43,8 +43,28 @@ def per_dispatch(d: Path, counter: str):
     return vals
 
 
-def main(out):
+# the access form each kernel's reads / writes mostly use (tools/calib_fetch.hip kernel names):
+# FETCH_SIZE / WRITE_SIZE are divided by that form's measured scale (profiles/r6_fetch_calibration.json)
+FORMS = {"stft_mel": ("stream_read<float2>", "stream_write<float>"),
+         "tuning_peaks": ("stream_read<float2>", "stream_write<float>"),
+         "window_tg": ("stream_read<float2>", "stream_write<float>"),
+         "trim_blocks": ("stream_read<float4>", "stream_write<float>"),
+         "decimate": ("stream_read<float4>", "stream_write<float4>"),
+         "cqt_low": ("stream_read<float4>", "stream_write<float>"),      # dwordx4 blocks; slices by LDS-DMA
+         "cqt_high": ("lds_dma_read", "stream_write<float>"),            # slices by LDS-DMA; images dwordx4
+         "cqt_tail": ("stream_read<float4>", "stream_write<float>")}
+
+
+def _scales(calib):
+    if not calib:
+        return None
+    c = json.loads(Path(calib).read_text())
+    return c.get("read_scale", {}), c.get("write_scale", {})
+
+
+def main(out, name=None, calib=None):
     out = Path(out)
+    sc = _scales(calib)
     fetch = per_dispatch(out / "FETCH_SIZE", "FETCH_SIZE")
     write = per_dispatch(out / "WRITE_SIZE", "WRITE_SIZE")
     sys.path.insert(0, str(REPO))
@@ -61,6 +81,11 @@ def main(out):
         w = sum(write.get(tag, [0])) / max(1, len(write.get(tag, [])))
         k = {"launches": len(fetch.get(tag, [])), "fetch_size_kib_raw": round(f, 2), "write_size_kib": round(w, 2),
              "hbm_bytes_per_launch": int(round((2 * f + w) * 1024))}
+        if sc is not None and tag in FORMS:
+            rf, wf = FORMS[tag]
+            rs, ws = sc[0].get(rf, 0.5), sc[1].get(wf, 1.0)
+            k["calibration"] = {"read_form": rf, "read_scale": rs, "write_form": wf, "write_scale": ws}
+            k["hbm_bytes_per_launch"] = int(round((f / rs + w / ws) * 1024))
         k["launches_per_step"] = round(k["launches"] / calls, 3)
         if tag in ALG_STEP and fetch.get(tag):
             # mean over launches of unequal groups: per-step bytes / launches per step
@@ -86,10 +111,14 @@ def main(out):
                          "the bytes of a wide coalesced read (MI355X_MICROARCH.md; calibrated with "
                          "tools/calib_fetch.hip: a 1 GiB stream read reports 0.500 GiB)",
            "kernels": kern}
-    name = sys.argv[2] if len(sys.argv) > 2 else "r3_traffic.json"
+    if sc is not None:
+        doc["correction"] = ("hbm_bytes = FETCH_SIZE / read_scale + WRITE_SIZE / write_scale (KiB -> bytes), the "
+                             "scales of each kernel's dominant access form measured by tools/calib_fetch.hip "
+                             f"({Path(calib).name}; per kernel under 'calibration')")
+    name = name or "r3_traffic.json"
     (REPO / "profiles" / name).write_text(json.dumps(doc, indent=1) + "\n")
     print(json.dumps(doc, indent=1))
 
 
 if __name__ == "__main__":
-    main(sys.argv[1])
+    main(*sys.argv[1:4])
