@@ -1112,8 +1112,8 @@ class Engine:
                 t0 = time.perf_counter()
                 mark(f"b{bi} g{gi} launch")
                 # NC_BLOCK_ENERGY=0 (A/B measurement only): the round-5 per-frame energies in the STFT
-            tb = next((b for b in blocks if b.f0 <= 2 * g0 and 2 * g1 <= b.f1), None) \
-                if os.environ.get("NC_BLOCK_ENERGY", "1") != "0" else None
+                tb = next((b for b in blocks if b.f0 <= 2 * g0 and 2 * g1 <= b.f1), None) \
+                    if os.environ.get("NC_BLOCK_ENERGY", "1") != "0" else None
                 g = self._launch_group(sub, p, start[sl].copy(), end[sl].copy(),
                                        align[g0:g1] if align is not None else None, log is not None,
                                        blocks=(tb, 2 * g0 - tb.f0) if tb is not None else None)
