@@ -1367,22 +1367,37 @@ __device__ __forceinline__ void cqt_low_tile(const CqmArgs& a, int bx, int c) {
 #ifndef CQL_ONLY
 #define CQL_ONLY -1
 #endif
+// C2_XCD_=1 (probe): workgroups dispatched to one XCD (linear ids b, b + 8, ...; placement
+// round-robin, speed only) take consecutive (tile pair, chunk, octave) items, so the tiles of one
+// (chunk, octave) and their tuning's 320 KB filter set share one L2 instead of seven
+#ifndef C2_XCD_
+#define C2_XCD_ 0
+#endif
 __global__ __launch_bounds__(C2_NW * 64, C2_MINB_) void cqt_mfma_low_kernel(CqmArgs a) {
-  const unsigned oz = CQL_ONLY >= 0 ? (unsigned)CQL_ONLY : blockIdx.z;
+  unsigned bx = blockIdx.x, by = blockIdx.y, bz = blockIdx.z;
+  if (C2_XCD_) {
+    const unsigned X = gridDim.x, Y = gridDim.y, nb = X * Y * gridDim.z;
+    const unsigned b = bx + X * (by + Y * bz), xcd = b & 7, i = b >> 3, q = nb >> 3, rem = nb & 7;
+    const unsigned w = xcd < rem ? xcd * (q + 1) + i : rem * (q + 1) + (xcd - rem) * q + i;
+    bx = w % X;
+    by = (w / X) % Y;
+    bz = w / (X * Y);
+  }
+  const unsigned oz = CQL_ONLY >= 0 ? (unsigned)CQL_ONLY : bz;
   if (oz == 0) {
-    cqt_low_tile<0, false>(a, blockIdx.x, blockIdx.y);
-    cqt_low_tile<0, true>(a, blockIdx.x, blockIdx.y);
+    cqt_low_tile<0, false>(a, bx, by);
+    cqt_low_tile<0, true>(a, bx, by);
   } else if (oz == 1) {
-    cqt_low_tile<1, false>(a, blockIdx.x, blockIdx.y);
-    cqt_low_tile<1, true>(a, blockIdx.x, blockIdx.y);
+    cqt_low_tile<1, false>(a, bx, by);
+    cqt_low_tile<1, true>(a, bx, by);
   } else if (CQL_ONLY != 3) {
-    cqt_low_tile<2, false>(a, blockIdx.x, blockIdx.y);
-    cqt_low_tile<2, true>(a, blockIdx.x, blockIdx.y);
+    cqt_low_tile<2, false>(a, bx, by);
+    cqt_low_tile<2, true>(a, bx, by);
   }
 #if CQL_ONLY == 3
   else {
-    cqt_low_tile<3, false>(a, blockIdx.x, blockIdx.y);
-    cqt_low_tile<3, true>(a, blockIdx.x, blockIdx.y);
+    cqt_low_tile<3, false>(a, bx, by);
+    cqt_low_tile<3, true>(a, bx, by);
   }
 #endif
 }
