@@ -163,7 +163,6 @@ int nc_create_rate(int device, int sample_rate, nc_ctx** out) {
     c->c.num_cu = cu;
   if (const char* v = std::getenv("NC_STFT_CUS")) c->c.stft_cus = std::max(0, std::atoi(v));
   if (const char* v = std::getenv("NC_CHROMA_CUS")) c->c.chroma_cus = std::max(0, std::atoi(v));
-  if (const char* v = std::getenv("NC_STFT_DYN")) c->c.stft_dyn = std::max(0, std::atoi(v));
   nc::build_tables(c->c);
   if (!c->c.t.tw || !c->c.t.cqt_w || !c->c.t.halfband) {
     nc::free_tables(c->c);

@@ -75,11 +75,7 @@ struct Context {
   // filterbank and the tempogram windows (tempo.py:27-173 at any sr); the CQT / tuning / trim
   // tables stay at kSR and their entry points need sr == kSR
   int sr = kSR;
-  // stft_mel's dynamic schedule (NC_STFT_DYN = frames per dequeue, 0: static ranges): a ring of
-  // zeroed work counters, one per launch (launches on different streams may overlap)
-  int stft_dyn = 0;
-  unsigned* work_ring = nullptr;
-  int work_slot = 0;
+
   hipStream_t stream = nullptr;
   Tables t;
   KernelTimers* timers = nullptr;  // non-null while per-kernel profiling is enabled

@@ -450,10 +450,6 @@ void build_tables(Context& ctx) {
 }
 
 void free_tables(Context& ctx) {
-  if (ctx.work_ring) {
-    (void)hipFree(ctx.work_ring);
-    ctx.work_ring = nullptr;
-  }
   Tables& t = ctx.t;
   void* ptrs[] = {t.tw, t.hann2048, t.hann_ac512, t.hann_ac64, t.wsq512, t.wsq64, t.mel_lo,  t.mel_len, t.mel_off,
                   t.mel_w,  t.cqt_lo,   t.cqt_len,    t.cqt_off,  t.cqt_w,   t.cqt_inv_sqrt_len, t.halfband,

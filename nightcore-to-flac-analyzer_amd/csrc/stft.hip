@@ -248,34 +248,20 @@ __global__ __launch_bounds__(SM_THREADS) void stft_mel_kernel(StftMelArgs a) {
   const int64_t gb = n_groups * blockIdx.x / gridDim.x, ge = n_groups * (blockIdx.x + 1) / gridDim.x;
   float2 hw[16];  // this lane's Hann taps, w[2 (j1 + 64 r)] and w[2 (j1 + 64 r) + 1]
   lds_read16_strided<0, 64 * 8>(hw, lds_addr(sh_hann + sm_j1(lane0)));
-  // the wave's frames rise (static: g = grp * SM_WAVES + wave over the workgroup's range; dynamic:
-  // runs of dyn_frames contiguous frames taken from a.work): their sequence is tracked forward,
-  // its bounds, flags, length and offset reloaded only when g crosses into a later sequence,
-  // instead of a 64-bit division or binary search and dependent loads per frame
+  // the wave's frames g = grp * SM_WAVES + wave rise by SM_WAVES: their sequence is tracked
+  // forward, its bounds, flags, length and offset reloaded only when g crosses into a later
+  // sequence, instead of a 64-bit division or binary search and dependent loads per frame.
+  // (Round 6 measured a dynamic schedule — each wave taking runs of N contiguous frames from an
+  // atomic counter — against these static ranges: N = 128 4.64 against 3.42 ms per step isolated,
+  // N = 512 11.5: a run per wave leaves waves idle and breaks the CU's shared frame overlap;
+  // profiles/r6_ab_summary.txt.  Not kept.)
   int s = -1;
   int64_t sb = 0, se = -1, t0 = 0, L = 0, off = 0;
   int wc = -1;
   bool act = true;
-  const bool dyn = a.work != nullptr;
-  int64_t run = 0, run_end = 0;  // dynamic: the wave's current run [run, run_end)
-  for (int64_t grp = gb;;) {
-    int64_t g;
-    if (dyn) {
-      if (run >= run_end) {
-        unsigned q = 0;
-        if (lane0 == 0) q = atomicAdd(a.work, 1u);
-        q = __builtin_amdgcn_readfirstlane(q);
-        run = (int64_t)q * a.dyn_frames;
-        run_end = min(run + a.dyn_frames, a.total_frames);
-        if (run >= a.total_frames) break;
-      }
-      g = run++;
-    } else {
-      if (grp >= ge) break;
-      g = grp * SM_WAVES + wave;
-      ++grp;
-      if (g >= a.total_frames) break;
-    }
+  for (int64_t grp = gb; grp < ge; ++grp) {
+    const int64_t g = grp * SM_WAVES + wave;
+    if (g >= a.total_frames) break;
     if (g >= se) {
       if (s < 0) {
         s = a.frame_base ? seq_of_frame(a.frame_base, a.n_seq, g) : (int)(g / a.uniform_T);
@@ -487,17 +473,6 @@ int launch_stft_mel(Context& ctx, const StftMelArgs& args, hipStream_t st) {
   const int64_t n_groups = (a.total_frames + SM_WAVES - 1) / SM_WAVES;
   const int cus = ctx.stft_cus > 0 ? ctx.stft_cus : ctx.num_cu;
   const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(n_groups, (int64_t)cus * (lds <= 80 * 1024 ? 2 : 1)));
-  if (ctx.stft_dyn > 0) {  // dynamic schedule: a zeroed counter from the context's ring
-    constexpr int kRing = 64;
-    if (!ctx.work_ring) {
-      NC_HIP(hipMalloc(&ctx.work_ring, kRing * 64 * sizeof(unsigned)));
-      NC_HIP(hipMemset(ctx.work_ring, 0, kRing * 64 * sizeof(unsigned)));
-    }
-    unsigned* w = ctx.work_ring + 64 * (ctx.work_slot++ % kRing);  // one 256-B line per counter
-    NC_HIP(hipMemsetAsync(w, 0, sizeof(unsigned), st));
-    a.work = w;
-    a.dyn_frames = ctx.stft_dyn;
-  }
   {
     KTimer kt_(ctx, "stft_mel", st);
     a.span = kt_.span();

@@ -45,10 +45,6 @@ struct StftMelArgs {
   float* peak_mag;
   int* chunk_npk;
   unsigned long long* span = nullptr;  // nc_profile execution span (nc_device.h)
-  // dynamic schedule (nullable): each wave takes runs of dyn_frames contiguous frames from this
-  // zeroed counter instead of a static range per workgroup (round 6, NC_STFT_DYN)
-  unsigned* work = nullptr;
-  int dyn_frames = 0;
 };
 
 int launch_stft_mel(Context& ctx, const StftMelArgs& args, hipStream_t st);

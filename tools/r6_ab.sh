@@ -6,7 +6,7 @@
 # gather (tools/rank_step_probe.py).
 # usage: tools/r6_ab.sh TAG [ROUNDS] [SPECS]   SPEC = name:VAR=val[,VAR=val]  ("base" = no variables)
 set -o pipefail
-TAG=${1:-r6ab}; ROUNDS=${2:-2}; SPECS=${3:-"base blocks0:NC_BLOCK_ENERGY=0 dyn128:NC_STFT_DYN=128 dyn512:NC_STFT_DYN=512 xcd:NCGPU_LIB=tools/var/xcd/libncgpu.so"}
+TAG=${1:-r6ab}; ROUNDS=${2:-2}; SPECS=${3:-"base blocks0:NC_BLOCK_ENERGY=0 dyn128:NC_STFT_DYN=128 dyn512:NC_STFT_DYN=512 xcd:NCGPU_LIB=$GRAFT_REPO_ROOT/tools/var/xcd/libncgpu.so"}
 O=gpurun_out/$TAG
 mkdir -p $O
 export TMPDIR=/tmp
@@ -22,7 +22,7 @@ print('$name round $r', round(d['ms_per_step'],3), 'ms/step; stft_mel', round(d[
   done
 done
 if [ -z "$NO_PMC" ] && [ -f tools/var/xcd/libncgpu.so ]; then   # cqt_low bytes with the XCD-contiguous order
-  NCGPU_LIB=tools/var/xcd/libncgpu.so bash tools/pmc_traffic.sh $O/pmc_xcd xcd_probe_traffic.json > $O/pmc_xcd.log 2>&1 || { echo "xcd pmc failed"; tail -5 $O/pmc_xcd.log; exit 1; }
+  NCGPU_LIB=$GRAFT_REPO_ROOT/tools/var/xcd/libncgpu.so bash tools/pmc_traffic.sh $O/pmc_xcd xcd_probe_traffic.json > $O/pmc_xcd.log 2>&1 || { echo "xcd pmc failed"; tail -5 $O/pmc_xcd.log; exit 1; }
   python3 -c "
 import json; d=json.load(open('profiles/xcd_probe_traffic.json'))['kernels']
 print('xcd probe traffic', {k: d[k]['hbm_bytes_per_launch'] for k in ('cqt_low', 'cqt_high', 'stft_mel') if k in d})"
