@@ -772,7 +772,8 @@ def main():
             "config": {"workload": ("config 3: per GPU a batch of 64 x 3-min 22.05 kHz mono pairs" if world == 1 else
                                     f"config 4 shape: a batch of {world} x 64 x 3-min 22.05 kHz mono pairs, its windows "
                                     "and chunk pairs split over the ranks (sharded.shard_plan), every step's outcomes "
-                                    "all-gathered to every rank (analyze_sharded's default gather=True; without it: "
+                                    "all-gathered to every rank as record tables and every pair's result row read on "
+                                    "every rank (analyze_sharded's default gather=True; without it: "
                                     "modes.windows_nogather)" if win_mode else
                                     f"{world} x 64 x 3-min pairs, whole pairs per rank")
                                    + "; step = pipeline.run analysis of the batch without the hop-64 IBI pass"
