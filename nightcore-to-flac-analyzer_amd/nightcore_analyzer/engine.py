@@ -224,7 +224,9 @@ class _Arena:
         host = self.host
         host.copy_(self.buf, non_blocking=True)
         hb = host.numpy()
-        return host, {name: hb[o:o + n * dt.itemsize].view(dt) for (name, dt, n), o in zip(self.parts, self.offs)}
+        views = {name: hb[o:o + n * dt.itemsize].view(dt) for (name, dt, n), o in zip(self.parts, self.offs)}
+        self.host_layout = (hb, {name: (views[name], o) for (name, _, _), o in zip(self.parts, self.offs)})
+        return host, views
 
 
 @dataclass
@@ -336,6 +338,10 @@ class AsmContext:
     nj: int
     n_pitch_jobs: int
     align: Optional[list]
+    # the pinned host arena the views of ``h`` were carved from (engine._Arena.to_host: the
+    # bytes and {name: (view, byte offset)}): the record gather sends it as one array
+    arena: Optional[tuple] = None
+    starts_a: Optional[list] = None     # ``starts`` as the plan's int arrays (the record gather's form)
 
     def assemble(self, b: int, p: "Params", out: Optional["PairOutcome"] = None, wait=None, span=None) -> "PairOutcome":
         o = assemble_pair(b, p, self.h, self.ibi, self.starts, self.w0, self.w1, self.f_len, self.strip_len,
@@ -1043,11 +1049,13 @@ class Engine:
             except StopIteration as stop:
                 return stop.value
 
-    def _analyze_gen(self, batches: List[DeviceSignals], p: Params, group_pairs, log=None):
+    def _analyze_gen(self, batches: List[DeviceSignals], p: Params, group_pairs, log=None, on_group=None):
         """The body of ``_analyze_many`` as a generator that yields after each pair group is
         launched (the host is then free until the next ``next``): a caller can interleave
         other host work — the window-sharded record exchanges — with the pipelined groups
-        while up to GROUPS_IN_FLIGHT of them keep the device busy.  Returns the results."""
+        while up to GROUPS_IN_FLIGHT of them keep the device busy.  ``on_group(batch, first
+        pair, outcomes)`` runs as each group is assembled, while the later groups are still on
+        the device (the sharded result gather packs its records there).  Returns the results."""
         hs = self.host_stats
         launch = torch.cuda.current_stream(self.dev)
         # the signals are complete on the launch stream here; trims of later batches wait for
@@ -1080,6 +1088,13 @@ class Engine:
         def mark(label):
             if trace is not None:
                 trace.append((time.perf_counter(), label))
+
+        def finish(g):
+            mark(f"finish b{g['bi']} g{g['g0']}")
+            outs = self._finish_group(g, log)
+            results[g["bi"]] += outs
+            if on_group is not None:
+                on_group(g["bi"], g["g0"], outs)
 
         nxt = None
         for bi, signals in enumerate(batches):
@@ -1130,18 +1145,13 @@ class Engine:
                     # leaves the device with just a small group queued
                     while pending and (len(pending) > self.MAX_GROUPS_IN_FLIGHT or
                                        (len(pending) > 1 and pending[0]["event"].query())):
-                        g = pending.pop(0)
-                        mark(f"finish b{g['bi']} g{g['g0']}")
-                        results[g["bi"]] += self._finish_group(g, log)
+                        finish(pending.pop(0))
                 elif len(pending) > self.GROUPS_IN_FLIGHT:
-                    g = pending.pop(0)
-                    mark(f"finish b{g['bi']} g{g['g0']}")
-                    results[g["bi"]] += self._finish_group(g, log)
+                    finish(pending.pop(0))
                 mark("yield")
                 yield
         for g in pending:
-            mark(f"finish b{g['bi']} g{g['g0']}")
-            results[g["bi"]] += self._finish_group(g, log)
+            finish(g)
         mark("end")
         return results
 
@@ -1497,7 +1507,8 @@ class Engine:
                         host["ibi_" + k] = v
             ev = torch.cuda.Event()
             ev.record(s3)
-        return dict(p=p, host=host, pinned=pinned, event=ev, stage_ev=stage_ev, keep=(d, o, ar, ibi, peaks),
+        return dict(p=p, host=host, arena=ar.host_layout, pinned=pinned, event=ev, stage_ev=stage_ev,
+                    keep=(d, o, ar, ibi, peaks),
                     has_ibi=ibi is not None,
                     align=align,
                     starts=starts, w0=w0, w1=w1, f_len=f_len,
@@ -1528,7 +1539,8 @@ class Engine:
         g["w0"], g["w1"] = g["w0"].tolist(), g["w1"].tolist()
         ibi = {k[4:]: v for k, v in g["host"].items() if k.startswith("ibi_")} if g["has_ibi"] else None
         ctx = AsmContext(h, ibi, g["starts_l"], g["w0"], g["w1"], g["f_len"], g["strip_len"], g["lead"], g["trail"],
-                         g["intro"], g["win_n"], g["pair_chunks"], g["n_cp"], g["nj"], g["n_pitch_jobs"], g["align"])
+                         g["intro"], g["win_n"], g["pair_chunks"], g["n_cp"], g["nj"], g["n_pitch_jobs"], g["align"],
+                         g.get("arena"), g["starts"])
         out = []
         for b in range(g["B"]):
             o = PairOutcome()

@@ -67,8 +67,9 @@ import collections.abc
 import contextlib
 import dataclasses
 import gc
-import math
 import json
+import math
+import operator
 from dataclasses import dataclass
 from typing import Dict, List, Optional, Sequence, Tuple
 
@@ -356,48 +357,66 @@ def _opt(v) -> float:
     return _NAN if v is None else float(v)
 
 
-def result_row(o: PairOutcome) -> List[float]:
+_ROW_GET = operator.attrgetter("tempo_ratio", "tempo_ci", "pitch_ratio", "pitch_ci", "ibi_ratio", "ibi_ci",
+                                "n_source_pitch_windows", "n_nc_pitch_windows", "n_source_tempo_windows",
+                                "n_nc_tempo_windows", "nc_duration", "src_duration", "nc_median_bpm",
+                                "src_median_bpm", "intro_offset_sec")
+_ERR_ROW = (0.0,) + (_NAN,) * (len(RES_FIELDS) - 1)
+
+
+def result_row(o: PairOutcome) -> tuple:
     """The RES_FIELDS row of one outcome (NaN for None; ok = 0 for an error outcome)."""
     r = o.result
     if r is None:
-        return [0.0] + [_NAN] * (len(RES_FIELDS) - 1)
-    ic = r.ibi_ci or (None, None)
-    return [1.0, r.tempo_ratio, r.tempo_ci[0], r.tempo_ci[1], r.pitch_ratio, r.pitch_ci[0], r.pitch_ci[1],
-            _opt(r.ibi_ratio), _opt(ic[0]), _opt(ic[1]), r.n_source_pitch_windows, r.n_nc_pitch_windows,
-            r.n_source_tempo_windows, r.n_nc_tempo_windows, _opt(r.nc_duration), _opt(r.src_duration),
-            _opt(r.nc_median_bpm), _opt(r.src_median_bpm), _opt(r.intro_offset_sec)]
+        return _ERR_ROW
+    tr, tc, pr, pc, ir, ic, a, b, c, d, e, f, g, h, i = _ROW_GET(r)
+    ic = ic or (None, None)
+    return (1.0, tr, tc[0], tc[1], pr, pc[0], pc[1], _opt(ir), _opt(ic[0]), _opt(ic[1]), a, b, c, d,
+            _opt(e), _opt(f), _opt(g), _opt(h), _opt(i))
 
 
-def pack_tables(tables: Dict[str, np.ndarray]) -> bytes:
+_DTYPES: Dict[str, np.dtype] = {}
+
+
+def pack_tables(tables: Dict[str, np.ndarray], views: Optional[Dict[str, tuple]] = None) -> bytes:
     """Named numeric arrays as one byte string: an 8-byte header length, a JSON header (name,
-    dtype, shape, offset of each array) and the raw bytes, each array 8-byte aligned."""
-    meta, chunks, off = [], [], 0
+    dtype, shape, offset of each array) and the raw bytes, each array 8-byte aligned.
+    ``views``: {name: (table name, byte offset, dtype str, shape)} — arrays that are
+    stretches of another table's bytes, sent as header entries only (an arena's views)."""
+    meta, chunks, off, at = [], [], 0, {}
     for name, a in tables.items():
         a = np.asarray(a)
-        a = a if a.flags.c_contiguous else a.copy()       # (ascontiguousarray would make 0-d 1-d)
         if a.dtype.kind not in "biuf":
             raise TypeError(f"record table {name!r}: dtype {a.dtype} is not numeric")
-        meta.append((name, a.dtype.str, list(a.shape), off))
-        chunks.append(a.tobytes())
-        pad = -a.nbytes % 8
-        if pad:
-            chunks.append(b"\0" * pad)
-        off += a.nbytes + pad
+        if not a.flags.c_contiguous:
+            a = a.copy()
+        meta.append((name, a.dtype.str, a.shape, off))
+        at[name] = off
+        n = a.nbytes
+        if n:
+            chunks.append(memoryview(a.reshape(-1)).cast("B"))
+        if n % 8:
+            chunks.append(b"\0" * (-n % 8))
+        off += (n + 7) & ~7
+    for name, (base, o, dt, shape) in (views or {}).items():
+        meta.append((name, dt, shape, at[base] + o))
     head = json.dumps(meta, separators=(",", ":")).encode()
     head += b" " * (-len(head) % 8)
-    return np.array([len(head)], np.int64).tobytes() + head + b"".join(chunks)
+    return b"".join([len(head).to_bytes(8, "little"), head] + chunks)
 
 
 def unpack_tables(buf) -> Dict[str, np.ndarray]:
     """pack_tables' arrays as read-only views of ``buf`` (nothing is copied)."""
     mv = memoryview(buf)
-    n = int(np.frombuffer(mv[:8], np.int64)[0])
+    n = int.from_bytes(mv[:8], "little")
     base = 8 + n
     out = {}
     for name, dt, shape, off in json.loads(bytes(mv[8:base])):
-        dt = np.dtype(dt)
-        cnt = int(np.prod(shape)) if shape else 1
-        out[name] = np.frombuffer(mv, dt, cnt, base + off).reshape(tuple(shape))
+        d = _DTYPES.get(dt)
+        if d is None:
+            d = _DTYPES[dt] = np.dtype(dt)
+        a = np.frombuffer(mv, d, math.prod(shape), base + off)
+        out[name] = a if len(shape) == 1 else a.reshape(tuple(shape))
     return out
 
 
@@ -408,11 +427,17 @@ def _list_array(v) -> np.ndarray:
     return a if a.size else np.zeros(0, np.float64)
 
 
-def _ctx_tables(ctx: AsmContext, pre: str, out: Dict[str, np.ndarray]) -> None:
+def _ctx_tables(ctx: AsmContext, pre: str, out: Dict[str, np.ndarray], views: Dict[str, tuple]) -> None:
     """An assembly context as arrays (keys prefixed ``pre``).  Host views: every array, not the
     derived python lists ("x_l" is rebuilt from "x" by _HostViews) nor the engine's boolean
-    screens; a list with no array behind it (the split-pair path's "clag_l", ...) as its array."""
+    screens; a list with no array behind it (the split-pair path's "clag_l", ...) as its array.
+    The views still carved from the group's host arena travel as the arena's bytes once plus
+    a header entry each (``views``)."""
     h = ctx.h
+    lay = {}
+    if ctx.arena is not None:
+        hb, lay = ctx.arena
+        out[pre + "arena"] = hb
     for k, v in h.items():
         if k.startswith("ibi_") or isinstance(v, bool):
             continue
@@ -420,11 +445,16 @@ def _ctx_tables(ctx: AsmContext, pre: str, out: Dict[str, np.ndarray]) -> None:
             if k[:-2] not in h:
                 out[pre + "h." + k[:-2]] = _list_array(v)
             continue
-        out[pre + "h." + k] = np.asarray(v)
+        a = lay.get(k)
+        if a is not None and a[0] is v:
+            views[pre + "h." + k] = (pre + "arena", a[1], v.dtype.str, v.shape)
+        else:
+            out[pre + "h." + k] = np.asarray(v)
     if ctx.ibi is not None:
         for k, v in ctx.ibi.items():
             out[pre + "i." + k] = np.asarray(v)
-    starts = [np.asarray(s, np.int64) for s in ctx.starts]
+    starts = ctx.starts_a if ctx.starts_a is not None else ctx.starts
+    starts = [np.asarray(s, np.int64) for s in starts]
     out[pre + "starts"] = np.concatenate(starts) if starts else np.zeros(0, np.int64)
     out[pre + "starts_n"] = np.array([len(s) for s in starts], np.int64)
     out[pre + "w0"] = np.asarray(ctx.w0, np.int64)
@@ -443,7 +473,7 @@ def _ctx_tables(ctx: AsmContext, pre: str, out: Dict[str, np.ndarray]) -> None:
 def _ctx_from_tables(t: Dict[str, np.ndarray], pre: str) -> AsmContext:
     """_ctx_tables' inverse: the same values, types and python lists assemble_pair reads."""
     n = len(pre)
-    h = _HostViews({k[n + 2:]: v for k, v in t.items() if k.startswith(pre + "h.")})
+    h = _HostViews({k[n + 2:]: v for k, v in t.items() if k.startswith(pre + "h.")})   # (arena views included)
     win_n, n_cp, nj, n_pj, has_ibi = t[pre + "scal"].tolist()
     ibi = {k[n + 2:]: v for k, v in t.items() if k.startswith(pre + "i.")} if has_ibi else None
     flat, cnt = t[pre + "starts"].tolist(), t[pre + "starts_n"].tolist()
@@ -496,61 +526,112 @@ class _MelodiaReplay:
         return self.pick
 
 
+class _StepRecords:
+    """One rank's owned outcomes of one step as records, built a segment at a time (``add``:
+    the engine's pipeline adds each pair group as it is assembled, while later groups are still
+    on the device; the split pairs are added after their consensus).  ``bytes()``: a fixed
+    prefix the result table reads without parsing anything else — the row, segment and
+    context counts, "pairs" = (pair, context, index in the context) int64 rows, "res" =
+    RES_FIELDS f64 rows, the segment of each context and the segment lengths — then the
+    segments: pack_tables of each distinct assembly context once ("c<k>.…") and the MELODIA
+    hook's recorded answer where it ran ("m<pair>.…"), parsed only when an outcome is rebuilt."""
+
+    def __init__(self):
+        self.rows: List[Tuple[int, int, int]] = []
+        self.res: List[tuple] = []
+        self.ctx_seg: List[int] = []
+        self.segs: List[bytes] = []
+
+    def add(self, outs) -> None:
+        ctx_id: Dict[int, int] = {}
+        tables: Dict[str, np.ndarray] = {}
+        views: Dict[str, tuple] = {}
+        for b, o in outs:
+            a = o._asm
+            if a is None:
+                if o != PairOutcome():
+                    raise ValueError(f"pair {b}'s outcome was not built by assemble_pair: it cannot travel as records")
+                self.rows.append((b, -1, 0))   # an empty outcome (nothing to rebuild)
+                self.res.append(_ERR_ROW)
+                continue
+            ctx, j = a
+            k = ctx_id.get(id(ctx))
+            if k is None:
+                k = ctx_id[id(ctx)] = len(self.ctx_seg)
+                self.ctx_seg.append(len(self.segs))
+                _ctx_tables(ctx, f"c{k}.", tables, views)
+            self.rows.append((b, k, j))
+            self.res.append(result_row(o))
+            if o._melodia is not None:
+                _melodia_tables(o._melodia, f"m{b}.", tables)
+        if tables:
+            self.segs.append(pack_tables(tables, views))
+
+    def bytes(self) -> bytes:
+        n = len(self.rows)
+        head = np.array([n, len(self.segs), len(self.ctx_seg)], np.int64).tobytes()
+        return b"".join([head, np.array(self.rows, np.int64).tobytes(),
+                         np.array(self.res, np.float64).reshape(n, len(RES_FIELDS)).tobytes(),
+                         np.array(self.ctx_seg, np.int64).tobytes(),
+                         np.array([len(x) for x in self.segs], np.int64).tobytes()] + self.segs)
+
+
 def pack_outcomes(outs: List[Tuple[int, PairOutcome]]) -> bytes:
-    """A rank's owned [(global pair index, outcome)] of one step as record tables: "pairs"
-    (pair, context, index in the context), "res" (RES_FIELDS rows), each distinct assembly
-    context once ("c<k>.…") and the MELODIA hook's recorded answer where it ran ("m<i>.…")."""
-    ctx_id: Dict[int, int] = {}
-    tables: Dict[str, np.ndarray] = {}
-    rows, res = [], []
-    for i, (b, o) in enumerate(outs):
-        if o._asm is None:
-            if o != PairOutcome():
-                raise ValueError(f"pair {b}'s outcome was not built by assemble_pair: it cannot travel as records")
-            rows.append((b, -1, 0))            # an empty outcome (nothing to rebuild)
-            res.append(result_row(o))
-            continue
-        ctx, j = o._asm
-        k = ctx_id.get(id(ctx))
-        if k is None:
-            k = ctx_id[id(ctx)] = len(ctx_id)
-            _ctx_tables(ctx, f"c{k}.", tables)
-        rows.append((b, k, j))
-        res.append(result_row(o))
-        if o._melodia is not None:
-            _melodia_tables(o._melodia, f"m{i}.", tables)
-    tables["pairs"] = np.array(rows, np.int64).reshape(-1, 3)
-    tables["res"] = np.array(res, np.float64).reshape(-1, len(RES_FIELDS))
-    return pack_tables(tables)
+    """A rank's owned [(global pair index, outcome)] of one step as records (_StepRecords, one
+    segment)."""
+    rec = _StepRecords()
+    rec.add(outs)
+    return rec.bytes()
 
 
 class _Part:
-    """One rank's record tables of one step, parsed on first use."""
-    __slots__ = ("raw", "t", "ctx", "where")
+    """One rank's records of one step: the result rows read in place, a segment's assembly
+    tables parsed on the first rebuild of one of its pairs."""
+    __slots__ = ("raw", "pairs", "res", "ctx_seg", "seg", "t", "ctx", "where")
 
     def __init__(self, raw):
-        self.raw, self.t, self.ctx, self.where = raw, None, {}, None
+        mv = memoryview(raw)
+        if len(mv) < 24:
+            raise ShardError(f"a gathered record part of {len(mv)} bytes has no header")
+        n, ns, nc = np.frombuffer(mv, np.int64, 3).tolist()
+        o = 24 + 8 * n * (3 + len(RES_FIELDS)) + 8 * (nc + ns)
+        if min(n, ns, nc) < 0 or len(mv) < o:
+            raise ShardError(f"a gathered record part of {len(mv)} bytes is shorter than its header says")
+        self.pairs = np.frombuffer(mv, np.int64, 3 * n, 24).reshape(n, 3)
+        self.res = np.frombuffer(mv, np.float64, len(RES_FIELDS) * n, 24 + 24 * n).reshape(n, len(RES_FIELDS))
+        self.ctx_seg = np.frombuffer(mv, np.int64, nc, o - 8 * (nc + ns))
+        ends = o + np.cumsum(np.frombuffer(mv, np.int64, ns, o - 8 * ns))
+        if ns and ends[-1] > len(mv):
+            raise ShardError(f"a gathered record part of {len(mv)} bytes is shorter than its segments")
+        self.seg = [(int(e - l), int(e)) for l, e in zip(np.diff(ends, prepend=o), ends)]
+        self.raw = mv
+        self.t: Dict[int, Dict[str, np.ndarray]] = {}
+        self.ctx: Dict[int, AsmContext] = {}
+        self.where = None
 
-    def tables(self) -> Dict[str, np.ndarray]:
-        if self.t is None:
-            self.t = unpack_tables(self.raw)
-            self.where = {int(b): i for i, b in enumerate(self.t["pairs"][:, 0].tolist())}
-        return self.t
+    def tables(self, seg: int) -> Dict[str, np.ndarray]:
+        t = self.t.get(seg)
+        if t is None:
+            a, e = self.seg[seg]
+            t = self.t[seg] = unpack_tables(self.raw[a:e])
+        return t
 
     def outcome(self, b: int, p: Params) -> Optional[PairOutcome]:
-        t = self.tables()
+        if self.where is None:
+            self.where = {x: i for i, x in enumerate(self.pairs[:, 0].tolist())}
         i = self.where.get(b)
         if i is None:
             return None
-        _, k, j = t["pairs"][i].tolist()
+        _, k, j = self.pairs[i].tolist()
         if k < 0:
             return PairOutcome()
+        t = self.tables(int(self.ctx_seg[k]))
         ctx = self.ctx.get(k)
         if ctx is None:
             ctx = self.ctx[k] = _ctx_from_tables(t, f"c{k}.")
         span, q = None, p
-        if f"m{i}.nlines" in t:        # replay the owner's MELODIA answer and lines
-            q, span = dataclasses.replace(p, melodia=_MelodiaReplay(t, f"m{i}.")), (b, None)
+        if f"m{b}.nlines" in t:        # replay the owner's MELODIA answer and lines
+            q, span = dataclasses.replace(p, melodia=_MelodiaReplay(t, f"m{b}.")), (b, None)
         elif p.melodia is not None:
             q = dataclasses.replace(p, melodia=None)
         return ctx.assemble(j, q, span=span)
@@ -606,8 +687,7 @@ class GatheredOutcomes(collections.abc.Sequence):
         if self._table is None:
             tab = np.full((self._n, len(RES_FIELDS)), np.nan)
             for part in self._parts.values():
-                t = part.tables()
-                tab[t["pairs"][:, 0]] = t["res"]
+                tab[part.pairs[:, 0]] = part.res
             own = [(b, o) for b, o in self._items.items() if int(self._owner[b]) not in self._parts]
             if own:
                 tab[[b for b, _ in own]] = [result_row(o) for _, o in own]
@@ -668,12 +748,13 @@ class DeviceStages:
         f = np.asarray(files, np.int64)
         return DeviceStages(self.eng, DeviceSignals(self.sig.buf, self.off[f], self.length[f]), self.stream)
 
-    def pipeline(self, files: Sequence[int], p: Params, steps: int = 1):
+    def pipeline(self, files: Sequence[int], p: Params, steps: int = 1, on_group=None):
         """The engine's pipelined group generator over the pairs of `files` (interior pairs),
-        ``steps`` complete analyses back to back (Engine.analyze_batches)."""
+        ``steps`` complete analyses back to back (Engine.analyze_batches); ``on_group(step,
+        first pair, outcomes)`` as each group is assembled (Engine._analyze_gen)."""
         f = np.asarray(files, np.int64)
         return self.eng._analyze_gen([DeviceSignals(self.sig.buf, self.off[f], self.length[f])] * steps, p, None,
-                                     None)
+                                     None, on_group)
 
     def trim(self, p: Params) -> Tuple[np.ndarray, np.ndarray]:
         with torch.cuda.stream(self.stream):
@@ -1031,7 +1112,15 @@ def _analyze_sharded(stages, p, group, lengths, local_pairs, split_offset, gathe
     interior = [b for b in touched if not sp.split[b]] if err is None else []
     fast = getattr(stages, "pipeline", None) is not None and bool(interior)
     stage_pairs = ([b for b in needed if sp.split[b]] if fast else needed) if err is None else []
-    pump = _Pump(stages.pipeline(_files([pos[b] for b in interior]), _local_melodia(p, interior), steps)
+    # the result gather's records (gather over ranks): the interior groups are packed as the
+    # pipeline assembles them, while the later groups still run on the device
+    recs = [_StepRecords() for _ in range(steps)] if gather and not ex.local else None
+
+    def on_group(k, g0, outs):
+        recs[k].add(list(zip(interior[g0:g0 + len(outs)], outs)))
+
+    pump = _Pump(stages.pipeline(_files([pos[b] for b in interior]), _local_melodia(p, interior), steps,
+                                 **({"on_group": on_group} if recs is not None else {}))
                  if fast else None)
     pump(3)                                     # Engine.GROUPS_IN_FLIGHT groups queued before any wait
     split_st = stages.restrict(_files([pos[b] for b in stage_pairs]))
@@ -1044,6 +1133,8 @@ def _analyze_sharded(stages, p, group, lengths, local_pairs, split_offset, gathe
         outs, err = res
         if err is None:
             per_step.append(outs)
+            if recs is not None:
+                _, err = _try(recs[len(per_step) - 1].add, outs)
         elif not exchange:                      # no collective before the final check
             break
         # else: the next step's first gather carries the error (or the final check does)
@@ -1063,11 +1154,11 @@ def _analyze_sharded(stages, p, group, lengths, local_pairs, split_offset, gathe
     elif ex.local:
         result = [[o for _, o in outs] for outs in per_step]
     else:
-        # every rank's owned outcomes to every rank as record tables (pack_outcomes: result rows
+        # every rank's owned outcomes to every rank as record tables (_StepRecords: result rows
         # and the assembly inputs, plain arrays): one byte all-gather for the call's steps (a
         # rank's part is its steps' blobs behind a table of their lengths); the other ranks'
         # outcomes rebuilt by assemble_pair on access, their result rows readable at once
-        blobs, err = _try(lambda: _pack_steps([pack_outcomes(outs) for outs in per_step]))
+        blobs, err = _try(lambda: _pack_steps([recs[k].bytes() for k in range(len(per_step))]))
         parts = ex.gather_bytes(blobs or b"", err)          # a packing error raises on every rank
         mine = {q: _unpack_steps(parts[q], len(per_step)) for q in range(world) if q != r}
         result = [GatheredOutcomes(sp.B, sp.owner, outs, {q: mine[q][k] for q in mine}, p)

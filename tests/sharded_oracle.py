@@ -189,17 +189,20 @@ class FakeStages:
             if root._left == 0:
                 raise RuntimeError(f"injected failure in {name}")
 
-    def pipeline(self, files, p, steps=1):
+    def pipeline(self, files, p, steps=1, on_group=None):
         n = len(files) // 2
         fail = self.fail_in == "pipeline"
 
         def gen():
             from nightcore_analyzer.engine import PairOutcome
-            for _ in range(2 * steps):
+            res = [[PairOutcome() for _ in range(n)] for _ in range(steps)]
+            for k in range(2 * steps):
                 yield
                 if fail:
                     raise RuntimeError("injected failure in pipeline")
-            return [[PairOutcome() for _ in range(n)] for _ in range(steps)]
+                if on_group is not None and k % 2:        # one group per step, as it is assembled
+                    on_group(k // 2, 0, res[k // 2])
+            return res
         return gen()
 
     def trim(self, p):

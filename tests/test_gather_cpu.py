@@ -114,7 +114,69 @@ def test_result_table_without_rebuilding(outcomes):
     assert tab[2, S.RES_FIELDS.index("tempo_ratio")] == r.tempo_ratio
     assert tab[2, S.RES_FIELDS.index("ibi_hi")] == r.ibi_ci[1]
     assert np.array_equal(tab[0], tab[2], equal_nan=True) and tab[1, 0] == 0.0 and np.isnan(tab[1, 1:]).all()
-    assert _norm(tab[2].tolist()) == _norm(S.result_row(outcomes["ibi"]))
+    assert _norm(tab[2].tolist()) == _norm(list(S.result_row(outcomes["ibi"])))
+
+
+def test_records_in_segments(outcomes):
+    """A step's records built a pair group at a time (the engine pipeline's on_group hook adds
+    each group as it is assembled): every segment's pairs rebuild from their own segment, the
+    result table reads every row without parsing a segment, and a truncated part is refused."""
+    from nightcore_analyzer.engine import PairOutcome
+    o = outcomes["ibi"]
+    rec = S._StepRecords()
+    rec.add([(3, o)])
+    rec.add([(1, PairOutcome()), (0, o)])
+    rec.add([])
+    blob = rec.bytes()
+    g = S.GatheredOutcomes(4, np.array([1, 1, 0, 1]), [], {1: memoryview(blob)})
+    tab = g.table()
+    assert g.decoded() == 4 and len(g._parts[1].seg) == 2
+    assert tab[1, 0] == 0.0 and np.isnan(tab[2]).all()
+    assert _norm(tab[0].tolist()) == _norm(tab[3].tolist()) == _norm(list(S.result_row(o)))
+    assert _key(g[3]) == _key(o) and _key(g[0]) == _key(o) and g[1] == PairOutcome()
+    assert len(g._parts[1].t) == 2             # both segments parsed, once each
+    for cut in (10, len(blob) - 1):
+        with pytest.raises(S.ShardError):
+            S.GatheredOutcomes(4, np.array([1, 1, 0, 1]), [], {1: memoryview(blob[:cut])})
+
+
+def test_arena_views_travel_as_one_array(outcomes):
+    """The engine's host views are carved from one pinned arena (engine._Arena.to_host): the
+    records send the arena's bytes once and a header entry per view, and the rebuilt outcome
+    equals the owner's.  A view replaced after the arena was made travels as its own array."""
+    import dataclasses as dc
+    from nightcore_analyzer.engine import _HostViews
+    o = outcomes["ibi"]
+    ctx, j = o._asm
+    arrays = {k: np.asarray(v) for k, v in ctx.h.items()
+              if isinstance(v, np.ndarray) and not k.endswith("_l") and not k.startswith("ibi_")}
+    offs, total = {}, 0
+    for k, v in arrays.items():
+        total = (total + 15) & ~15
+        offs[k] = total
+        total += v.nbytes
+    hb = np.zeros(max(16, total), np.uint8)
+    h = _HostViews({k: v for k, v in ctx.h.items() if k not in arrays and k[:-2] not in arrays})
+    lay = {}
+    for k, v in arrays.items():
+        view = hb[offs[k]:offs[k] + v.nbytes].view(v.dtype).reshape(v.shape)
+        view[...] = v
+        h[k] = view
+        lay[k] = (view, offs[k])
+    moved = next(iter(arrays))
+    h[moved] = arrays[moved].copy()            # no longer the arena's view
+    actx = dc.replace(ctx, h=h, arena=(hb, lay))
+    ref = actx.assemble(j, CASES["ibi"])
+    assert _key(ref) == _key(o)
+    rec = S._StepRecords()
+    rec.add([(1, ref)])
+    g = S.GatheredOutcomes(2, np.array([0, 1]), [], {1: memoryview(rec.bytes())}, CASES["ibi"])
+    assert _key(g[1]) == _key(o)
+    t = g._parts[1].tables(0)
+    assert "c0.arena" in t and t["c0.arena"].nbytes == hb.nbytes
+    for k in arrays:                            # every view but the replaced one points into the arena
+        inside = np.shares_memory(t["c0.h." + k], t["c0.arena"])
+        assert inside == (k != moved), k
 
 
 def test_outcome_without_assembly_inputs_is_refused():
@@ -192,7 +254,7 @@ def test_byte_gather_three_ranks_every_rank_holds_every_outcome(outcomes):
     for r in range(3):
         keys, tab = res[r]
         assert keys == ref, (r, keys)
-        assert _norm(tab) == _norm([S.result_row(o)] * 4)
+        assert _norm(tab) == _norm([list(S.result_row(o))] * 4)
 
 
 def test_one_rank_group_runs_the_collectives_with_collect_at_one(outcomes):

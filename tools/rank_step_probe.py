@@ -62,7 +62,8 @@ def main():
             best[k].append((time.perf_counter() - t0) / K * 1e3)
             del res
     for k, v in best.items():
-        print(f"{k:>18}: {min(v):7.3f} ms/step (runs {[round(x, 3) for x in v]})", flush=True)
+        print(f"{k:>18}: {min(v):7.3f} ms/step min, {sorted(v)[len(v) // 2]:7.3f} median "
+              f"(runs {[round(x, 3) for x in v]})", flush=True)
     # where the gather's host time goes: one more windows_gather call with its parts timed
     acc = {}
 
@@ -79,7 +80,10 @@ def main():
         setattr(owner, name, w)
         return f
 
-    saved = [(S, "pack_outcomes", timed(S, "pack_outcomes")),
+    # records.add runs inside the pipeline as each group is assembled (overlapping the device);
+    # records.bytes and gather_bytes run after the last step
+    saved = [(S._StepRecords, "add", timed(S._StepRecords, "add")),
+             (S._StepRecords, "bytes", timed(S._StepRecords, "bytes")),
              (S.Exchange, "gather_bytes", timed(S.Exchange, "gather_bytes"))]
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -90,22 +94,41 @@ def main():
         setattr(owner, name, f)
     print(f"windows_gather (parts timed) {tot:.3f} ms/step; per step: " +
           ", ".join(f"{k} {v[1] / K * 1e3:.3f} ms ({v[0] / K:.1f} calls)" for k, v in acc.items()), flush=True)
+    # where records.add's time goes (cProfile around each call only)
+    import cProfile
+    import pstats
+    prof = cProfile.Profile()
+    add = S._StepRecords.add
+
+    def profiled(self, outs):
+        prof.enable()
+        try:
+            return add(self, outs)
+        finally:
+            prof.disable()
+    S._StepRecords.add = profiled
+    windows(True)
+    S._StepRecords.add = add
+    pstats.Stats(prof, stream=sys.stdout).sort_stats("tottime").print_stats(14)
     # the receive side of one rank of an 8-GPU job: 7 parts of 64 pairs per step read as tables
     own = windows(False)
-    blobs = [S.pack_outcomes(outs) for outs in own]
     import numpy as np
     B = 8 * 64
     owner = np.repeat(np.arange(8), 64)
+    # rank q's part of step k: this rank's records with the pairs numbered as rank q's (64 q + i),
+    # one segment per assembly group as the pipeline builds them
+
+    def step_blob(outs, q):
+        rec, groups = S._StepRecords(), {}
+        for b, o in outs:
+            groups.setdefault(id(o._asm[0]) if o._asm is not None else -1, []).append((b + 64 * q, o))
+        for v in groups.values():
+            rec.add(v)
+        return rec.bytes()
+    blobs = [{q: step_blob(outs, q) for q in range(1, 8)} for outs in own]
     t0 = time.perf_counter()
     for k in range(K):
-        parts = {q: memoryview(blobs[k]) for q in range(1, 8)}
-        g = S.GatheredOutcomes(B, owner, [], parts, params)
-        # rank q's part holds pairs 0..63 of its own numbering: shift to the global indices
-        for q, part in g._parts.items():
-            t = part.tables()
-            t["pairs"] = t["pairs"].copy()
-            t["pairs"][:, 0] += 64 * q
-            part.where = {int(b): i for i, b in enumerate(t["pairs"][:, 0].tolist())}
+        g = S.GatheredOutcomes(B, owner, [], {q: memoryview(v) for q, v in blobs[k].items()}, params)
         tab = g.table()
     rx = (time.perf_counter() - t0) / K * 1e3
     t0 = time.perf_counter()
@@ -116,7 +139,7 @@ def main():
     rb = (time.perf_counter() - t0) / n * 1e3
     print(f"receive (7 parts x 64 pairs as result tables): {rx:.3f} ms/step; {np.isnan(tab[64:, 1]).sum()} missing "
           f"rows; whole-outcome rebuild from records: {rb:.3f} ms per pair; "
-          f"blob {len(blobs[0]) / 1024:.1f} KiB per rank-step", flush=True)
+          f"blob {len(blobs[0][1]) / 1024:.1f} KiB per rank-step", flush=True)
     dist.destroy_process_group()
 
 
