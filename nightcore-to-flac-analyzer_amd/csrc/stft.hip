@@ -44,6 +44,9 @@ constexpr size_t SM_LDS_RESERVE = 150 * 1024;
 #ifndef SM_NOEN_
 #define SM_NOEN_ 0  // timing probe: the frame energies left out even when asked for (outputs wrong)
 #endif
+#ifndef SM_SYNC_
+#define SM_SYNC_ 0  // probe: a workgroup barrier every SM_SYNC_ frame groups (keeps the waves' frames together)
+#endif
 using SmTw = StagedTw<1024>;  // per-stage twiddle table in LDS (conflict-free reads)
 
 // Mel band loops with compile-time trip counts, unrolled in load batches: 562-576 against
@@ -260,6 +263,7 @@ __global__ __launch_bounds__(SM_THREADS) void stft_mel_kernel(StftMelArgs a) {
   int wc = -1;
   bool act = true;
   for (int64_t grp = gb; grp < ge; ++grp) {
+    if (SM_SYNC_ > 0 && (grp - gb) % SM_SYNC_ == 0) __syncthreads();
     const int64_t g = grp * SM_WAVES + wave;
     if (g >= a.total_frames) break;
     if (g >= se) {

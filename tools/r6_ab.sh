@@ -5,6 +5,7 @@
 # then the CU-partitioned chains (tools/cu_split_ab.sh) and one rank's N > 1 step with the record
 # gather (tools/rank_step_probe.py).
 # usage: tools/r6_ab.sh TAG [ROUNDS] [SPECS]   SPEC = name:VAR=val[,VAR=val]  ("base" = no variables)
+# NO_PMC / NO_CU / NO_RANK skip the XCD counter pass, the CU split and the rank probe
 set -o pipefail
 TAG=${1:-r6ab}; ROUNDS=${2:-2}; SPECS=${3:-"base blocks0:NC_BLOCK_ENERGY=0 dyn128:NC_STFT_DYN=128 dyn512:NC_STFT_DYN=512 xcd:NCGPU_LIB=$GRAFT_REPO_ROOT/tools/var/xcd/libncgpu.so"}
 O=gpurun_out/$TAG
@@ -30,5 +31,7 @@ fi
 if [ -z "$NO_CU" ]; then
   bash tools/cu_split_ab.sh $TAG/cu 2 "none 128 160 96 128:low" || exit 1
 fi
-timeout -k 10 300 python3 -u tools/rank_step_probe.py 10 3 > $O/rank_step_probe.txt 2>&1 || { echo "rank probe failed"; tail -10 $O/rank_step_probe.txt; exit 1; }
-cat $O/rank_step_probe.txt
+if [ -z "$NO_RANK" ]; then
+  timeout -k 10 300 python3 -u tools/rank_step_probe.py 10 3 > $O/rank_step_probe.txt 2>&1 || { echo "rank probe failed"; tail -10 $O/rank_step_probe.txt; exit 1; }
+  cat $O/rank_step_probe.txt
+fi
