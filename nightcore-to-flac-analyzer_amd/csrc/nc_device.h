@@ -32,6 +32,24 @@ __device__ __forceinline__ float2 cscale(float2 a, float s) { return make_float2
 // multiply by -i
 __device__ __forceinline__ float2 cmul_mi(float2 a) { return make_float2(a.y, -a.x); }
 
+// 10 * log10f(fmaxf(1e-10f, x)) bit for bit (librosa power_to_db's floor, amin = 1e-10): the
+// floored argument is a normal float, so log10f's denormal rescale (v_ldexp, two selects and the
+// subtract of its offset) is dropped; what stays is its own sequence, v_log_f32 and the product
+// with log10(2) compensated in f32 (ch + cl), and its non-finite select.  9 VALU against 14.
+#ifndef NC_DB_LIB_
+#define NC_DB_LIB_ 0  // A/B probe: the library log10f instead
+#endif
+__device__ __forceinline__ float db10_floor(float x) {
+  if (NC_DB_LIB_) return 10.0f * log10f(fmaxf(1e-10f, x));
+  const float l = __builtin_amdgcn_logf(fmaxf(1e-10f, x));
+  const float ch = __uint_as_float(0x3e9a209au), cl = __uint_as_float(0x3284fbcfu);
+  const float ph = __fmul_rn(l, ch);
+  float e = __builtin_fmaf(l, ch, -ph);
+  e = __builtin_fmaf(l, cl, e);
+  const float r = __builtin_fmaf(ch, l, e);
+  return 10.0f * (__builtin_fabsf(l) < __builtin_inff() ? r : l);
+}
+
 // ------------------------------------------------------------------ wave reductions
 __device__ __forceinline__ float wave_max(float v) {
 #pragma unroll

@@ -163,7 +163,7 @@ __global__ __launch_bounds__(SF_THREADS) void spectral_frames_kernel(SpecArgs a)
     // 9 % slower: 5.19 against 4.78 ms per 128 files)
     auto bin = [&](int k) {
       const float s = mag[k];
-      row[k] = 10.0f * log10f(fmaxf(1e-10f, s * s));
+      row[k] = db10_floor(s * s);  // = 10 log10f(max(1e-10, s^2)), bit for bit
       l1 += (double)s;
       m1 = fma((double)k, (double)s, m1);
       mx = fmaxf(mx, s);

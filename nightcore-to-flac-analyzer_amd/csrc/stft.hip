@@ -44,8 +44,18 @@ constexpr size_t SM_LDS_RESERVE = 150 * 1024;
 #ifndef SM_NOEN_
 #define SM_NOEN_ 0  // timing probe: the frame energies left out even when asked for (outputs wrong)
 #endif
+// Round 6 (profiles/r6_stft_sync_*.txt): the free-running waves of a workgroup
+// drift apart by tens of frame groups, so the 4x frame overlap is re-fetched from beyond the L2:
+// reads 1.62x the algorithmic bytes.  Keeping them together with a bare s_barrier every 8 groups
+// (SM_SYNC_=8) cuts the reads to 1.02x, but costs 3.6 % of the kernel's time (457.4 against 441.3 us
+// per 560 windows; every 32 groups: 1.44x, +1.2 %; __syncthreads every 1-32 groups: +4-22 %); each
+// wave walking its own contiguous run (SM_RUN_=1) reads 1.96x and is 1-10 % slower.  The kernel is
+// not bound by its HBM bytes, so the waves stay free-running.
 #ifndef SM_SYNC_
 #define SM_SYNC_ 0  // probe: a workgroup barrier every SM_SYNC_ frame groups (keeps the waves' frames together)
+#endif
+#ifndef SM_RUN_
+#define SM_RUN_ 0  // probe: each wave walks a contiguous run of the workgroup's frames (1/16 of its range)
 #endif
 using SmTw = StagedTw<1024>;  // per-stage twiddle table in LDS (conflict-free reads)
 
@@ -262,9 +272,16 @@ __global__ __launch_bounds__(SM_THREADS) void stft_mel_kernel(StftMelArgs a) {
   int64_t sb = 0, se = -1, t0 = 0, L = 0, off = 0;
   int wc = -1;
   bool act = true;
-  for (int64_t grp = gb; grp < ge; ++grp) {
-    if (SM_SYNC_ > 0 && (grp - gb) % SM_SYNC_ == 0) __syncthreads();
-    const int64_t g = grp * SM_WAVES + wave;
+  int64_t it0 = gb, it1 = ge;
+  if (SM_RUN_) {
+    const int64_t fb = a.total_frames * blockIdx.x / gridDim.x, fe = a.total_frames * (blockIdx.x + 1) / gridDim.x;
+    it0 = fb + (fe - fb) * wave / SM_WAVES;
+    it1 = fb + (fe - fb) * (wave + 1) / SM_WAVES;
+  }
+  for (int64_t grp = it0; grp < it1; ++grp) {
+    // (the probe's barrier orders nothing in memory: a bare s_barrier, no vmcnt / lgkmcnt drain)
+    if (!SM_RUN_ && SM_SYNC_ > 0 && (grp - gb) % SM_SYNC_ == 0) __builtin_amdgcn_s_barrier();
+    const int64_t g = SM_RUN_ ? grp : grp * SM_WAVES + wave;
     if (g >= a.total_frames) break;
     if (g >= se) {
       if (s < 0) {
@@ -401,8 +418,8 @@ __global__ __launch_bounds__(SM_THREADS) void stft_mel_kernel(StftMelArgs a) {
     const int mt0 = sh_mt[lane], mt1 = sh_mt[64 + lane];
     mel_unrolled<J0>(pw, mw4, mt0 & 2047, (mt0 >> 11) & 31, lane, acc0);
     mel_unrolled<J1>(pw, mw4 + J0 * 64, mt1 & 2047, (mt1 >> 11) & 31, lane, acc1);
-    const float db0 = 10.0f * log10f(fmaxf(1e-10f, acc0));
-    const float db1 = 10.0f * log10f(fmaxf(1e-10f, acc1));
+    const float db0 = db10_floor(acc0);  // = 10 log10f(max(1e-10, acc0)), bit for bit
+    const float db1 = db10_floor(acc1);
     float* row = a.sdb + g * 128;
     row[mt0 >> 16] = db0;
     row[mt1 >> 16] = db1;
