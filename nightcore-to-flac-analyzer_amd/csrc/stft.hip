@@ -280,7 +280,7 @@ __global__ __launch_bounds__(SM_THREADS) void stft_mel_kernel(StftMelArgs a) {
   }
   for (int64_t grp = it0; grp < it1; ++grp) {
     // (the probe's barrier orders nothing in memory: a bare s_barrier, no vmcnt / lgkmcnt drain)
-    if (!SM_RUN_ && SM_SYNC_ > 0 && (grp - gb) % SM_SYNC_ == 0) __builtin_amdgcn_s_barrier();
+    if (!SM_RUN_ && SM_SYNC_ > 0 && (grp - gb) % (SM_SYNC_ > 0 ? SM_SYNC_ : 1) == 0) __builtin_amdgcn_s_barrier();
     const int64_t g = SM_RUN_ ? grp : grp * SM_WAVES + wave;
     if (g >= a.total_frames) break;
     if (g >= se) {
