@@ -1118,6 +1118,14 @@ struct C2 {
 #ifndef C2_SAFE_
 #define C2_SAFE_ 0
 #endif
+// C2_NOBW_=1 (timing probe, outputs wrong): octave C2_NOBW_OCT_ splits its next block without
+// waiting for its loads, i.e. the cost of the block loads' exposed latency
+#ifndef C2_NOBW_
+#define C2_NOBW_ 0
+#endif
+#ifndef C2_NOBW_OCT_
+#define C2_NOBW_OCT_ 0
+#endif
 template <int OCT, int Q>
 __device__ __forceinline__ void c2_wait_slice(bool last) {
   if (C2_SAFE_) {
@@ -1315,7 +1323,7 @@ __device__ __forceinline__ void cqt_low_tile(const CqmArgs& a, int bx, int c) {
       // group g is done (their registers were consumed above).  vmcnt(0), not a count: younger
       // slice pieces can retire before the block loads (header).  Splitting after the first or
       // third column tile of the step instead: 351.4 / 350.2 against 347.7 us (round 5)
-      c2_vmwait_st<0>(st);
+      if (!(C2_NOBW_ && OCT == C2_NOBW_OCT_)) c2_vmwait_st<0>(st);
       if (active) c2_split<OCT>(st, img, sx, s0, g + 1, Ly, EDGE, lane);
     }
   };
@@ -1324,6 +1332,7 @@ __device__ __forceinline__ void cqt_low_tile(const CqmArgs& a, int bx, int c) {
     const bool last = g == G - 1;
     static_for<M>([&](auto qc) { step(qc, g, last); });
   }
+  if (C2_NOBW_) c2_vmwait<0>();  // (probe) the skipped block waits' loads land before the epilogue
   if (!active) return;
   const int nrow = min(C2_FR, T - t0);
   float* mg = reinterpret_cast<float*>(img);  // [C2_FR][36] rows over this wave's own images
