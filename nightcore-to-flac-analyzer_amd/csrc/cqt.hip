@@ -327,6 +327,9 @@ __global__ __launch_bounds__(D3_NT) void decimate3_kernel(const float* sig, cons
 // at an atomically reserved position: the median and the histogram that consume them
 // do not depend on the order, so the result stays deterministic.
 constexpr int TP_WAVES = 16;  // 14 -> 16 waves: 537 -> 495 us per 224 chunks (with the LDS Hann window)
+#ifndef TP_DYN_
+#define TP_DYN_ 1  // the workgroup's frames from its LDS counter (0: the static interleave; A/B)
+#endif
 using TpTw = StagedTw<1024>;
 
 struct PeakArgs {
@@ -354,6 +357,8 @@ __global__ __launch_bounds__(TP_WAVES * 64) void tuning_peaks_kernel(PeakArgs a)
   const int lane0 = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform (SGPR)
   float2* sh_hann = sh_tw + ((TpTw::size + 1) & ~1);  // [1024] window pairs (h[2n], h[2n + 1])
   float2* fftbuf = sh_hann + 1024 + wave * LdsSize<1024>::value;
+  __shared__ int sh_next;  // the workgroup's frame queue (WgFrameQueue)
+  if (threadIdx.x == 0) sh_next = 0;
   fill_staged_tw<1024>(sh_tw, a.tw, threadIdx.x, TP_WAVES * 64);
   for (int i = threadIdx.x; i < 1024; i += TP_WAVES * 64) sh_hann[i] = reinterpret_cast<const float2*>(a.hann2048)[i];
   __syncthreads();
@@ -362,14 +367,17 @@ __global__ __launch_bounds__(TP_WAVES * 64) void tuning_peaks_kernel(PeakArgs a)
   lds_read16_strided<0, 64 * 8>(hw, lds_addr(sh_hann + fft_in_lane(lane0)));
   const int64_t n_groups = (a.total_tframes + TP_WAVES - 1) / TP_WAVES;
   const int64_t gb = n_groups * blockIdx.x / gridDim.x, ge = n_groups * (blockIdx.x + 1) / gridDim.x;
-  // The wave's work-list frames gf rise by TP_WAVES: their chunk is tracked forward, its
-  // bounds and descriptors reloaded only when gf crosses into a later chunk (no binary search
-  // and dependent loads per frame)
+  // The workgroup's work-list frames [f0, f1) go to its waves one at a time (WgFrameQueue, as in
+  // stft_mel); a wave's frames gf rise: their chunk is tracked forward, its bounds and
+  // descriptors reloaded only when gf crosses into a later chunk (no binary search and
+  // dependent loads per frame).  TP_DYN_=0: the static interleave (wave w: frames 16 G + w)
+  const int64_t f0 = gb * TP_WAVES, f1 = std::min<int64_t>(ge * TP_WAVES, a.total_tframes);
+  WgFrameQueue fq(&sh_next, lane0);
   int c = -1, nt = 0, skip = 0;
   int64_t cb = 0, ce = -1, coff = 0, clen = 0, ctf = 0;
-  for (int64_t grp = gb; grp < ge; ++grp) {
-    const int64_t gf = grp * TP_WAVES + wave;
-    if (gf >= a.total_tframes) break;
+  for (int64_t grp = gb; TP_DYN_ || grp < ge; ++grp) {
+    const int64_t gf = TP_DYN_ ? f0 + fq.take(lane0) : grp * TP_WAVES + wave;
+    if (gf >= (TP_DYN_ ? f1 : a.total_tframes)) break;
     if (gf >= ce) {
       if (c < 0) {
         int lo = 0, hi = a.n_chunks - 1;

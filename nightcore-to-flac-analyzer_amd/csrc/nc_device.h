@@ -50,6 +50,32 @@ __device__ __forceinline__ float db10_floor(float x) {
   return 10.0f * (__builtin_fabsf(l) < __builtin_inff() ? r : l);
 }
 
+// ------------------------------------------------------------------ workgroup frame queue
+// A persistent workgroup's frames handed to its waves one at a time from an LDS counter (round 6):
+// the frames in flight are always the ones taken last, whatever the waves' relative speeds, so
+// neighbouring frames (which share 3/4 of their samples) meet in L1 / L2 together, and no wave
+// idles at the end while another still holds a static share.  A static interleave (wave w: frames
+// 16 G + w) let the waves drift tens of groups apart: stft_mel read 1.62x its algorithmic bytes
+// and ran 9.8 % slower.  Each wave reserves its next frame when it starts one, so the atomic's
+// latency hides under the frame.  `ctr` is zeroed before the workgroup barrier that precedes the
+// first take; frames come out increasing per wave (the descriptor tracking relies on it).
+struct WgFrameQueue {
+  int* ctr;
+  int nx;  // lane 0: the reserved frame
+  __device__ __forceinline__ int reserve(int lane) {
+    int r = 0;
+    if (lane == 0) r = atomicAdd(ctr, 1);
+    return r;
+  }
+  __device__ __forceinline__ WgFrameQueue(int* c, int lane) : ctr(c) { nx = reserve(lane); }
+  // the next frame index of this workgroup's range (>= its frame count: done)
+  __device__ __forceinline__ int take(int lane) {
+    const int n = __builtin_amdgcn_readfirstlane(nx);
+    nx = reserve(lane);
+    return n;
+  }
+};
+
 // ------------------------------------------------------------------ wave reductions
 __device__ __forceinline__ float wave_max(float v) {
 #pragma unroll

@@ -79,20 +79,25 @@ __global__ __launch_bounds__(SF_THREADS) void spectral_frames_kernel(SpecArgs a)
   const int lane0 = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   float2* fftbuf = sh_tw + sf_al4(SfTw::size) + wave * LdsSize<1024>::value;
 
+  __shared__ int sh_next;  // the workgroup's frame queue (WgFrameQueue)
+  if (threadIdx.x == 0) sh_next = 0;
   fill_staged_tw<1024>(sh_tw, a.tw, threadIdx.x, SF_THREADS);
   __syncthreads();
 
   const int64_t n_groups = (a.total_frames + SF_WAVES - 1) / SF_WAVES;
   const int64_t gb = n_groups * blockIdx.x / gridDim.x, ge = n_groups * (blockIdx.x + 1) / gridDim.x;
-  // The wave's frames rise by SF_WAVES: the file and its descriptors (bounds, length, offset,
-  // band bins) are reloaded only when g crosses into a later file, instead of a binary search
-  // and a chain of dependent loads per frame (the stft_mel scheme)
+  // The workgroup's frames [f0, f1) go to its waves one at a time (WgFrameQueue, the stft_mel
+  // scheme); a wave's frames rise: the file and its descriptors (bounds, length, offset, band
+  // bins) are reloaded only when g crosses into a later file, instead of a binary search and a
+  // chain of dependent loads per frame
+  const int64_t f0 = gb * SF_WAVES, f1 = std::min<int64_t>(ge * SF_WAVES, a.total_frames);
+  WgFrameQueue fq(&sh_next, lane0);
   int f = -1;
   int64_t fb = 0, fe = -1, L = 0, off = 0;
   int blo[SF_NBANDS], bhi[SF_NBANDS];
-  for (int64_t grp = gb; grp < ge; ++grp) {
-    const int64_t g = grp * SF_WAVES + wave;
-    if (g >= a.total_frames) break;
+  for (;;) {
+    const int64_t g = f0 + fq.take(lane0);
+    if (g >= f1) break;
     if (g >= fe) {
       if (f < 0) {
         f = sf_file_of(a.frame_base, a.n_files, g);

@@ -44,18 +44,23 @@ constexpr size_t SM_LDS_RESERVE = 150 * 1024;
 #ifndef SM_NOEN_
 #define SM_NOEN_ 0  // timing probe: the frame energies left out even when asked for (outputs wrong)
 #endif
-// Round 6 (profiles/r6_stft_sync_*.txt): the free-running waves of a workgroup
-// drift apart by tens of frame groups, so the 4x frame overlap is re-fetched from beyond the L2:
-// reads 1.62x the algorithmic bytes.  Keeping them together with a bare s_barrier every 8 groups
+// Round 6 (profiles/r6_stft_sync_*.txt): with a static interleave (wave w: frames
+// 16 G + w) the free-running waves of a workgroup drift apart by tens of frame groups, so the 4x
+// frame overlap is re-fetched from beyond the L2: reads 1.62x the algorithmic bytes.  Keeping them together with a bare s_barrier every 8 groups
 // (SM_SYNC_=8) cuts the reads to 1.02x, but costs 3.6 % of the kernel's time (457.4 against 441.3 us
 // per 560 windows; every 32 groups: 1.44x, +1.2 %; __syncthreads every 1-32 groups: +4-22 %); each
-// wave walking its own contiguous run (SM_RUN_=1) reads 1.96x and is 1-10 % slower.  The kernel is
+// wave walking its own contiguous run (a probe since removed) reads 1.96x and is 1-10 % slower.  The kernel is
 // not bound by its HBM bytes, so the waves stay free-running.
 #ifndef SM_SYNC_
-#define SM_SYNC_ 0  // probe: a workgroup barrier every SM_SYNC_ frame groups (keeps the waves' frames together)
+#define SM_SYNC_ 0  // probe (static interleave only): a barrier every SM_SYNC_ frame groups
 #endif
-#ifndef SM_RUN_
-#define SM_RUN_ 0  // probe: each wave walks a contiguous run of the workgroup's frames (1/16 of its range)
+// The fix (round 6): the sixteen waves take the workgroup's frames one at a time from an LDS
+// counter (SM_DYN_, default), so the frames in flight are always the sixteen most recently taken,
+// whatever the waves' relative speeds: reads 1.62x -> 1.00x algorithmic, 443.1 -> 399.8 us per 560
+// windows (-9.8 %), the wave that finishes first no longer idles at the end of the range, outputs
+// bit-identical (profiles/r6_stft_dyn_var_bench.txt).  SM_DYN_=0 restores the static interleave.
+#ifndef SM_DYN_
+#define SM_DYN_ 1
 #endif
 using SmTw = StagedTw<1024>;  // per-stage twiddle table in LDS (conflict-free reads)
 
@@ -244,6 +249,8 @@ __global__ __launch_bounds__(SM_THREADS) void stft_mel_kernel(StftMelArgs a) {
   int* sh_mt = reinterpret_cast<int*>(sh_hann + SM_HANN2);
   float2* slot = reinterpret_cast<float2*>(sh_mt + SM_MT) + wave * SM_HALF;
 
+  __shared__ int sh_next;  // SM_DYN_: the workgroup's next frame
+  if (threadIdx.x == 0) sh_next = 0;
   fill_staged_tw<1024>(sh_tw, a.tw, threadIdx.x, SM_THREADS);
   for (int i = threadIdx.x; i < SM_HANN2; i += SM_THREADS) sh_hann[i] = reinterpret_cast<const float2*>(a.hann2048)[i];
   for (int i = threadIdx.x; i < (a.mel_j0 + a.mel_j1) * 64; i += SM_THREADS) sh_w4[i] = a.mel_w4[i];
@@ -264,25 +271,28 @@ __global__ __launch_bounds__(SM_THREADS) void stft_mel_kernel(StftMelArgs a) {
   // the wave's frames g = grp * SM_WAVES + wave rise by SM_WAVES: their sequence is tracked
   // forward, its bounds, flags, length and offset reloaded only when g crosses into a later
   // sequence, instead of a 64-bit division or binary search and dependent loads per frame.
-  // (Round 6 measured a dynamic schedule — each wave taking runs of N contiguous frames from an
-  // atomic counter — against these static ranges: N = 128 4.64 against 3.42 ms per step isolated,
-  // N = 512 11.5: a run per wave leaves waves idle and breaks the CU's shared frame overlap;
-  // profiles/r6_ab_summary.txt.  Not kept.)
+  // (The workgroups keep static, balanced frame ranges: a chip-wide counter handing each wave runs
+  // of N contiguous frames measured 4.64 (N = 128) and 11.5 (N = 512) against 3.42 ms per step
+  // isolated — runs leave waves idle and break the CU's shared frame overlap,
+  // profiles/r6_ab_summary.txt.  Inside a workgroup the frames are handed out one at a time.)
   int s = -1;
   int64_t sb = 0, se = -1, t0 = 0, L = 0, off = 0;
   int wc = -1;
   bool act = true;
-  int64_t it0 = gb, it1 = ge;
-  if (SM_RUN_) {
-    const int64_t fb = a.total_frames * blockIdx.x / gridDim.x, fe = a.total_frames * (blockIdx.x + 1) / gridDim.x;
-    it0 = fb + (fe - fb) * wave / SM_WAVES;
-    it1 = fb + (fe - fb) * (wave + 1) / SM_WAVES;
-  }
-  for (int64_t grp = it0; grp < it1; ++grp) {
-    // (the probe's barrier orders nothing in memory: a bare s_barrier, no vmcnt / lgkmcnt drain)
-    if (!SM_RUN_ && SM_SYNC_ > 0 && (grp - gb) % (SM_SYNC_ > 0 ? SM_SYNC_ : 1) == 0) __builtin_amdgcn_s_barrier();
-    const int64_t g = SM_RUN_ ? grp : grp * SM_WAVES + wave;
-    if (g >= a.total_frames) break;
+  // SM_DYN_: the workgroup's frames [f0, f1) one at a time from its LDS counter (WgFrameQueue)
+  const int64_t f0 = gb * SM_WAVES, f1 = std::min<int64_t>(ge * SM_WAVES, a.total_frames);
+  WgFrameQueue fq(&sh_next, lane0);
+  for (int64_t grp = gb; SM_DYN_ || grp < ge; ++grp) {
+    int64_t g;
+    if (SM_DYN_) {
+      g = f0 + fq.take(lane0);
+      if (g >= f1) break;
+    } else {
+      // (the probe's barrier orders nothing in memory: a bare s_barrier, no vmcnt / lgkmcnt drain)
+      if (SM_SYNC_ > 0 && (grp - gb) % (SM_SYNC_ > 0 ? SM_SYNC_ : 1) == 0) __builtin_amdgcn_s_barrier();
+      g = grp * SM_WAVES + wave;
+      if (g >= a.total_frames) break;
+    }
     if (g >= se) {
       if (s < 0) {
         s = a.frame_base ? seq_of_frame(a.frame_base, a.n_seq, g) : (int)(g / a.uniform_T);
