@@ -60,7 +60,11 @@ int nc_num_cu(const nc_ctx* ctx);
  *         ("stft_mel", "cqt_low", "cqt_high", "window_tg"), spans for every kernel (the
  *         other kernels' event records are host and queue work a timed region need not
  *         carry); on = 4: the events of on = 3 without spans (the spans' per-workgroup clock
- *         reads and atomics cost the step ~3 %); on = 0: off.
+ *         reads and atomics cost the step ~3 %); on = 5: the spans of on = 2 plus marker
+ *         spans around the small entry points (nc_energy_gate, nc_collect_valid, nc_pitch_hz,
+ *         nc_tempo_prior, nc_bootstrap_ratio, nc_chroma_lag*, nc_window_energy_blocks and the
+ *         chroma plan / tail and trim bounds inside the larger ones: two one-thread marker
+ *         launches each, timeline diagnosis only); on = 0: off.
  * nc_profile_read(tag) waits for the recorded launches, returns their summed event
  * duration and count, and resets the tag's events.  nc_profile_read_span(tag) returns
  * the summed execution spans (first wave start .. last wave end on the device wall
@@ -68,7 +72,7 @@ int nc_num_cu(const nc_ctx* ctx);
  * queues behind other streams' work) and resets the tag's spans.  Tags: "stft_mel",
  * "window_tg", "tuning_peaks", "decimate", "cqt_chroma", "trim_blocks", "tempo_beat",
  * "tg_slide", "spectral_frames", "spectral_bins".  Enabling (or disabling) discards
- * pending records.  nc_profile_read_busy (modes 1-3) returns the union of every span
+ * pending records.  nc_profile_read_busy (modes 1-3, 5) returns the union of every span
  * recorded since the last read, all tags together (device busy time), the extent from the
  * first start to the last end, and the number of spanned launches, and clears the spans:
  * 1 - busy / extent is the device's idle fraction over those launches. */

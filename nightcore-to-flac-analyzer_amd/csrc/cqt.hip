@@ -1586,9 +1586,12 @@ int launch_chroma_mean(Context& ctx, const float* sig, const int64_t* chunk_off,
     w.chunk_npk = ext_npk;
   }
 
-  hipLaunchKernelGGL(chroma_plan_kernel, dim3(1), dim3(256), 0, st, chunk_len, n, w.oct_off, w.oct_len, w.n_frames,
-                     w.n_tframes, w.tf_base, w.oct_base, tf_skip, tp_base);
-  if (!ext) NC_HIP(hipMemsetAsync(w.chunk_npk, 0, sizeof(int) * n, st));
+  {
+    MarkSpan ms_(ctx, "chroma_plan", st);
+    hipLaunchKernelGGL(chroma_plan_kernel, dim3(1), dim3(256), 0, st, chunk_len, n, w.oct_off, w.oct_len, w.n_frames,
+                       w.n_tframes, w.tf_base, w.oct_base, tf_skip, tp_base);
+    if (!ext) NC_HIP(hipMemsetAsync(w.chunk_npk, 0, sizeof(int) * n, st));
+  }
   // grids are sized by the longest chunk; blocks past a chunk's own length exit.  (Forking
   // the decimation onto a second stream, concurrent with the tuning estimate, measured no
   // gain: the chip is already full with the window chain on the caller's other stream.)
@@ -1675,9 +1678,12 @@ int launch_chroma_mean(Context& ctx, const float* sig, const int64_t* chunk_off,
       hipLaunchKernelGGL(cqt_mfma_kernel, dim3((unsigned)((1 + max_chunk_len / 512 + CH_FR - 1) / CH_FR), n),
                          dim3(CM_NTH), cqm_lds_bytes(), st, ma);
   }
-  hipLaunchKernelGGL(cqt_tail_kernel, dim3(ntile, n), dim3(256), 0, st, w.gpart, w.tf_base, w.n_frames, w.partial);
-  hipLaunchKernelGGL(chroma_finalize_kernel, dim3(n), dim3(64), 0, st, w.partial, w.tf_base, w.n_frames, n, CM_FR,
-                     out_chroma);
+  {
+    MarkSpan ms_(ctx, "cqt_tail", st);
+    hipLaunchKernelGGL(cqt_tail_kernel, dim3(ntile, n), dim3(256), 0, st, w.gpart, w.tf_base, w.n_frames, w.partial);
+    hipLaunchKernelGGL(chroma_finalize_kernel, dim3(n), dim3(64), 0, st, w.partial, w.tf_base, w.n_frames, n, CM_FR,
+                       out_chroma);
+  }
   NC_HIP(hipGetLastError());
   return 0;
 }

@@ -73,6 +73,19 @@ int launch_window_energy(const float* sig, const int64_t* off, int n, int win_le
   return 0;
 }
 
+// profile mode 5 (MarkSpan, nc_prof.cpp): the wall clock when the stream reaches this launch,
+// into the span slot's first line (start: min, end: max), as span_record does for a kernel
+__global__ void span_mark_kernel(unsigned long long* sp, int end) {
+  const unsigned long long t = wall_clock64();
+  if (end) atomicMax(sp + 1, t);
+  else atomicMin(sp, t);
+}
+
+int launch_span_mark(unsigned long long* span, int end, hipStream_t st) {
+  hipLaunchKernelGGL(span_mark_kernel, dim3(1), dim3(1), 0, st, span, end);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
 int launch_energy_gate(const double* energy, const int* w0, const int* w1, int n_groups, double gate_db,
                        uint8_t* active, hipStream_t st) {
   if (n_groups <= 0) return 0;

@@ -188,9 +188,10 @@ int nc_num_cu(const nc_ctx* ctx) { return ctx ? ctx->c.num_cu : -1; }
 int nc_profile_enable(nc_ctx* ctx, int on) {
   CHECK_CTX(ctx);
   SET_DEVICE(ctx);
-  if (on < 0 || on > 4) {
+  if (on < 0 || on > 5) {
     nc::set_error("nc_profile_enable: mode must be 0 (off), 1 (events + spans), 2 (spans only), 3 "
-                  "(events around the roofline kernels + spans) or 4 (events around the roofline kernels)");
+                  "(events around the roofline kernels + spans), 4 (events around the roofline kernels) or 5 "
+                  "(spans + marker spans around the small entry points)");
     return -1;
   }
   nc::profile_enable(ctx->c, on);
@@ -299,6 +300,7 @@ int nc_tempo_prior(nc_ctx* ctx, const double* bpm, const int* nbeats, const uint
                    double* prior_out, void* stream) {
   CHECK_CTX(ctx);
   SET_DEVICE(ctx);
+  nc::MarkSpan ms_(ctx->c, "tempo_prior", (hipStream_t)stream);
   return nc::launch_nc_prior(bpm, nbeats, active, src_w0, src_w1, src_len, nc_len, n_pairs, prior_out,
                              (hipStream_t)stream, ctx->c.sr);
 }
@@ -350,6 +352,7 @@ int nc_chroma_lag(nc_ctx* ctx, const float* chroma, const int* src_idx, const in
                   void* stream) {
   CHECK_CTX(ctx);
   SET_DEVICE(ctx);
+  nc::MarkSpan ms_(ctx->c, "chroma_lag", (hipStream_t)stream);
   return nc::launch_chroma_lag(chroma, src_idx, nc_idx, n_pairs, lag_out, nullptr, (hipStream_t)stream);
 }
 
@@ -357,6 +360,7 @@ int nc_chroma_lag_margin(nc_ctx* ctx, const float* chroma, const int* src_idx, c
                          int* lag_out, double* margin_out, void* stream) {
   CHECK_CTX(ctx);
   SET_DEVICE(ctx);
+  nc::MarkSpan ms_(ctx->c, "chroma_lag", (hipStream_t)stream);
   return nc::launch_chroma_lag(chroma, src_idx, nc_idx, n_pairs, lag_out, margin_out, (hipStream_t)stream);
 }
 
@@ -371,6 +375,7 @@ int nc_energy_gate(nc_ctx* ctx, const double* energy_db, const int* w0, const in
                    double threshold_db, uint8_t* active_out, void* stream) {
   CHECK_CTX(ctx);
   SET_DEVICE(ctx);
+  nc::MarkSpan ms_(ctx->c, "energy_gate", (hipStream_t)stream);
   return nc::launch_energy_gate(energy_db, w0, w1, n_groups, threshold_db, active_out, (hipStream_t)stream);
 }
 
@@ -378,6 +383,7 @@ int nc_collect_valid(nc_ctx* ctx, const double* bpm, const int* nbeats, const ui
                      const int* w1, int n_groups, int min_beats, double* out_values, int* out_n, void* stream) {
   CHECK_CTX(ctx);
   SET_DEVICE(ctx);
+  nc::MarkSpan ms_(ctx->c, "collect_valid", (hipStream_t)stream);
   return nc::launch_collect_valid(bpm, nbeats, active, w0, w1, n_groups, min_beats, out_values, out_n,
                                   (hipStream_t)stream);
 }
@@ -386,6 +392,7 @@ int nc_pitch_hz(nc_ctx* ctx, const int* lags, int n, double* shift_out, double* 
                 void* stream) {
   CHECK_CTX(ctx);
   SET_DEVICE(ctx);
+  nc::MarkSpan ms_(ctx->c, "pitch_hz", (hipStream_t)stream);
   return nc::launch_pitch_hz(lags, n, shift_out, nc_hz, src_hz, (hipStream_t)stream);
 }
 
@@ -425,6 +432,7 @@ int nc_bootstrap_ratio(nc_ctx* ctx, const double* values, const int64_t* a_off, 
   a.cap = job_cap;
   a.ws = static_cast<char*>(ws);
   a.min_n = min_n;
+  nc::MarkSpan ms_(ctx->c, "bootstrap", (hipStream_t)stream);
   return nc::launch_bootstrap(a, n_jobs, (hipStream_t)stream);
 }
 
@@ -556,6 +564,7 @@ int nc_window_energy_blocks(nc_ctx* ctx, const float* sig, const void* trim_ws, 
                             void* stream) {
   CHECK_CTX(ctx);
   SET_DEVICE(ctx);
+  nc::MarkSpan ms_(ctx->c, "window_energy", (hipStream_t)stream);
   return nc::launch_window_energy_blocks(sig, trim_ws, n_files, file_off, win_off, win_file, n_win, win_len,
                                          energy_out, (hipStream_t)stream);
 }

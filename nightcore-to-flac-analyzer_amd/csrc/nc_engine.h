@@ -81,6 +81,23 @@ struct Context {
   KernelTimers* timers = nullptr;  // non-null while per-kernel profiling is enabled
 };
 
+// Profile mode 5 only: a span for a small entry point whose kernels record none themselves,
+// made by two one-thread marker launches on its stream around them (the first records the
+// wall clock when the stream reaches it, the second after the kernels): the span includes the
+// markers' own dispatch, so it is an upper bound.  No-op in every other mode.
+class MarkSpan {
+ public:
+  MarkSpan(Context& ctx, const char* tag, hipStream_t st);
+  ~MarkSpan();
+  MarkSpan(const MarkSpan&) = delete;
+  MarkSpan& operator=(const MarkSpan&) = delete;
+
+ private:
+  unsigned long long* span_ = nullptr;
+  hipStream_t st_;
+};
+int launch_span_mark(unsigned long long* span, int end, hipStream_t st);
+
 // Brackets one kernel launch with HIP events on its stream when profiling is enabled
 // (nc_profile_enable); no-op otherwise.  Used to time the dominant kernels live.
 class KTimer {

@@ -37,6 +37,7 @@ struct KernelTimers {
   std::vector<std::pair<hipEvent_t, hipEvent_t>> pool;
   bool events = true;
   bool roof_only = false;   // mode 3: events only around the roofline kernels
+  bool marks = false;       // mode 5: marker spans around the small entry points (MarkSpan)
   unsigned long long* span_buf = nullptr;   // [kSpanCap][kSpanLines][kSpanStride]: (start, end, pad)
   int span_used = 0;
   double clock_khz = 100000.0;
@@ -94,6 +95,18 @@ KTimer::~KTimer() {
   if (stop_) (void)hipEventRecord(static_cast<hipEvent_t>(stop_), st_);
 }
 
+MarkSpan::MarkSpan(Context& ctx, const char* tag, hipStream_t st) : st_(st) {
+  KernelTimers* t = ctx.timers;
+  if (!t || !t->marks || !t->span_buf || t->span_used >= kSpanCap) return;
+  t->slots[tag].spans.push_back(t->span_used);
+  span_ = t->span_buf + (size_t)t->span_used++ * kSpanLaunchU64;
+  (void)launch_span_mark(span_, 0, st_);
+}
+
+MarkSpan::~MarkSpan() {
+  if (span_) (void)launch_span_mark(span_, 1, st_);
+}
+
 void free_timers(Context& ctx) {
   delete ctx.timers;
   ctx.timers = nullptr;
@@ -104,13 +117,15 @@ void free_timers(Context& ctx) {
 namespace nc {
 
 // mode 0: off; 1: events + spans; 2: spans only; 3: events around the roofline kernels + spans;
-// 4: events around the roofline kernels, no spans
+// 4: events around the roofline kernels, no spans; 5: spans, plus marker spans around the small
+// entry points (MarkSpan: timeline diagnosis only, the markers are launches of their own)
 void profile_enable(Context& ctx, int mode) {
   free_timers(ctx);
   if (!mode) return;
   auto* t = new KernelTimers();
   t->events = mode == 1 || mode == 3 || mode == 4;
   t->roof_only = mode == 3 || mode == 4;
+  t->marks = mode == 5;
   if (t->events) {
     constexpr int kPoolPairs = 1024;   // a 10-step bench region launches ~500 timed kernels
     t->pool.reserve(kPoolPairs);

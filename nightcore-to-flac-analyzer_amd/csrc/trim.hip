@@ -181,8 +181,11 @@ int launch_trim(Context& ctx, const float* sig, const int64_t* file_off, const i
     hipLaunchKernelGGL(trim_blocks_kernel, dim3((unsigned)tiles), dim3(256), 0, st, sig, file_off, file_len,
                        frame_base, tile_base, n_files, blk, kt_.span());
   }
-  hipLaunchKernelGGL(trim_bounds_kernel, dim3(n_files), dim3(256), 0, st, blk, frame_base, file_len, top_db,
-                     out_start, out_end);
+  {
+    MarkSpan ms_(ctx, "trim_bounds", st);
+    hipLaunchKernelGGL(trim_bounds_kernel, dim3(n_files), dim3(256), 0, st, blk, frame_base, file_len, top_db,
+                       out_start, out_end);
+  }
   NC_HIP(hipGetLastError());
   return 0;
 }

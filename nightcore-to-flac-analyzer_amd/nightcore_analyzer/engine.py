@@ -614,7 +614,7 @@ class Engine:
         # NC_STREAM_PRIO="chroma,tail" sets the two side streams' priorities (torch: lower = more
         # urgent; the launch stream stays at 0).  Round 1 measured -1,-1 against 0,0 at 14.20
         # against 14.26 ms per step: within box-to-box spread, so the default is arbitrary
-        prio = [int(v) for v in os.environ.get("NC_STREAM_PRIO", "-1,-1").split(",")]
+        prio = [int(v) for v in os.environ.get("NC_STREAM_PRIO", "-1,-1").replace(":", ",").split(",")]
         self.chroma_stream = torch.cuda.current_stream(self.dev) if os.environ.get("NC_SERIAL_STREAMS") == "1" \
             else torch.cuda.Stream(self.dev, priority=prio[0])
         # consensus tail (bootstraps + D2H of a group) on a third stream: the window chain of the
@@ -716,7 +716,8 @@ class Engine:
         """The library's per-kernel timers (nc_profile_enable): False/0 off, True/1 HIP events
         around each launch plus the kernels' own execution spans, 2 spans only (cheap enough
         to leave on in a timed region), 3 events around the roofline kernels only plus spans,
-        4 those events alone."""
+        4 those events alone, 5 spans plus marker spans around the small entry points (timeline
+        diagnosis: tools/concurrency_spans.py --marks)."""
         self.ctx.call("nc_profile_enable", int(on))
 
     def _profile_read(self, fn: str) -> Dict[str, Tuple[float, int]]:

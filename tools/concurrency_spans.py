@@ -3,8 +3,10 @@
 over K batches with every timed kernel recording its execution span (profile mode 2), the spans
 dumped (nc_profile_dump_spans), and the time spent in each set of concurrently running kernels.
 Only the timed (tagged) kernels record spans; the small ones (bootstraps, plans, gathers,
-tails) count as "nothing", so the "-" row is an upper bound of the device idle.
-    python3 tools/concurrency_spans.py [K]"""
+tails) count as "nothing", so the "-" row is an upper bound of the device idle.  With --marks
+(profile mode 5) the small entry points get marker spans too (lower-case classes; each includes
+its two one-thread marker launches), and "-" is the time nothing of the engine's runs.
+    python3 tools/concurrency_spans.py [K] [--marks]"""
 import sys
 from pathlib import Path
 
@@ -13,7 +15,10 @@ sys.path.insert(0, str(REPO))
 sys.path.insert(0, str(REPO / "nightcore-to-flac-analyzer_amd"))
 
 CLS = {"stft_mel": "S", "window_tg": "W", "tuning_peaks": "T", "decimate": "D", "cqt_low": "L", "cqt_high": "H",
-       "tempo_beat": "B", "trim_blocks": "R", "tuning_select": "s"}
+       "tempo_beat": "B", "trim_blocks": "R", "tuning_select": "s",
+       # marker spans (--marks): the small entry points
+       "energy_gate": "g", "collect_valid": "v", "pitch_hz": "z", "tempo_prior": "r", "bootstrap": "b",
+       "chroma_lag": "l", "chroma_plan": "p", "cqt_tail": "t", "window_energy": "e", "trim_bounds": "u"}
 
 
 def table(spans, steps):
@@ -59,19 +64,27 @@ def main():
     import torch
     import bench
     from nightcore_analyzer import engine as E
-    K = int(sys.argv[1]) if len(sys.argv) > 1 else 10
+    args = [a for a in sys.argv[1:] if not a.startswith("--")]
+    K = int(args[0]) if args else 10
+    mode = 5 if "--marks" in sys.argv else 2
     pairs = bench.make_pairs(64, 180.0, 1000, 16)
     eng = E.get_engine(0)
     sig = eng.upload_signals([a for nc, src in pairs for a in (nc, src)])
     p = E.Params(compute_ibi=False)
     eng.analyze_batches([sig] * K, p)
-    eng.kernel_profile(2)
+    eng.kernel_profile(mode)
     torch.cuda.synchronize()
     eng.analyze_batches([sig] * K, p)
     spans = eng.device_spans()
     eng.kernel_profile(0)
     table(spans, K)
     gaps(spans, K)
+    if mode == 5:   # time per step in each small entry point (marker spans, summed)
+        tot = {}
+        for t, a, b in spans:
+            if CLS.get(t, "o").islower() and t != "tuning_select":
+                tot[t] = tot.get(t, 0.0) + (b - a)
+        print("marker spans, ms per step:", {k: round(v / K, 3) for k, v in sorted(tot.items(), key=lambda x: -x[1])})
 
 
 if __name__ == "__main__":
