@@ -208,6 +208,30 @@ def test_profile_modes_time_what_they_say(eng):
         assert all(ms > 0 and n > 0 for ms, n in ev.values())
 
 
+def test_profile_marker_spans(eng):
+    """Profile mode 5: the timed kernels' spans plus marker spans around the small entry points
+    (bootstraps, gate, valid-tempo collection, prior, chroma plan / tail / lag, trim bounds,
+    window energies); results unchanged, and the markers leave modes 2 and 4 alone."""
+    nc, src = synth.make_pair(40.0, 1013)
+    p = E.Params(compute_ibi=False)
+    ref = eng.analyze([(nc, src)], p)[0].result
+    eng.kernel_profile(5)
+    out = eng.analyze([(nc, src)], p)[0].result
+    spans = eng.device_spans()
+    eng.kernel_profile(2)
+    eng.analyze([(nc, src)], p)
+    spans2 = eng.device_spans()
+    eng.kernel_profile(0)
+    assert (out.tempo_ratio, out.pitch_ratio, out.tempo_ci, out.pitch_ci) == \
+           (ref.tempo_ratio, ref.pitch_ratio, ref.tempo_ci, ref.pitch_ci)
+    tags = {t for t, _, _ in spans}
+    small = {"bootstrap", "energy_gate", "collect_valid", "tempo_prior", "chroma_plan", "cqt_tail", "chroma_lag",
+             "trim_bounds", "window_energy"}
+    assert small <= tags and {"stft_mel", "cqt_low", "cqt_high"} <= tags, tags
+    assert all(0.0 <= a <= b for _, a, b in spans)
+    assert not small & {t for t, _, _ in spans2}      # mode 2 records no markers
+
+
 def test_profile_span_dump_and_busy_agree(eng):
     """nc_profile_dump_spans (mode 2): every timed launch of one analysis with its tag, start
     <= end, inside one extent; the union of the dumped spans equals what nc_profile_read_busy
