@@ -380,19 +380,22 @@ def _group_bounds(B: int, group_pairs, ) -> List[Tuple[int, int]]:
             left -= n
             i += 1
     elif group_pairs is None:
-        # default: groups of 16 pairs, the last two evened out when 16 does not divide the batch
-        # (no group under 8 pairs once B > 16).  Round 5, with the oldest group assembled as soon
+        # default: groups of 32 pairs, the last two evened out when 32 does not divide the batch
+        # (no group under 16 pairs once B > 32).  Round 5, with the oldest group assembled as soon
         # as it completes (Engine.EAGER_FINISH): 4 x 16 ran the 64-pair step 4-5 % faster than the
-        # earlier 6/26/26/6 (8.73-8.84 against 9.18-9.40 ms in five rotated rounds on one box;
-        # 10/18/18/18 8.79-8.97, 12/20/20/12 8.83-9.01, 14/18/18/14 8.79-9.02, 8/14x4 8.96-9.32,
-        # 8x8 10.0; profiles/r5_group_schedule.txt, tools/idle_probe.py)
-        q, r = divmod(B, 16)
-        if B <= 16:
+        # earlier 6/26/26/6 (profiles/r5_group_schedule.txt).  Round 6, after the STFT frame queue
+        # made each group's device work shorter against its fixed tail (two bootstraps, the chroma
+        # plan and tail, six small launches per group): 2 x 32 7.96-8.59 against 4 x 16
+        # 8.44-9.32 ms per step in alternating bench runs, device idle 2.6-3.0 against 4.8 %
+        # (profiles/r6_group_schedule.txt; 21/21/22 and 64 no better).  NC_GROUP_PAIRS=G: A/B knob
+        G = max(1, int(os.environ.get("NC_GROUP_PAIRS", "32")))
+        q, r = divmod(B, G)
+        if B <= G:
             sizes = [B] if B else []
-        elif r == 0 or r >= 8:
-            sizes = [16] * q + ([r] if r else [])
+        elif r == 0 or r >= G // 2:
+            sizes = [G] * q + ([r] if r else [])
         else:
-            sizes = [16] * (q - 1) + [(16 + r + 1) // 2, (16 + r) // 2]
+            sizes = [G] * (q - 1) + [(G + r + 1) // 2, (G + r) // 2]
     else:
         gp = max(1, int(group_pairs))
         sizes = [gp] * (B // gp) + ([B % gp] if B % gp else [])

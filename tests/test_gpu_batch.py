@@ -13,7 +13,7 @@ these tests check, on batches that take it:
   (oracle/refglue.run_arrays: the port of pipeline.py:23-216), run in a process
   pool that starts with the module so it overlaps the GPU tests;
 * every PIPELINE_CASES golden (the reference's own pipeline.run outputs) inside a
-  17-pair batch, with the default schedule and with group_pairs=2 (9 groups, more
+  17-pair batch, with the default schedule (one group), group_pairs=9 (9/8) and group_pairs=2 (9 groups, more
   than the peak ring's max(GROUPS_IN_FLIGHT, MAX_GROUPS_IN_FLIGHT) + 1 = 6 slots, the
   ring reset before the call so it wraps within it), equals the fixture field for
   field, including str(result), the logs and the CLI JSON.
@@ -134,7 +134,7 @@ def _key(o: E.PairOutcome):
 
 
 def test_group_schedule_is_multi_group():
-    assert [b - a for a, b in E._group_bounds(N_PAIRS, None)] == [16, 16, 16, 16]
+    assert [b - a for a, b in E._group_bounds(N_PAIRS, None)] == [32, 32]
     ring = max(E.Engine.GROUPS_IN_FLIGHT, E.Engine.MAX_GROUPS_IN_FLIGHT) + 1
     assert len(E._group_bounds(17, 2)) == 9 > ring + 1
 
@@ -159,7 +159,7 @@ def _kw_classes():
     return sorted(out.items(), key=lambda kv: kv[1][0])
 
 
-@pytest.mark.parametrize("group_pairs", [None, 2])
+@pytest.mark.parametrize("group_pairs", [None, 2, 9])
 @pytest.mark.parametrize("kw_names", _kw_classes(), ids=lambda kv: "+".join(kv[1]))
 def test_goldens_inside_multi_group_batch(eng, bench_pairs, golden_pipeline, kw_names, group_pairs):
     kwkey, names = kw_names
@@ -230,9 +230,9 @@ def test_pipelined_batches_equal_separate_calls(eng, bench_pairs):
     batch and a repeated batch."""
     p = E.Params(compute_ibi=False)
     flat = lambda prs: [a for nc, src in prs for a in (nc, src)]
-    a = eng.upload_signals(flat(bench_pairs[:20]))
-    b = eng.upload_signals(flat(bench_pairs[20:25]))
-    c = eng.upload_signals(flat(bench_pairs[25:45]))
+    a = eng.upload_signals(flat(bench_pairs[:40]))      # two groups of the default schedule (20/20)
+    b = eng.upload_signals(flat(bench_pairs[40:45]))
+    c = eng.upload_signals(flat(bench_pairs[45:64]))
     batches = [a, b, c, a]
     got = eng.analyze_batches(batches, p)
     assert len(got) == len(batches)

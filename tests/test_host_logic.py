@@ -118,17 +118,18 @@ def test_pair_groups_cover_the_batch_in_order():
 
 
 def test_default_pair_group_schedule():
-    """The engine's default schedule (groups of 16, the last two evened out) covers any batch in
-    order with no empty or small stragglers; the config-3 batch gets 16/16/16/16."""
+    """The engine's default schedule (groups of 32, the last two evened out) covers any batch in
+    order with no empty or small stragglers; the config-3 batch gets 32/32."""
     from nightcore_analyzer.engine import _group_bounds
-    assert [b - a for a, b in _group_bounds(64, None)] == [16, 16, 16, 16]
-    assert [b - a for a, b in _group_bounds(70, None)] == [16, 16, 16, 11, 11]
-    assert [b - a for a, b in _group_bounds(17, None)] == [9, 8]
+    assert [b - a for a, b in _group_bounds(64, None)] == [32, 32]
+    assert [b - a for a, b in _group_bounds(70, None)] == [32, 19, 19]
+    assert [b - a for a, b in _group_bounds(17, None)] == [17]
+    assert [b - a for a, b in _group_bounds(33, None)] == [17, 16]
     assert _group_bounds(0, None) == []
     for B in range(1, 200):
         g = _group_bounds(B, None)
         sizes = [b - a for a, b in g]
         assert g[0][0] == 0 and g[-1][1] == B and sum(sizes) == B
         assert all(a1 == b0 for (a0, a1), (b0, b1) in zip(g, g[1:]))
-        assert min(sizes) >= min(B, 8) and max(sizes) <= 16
+        assert min(sizes) >= min(B, 16) and max(sizes) <= 32
     assert [b - a for a, b in _group_bounds(10, [3, 4])] == [3, 4, 3]
