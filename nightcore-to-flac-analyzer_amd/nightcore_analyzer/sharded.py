@@ -365,14 +365,14 @@ _ERR_ROW = (0.0,) + (_NAN,) * (len(RES_FIELDS) - 1)
 
 
 def result_row(o: PairOutcome) -> tuple:
-    """The RES_FIELDS row of one outcome (NaN for None; ok = 0 for an error outcome)."""
+    """The RES_FIELDS row of one outcome (None where the result has None: the f64 table makes
+    it NaN; ok = 0 for an error outcome)."""
     r = o.result
     if r is None:
         return _ERR_ROW
     tr, tc, pr, pc, ir, ic, a, b, c, d, e, f, g, h, i = _ROW_GET(r)
     ic = ic or (None, None)
-    return (1.0, tr, tc[0], tc[1], pr, pc[0], pc[1], _opt(ir), _opt(ic[0]), _opt(ic[1]), a, b, c, d,
-            _opt(e), _opt(f), _opt(g), _opt(h), _opt(i))
+    return (1.0, tr, tc[0], tc[1], pr, pc[0], pc[1], ir, ic[0], ic[1], a, b, c, d, e, f, g, h, i)
 
 
 _DTYPES: Dict[str, np.dtype] = {}
@@ -380,26 +380,34 @@ _DTYPES: Dict[str, np.dtype] = {}
 
 def pack_tables(tables: Dict[str, np.ndarray], views: Optional[Dict[str, tuple]] = None) -> bytes:
     """Named numeric arrays as one byte string: an 8-byte header length, a JSON header (name,
-    dtype, shape, offset of each array) and the raw bytes, each array 8-byte aligned.
-    ``views``: {name: (table name, byte offset, dtype str, shape)} — arrays that are
-    stretches of another table's bytes, sent as header entries only (an arena's views)."""
-    meta, chunks, off, at = [], [], 0, {}
+    dtype, shape, offset of each array) and the raw bytes.  Arrays of one dtype are laid out
+    back to back (one concatenation per dtype, each dtype block 8-byte aligned).  ``views``:
+    {name: (table name, byte offset, dtype str, shape)} — arrays that are stretches of another
+    table's bytes, sent as header entries only (an arena's views)."""
+    groups: Dict[str, list] = {}
     for name, a in tables.items():
         a = np.asarray(a)
         if a.dtype.kind not in "biuf":
             raise TypeError(f"record table {name!r}: dtype {a.dtype} is not numeric")
-        if not a.flags.c_contiguous:
-            a = a.copy()
-        meta.append((name, a.dtype.str, a.shape, off))
-        at[name] = off
-        n = a.nbytes
-        if n:
-            chunks.append(memoryview(a.reshape(-1)).cast("B"))
-        if n % 8:
-            chunks.append(b"\0" * (-n % 8))
-        off += (n + 7) & ~7
+        groups.setdefault(a.dtype.str, []).append((name, a))
+    chunks, off, at = [], 0, {}
+    for dt, items in groups.items():
+        flat = [a.reshape(-1) for _, a in items]
+        block = np.concatenate(flat) if len(flat) > 1 else np.ascontiguousarray(flat[0])
+        isz = block.itemsize
+        o = off
+        for name, a in items:
+            at[name] = (dt, a.shape, o)
+            o += a.size * isz
+        if block.nbytes:
+            chunks.append(block.view(np.uint8))
+        pad = -block.nbytes % 8
+        if pad:
+            chunks.append(bytes(pad))
+        off += block.nbytes + pad
+    meta = [(name,) + at[name] for name in tables]            # the tables' own order
     for name, (base, o, dt, shape) in (views or {}).items():
-        meta.append((name, dt, shape, at[base] + o))
+        meta.append((name, dt, shape, at[base][2] + o))
     head = json.dumps(meta, separators=(",", ":")).encode()
     head += b" " * (-len(head) % 8)
     return b"".join([len(head).to_bytes(8, "little"), head] + chunks)
@@ -461,7 +469,7 @@ def _ctx_tables(ctx: AsmContext, pre: str, out: Dict[str, np.ndarray], views: Di
     out[pre + "w1"] = np.asarray(ctx.w1, np.int64)
     for k in ("f_len", "strip_len", "lead", "trail"):
         out[pre + k] = np.asarray(getattr(ctx, k))
-    out[pre + "intro"] = np.array([_opt(v) for v in ctx.intro], np.float64)
+    out[pre + "intro"] = np.array(ctx.intro, np.float64).reshape(-1)       # None -> NaN
     out[pre + "intro_none"] = np.array([v is None for v in ctx.intro], np.bool_)
     if ctx.align is not None:
         out[pre + "align"] = np.array([(_NAN, _NAN) if a is None else a for a in ctx.align], np.float64).reshape(-1, 2)

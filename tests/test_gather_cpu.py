@@ -114,7 +114,7 @@ def test_result_table_without_rebuilding(outcomes):
     assert tab[2, S.RES_FIELDS.index("tempo_ratio")] == r.tempo_ratio
     assert tab[2, S.RES_FIELDS.index("ibi_hi")] == r.ibi_ci[1]
     assert np.array_equal(tab[0], tab[2], equal_nan=True) and tab[1, 0] == 0.0 and np.isnan(tab[1, 1:]).all()
-    assert _norm(tab[2].tolist()) == _norm(list(S.result_row(outcomes["ibi"])))
+    assert _norm(tab[2].tolist()) == _norm(np.array(S.result_row(outcomes["ibi"]), np.float64).tolist())
 
 
 def test_records_in_segments(outcomes):
@@ -132,7 +132,7 @@ def test_records_in_segments(outcomes):
     tab = g.table()
     assert g.decoded() == 4 and len(g._parts[1].seg) == 2
     assert tab[1, 0] == 0.0 and np.isnan(tab[2]).all()
-    assert _norm(tab[0].tolist()) == _norm(tab[3].tolist()) == _norm(list(S.result_row(o)))
+    assert _norm(tab[0].tolist()) == _norm(tab[3].tolist()) == _norm(np.array(S.result_row(o), np.float64).tolist())
     assert _key(g[3]) == _key(o) and _key(g[0]) == _key(o) and g[1] == PairOutcome()
     assert len(g._parts[1].t) == 2             # both segments parsed, once each
     for cut in (10, len(blob) - 1):
@@ -254,7 +254,7 @@ def test_byte_gather_three_ranks_every_rank_holds_every_outcome(outcomes):
     for r in range(3):
         keys, tab = res[r]
         assert keys == ref, (r, keys)
-        assert _norm(tab) == _norm([list(S.result_row(o))] * 4)
+        assert _norm(tab) == _norm([np.array(S.result_row(o), np.float64).tolist()] * 4)
 
 
 def test_one_rank_group_runs_the_collectives_with_collect_at_one(outcomes):

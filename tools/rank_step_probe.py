@@ -47,8 +47,18 @@ def main():
                 r.table()                   # the caller's read of every pair's result row
         return res
 
+    def windows_nopack():
+        # the gather with empty records (timing only): what the packing itself costs the step
+        add = S._StepRecords.add
+        S._StepRecords.add = lambda self, outs: None
+        try:
+            return windows(True)
+        finally:
+            S._StepRecords.add = add
+
     variants = {"analyze_batches": lambda: eng.analyze_batches([sig] * K, params),
                 "windows_gather": lambda: windows(True),
+                "windows_gather_nopack": windows_nopack,
                 "windows_nogather": lambda: windows(False)}
     for f in variants.values():
         f()
