@@ -354,7 +354,8 @@ def main():
         if any(o.error is not None for o in mine):
             raise RuntimeError("a window-sharded step failed")
         win_total = sum(o.detail["energy_src"].size + o.detail["energy_nc"].size for o in mine)
-        if any(not np.array_equal(tabs[0][b], result_row(o), equal_nan=True) for b, o in enumerate(mine)):
+        if any(not np.array_equal(tabs[0][b], np.array(result_row(o), np.float64), equal_nan=True)
+               for b, o in enumerate(mine)):
             raise RuntimeError("a gathered result row differs from its rebuilt outcome")
         del res, mine, tabs                     # not kept (see below)
     elif pipelined:
