@@ -406,7 +406,16 @@ def main():
         # keeps the outcomes of the pairs it owns)
         variants = [("windows_nogather", 0.0, False), ("pairs", None, False), ("windows_split", 0.5, True)] \
             if win_mode else [("windows", 0.0, True), ("windows_split", 0.5, True)]
+        # NC_BENCH_MODES_EXTRA=1 (rehearsal diagnostics): the headline's steps again after the
+        # modes, untraced with and without the gather, then under the headline's roofline events
+        # (profile mode 4)
+        extra = win_mode and os.environ.get("NC_BENCH_MODES_EXTRA", "0") == "1"
+        if extra:
+            variants += [("windows_gather_again", 0.0, True), ("windows_nogather_again", 0.0, False),
+                         ("windows_gather_again_prof4", 0.0, True)]
         for name, off, gat in variants:
+            if name.endswith("_prof4"):
+                eng.kernel_profile(4)
             barrier()
             torch.cuda.synchronize()
             t1 = time.perf_counter()
@@ -427,6 +436,9 @@ def main():
                          sum_over_ranks(sum(o.detail["energy_src"].size + o.detail["energy_nc"].size
                                             for _, o in r_[0])))
             modes[name] = {"value": n_win * args.steps / e1, "ms_per_step": e1 / args.steps * 1e3}
+            if name.endswith("_prof4"):
+                eng.kernel_times()
+                eng.kernel_profile(False)
         from nightcore_analyzer.sharded import shard_plan
         sp = shard_plan(lengths, params, world, 0.5)
         modes["windows_split"].update(split_pairs=int(sp.split.sum()),
